@@ -1,0 +1,44 @@
+/* sbpmf_oracle.h -- TEST INFRASTRUCTURE ONLY (see sbpmf_oracle.c header). */
+#ifndef SBPMF_ORACLE_H_
+#define SBPMF_ORACLE_H_
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORACLE_QUIRKS_FINAL = 0, ORACLE_QUIRKS_SBPMF2 = 1, ORACLE_QUIRKS_NONE = 2 };
+
+typedef struct {
+    uint32_t K, iters, burnin;
+    unsigned seed;
+    int quirks;
+    double init_stdev, clamp_lo, clamp_hi;
+    double sweep_seconds_limit; /* >0: stop after this many seconds (bounded CPU baseline) */
+} oracle_config;
+
+typedef struct {
+    double *rmse, *rmse_this, *tau; /* [rmse_cap] or NULL */
+    uint32_t rmse_cap;
+    double *U, *V;     /* row-major [I][K], [J][K] or NULL */
+    double *hyper;     /* [4K] or NULL */
+    double *pred_sum;  /* [n_test] or NULL */
+    uint32_t num_users, num_items, sweeps_done;
+    double seconds;
+} oracle_result;
+
+void oracle_config_default(oracle_config *c);
+int oracle_run_arrays(const oracle_config *cfg, uint64_t n_train, const uint32_t *tu, const uint32_t *ti,
+                      const double *tr, uint64_t n_test, const uint32_t *su, const uint32_t *si,
+                      const double *sr, uint32_t num_users, uint32_t num_items, oracle_result *res);
+int oracle_load_triples(const char *path, uint64_t *n, uint32_t **u, uint32_t **i, double **r);
+void oracle_free(void *p);
+void oracle_srand(unsigned seed);
+int oracle_rand(void);
+double oracle_ran_uniform(void);
+double oracle_ran_gaussian(void);
+double oracle_ran_gamma(double alpha);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
