@@ -1,0 +1,194 @@
+/*
+ * sbmf.h -- C ABI of the MI355X-native Scalable-BPMF (SBPMF) Gibbs sampler.
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference
+ * has no library interface: its sampler is the body of main() in
+ * src/libfm/gibbs_sbpmf_final.cpp:23-595 (and the libFM learner behind
+ * `bin/libFM -method mcmc`, src/libfm/libfm.cpp:72-644 ->
+ * fm_learn_mcmc::learn, fm_learn_mcmc.h:1154).  Each entry point below names
+ * the reference code it replaces.  Plain C types only: no torch, no HIP types.
+ * The CLI (`sbmf`, libFM flag grammar) and the Python mirror (package
+ * sbmf/) are built on exactly these calls; INTEGRATION.md shows the ctypes
+ * binding a maintainer would add.
+ *
+ * Ownership: the caller owns every host array it passes (they are copied in);
+ * the library owns all device memory, streams and RCCL communicators.
+ * Errors: every call returns SBMF_OK (0) or a negative SBMF_E_* code and
+ * records a message readable with sbmf_last_error(ctx) (or
+ * sbmf_last_global_error() when no context exists).  The reference instead
+ * throws std::string / const char* and still exits 0 (libfm.cpp:636-640).
+ * Threading: a context is used by one host thread at a time.
+ * Device: every compute entry point requires a gfx950 GPU; there is no CPU
+ * fallback (sbmf_create fails with SBMF_E_DEVICE without one).
+ */
+#ifndef SBMF_H_
+#define SBMF_H_
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBMF_ABI_VERSION 1
+
+enum sbmf_status {
+    SBMF_OK = 0,
+    SBMF_E_ARG = -1,      /* invalid argument / configuration                    */
+    SBMF_E_STATE = -2,    /* call out of order (e.g. run before set_train)       */
+    SBMF_E_DEVICE = -3,   /* HIP runtime error or no usable GPU                  */
+    SBMF_E_IO = -4,       /* file open / parse error                             */
+    SBMF_E_COMM = -5,     /* RCCL error                                          */
+    SBMF_E_NOMEM = -6     /* host or device allocation failed                    */
+};
+
+/* RNG mode. REFERENCE replays the reference's exact variate stream (glibc
+ * rand(), Leva normals, Marsaglia-Tsang gammas; src/util/random.h:118-176),
+ * generated on the host and consumed by the GPU; PHILOX draws counter-based
+ * normals inside the kernels (throughput mode, rank-count independent). */
+enum sbmf_rng_mode { SBMF_RNG_REFERENCE = 0, SBMF_RNG_PHILOX = 1 };
+
+/* Quirk set. FINAL = gibbs_sbpmf_final.cpp semantics (posterior VARIANCE
+ * passed as the stdev of ran_gaussian, :393,413,485,529; init N(0,1); clamp
+ * [1,5]).  SBPMF2 = src/libfm/gibbs_sbpmf2.cpp (:240,248,386,406,412,557:
+ * init N(0,0.1), nu0 without 1/2, mu_v uses sigma_u*, clamp [0.5,5]).
+ * NONE = the statistically correct sampler (stdev = sqrt(variance)). */
+enum sbmf_quirks { SBMF_QUIRKS_FINAL = 0, SBMF_QUIRKS_SBPMF2 = 1, SBMF_QUIRKS_NONE = 2 };
+
+/* Arithmetic type of factors, residuals and reductions on the GPU.  F64 is
+ * the reference's (all-double) arithmetic. */
+enum sbmf_precision { SBMF_F64 = 0, SBMF_F32 = 1 };
+
+typedef struct sbmf_config {
+    uint32_t num_factor;   /* K: -dim 'k0,k1,K' (libfm.cpp:93); reference D=20 (:218)          */
+    uint32_t num_iter;     /* collection sweeps: -iter (libfm.cpp:97); reference 100 (:299)     */
+    uint32_t burnin;       /* burn-in sweeps before collection; reference 0 (:300)              */
+    uint64_t seed;         /* -seed (honoured; the reference ignores it, libfm.cpp:124)         */
+    int32_t rng_mode;      /* enum sbmf_rng_mode                                               */
+    int32_t quirks;        /* enum sbmf_quirks                                                 */
+    int32_t precision;     /* enum sbmf_precision                                              */
+    int32_t device;        /* HIP device ordinal for this context                              */
+    double init_stdev;     /* <0: quirk-set default (1.0 final / 0.1 sbpmf2); -init_stdev      */
+    double clamp_lo;       /* prediction clamp; <0: quirk-set default (1.0 / 0.5)              */
+    double clamp_hi;       /* default 5.0 (gibbs_sbpmf_final.cpp:556)                          */
+    /* hyperpriors (gibbs_sbpmf_final.cpp:256-269) */
+    double a0, b0, alpha0, beta0, nu0, mu0;
+    uint32_t recompute_every; /* recompute E=r-UV from scratch every n sweeps (reference: every
+                                 sweep, :317-334); 0 = only at start                            */
+    uint32_t eval_train;      /* 1: compute train RMSE of the current sample each sweep          */
+    uint32_t eval_test;       /* 1: test prediction + running-mean RMSE each sweep (:539-563)    */
+    uint32_t gram_threshold;  /* rows with more ratings use the Gram route (0 = default)         */
+    uint32_t reserved[8];
+} sbmf_config;
+
+/* Per-sweep report passed to the run callback. */
+typedef struct sbmf_sweep_info {
+    uint32_t sweep;            /* 0-based sweep index (burn-in included)                     */
+    uint32_t collected;        /* 1 if this sweep entered the running mean                   */
+    double rmse_avg;           /* test RMSE of the running-mean prediction (the reference's
+                                  "rmse is", gibbs_sbpmf_final.cpp:562); NaN if no test set  */
+    double rmse_this;          /* test RMSE of this sweep's sample alone                      */
+    double rmse_train;         /* train RMSE of this sample (clamped), NaN if not evaluated   */
+    double tau;                /* noise precision drawn this sweep                           */
+    double ms_sweep;           /* device time of the sweep (half-sweeps + hyper), ms          */
+    double ms_eval;            /* device time of the test evaluation, ms                      */
+} sbmf_sweep_info;
+
+/* Return non-zero to stop the run early. */
+typedef int (*sbmf_sweep_cb)(const sbmf_sweep_info* info, void* user);
+
+typedef struct sbmf_ctx sbmf_ctx;
+
+/* --- configuration / lifetime -------------------------------------------------------------- */
+/* Fill reference defaults (gibbs_sbpmf_final.cpp:218,256-269,299-300). */
+int sbmf_config_default(sbmf_config* cfg);
+/* Create a context on cfg->device.  Replaces the reference's setup in main()
+ * (gibbs_sbpmf_final.cpp:252-306).  Fails with SBMF_E_DEVICE without a GPU. */
+int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out);
+void sbmf_destroy(sbmf_ctx* ctx);
+const char* sbmf_last_error(const sbmf_ctx* ctx);
+const char* sbmf_last_global_error(void);
+int sbmf_abi_version(void);
+
+/* --- data ---------------------------------------------------------------------------------- */
+/* Training triples (0-based ids, any order; file order is preserved as the
+ * reference's R / R_t entry order, gibbs_sbpmf_final.cpp:192-215). */
+int sbmf_set_train(sbmf_ctx* ctx, uint64_t n, const uint32_t* user, const uint32_t* item, const double* rating);
+int sbmf_set_test(sbmf_ctx* ctx, uint64_t n, const uint32_t* user, const uint32_t* item, const double* rating);
+/* Optional: row counts.  Default (0,0) = max id + 1 over train and test
+ * (gibbs_sbpmf_final.cpp:146-148); empty ids are kept and sampled. */
+int sbmf_set_dims(sbmf_ctx* ctx, uint32_t num_users, uint32_t num_items);
+
+/* Build the device layout (CSR / CSC, degree bins), upload, and initialise
+ * U, V (draws the init variates, :236-250).  Implicitly called by sbmf_run. */
+int sbmf_prepare(sbmf_ctx* ctx);
+
+/* Run `sweeps` Gibbs sweeps (continuing the chain across calls).  One sweep =
+ * the reference loop body gibbs_sbpmf_final.cpp:309-564: tau, per-factor
+ * hyperparameters, user half-sweep, item half-sweep, test evaluation. */
+int sbmf_run(sbmf_ctx* ctx, uint32_t sweeps, sbmf_sweep_cb cb, void* user);
+
+/* --- results ------------------------------------------------------------------------------- */
+/* Averaged clamped test prediction (sum / collected sweeps; libfm -out,
+ * libfm.cpp:629-634).  out: [n_test]. */
+int sbmf_predict(sbmf_ctx* ctx, double* out);
+/* Factors as row-major doubles: U [num_users][K], V [num_items][K]. Either may be NULL. */
+int sbmf_get_factors(sbmf_ctx* ctx, double* U, double* V);
+/* Overwrite the factors (row-major doubles).  For checkpoints and tests. */
+int sbmf_set_factors(sbmf_ctx* ctx, const double* U, const double* V);
+/* Hyperparameters [sigma_u | mu_u | sigma_v | mu_v] (4K doubles) and tau. */
+int sbmf_get_hyper(sbmf_ctx* ctx, double* hyper4k, double* tau);
+int sbmf_get_dims(sbmf_ctx* ctx, uint32_t* num_users, uint32_t* num_items, uint64_t* n_train, uint64_t* n_test);
+
+/* --- measurement --------------------------------------------------------------------------- */
+/* Device times of the last sweep (HIP events on the context's stream).
+ * kern_*[side][kind]: side 0 = user half, 1 = item half; kind 0..3 = the
+ * row-kernel bins (1 wave / row with 2 or 8 rating slots per lane, 4 or 8
+ * waves / row), 4 = Gram route (all its launches).  kern_bytes is the
+ * algorithmic traffic of that launch per SURVEY.md §8(d): per rating
+ * s*K (partner row) + 4 (partner id) + s (residual), per row 2*s*K (own row
+ * read + write), s = 4 (f32) or 8 (f64). */
+typedef struct sbmf_timing {
+    double ms_user_half, ms_item_half, ms_hyper, ms_eval, ms_comm;
+    double kern_ms[2][5];
+    uint64_t kern_bytes[2][5];
+    uint32_t kern_rows[2][5];
+    uint64_t bytes_algorithmic;  /* whole sweep, both halves                                    */
+    uint32_t n_launch;           /* kernel launches in the last sweep                           */
+} sbmf_timing;
+int sbmf_get_timing(sbmf_ctx* ctx, sbmf_timing* t);
+
+/* --- multi-GPU (one process per GPU, RCCL over xGMI) ---------------------------------------- */
+/* 128-byte RCCL unique id, produced by rank 0 and shared by the launcher. */
+int sbmf_comm_unique_id(uint8_t id[128]);
+/* Join an nranks-wide communicator; users and items are then block-partitioned
+ * (nnz-balanced) and U / V blocks are all-gathered between half-sweeps. */
+int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]);
+
+/* --- loaders (the reference's input formats) ------------------------------------------------ */
+typedef struct sbmf_ratings {
+    uint64_t n;
+    uint32_t* user;
+    uint32_t* item;
+    double* rating;
+} sbmf_ratings;
+/* SBPMF triple format "u<sep>i<sep>r" per line, lines accepted iff
+ * sscanf("%u%c%u%c%lf") >= 5 (gibbs_sbpmf_final.cpp:43). */
+int sbmf_load_triples(const char* path, sbmf_ratings* out);
+/* libFM text "r f1:v f2:v" (Data.h:192-217) with exactly one user and one
+ * item feature per line: the first feature is the user id, the second the
+ * item id minus item_offset (users-first layout, e.g. data/m1m/m100k). */
+int sbmf_load_libfm(const char* path, uint32_t item_offset, sbmf_ratings* out);
+void sbmf_free_ratings(sbmf_ratings* r);
+
+/* --- test hooks ---------------------------------------------------------------------------- */
+/* The host glibc-compatible stream (reference mode): n values of rand(),
+ * ran_gaussian() and ran_gamma(shape) for seed. */
+int sbmf_ref_stream(uint32_t seed, int kind, double shape, uint64_t n, double* out);
+/* Philox normals as the kernels draw them: z for (seed, sweep, tag, row, k<K). out [K]. */
+int sbmf_philox_normals(uint64_t seed, uint32_t sweep, uint32_t tag, uint32_t row, uint32_t K, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SBMF_H_ */

@@ -1,0 +1,110 @@
+"""oracle.py -- TEST INFRASTRUCTURE ONLY: ctypes wrapper of liboracle.so.
+
+The CPU restatement of the reference sampler (sbpmf_oracle.c), used only by
+tests/, __graft_entry__.smoke() (as the checker) and bench.py's cpu_baseline.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+QUIRKS = {"final": 0, "sbpmf2": 1, "none": 2}
+
+
+class OracleConfig(C.Structure):
+    _fields_ = [("K", C.c_uint32), ("iters", C.c_uint32), ("burnin", C.c_uint32), ("seed", C.c_uint),
+                ("quirks", C.c_int), ("init_stdev", C.c_double), ("clamp_lo", C.c_double),
+                ("clamp_hi", C.c_double), ("sweep_seconds_limit", C.c_double)]
+
+
+class OracleResult(C.Structure):
+    _fields_ = [("rmse", C.POINTER(C.c_double)), ("rmse_this", C.POINTER(C.c_double)),
+                ("tau", C.POINTER(C.c_double)), ("rmse_cap", C.c_uint32),
+                ("U", C.POINTER(C.c_double)), ("V", C.POINTER(C.c_double)), ("hyper", C.POINTER(C.c_double)),
+                ("pred_sum", C.POINTER(C.c_double)), ("num_users", C.c_uint32), ("num_items", C.c_uint32),
+                ("sweeps_done", C.c_uint32), ("seconds", C.c_double)]
+
+
+def build():
+    import subprocess
+    subprocess.run(["make", "-C", HERE, "all"], check=True, capture_output=True)
+
+
+def _lib():
+    if not os.path.exists(LIB):
+        build()
+    lib = C.CDLL(LIB)
+    lib.oracle_run_arrays.restype = C.c_int
+    lib.oracle_config_default.argtypes = [C.POINTER(OracleConfig)]
+    lib.oracle_ran_gaussian.restype = C.c_double
+    lib.oracle_ran_gamma.restype = C.c_double
+    lib.oracle_ran_gamma.argtypes = [C.c_double]
+    lib.oracle_ran_uniform.restype = C.c_double
+    lib.oracle_srand.argtypes = [C.c_uint]
+    return lib
+
+
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        _L = _lib()
+    return _L
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def run(train, test, K=20, iters=100, seed=1, quirks="final", burnin=0, num_users=0, num_items=0,
+        seconds_limit=0.0, want_factors=True):
+    """train/test: (user, item, rating) arrays.  Returns dict with per-sweep
+    'rmse' (running mean, the reference's "rmse is"), 'rmse_this', 'tau',
+    final 'U' [I][K], 'V' [J][K], 'hyper', 'pred_sum', 'seconds'."""
+    L = lib()
+    cfg = OracleConfig()
+    L.oracle_config_default(C.byref(cfg))
+    cfg.K, cfg.iters, cfg.burnin, cfg.seed, cfg.quirks = K, iters, burnin, seed, QUIRKS[quirks]
+    cfg.sweep_seconds_limit = seconds_limit
+    tu, ti, tr = (np.ascontiguousarray(train[0], np.uint32), np.ascontiguousarray(train[1], np.uint32),
+                  np.ascontiguousarray(train[2], np.float64))
+    su, si, sr = (np.ascontiguousarray(test[0], np.uint32), np.ascontiguousarray(test[1], np.uint32),
+                  np.ascontiguousarray(test[2], np.float64))
+    I = num_users or int(max(tu.max(initial=0), su.max(initial=0))) + 1
+    J = num_items or int(max(ti.max(initial=0), si.max(initial=0))) + 1
+    n_sw = iters + burnin
+    res = OracleResult()
+    rm, rt, ta = np.full(n_sw, np.nan), np.full(n_sw, np.nan), np.full(n_sw, np.nan)
+    res.rmse, res.rmse_this, res.tau, res.rmse_cap = _p(rm, C.c_double), _p(rt, C.c_double), _p(ta, C.c_double), n_sw
+    U = V = None
+    if want_factors:
+        U, V = np.zeros((I, K)), np.zeros((J, K))
+        res.U, res.V = _p(U, C.c_double), _p(V, C.c_double)
+    hyper = np.zeros(4 * K)
+    res.hyper = _p(hyper, C.c_double)
+    ps = np.zeros(max(len(sr), 1))
+    res.pred_sum = _p(ps, C.c_double)
+    rc = L.oracle_run_arrays(C.byref(cfg), C.c_uint64(len(tr)), _p(tu, C.c_uint32), _p(ti, C.c_uint32),
+                             _p(tr, C.c_double), C.c_uint64(len(sr)), _p(su, C.c_uint32), _p(si, C.c_uint32),
+                             _p(sr, C.c_double), C.c_uint32(num_users), C.c_uint32(num_items), C.byref(res))
+    assert rc == 0
+    n = res.sweeps_done
+    return {"rmse": rm[:n], "rmse_this": rt[:n], "tau": ta[:n], "U": U, "V": V, "hyper": hyper,
+            "pred_sum": ps[:len(sr)], "seconds": res.seconds, "sweeps": n, "num_users": res.num_users,
+            "num_items": res.num_items}
+
+
+def stream(seed, kind, n, shape=1.0):
+    """The reference RNG via glibc itself: kind 0 rand(), 1 ran_gaussian(), 2 ran_gamma(shape)."""
+    L = lib()
+    L.oracle_srand(seed)
+    if kind == 0:
+        L.oracle_rand.restype = C.c_int
+        return np.array([L.oracle_rand() for _ in range(n)], dtype=np.float64)
+    if kind == 1:
+        return np.array([L.oracle_ran_gaussian() for _ in range(n)])
+    return np.array([L.oracle_ran_gamma(shape) for _ in range(n)])

@@ -1,0 +1,32 @@
+// comm.h -- RCCL (over xGMI) exchange between the ranks of one node.
+// One process per GPU.  Users and items are block-partitioned by row; after
+// each half-sweep every rank holds fresh rows only for its own block, and the
+// blocks are exchanged with one grouped set of in-place ncclBroadcast calls
+// (an all-gather with per-rank row counts: no padding, no repack).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace sbmf {
+
+class Comm {
+  public:
+    Comm() = default;
+    ~Comm();
+    Comm(const Comm&) = delete;
+    Comm& operator=(const Comm&) = delete;
+    static void unique_id(uint8_t id[128]);
+    void init(int nranks, int rank, const uint8_t id[128]);
+    bool active() const { return comm_ != nullptr; }
+    // Rank k owns units [bounds[k], bounds[k+1]) of unit_bytes each, starting
+    // at base; after the call every rank holds every rank's units.
+    void bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_t>& bounds, hipStream_t st);
+
+  private:
+    void* comm_ = nullptr;  // ncclComm_t
+    int nranks_ = 1, rank_ = 0;
+};
+
+}  // namespace sbmf

@@ -1,0 +1,92 @@
+// kernels.h -- host-callable launchers for the gfx950 kernels in kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sbmf {
+
+// Arguments of one half-sweep over the rows of one orientation (users: own =
+// U, partner = V, CSR; items: own = V, partner = U, CSC).  T = float|double.
+template <typename T>
+struct HalfArgs {
+    const uint32_t* ptr;   // [R+1] rating offsets of this orientation
+    const uint32_t* part;  // [N] partner row id per rating
+    const uint32_t* perm;  // [N] position of the rating in the other orientation (E gather)
+    const T* E_in;         // [N] residuals in the other orientation's order
+    T* E_out;              // [N] residuals in this orientation's order
+    const T* r_this;       // [N] ratings in this order (E_FROM_DOT, train RMSE, Gram update)
+    T* own;                // [R][Kp]
+    const T* partner;      // [P][Kp]
+    const T* sig;          // [K] precision hyperparameter of this side
+    const T* mu;           // [K] mean hyperparameter of this side
+    const T* zbuf;         // reference mode: [R][K] N(0,1) variates; nullptr -> Philox
+    T tau;
+    uint32_t K, Kp;
+    int sd_is_var;         // quirk FINAL/SBPMF2: posterior variance used as stdev
+    uint64_t seed;
+    uint32_t sweep, tag;
+    double* row_sq;        // [R] per-row sum of squared residuals after the half (or null)
+    double* row_tr;        // [R] per-row train squared error of the clamped sample (or null)
+    T lo, hi;
+    int e_from_dot;        // 1: e0 = r - own.partner (no gather; multi-GPU)
+};
+
+// Heavy-row (Gram route) work description.
+struct GramItem {
+    uint32_t row;     // global row id
+    uint32_t beg;     // first rating (absolute index into the orientation arrays)
+    uint32_t len;     // ratings in this chunk
+    uint32_t slab;    // chunk slab index
+};
+struct GramRow {
+    uint32_t row;
+    uint32_t slab0;   // first slab of the row
+    uint32_t nslab;   // number of chunk slabs
+};
+
+// Bin launch descriptor for the light / medium row kernels.
+// W2/W8: one wave per row, 2/8 rating slots per lane; B4/B8: 4/8 waves per
+// row, 8 slots per lane.  Heavier rows take the Gram route.
+enum RowKernelKind { RK_W2 = 0, RK_W8 = 1, RK_B4 = 2, RK_B8 = 3, RK_NUM = 4 };
+static const uint32_t RK_MAXDEG[RK_NUM] = {128, 512, 2048, 4096};
+
+template <typename T>
+hipError_t launch_rows(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
+
+template <typename T>
+hipError_t launch_gram(const GramItem* items, uint32_t nitems, const GramRow* grows, uint32_t ngrows,
+                       double* slabs, T* delta, double* chunk_sq, double* chunk_tr, const HalfArgs<T>& a,
+                       hipStream_t st);
+
+// E = r - dot(own, partner) over all ratings of the orientation (row-major
+// walk; one wave per row) + per-row sum of squares.  own rows [r0,r1).
+template <typename T>
+hipError_t launch_resid(const uint32_t* ptr, const uint32_t* part, const T* r, const T* own, const T* partner,
+                        uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, T* E, double* row_sq, hipStream_t st);
+
+// Column partials over table rows [r0,r1): out[c][0..K) = sum (x-mu)^2,
+// out[c][K..2K) = sum x, c = chunk of 256 rows (global chunk index).
+template <typename T>
+hipError_t launch_colstats(const T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, const T* mu,
+                           double* out, hipStream_t st);
+
+// Test predictions: pred = clamp(dot(U[u],V[i])); sum[t] += pred if collect;
+// part[b][0] += (r - sum/div)^2, part[b][1] += (r-pred)^2 per 256-rating block.
+template <typename T>
+hipError_t launch_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t t0, uint64_t t1,
+                       const T* U, const T* V, uint32_t K, uint32_t Kp, T lo, T hi, int collect, double div,
+                       double* sum, double* part, hipStream_t st);
+
+// Deterministic fixed-order sum of in[n] (contiguous) into one double at out.
+// scratch: >= ceil(n/1024) + ceil(n/1024^2) + 2 doubles.
+hipError_t launch_sum(const double* in, uint64_t n, double* out, double* scratch, hipStream_t st);
+// out[w] = sum_c in[c*width + w], c ascending (width columns, nchunk rows)
+hipError_t launch_sum_cols(const double* in, uint32_t nchunk, uint32_t width, double* out, hipStream_t st);
+
+// Philox init: tab[r][k] = sd * z(seed, sweep=0xffffffff, tag, r, k), rows [r0,r1).
+template <typename T>
+hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, double sd, uint64_t seed,
+                              uint32_t tag, hipStream_t st);
+
+}  // namespace sbmf

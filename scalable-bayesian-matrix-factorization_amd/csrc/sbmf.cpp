@@ -1,0 +1,972 @@
+// sbmf.cpp -- host side of the MI355X SBPMF sampler: the C ABI of include/sbmf.h.
+//
+// Per sweep (reference loop body gibbs_sbpmf_final.cpp:309-564):
+//   1. residual sum of squares + column statistics of U and V (device,
+//      fixed-order reductions)            -> one small D2H
+//   2. tau, sigma_u/mu_u, sigma_v/mu_v drawn on the host in fp64 with the
+//      reference's expressions (:339-342, :375-414)  -> H2D hyper buffer
+//   3. user half-sweep (kernels.hip), [RCCL: broadcast U row blocks]
+//   4. item half-sweep,               [RCCL: broadcast V row blocks]
+//   5. test prediction + running mean RMSE (:539-563)
+// Reference RNG mode pre-generates the sweep's whole variate stream on the
+// host (it is data independent, see rng.h) and uploads it; Philox mode draws
+// in-kernel.  No CPU compute fallback exists: without a GPU, sbmf_create fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/sbmf.h"
+#include "comm.h"
+#include <rccl/rccl.h>
+#include "kernels.h"
+#include "rng.h"
+
+namespace {
+thread_local std::string g_err;
+}
+
+struct sbmf_ctx;
+
+namespace sbmf {
+
+struct Error {
+    int code;
+    std::string msg;
+};
+[[noreturn]] static void fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    throw Error{code, buf};
+}
+[[noreturn]] void comm_fail(const char* what, ncclResult_t r) {
+    fail(SBMF_E_COMM, "%s failed: %s", what, ncclGetErrorString(r));
+}
+#define HIPCHK(x)                                                                                     \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) sbmf::fail(SBMF_E_DEVICE, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                                         __FILE__, __LINE__);                                         \
+    } while (0)
+
+// ------------------------------------------------------------------ device buffer
+struct DBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void alloc(size_t b) {
+        release();
+        if (b == 0) b = 16;
+        hipError_t e = hipMalloc(&p, b);
+        if (e != hipSuccess) fail(SBMF_E_NOMEM, "hipMalloc(%zu) failed: %s", b, hipGetErrorString(e));
+        bytes = b;
+    }
+    template <typename U>
+    U* as() const {
+        return static_cast<U*>(p);
+    }
+};
+template <typename U>
+static void upload(DBuf& d, const std::vector<U>& h, hipStream_t st) {
+    d.alloc(h.size() * sizeof(U));
+    if (!h.empty()) HIPCHK(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(U), hipMemcpyHostToDevice, st));
+}
+
+// ------------------------------------------------------------------ host layout
+// One orientation: users (CSR by user, partner = item) or items (CSC).
+struct Side {
+    uint32_t R = 0;                     // rows
+    std::vector<uint32_t> ptr;          // [R+1]
+    std::vector<uint32_t> part;         // [N] partner id
+    std::vector<uint32_t> perm;         // [N] position in the other orientation
+    std::vector<double> r;              // [N] ratings
+    uint32_t r0 = 0, r1 = 0;            // owned row range (multi-GPU)
+    std::vector<uint64_t> bounds;       // [nranks+1] row ranges of every rank
+    std::vector<uint32_t> bin_rows[RK_NUM];
+    std::vector<GramItem> gitems;
+    std::vector<GramRow> grows;
+};
+
+static void build_side(uint64_t N, const uint32_t* key, const uint32_t* other, const double* rat, uint32_t R,
+                       Side& s, std::vector<uint32_t>& pos_of_case) {
+    s.R = R;
+    s.ptr.assign((size_t)R + 1, 0);
+    for (uint64_t c = 0; c < N; ++c) s.ptr[key[c] + 1]++;
+    for (uint32_t i = 0; i < R; ++i) s.ptr[i + 1] += s.ptr[i];
+    std::vector<uint32_t> fill(s.ptr.begin(), s.ptr.end() - 1);
+    s.part.resize(N);
+    s.r.resize(N);
+    pos_of_case.resize(N);
+    for (uint64_t c = 0; c < N; ++c) {  // file order within a row (gibbs_sbpmf_final.cpp:204-209)
+        const uint32_t p = fill[key[c]]++;
+        s.part[p] = other[c];
+        s.r[p] = rat[c];
+        pos_of_case[c] = p;
+    }
+}
+
+// nnz-balanced contiguous partition, boundaries aligned to 256 rows.
+static void partition(Side& s, int nranks, int rank) {
+    const std::vector<uint32_t>& ptr = s.ptr;
+    const uint32_t R = (uint32_t)ptr.size() - 1;
+    s.bounds.assign(nranks + 1, 0);
+    for (int k = 1; k <= nranks; ++k) {
+        uint32_t row = R;
+        if (k < nranks) {
+            const double target = (double)ptr[R] * k / nranks;
+            row = (uint32_t)(std::lower_bound(ptr.begin(), ptr.end(), (uint32_t)std::llround(target)) - ptr.begin());
+            row = std::min((row + 128) / 256 * 256, R);
+        }
+        s.bounds[k] = std::max<uint64_t>(s.bounds[k - 1], row);
+    }
+    s.r0 = (uint32_t)s.bounds[rank];
+    s.r1 = (uint32_t)s.bounds[rank + 1];
+}
+
+static void build_bins(Side& s, uint32_t gram_thr) {
+    for (auto& b : s.bin_rows) b.clear();
+    s.gitems.clear();
+    s.grows.clear();
+    std::vector<uint32_t> order(s.r1 - s.r0);
+    std::iota(order.begin(), order.end(), s.r0);
+    auto deg = [&](uint32_t r) { return s.ptr[r + 1] - s.ptr[r]; };
+    // heaviest first: blocks are dispatched roughly in index order, so the
+    // longest rows start earliest (LPT)
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return deg(a) > deg(b); });
+    const uint32_t chunk = 2048;
+    for (uint32_t r : order) {
+        const uint32_t d = deg(r);
+        if (d > gram_thr || d > RK_MAXDEG[RK_NUM - 1]) {
+            GramRow gr{r, (uint32_t)s.gitems.size(), 0};
+            for (uint32_t o = 0; o < d; o += chunk) {
+                s.gitems.push_back(GramItem{r, s.ptr[r] + o, std::min(chunk, d - o), (uint32_t)s.gitems.size()});
+                gr.nslab++;
+            }
+            s.grows.push_back(gr);
+            continue;
+        }
+        int kind = RK_W2;
+        while (d > RK_MAXDEG[kind]) ++kind;
+        s.bin_rows[kind].push_back(r);
+    }
+}
+
+}  // namespace sbmf
+
+using namespace sbmf;
+
+struct sbmf_ctx {
+    sbmf_config cfg{};
+    std::string err;
+    // host data
+    std::vector<uint32_t> tu, ti, su, si;
+    std::vector<double> tr, sr;
+    uint32_t I = 0, J = 0, I_req = 0, J_req = 0;
+    bool prepared = false;
+    // derived settings
+    double init_sd = 1.0, lo = 1.0, hi = 5.0;
+    int sd_is_var = 1;
+    uint32_t K = 0, Kp = 0;
+    // layout
+    Side users, items;
+    uint64_t t0 = 0, t1 = 0;  // owned test range
+    std::vector<uint64_t> tbounds, tbblocks;  // every rank's test range (ratings, 256-blocks)
+    // hyper state (fp64 host copy)
+    std::vector<double> sig_u, mu_u, sig_v, mu_v;
+    double tau = 1.0;
+    uint32_t sweep = 0, collected = 0;
+    // rng
+    GlibcRand grand{1};
+    // multi-GPU
+    int nranks = 1, rank = 0;
+    Comm comm;
+    // device
+    hipStream_t st = nullptr;
+    hipEvent_t ev[8] = {};
+    hipEvent_t kev[2][5][2] = {};
+    DBuf d_uptr, d_upart, d_uperm, d_ur, d_vptr, d_vpart, d_vperm, d_vr;
+    DBuf d_U, d_V, d_Eu, d_Ev, d_zU, d_zV, d_hyper;
+    DBuf d_rowsq_u, d_rowtr_u, d_rowsq_v, d_rowtr_v;
+    DBuf d_bins_u[RK_NUM], d_bins_v[RK_NUM];
+    DBuf d_gitems_u, d_grows_u, d_gitems_v, d_grows_v, d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
+    DBuf d_colpart, d_res, d_scratch;
+    DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
+    std::vector<double> h_res;
+    double* h_pinned = nullptr;  // pinned staging for z streams
+    size_t h_pinned_bytes = 0;
+    sbmf_timing timing{};
+    ~sbmf_ctx();
+};
+
+namespace sbmf {
+
+// result slots in d_res
+enum { RES_ESQ = 0, RES_TRSQ = 1, RES_TEST_AVG = 2, RES_TEST_THIS = 3, RES_COL = 8 };
+
+static size_t tsize(const sbmf_ctx* c) { return c->cfg.precision == SBMF_F32 ? 4 : 8; }
+
+template <typename T>
+static std::vector<T> to_T(const std::vector<double>& v) {
+    return std::vector<T>(v.begin(), v.end());
+}
+
+// table [R][Kp] (T) from row-major doubles [R][K]
+template <typename T>
+static void upload_table(sbmf_ctx* c, DBuf& d, const double* src, uint32_t R) {
+    std::vector<T> h((size_t)R * c->Kp, T(0));
+    for (uint32_t r = 0; r < R; ++r)
+        for (uint32_t k = 0; k < c->K; ++k) h[(size_t)r * c->Kp + k] = (T)src[(size_t)r * c->K + k];
+    HIPCHK(hipMemcpy(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+template <typename T>
+static void download_table(sbmf_ctx* c, const DBuf& d, double* dst, uint32_t R) {
+    std::vector<T> h((size_t)R * c->Kp);
+    HIPCHK(hipMemcpy(h.data(), d.p, h.size() * sizeof(T), hipMemcpyDeviceToHost));
+    for (uint32_t r = 0; r < R; ++r)
+        for (uint32_t k = 0; k < c->K; ++k) dst[(size_t)r * c->K + k] = (double)h[(size_t)r * c->Kp + k];
+}
+
+static void ensure_pinned(sbmf_ctx* c, size_t bytes) {
+    if (c->h_pinned_bytes >= bytes) return;
+    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    c->h_pinned = nullptr;
+    HIPCHK(hipHostMalloc((void**)&c->h_pinned, bytes, hipHostMallocDefault));
+    c->h_pinned_bytes = bytes;
+}
+
+static void fill_kernel_bytes(sbmf_ctx* c);
+
+// ------------------------------------------------------------------ prepare
+template <typename T>
+static void prepare_T(sbmf_ctx* c) {
+    const sbmf_config& cf = c->cfg;
+    const uint64_t N = c->tu.size();
+    // dims: max id + 1 over train and test (gibbs_sbpmf_final.cpp:146-148)
+    uint32_t umax = 0, imax = 0;
+    for (uint64_t x = 0; x < N; ++x) {
+        umax = std::max(umax, c->tu[x]);
+        imax = std::max(imax, c->ti[x]);
+    }
+    for (size_t x = 0; x < c->su.size(); ++x) {
+        umax = std::max(umax, c->su[x]);
+        imax = std::max(imax, c->si[x]);
+    }
+    c->I = std::max(c->I_req, (N || !c->su.empty()) ? umax + 1 : 0);
+    c->J = std::max(c->J_req, (N || !c->si.empty()) ? imax + 1 : 0);
+    if (c->I == 0 || c->J == 0) fail(SBMF_E_STATE, "no ratings: call sbmf_set_train first");
+    if (N >= 0xffffffffull) fail(SBMF_E_ARG, "more than 2^32-1 ratings are not supported");
+    c->K = cf.num_factor;
+    c->Kp = (c->K + (uint32_t)(32 / sizeof(T)) - 1) / (uint32_t)(32 / sizeof(T)) * (uint32_t)(32 / sizeof(T));
+
+    std::vector<uint32_t> pos_u, pos_v;
+    build_side(N, c->tu.data(), c->ti.data(), c->tr.data(), c->I, c->users, pos_u);
+    build_side(N, c->ti.data(), c->tu.data(), c->tr.data(), c->J, c->items, pos_v);
+    c->users.perm.resize(N);
+    c->items.perm.resize(N);
+    for (uint64_t x = 0; x < N; ++x) {
+        c->users.perm[pos_u[x]] = pos_v[x];
+        c->items.perm[pos_v[x]] = pos_u[x];
+    }
+    partition(c->users, c->nranks, c->rank);
+    partition(c->items, c->nranks, c->rank);
+    const uint32_t thr = cf.gram_threshold ? std::min(cf.gram_threshold, RK_MAXDEG[RK_NUM - 1]) : RK_MAXDEG[RK_NUM - 1];
+    build_bins(c->users, thr);
+    build_bins(c->items, thr);
+    {  // test split in 256-aligned blocks
+        const uint64_t T_ = c->su.size(), nb = (T_ + 255) / 256;
+        c->tbounds.assign(c->nranks + 1, 0);
+        c->tbblocks.assign(c->nranks + 1, 0);
+        for (int k = 0; k <= c->nranks; ++k) {
+            c->tbblocks[k] = nb * k / c->nranks;
+            c->tbounds[k] = std::min<uint64_t>(T_, c->tbblocks[k] * 256);
+        }
+        c->t0 = c->tbounds[c->rank];
+        c->t1 = c->tbounds[c->rank + 1];
+    }
+
+    hipStream_t st = c->st;
+    upload(c->d_uptr, c->users.ptr, st);
+    upload(c->d_upart, c->users.part, st);
+    upload(c->d_uperm, c->users.perm, st);
+    upload(c->d_ur, to_T<T>(c->users.r), st);
+    upload(c->d_vptr, c->items.ptr, st);
+    upload(c->d_vpart, c->items.part, st);
+    upload(c->d_vperm, c->items.perm, st);
+    upload(c->d_vr, to_T<T>(c->items.r), st);
+    for (int k = 0; k < RK_NUM; ++k) {
+        upload(c->d_bins_u[k], c->users.bin_rows[k], st);
+        upload(c->d_bins_v[k], c->items.bin_rows[k], st);
+    }
+    upload(c->d_gitems_u, c->users.gitems, st);
+    upload(c->d_grows_u, c->users.grows, st);
+    upload(c->d_gitems_v, c->items.gitems, st);
+    upload(c->d_grows_v, c->items.grows, st);
+    const uint32_t Kt = (c->K + 15) / 16 * 16;
+    const size_t SL = (size_t)Kt * Kt + Kt;
+    const size_t nslab = std::max(c->users.gitems.size(), c->items.gitems.size());
+    const size_t ngrow = std::max(c->users.grows.size(), c->items.grows.size());
+    c->d_slabs.alloc((nslab + ngrow) * SL * sizeof(double));
+    c->d_delta.alloc(std::max<size_t>(ngrow, 1) * c->Kp * sizeof(T));
+    c->d_chunk_sq.alloc(std::max<size_t>(nslab, 1) * sizeof(double));
+    c->d_chunk_tr.alloc(std::max<size_t>(nslab, 1) * sizeof(double));
+
+    c->d_U.alloc((size_t)c->I * c->Kp * sizeof(T));
+    c->d_V.alloc((size_t)c->J * c->Kp * sizeof(T));
+    HIPCHK(hipMemsetAsync(c->d_U.p, 0, c->d_U.bytes, st));
+    HIPCHK(hipMemsetAsync(c->d_V.p, 0, c->d_V.bytes, st));
+    c->d_Eu.alloc(std::max<uint64_t>(N, 1) * sizeof(T));
+    c->d_Ev.alloc(std::max<uint64_t>(N, 1) * sizeof(T));
+    HIPCHK(hipMemsetAsync(c->d_Eu.p, 0, c->d_Eu.bytes, st));
+    HIPCHK(hipMemsetAsync(c->d_Ev.p, 0, c->d_Ev.bytes, st));
+    c->d_rowsq_u.alloc((size_t)c->I * sizeof(double));
+    c->d_rowtr_u.alloc((size_t)c->I * sizeof(double));
+    c->d_rowsq_v.alloc((size_t)c->J * sizeof(double));
+    c->d_rowtr_v.alloc((size_t)c->J * sizeof(double));
+    HIPCHK(hipMemsetAsync(c->d_rowsq_v.p, 0, c->d_rowsq_v.bytes, st));
+    HIPCHK(hipMemsetAsync(c->d_rowtr_v.p, 0, c->d_rowtr_v.bytes, st));
+    c->d_hyper.alloc(4 * (size_t)c->K * sizeof(T));
+    HIPCHK(hipMemsetAsync(c->d_hyper.p, 0, c->d_hyper.bytes, st));
+    const uint32_t nchunk = (std::max(c->I, c->J) + 255) / 256;
+    c->d_colpart.alloc((size_t)nchunk * 2 * c->K * sizeof(double));
+    c->h_res.assign(RES_COL + 4 * (size_t)c->K, 0.0);
+    c->d_res.alloc(c->h_res.size() * sizeof(double));
+    const uint64_t big = std::max<uint64_t>({(uint64_t)c->I, (uint64_t)c->J, (uint64_t)nslab, c->su.size() / 128 + 2});
+    c->d_scratch.alloc((big / 1024 + 16) * 2 * sizeof(double));
+    // test set
+    const uint64_t T_ = c->su.size();
+    upload(c->d_tu, c->su, st);
+    upload(c->d_ti, c->si, st);
+    upload(c->d_tr, c->sr, st);
+    c->d_tsum.alloc(std::max<uint64_t>(T_, 1) * sizeof(double));
+    HIPCHK(hipMemsetAsync(c->d_tsum.p, 0, c->d_tsum.bytes, st));
+    c->d_tpart.alloc(((T_ + 255) / 256 + 1) * 2 * sizeof(double));
+    HIPCHK(hipMemsetAsync(c->d_tpart.p, 0, c->d_tpart.bytes, st));
+    if (cf.rng_mode == SBMF_RNG_REFERENCE) {
+        c->d_zU.alloc((size_t)c->I * c->K * sizeof(T));
+        c->d_zV.alloc((size_t)c->J * c->K * sizeof(T));
+    }
+    c->sig_u.assign(c->K, 0.0);
+    c->mu_u.assign(c->K, 0.0);
+    c->sig_v.assign(c->K, 0.0);
+    c->mu_v.assign(c->K, 0.0);
+    c->tau = 1.0;
+
+    // initial factors (gibbs_sbpmf_final.cpp:236-250)
+    if (cf.rng_mode == SBMF_RNG_REFERENCE) {
+        c->grand.seed_((unsigned)cf.seed);
+        std::vector<double> U((size_t)c->I * c->K), V((size_t)c->J * c->K);
+        for (uint32_t i = 0; i < c->I; ++i)
+            for (uint32_t k = 0; k < c->K; ++k) U[(size_t)i * c->K + k] = 0.0 + c->init_sd * leva_normal(c->grand);
+        for (uint32_t k = 0; k < c->K; ++k)  // V is k-major in the reference
+            for (uint32_t j = 0; j < c->J; ++j) V[(size_t)j * c->K + k] = 0.0 + c->init_sd * leva_normal(c->grand);
+        HIPCHK(hipStreamSynchronize(st));
+        upload_table<T>(c, c->d_U, U.data(), c->I);
+        upload_table<T>(c, c->d_V, V.data(), c->J);
+    } else {
+        HIPCHK(launch_init_philox<T>(c->d_U.as<T>(), c->K, c->Kp, 0, c->I, c->init_sd, cf.seed, TAG_INIT_U, st));
+        HIPCHK(launch_init_philox<T>(c->d_V.as<T>(), c->K, c->Kp, 0, c->J, c->init_sd, cf.seed, TAG_INIT_V, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    c->sweep = 0;
+    c->collected = 0;
+    fill_kernel_bytes(c);
+    c->prepared = true;
+}
+
+// ------------------------------------------------------------------ one sweep
+struct HostStream {  // variates of one sweep, in the reference's consumption order
+    double g_tau;
+    std::vector<double> g_su, z_mu, g_sv, z_mv;
+};
+
+template <class G>
+static void draw_hyper_variates(G& g, sbmf_ctx* c, HostStream& hs) {
+    const sbmf_config& cf = c->cfg;
+    const uint64_t N = c->tu.size();
+    hs.g_tau = mt_gamma(g, cf.a0 + 0.5 * (double)N);
+    hs.g_su.resize(c->K);
+    hs.z_mu.resize(c->K);
+    hs.g_sv.resize(c->K);
+    hs.z_mv.resize(c->K);
+    for (uint32_t k = 0; k < c->K; ++k) {
+        hs.g_su[k] = mt_gamma(g, cf.alpha0 + 0.5 * (c->I + 1));
+        hs.z_mu[k] = leva_normal(g);
+        hs.g_sv[k] = mt_gamma(g, cf.alpha0 + 0.5 * (c->J + 1));
+        hs.z_mv[k] = leva_normal(g);
+    }
+}
+
+template <typename T>
+static void fill_z(sbmf_ctx* c, uint32_t R, DBuf& d) {
+    const size_t n = (size_t)R * c->K;
+    ensure_pinned(c, n * sizeof(T));
+    T* h = reinterpret_cast<T*>(c->h_pinned);
+    for (size_t x = 0; x < n; ++x) h[x] = (T)leva_normal(c->grand);
+    HIPCHK(hipMemcpy(d.p, h, n * sizeof(T), hipMemcpyHostToDevice));
+}
+
+template <typename T>
+static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
+    HalfArgs<T> a{};
+    const bool md = c->nranks > 1;
+    if (users) {
+        a.ptr = c->d_uptr.as<uint32_t>();
+        a.part = c->d_upart.as<uint32_t>();
+        a.perm = c->d_uperm.as<uint32_t>();
+        a.E_in = c->d_Ev.as<T>();
+        a.E_out = c->d_Eu.as<T>();
+        a.r_this = c->d_ur.as<T>();
+        a.own = c->d_U.as<T>();
+        a.partner = c->d_V.as<T>();
+        a.sig = c->d_hyper.as<T>();
+        a.mu = c->d_hyper.as<T>() + c->K;
+        a.zbuf = c->cfg.rng_mode == SBMF_RNG_REFERENCE ? c->d_zU.as<T>() : nullptr;
+        a.tag = TAG_USERS;
+        a.row_sq = nullptr;
+        a.row_tr = nullptr;
+    } else {
+        a.ptr = c->d_vptr.as<uint32_t>();
+        a.part = c->d_vpart.as<uint32_t>();
+        a.perm = c->d_vperm.as<uint32_t>();
+        a.E_in = c->d_Eu.as<T>();
+        a.E_out = c->d_Ev.as<T>();
+        a.r_this = c->d_vr.as<T>();
+        a.own = c->d_V.as<T>();
+        a.partner = c->d_U.as<T>();
+        a.sig = c->d_hyper.as<T>() + 2 * c->K;
+        a.mu = c->d_hyper.as<T>() + 3 * c->K;
+        a.zbuf = c->cfg.rng_mode == SBMF_RNG_REFERENCE ? c->d_zV.as<T>() : nullptr;
+        a.tag = TAG_ITEMS;
+        a.row_sq = c->d_rowsq_v.as<double>();
+        a.row_tr = c->cfg.eval_train ? c->d_rowtr_v.as<double>() : nullptr;
+    }
+    a.tau = (T)c->tau;
+    a.K = c->K;
+    a.Kp = c->Kp;
+    a.sd_is_var = c->sd_is_var;
+    a.seed = c->cfg.seed;
+    a.sweep = c->sweep;
+    a.lo = (T)c->lo;
+    a.hi = (T)c->hi;
+    a.e_from_dot = md ? 1 : 0;
+    return a;
+}
+
+template <typename T>
+static void run_half(sbmf_ctx* c, bool users) {
+    Side& s = users ? c->users : c->items;
+    HalfArgs<T> a = half_args<T>(c, users);
+    hipStream_t st = c->st;
+    DBuf* bins = users ? c->d_bins_u : c->d_bins_v;
+    const int sd = users ? 0 : 1;
+    if (!s.gitems.empty()) {
+        HIPCHK(hipEventRecord(c->kev[sd][4][0], st));
+        HIPCHK(launch_gram<T>((users ? c->d_gitems_u : c->d_gitems_v).as<GramItem>(), (uint32_t)s.gitems.size(),
+                              (users ? c->d_grows_u : c->d_grows_v).as<GramRow>(), (uint32_t)s.grows.size(),
+                              c->d_slabs.as<double>(), c->d_delta.as<T>(), c->d_chunk_sq.as<double>(),
+                              a.row_tr ? c->d_chunk_tr.as<double>() : nullptr, a, st));
+        HIPCHK(hipEventRecord(c->kev[sd][4][1], st));
+        c->timing.n_launch += 4;
+    }
+    for (int k = RK_NUM - 1; k >= 0; --k) {
+        if (s.bin_rows[k].empty()) continue;
+        HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
+        HIPCHK(launch_rows<T>(k, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
+        HIPCHK(hipEventRecord(c->kev[sd][k][1], st));
+        c->timing.n_launch++;
+    }
+}
+
+// SURVEY.md §8(d) algorithmic bytes of one launch over `rows`.
+static uint64_t alg_bytes(const Side& s, const std::vector<uint32_t>& rows, uint32_t K, uint64_t tsz) {
+    uint64_t b = 0;
+    for (uint32_t r : rows) b += (uint64_t)(s.ptr[r + 1] - s.ptr[r]) * (tsz * K + 4 + tsz) + 2 * tsz * K;
+    return b;
+}
+static void fill_kernel_bytes(sbmf_ctx* c) {
+    const uint64_t tsz = tsize(c);
+    for (int sd = 0; sd < 2; ++sd) {
+        const Side& s = sd == 0 ? c->users : c->items;
+        for (int k = 0; k < RK_NUM; ++k) {
+            c->timing.kern_bytes[sd][k] = alg_bytes(s, s.bin_rows[k], c->K, tsz);
+            c->timing.kern_rows[sd][k] = (uint32_t)s.bin_rows[k].size();
+        }
+        std::vector<uint32_t> gr;
+        for (const GramRow& g : s.grows) gr.push_back(g.row);
+        c->timing.kern_bytes[sd][4] = alg_bytes(s, gr, c->K, tsz);
+        c->timing.kern_rows[sd][4] = (uint32_t)gr.size();
+    }
+}
+
+static double ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return NAN;
+    return ms;
+}
+
+template <typename T>
+static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* user) {
+    const sbmf_config& cf = c->cfg;
+    hipStream_t st = c->st;
+    const uint32_t K = c->K;
+    const uint64_t N = c->tu.size();
+    const bool ref = cf.rng_mode == SBMF_RNG_REFERENCE;
+    const bool q2 = cf.quirks == SBMF_QUIRKS_SBPMF2;
+    double* d_res = c->d_res.as<double>();
+    double* scratch = c->d_scratch.as<double>();
+    for (uint32_t it = 0; it < nsweeps; ++it) {
+        c->timing.n_launch = 0;
+        HostStream hs;
+        if (ref) {
+            draw_hyper_variates(c->grand, c, hs);
+        } else {
+            PhiloxStream ps(cf.seed, c->sweep, 0);
+            draw_hyper_variates(ps, c, hs);
+        }
+        HIPCHK(hipEventRecord(c->ev[0], st));
+        // ---- 1. residual sum of squares (E recompute at sweep start, :317-334)
+        const bool recompute = c->sweep == 0 || (cf.recompute_every && c->sweep % cf.recompute_every == 0);
+        if (recompute) {
+            HIPCHK(launch_resid<T>(c->d_vptr.as<uint32_t>(), c->d_vpart.as<uint32_t>(), c->d_vr.as<T>(), c->d_V.as<T>(),
+                                   c->d_U.as<T>(), K, c->Kp, c->items.r0, c->items.r1, c->d_Ev.as<T>(),
+                                   c->d_rowsq_v.as<double>(), st));
+            c->timing.n_launch++;
+            if (c->nranks > 1) c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
+        }
+        HIPCHK(launch_sum(c->d_rowsq_v.as<double>(), c->J, d_res + RES_ESQ, scratch, st));
+        // ---- column statistics with the current mu (:378-381, :397-401)
+        const T* hyp = c->d_hyper.as<T>();
+        double* colpart = c->d_colpart.as<double>();
+        HIPCHK(launch_colstats<T>(c->d_U.as<T>(), K, c->Kp, 0, c->I, hyp + K, colpart, st));
+        HIPCHK(launch_sum_cols(colpart, (c->I + 255) / 256, 2 * K, d_res + RES_COL, st));
+        HIPCHK(launch_colstats<T>(c->d_V.as<T>(), K, c->Kp, 0, c->J, hyp + 3 * K, colpart, st));
+        HIPCHK(launch_sum_cols(colpart, (c->J + 255) / 256, 2 * K, d_res + RES_COL + 2 * K, st));
+        c->timing.n_launch += 5;
+        HIPCHK(hipMemcpyAsync(c->h_res.data(), d_res, c->h_res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        // ---- 2. host draws (:339-342, :375-414)
+        const double esq = c->h_res[RES_ESQ];
+        c->tau = hs.g_tau / (cf.b0 + 0.5 * esq);
+        const double* Su2 = &c->h_res[RES_COL];
+        const double* Su1 = Su2 + K;
+        const double* Sv2 = Su2 + 2 * K;
+        const double* Sv1 = Su2 + 3 * K;
+        auto sd = [&](double var) { return c->sd_is_var ? var : std::sqrt(var); };
+        for (uint32_t k = 0; k < K; ++k) {
+            const double du = c->mu_u[k] - cf.mu0;
+            const double bu = q2 ? cf.beta0 + cf.nu0 * du * du + (0.5) * Su2[k]
+                                 : cf.beta0 + 0.5 * cf.nu0 * du * du + (0.5) * Su2[k];
+            c->sig_u[k] = hs.g_su[k] / bu;
+            const double su_star = (double)1.0 / (cf.nu0 * c->sig_u[k] + c->sig_u[k] * c->I);
+            const double mu_star = su_star * (cf.nu0 * cf.mu0 * c->sig_u[k] + c->sig_u[k] * Su1[k]);
+            c->mu_u[k] = mu_star + sd(su_star) * hs.z_mu[k];
+            const double dv = c->mu_v[k] - cf.mu0;
+            const double bv = q2 ? cf.beta0 + cf.nu0 * dv * dv + (0.5) * Sv2[k]
+                                 : cf.beta0 + 0.5 * cf.nu0 * dv * dv + (0.5) * Sv2[k];
+            c->sig_v[k] = hs.g_sv[k] / bv;
+            const double sv_star = (double)1.0 / (cf.nu0 * c->sig_v[k] + c->sig_v[k] * c->J);
+            const double mv_star = (q2 ? su_star : sv_star) * (cf.nu0 * cf.mu0 * c->sig_v[k] + c->sig_v[k] * Sv1[k]);
+            c->mu_v[k] = mv_star + sd(sv_star) * hs.z_mv[k];
+        }
+        {
+            std::vector<T> h(4 * (size_t)K);
+            for (uint32_t k = 0; k < K; ++k) {
+                h[k] = (T)c->sig_u[k];
+                h[K + k] = (T)c->mu_u[k];
+                h[2 * K + k] = (T)c->sig_v[k];
+                h[3 * K + k] = (T)c->mu_v[k];
+            }
+            HIPCHK(hipMemcpyAsync(c->d_hyper.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st));
+            if (ref) {  // user variates then item variates (:485 then :529)
+                fill_z<T>(c, c->I, c->d_zU);
+                fill_z<T>(c, c->J, c->d_zV);
+            }
+            HIPCHK(hipStreamSynchronize(st));
+        }
+        HIPCHK(hipEventRecord(c->ev[1], st));
+        // ---- 3. user half-sweep
+        run_half<T>(c, true);
+        HIPCHK(hipEventRecord(c->ev[2], st));
+        if (c->nranks > 1) c->comm.bcast_ranges(c->d_U.p, c->Kp * sizeof(T), c->users.bounds, st);
+        HIPCHK(hipEventRecord(c->ev[3], st));
+        // ---- 4. item half-sweep
+        run_half<T>(c, false);
+        HIPCHK(hipEventRecord(c->ev[4], st));
+        if (c->nranks > 1) {
+            c->comm.bcast_ranges(c->d_V.p, c->Kp * sizeof(T), c->items.bounds, st);
+            c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
+            if (cf.eval_train) c->comm.bcast_ranges(c->d_rowtr_v.p, sizeof(double), c->items.bounds, st);
+        }
+        HIPCHK(hipEventRecord(c->ev[5], st));
+        // ---- 5. evaluation
+        const bool collect = q2 ? true : (c->sweep >= cf.burnin);
+        if (collect) c->collected++;
+        const double div = (cf.quirks == SBMF_QUIRKS_NONE) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
+        const uint64_t T_ = c->su.size();
+        if (cf.eval_test && T_) {
+            HIPCHK(launch_test<T>(c->d_tu.as<uint32_t>(), c->d_ti.as<uint32_t>(), c->d_tr.as<double>(), c->t0, c->t1,
+                                  c->d_U.as<T>(), c->d_V.as<T>(), K, c->Kp, (T)c->lo, (T)c->hi, collect ? 1 : 0, div,
+                                  c->d_tsum.as<double>(), c->d_tpart.as<double>(), st));
+            if (c->nranks > 1) c->comm.bcast_ranges(c->d_tpart.p, 2 * sizeof(double), c->tbblocks, st);
+            const uint32_t nb = (uint32_t)((T_ + 255) / 256);
+            HIPCHK(launch_sum_cols(c->d_tpart.as<double>(), nb, 2, d_res + RES_TEST_AVG, st));
+        }
+        if (cf.eval_train) HIPCHK(launch_sum(c->d_rowtr_v.as<double>(), c->J, d_res + RES_TRSQ, scratch, st));
+        HIPCHK(hipEventRecord(c->ev[6], st));
+        HIPCHK(hipMemcpyAsync(c->h_res.data(), d_res, 8 * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+
+        sbmf_sweep_info info{};
+        info.sweep = c->sweep;
+        info.collected = collect ? 1u : 0u;
+        info.tau = c->tau;
+        info.rmse_avg = (cf.eval_test && T_) ? std::sqrt(c->h_res[RES_TEST_AVG] / T_) : NAN;
+        info.rmse_this = (cf.eval_test && T_) ? std::sqrt(c->h_res[RES_TEST_THIS] / T_) : NAN;
+        info.rmse_train = cf.eval_train && N ? std::sqrt(c->h_res[RES_TRSQ] / N) : NAN;
+        c->timing.ms_hyper = ev_ms(c->ev[0], c->ev[1]);
+        c->timing.ms_user_half = ev_ms(c->ev[1], c->ev[2]);
+        c->timing.ms_item_half = ev_ms(c->ev[3], c->ev[4]);
+        c->timing.ms_comm = ev_ms(c->ev[2], c->ev[3]) + ev_ms(c->ev[4], c->ev[5]);
+        c->timing.ms_eval = ev_ms(c->ev[5], c->ev[6]);
+        for (int sd = 0; sd < 2; ++sd) {
+            const Side& sdd = sd == 0 ? c->users : c->items;
+            for (int k = 0; k < 5; ++k) {
+                const bool ran = k < RK_NUM ? !sdd.bin_rows[k].empty() : !sdd.gitems.empty();
+                c->timing.kern_ms[sd][k] = ran ? ev_ms(c->kev[sd][k][0], c->kev[sd][k][1]) : 0.0;
+            }
+        }
+        info.ms_sweep = ev_ms(c->ev[0], c->ev[5]);
+        info.ms_eval = c->timing.ms_eval;
+        c->sweep++;
+        if (cb && cb(&info, user)) break;
+    }
+}
+
+}  // namespace sbmf
+
+// ===================================================================== C ABI
+sbmf_ctx::~sbmf_ctx() {
+    if (h_pinned) (void)hipHostFree(h_pinned);
+    for (auto& e : ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& a : kev)
+        for (auto& b : a)
+            for (auto& e : b)
+                if (e) (void)hipEventDestroy(e);
+    if (st) (void)hipStreamDestroy(st);
+}
+
+#define API_BEGIN try {
+#define API_END(ctx)                                  \
+    }                                                 \
+    catch (const sbmf::Error& e) {                    \
+        g_err = e.msg;                                \
+        if (ctx) (ctx)->err = e.msg;                  \
+        return e.code;                                \
+    }                                                 \
+    catch (const std::bad_alloc&) {                   \
+        g_err = "host allocation failed";             \
+        if (ctx) (ctx)->err = g_err;                  \
+        return SBMF_E_NOMEM;                          \
+    }                                                 \
+    catch (const std::exception& e) {                 \
+        g_err = e.what();                             \
+        if (ctx) (ctx)->err = g_err;                  \
+        return SBMF_E_ARG;                            \
+    }                                                 \
+    return SBMF_OK;
+
+extern "C" {
+
+int sbmf_abi_version(void) { return SBMF_ABI_VERSION; }
+
+int sbmf_config_default(sbmf_config* c) {
+    if (!c) return SBMF_E_ARG;
+    std::memset(c, 0, sizeof *c);
+    c->num_factor = 20;  // gibbs_sbpmf_final.cpp:218
+    c->num_iter = 100;   // :299
+    c->burnin = 0;       // :300
+    c->seed = 1;         // glibc default seed (the sampler never calls srand)
+    c->rng_mode = SBMF_RNG_REFERENCE;
+    c->quirks = SBMF_QUIRKS_FINAL;
+    c->precision = SBMF_F64;
+    c->device = 0;
+    c->init_stdev = -1.0;
+    c->clamp_lo = -1.0;
+    c->clamp_hi = 5.0;
+    c->a0 = 1;
+    c->b0 = 1;
+    c->alpha0 = 1;
+    c->beta0 = 1;
+    c->nu0 = 1;
+    c->mu0 = 0.0;
+    c->recompute_every = 1;
+    c->eval_train = 0;
+    c->eval_test = 1;
+    c->gram_threshold = 0;
+    return SBMF_OK;
+}
+
+const char* sbmf_last_error(const sbmf_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+const char* sbmf_last_global_error(void) { return g_err.c_str(); }
+
+int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
+    sbmf_ctx* ctx = nullptr;
+    API_BEGIN
+    if (!cfg || !out) sbmf::fail(SBMF_E_ARG, "null argument");
+    *out = nullptr;
+    if (cfg->num_factor == 0 || cfg->num_factor > 256) sbmf::fail(SBMF_E_ARG, "num_factor must be in [1,256]");
+    if (cfg->rng_mode != SBMF_RNG_REFERENCE && cfg->rng_mode != SBMF_RNG_PHILOX) sbmf::fail(SBMF_E_ARG, "bad rng_mode");
+    if (cfg->quirks < 0 || cfg->quirks > 2) sbmf::fail(SBMF_E_ARG, "bad quirks");
+    if (cfg->precision != SBMF_F64 && cfg->precision != SBMF_F32) sbmf::fail(SBMF_E_ARG, "bad precision");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        sbmf::fail(SBMF_E_DEVICE, "no HIP device available (this library has no CPU fallback)");
+    if (cfg->device < 0 || cfg->device >= ndev) sbmf::fail(SBMF_E_DEVICE, "device %d out of range (%d)", cfg->device, ndev);
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, cfg->device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        sbmf::fail(SBMF_E_DEVICE, "device %d is %s; this build targets gfx950 (MI355X)", cfg->device, prop.gcnArchName);
+    HIPCHK(hipSetDevice(cfg->device));
+    std::unique_ptr<sbmf_ctx> c(new sbmf_ctx());
+    c->cfg = *cfg;
+    const bool q2 = cfg->quirks == SBMF_QUIRKS_SBPMF2;
+    c->init_sd = cfg->init_stdev >= 0 ? cfg->init_stdev : (q2 ? 0.1 : 1.0);
+    c->lo = cfg->clamp_lo >= 0 ? cfg->clamp_lo : (q2 ? 0.5 : 1.0);
+    c->hi = cfg->clamp_hi;
+    c->sd_is_var = cfg->quirks == SBMF_QUIRKS_NONE ? 0 : 1;
+    HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+    for (auto& a : c->kev)
+        for (auto& b : a)
+            for (auto& e : b) HIPCHK(hipEventCreate(&e));
+    *out = c.release();
+    API_END(ctx)
+}
+
+void sbmf_destroy(sbmf_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->cfg.device);
+    (void)hipStreamSynchronize(ctx->st);
+    delete ctx;
+}
+
+static void set_triples(uint64_t n, const uint32_t* u, const uint32_t* i, const double* r, std::vector<uint32_t>& U,
+                        std::vector<uint32_t>& I, std::vector<double>& R) {
+    if (n && (!u || !i || !r)) sbmf::fail(SBMF_E_ARG, "null array with n > 0");
+    U.assign(u, u + n);
+    I.assign(i, i + n);
+    R.assign(r, r + n);
+}
+
+int sbmf_set_train(sbmf_ctx* ctx, uint64_t n, const uint32_t* user, const uint32_t* item, const double* rating) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (ctx->prepared) sbmf::fail(SBMF_E_STATE, "data already prepared");
+    set_triples(n, user, item, rating, ctx->tu, ctx->ti, ctx->tr);
+    API_END(ctx)
+}
+
+int sbmf_set_test(sbmf_ctx* ctx, uint64_t n, const uint32_t* user, const uint32_t* item, const double* rating) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (ctx->prepared) sbmf::fail(SBMF_E_STATE, "data already prepared");
+    set_triples(n, user, item, rating, ctx->su, ctx->si, ctx->sr);
+    API_END(ctx)
+}
+
+int sbmf_set_dims(sbmf_ctx* ctx, uint32_t num_users, uint32_t num_items) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (ctx->prepared) sbmf::fail(SBMF_E_STATE, "data already prepared");
+    ctx->I_req = num_users;
+    ctx->J_req = num_items;
+    API_END(ctx)
+}
+
+int sbmf_prepare(sbmf_ctx* ctx) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    HIPCHK(hipSetDevice(ctx->cfg.device));
+    if (ctx->prepared) return SBMF_OK;
+    if (ctx->tu.empty()) sbmf::fail(SBMF_E_STATE, "no training data (sbmf_set_train)");
+    for (size_t x = 0; x < ctx->tu.size(); ++x)
+        if ((ctx->I_req && ctx->tu[x] >= ctx->I_req) || (ctx->J_req && ctx->ti[x] >= ctx->J_req))
+            sbmf::fail(SBMF_E_ARG, "rating %zu has an id beyond sbmf_set_dims", x);
+    if (ctx->cfg.precision == SBMF_F32)
+        prepare_T<float>(ctx);
+    else
+        prepare_T<double>(ctx);
+    API_END(ctx)
+}
+
+int sbmf_run(sbmf_ctx* ctx, uint32_t sweeps, sbmf_sweep_cb cb, void* user) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    HIPCHK(hipSetDevice(ctx->cfg.device));
+    if (!ctx->prepared) {
+        if (ctx->tu.empty()) sbmf::fail(SBMF_E_STATE, "no training data (sbmf_set_train)");
+        if (ctx->cfg.precision == SBMF_F32)
+            prepare_T<float>(ctx);
+        else
+            prepare_T<double>(ctx);
+    }
+    if (ctx->cfg.precision == SBMF_F32)
+        run_sweeps_T<float>(ctx, sweeps, cb, user);
+    else
+        run_sweeps_T<double>(ctx, sweeps, cb, user);
+    API_END(ctx)
+}
+
+int sbmf_predict(sbmf_ctx* ctx, double* out) {
+    API_BEGIN
+    if (!ctx || !out) sbmf::fail(SBMF_E_ARG, "null argument");
+    if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
+    HIPCHK(hipSetDevice(ctx->cfg.device));
+    const uint64_t T_ = ctx->su.size();
+    if (ctx->nranks > 1) ctx->comm.bcast_ranges(ctx->d_tsum.p, sizeof(double), ctx->tbounds, ctx->st);
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    HIPCHK(hipMemcpy(out, ctx->d_tsum.p, T_ * sizeof(double), hipMemcpyDeviceToHost));
+    const double div = ctx->cfg.quirks == SBMF_QUIRKS_NONE ? (double)std::max(1u, ctx->collected) : (double)std::max(1u, ctx->sweep);
+    for (uint64_t t = 0; t < T_; ++t) out[t] /= div;
+    API_END(ctx)
+}
+
+int sbmf_get_factors(sbmf_ctx* ctx, double* U, double* V) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
+    HIPCHK(hipSetDevice(ctx->cfg.device));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (ctx->cfg.precision == SBMF_F32) {
+        if (U) sbmf::download_table<float>(ctx, ctx->d_U, U, ctx->I);
+        if (V) sbmf::download_table<float>(ctx, ctx->d_V, V, ctx->J);
+    } else {
+        if (U) sbmf::download_table<double>(ctx, ctx->d_U, U, ctx->I);
+        if (V) sbmf::download_table<double>(ctx, ctx->d_V, V, ctx->J);
+    }
+    API_END(ctx)
+}
+
+int sbmf_set_factors(sbmf_ctx* ctx, const double* U, const double* V) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
+    HIPCHK(hipSetDevice(ctx->cfg.device));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (ctx->cfg.precision == SBMF_F32) {
+        if (U) sbmf::upload_table<float>(ctx, ctx->d_U, U, ctx->I);
+        if (V) sbmf::upload_table<float>(ctx, ctx->d_V, V, ctx->J);
+    } else {
+        if (U) sbmf::upload_table<double>(ctx, ctx->d_U, U, ctx->I);
+        if (V) sbmf::upload_table<double>(ctx, ctx->d_V, V, ctx->J);
+    }
+    API_END(ctx)
+}
+
+int sbmf_get_hyper(sbmf_ctx* ctx, double* h, double* tau) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
+    const uint32_t K = ctx->K;
+    if (h) {
+        std::copy(ctx->sig_u.begin(), ctx->sig_u.end(), h);
+        std::copy(ctx->mu_u.begin(), ctx->mu_u.end(), h + K);
+        std::copy(ctx->sig_v.begin(), ctx->sig_v.end(), h + 2 * K);
+        std::copy(ctx->mu_v.begin(), ctx->mu_v.end(), h + 3 * K);
+    }
+    if (tau) *tau = ctx->tau;
+    API_END(ctx)
+}
+
+int sbmf_get_dims(sbmf_ctx* ctx, uint32_t* nu, uint32_t* ni, uint64_t* ntr, uint64_t* nte) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (nu) *nu = ctx->I;
+    if (ni) *ni = ctx->J;
+    if (ntr) *ntr = ctx->tu.size();
+    if (nte) *nte = ctx->su.size();
+    API_END(ctx)
+}
+
+int sbmf_get_timing(sbmf_ctx* ctx, sbmf_timing* t) {
+    API_BEGIN
+    if (!ctx || !t) sbmf::fail(SBMF_E_ARG, "null argument");
+    *t = ctx->timing;
+    // per sweep, both halves: N*(sK + 4 + 4) + rows*2*sK
+    const uint64_t s = sbmf::tsize(ctx);
+    const uint64_t N = ctx->tu.size();
+    t->bytes_algorithmic = 2 * N * (s * ctx->K + 4 + s) + ((uint64_t)ctx->I + ctx->J) * 2 * s * ctx->K;
+    API_END(ctx)
+}
+
+int sbmf_comm_unique_id(uint8_t id[128]) {
+    sbmf_ctx* ctx = nullptr;
+    API_BEGIN
+    if (!id) sbmf::fail(SBMF_E_ARG, "null id");
+    sbmf::Comm::unique_id(id);
+    API_END(ctx)
+}
+
+int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
+    API_BEGIN
+    if (!ctx || !id) sbmf::fail(SBMF_E_ARG, "null argument");
+    if (ctx->prepared) sbmf::fail(SBMF_E_STATE, "sbmf_comm_init must precede sbmf_prepare");
+    if (nranks < 1 || rank < 0 || rank >= nranks) sbmf::fail(SBMF_E_ARG, "bad rank %d / %d", rank, nranks);
+    HIPCHK(hipSetDevice(ctx->cfg.device));
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    if (nranks > 1) ctx->comm.init(nranks, rank, id);
+    API_END(ctx)
+}
+
+int sbmf_ref_stream(uint32_t seed, int kind, double shape, uint64_t n, double* out) {
+    sbmf_ctx* ctx = nullptr;
+    API_BEGIN
+    if (!out && n) sbmf::fail(SBMF_E_ARG, "null out");
+    sbmf::GlibcRand g(seed);
+    for (uint64_t x = 0; x < n; ++x) {
+        if (kind == 0)
+            out[x] = g.next();
+        else if (kind == 1)
+            out[x] = sbmf::leva_normal(g);
+        else
+            out[x] = sbmf::mt_gamma(g, shape);
+    }
+    API_END(ctx)
+}
+
+int sbmf_philox_normals(uint64_t seed, uint32_t sweep, uint32_t tag, uint32_t row, uint32_t K, double* out) {
+    sbmf_ctx* ctx = nullptr;
+    API_BEGIN
+    if (!out && K) sbmf::fail(SBMF_E_ARG, "null out");
+    for (uint32_t k = 0; k < K; k += 2) {
+        double z0, z1;
+        sbmf::philox_normal_pair(seed, row, sweep, tag, k / 2, z0, z1);
+        out[k] = z0;
+        if (k + 1 < K) out[k + 1] = z1;
+    }
+    API_END(ctx)
+}
+
+}  // extern "C"

@@ -1,0 +1,255 @@
+// sbmf_cli.cpp -- `sbmf`, a drop-in for `bin/libFM -task r -method mcmc`
+// on the SBPMF path, driving the C ABI of include/sbmf.h.
+//
+// Flag grammar follows src/util/cmdline.h:33-70,113-119: "-name value" or
+// "--name value"; a flag directly followed by another flag gets the empty
+// value; a repeated flag or an unregistered flag is an error.  Registered
+// flags are libFM's (libfm.cpp:86-111) plus the sampler's own settings.
+// Output follows fm_learn_mcmc_simultaneous.h: per sweep
+//   "#Iter=%3d\tTrain=<rmse>\tTest=<rmse>"                      (:244)
+// and the file test_rmse_<k0><k1><K>_<method> (truncated at start, one
+// running-mean test RMSE per line, :57-62,146); -out writes one averaged
+// prediction per test line (libfm.cpp:629-634).
+// Differences, by design: -seed is honoured (libfm.cpp:124 ignores it); on
+// error the exit code is 1 (the reference prints "ERROR" and returns 0).
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/sbmf.h"
+
+extern "C" const char* sbmf_loader_error(void);
+
+namespace {
+
+struct CmdLine {
+    std::map<std::string, std::string> help, value;
+    static bool parse_name(std::string& s) {
+        if (!s.empty() && s[0] == '-') {
+            s = (s.size() > 1 && s[1] == '-') ? s.substr(2) : s.substr(1);
+            return true;
+        }
+        return false;
+    }
+    CmdLine(int argc, char** argv) {
+        for (int i = 1; i < argc; ++i) {
+            std::string s(argv[i]);
+            if (!parse_name(s)) throw std::runtime_error("cannot parse " + s);
+            if (value.count(s)) throw std::runtime_error("the parameter " + s + " is already specified");
+            if (i + 1 < argc) {
+                std::string nx(argv[i + 1]);
+                if (!parse_name(nx)) {
+                    value[s] = argv[i + 1];
+                    ++i;
+                } else {
+                    value[s] = "";
+                }
+            } else {
+                value[s] = "";
+            }
+        }
+    }
+    void reg(const std::string& n, const std::string& h) { help[n] = h; }
+    void check() const {
+        for (auto& kv : value)
+            if (!help.count(kv.first)) throw std::runtime_error("the parameter " + kv.first + " does not exist");
+    }
+    bool has(const std::string& n) const { return value.count(n) != 0; }
+    std::string get(const std::string& n, const std::string& d) const { return has(n) ? value.at(n) : d; }
+    double getd(const std::string& n, double d) const { return has(n) ? std::atof(value.at(n).c_str()) : d; }
+    long getl(const std::string& n, long d) const { return has(n) ? std::atol(value.at(n).c_str()) : d; }
+    void print_help() const {
+        for (auto& kv : help) {
+            std::cout << "-" << kv.first;
+            for (size_t i = kv.first.size() + 1; i < 16; ++i) std::cout << " ";
+            std::cout << kv.second << "\n";
+        }
+    }
+};
+
+std::vector<int> split_ints(const std::string& s) {
+    std::vector<int> out;
+    std::string cur;
+    for (char ch : s) {
+        if (ch == ',' || ch == ';') {
+            out.push_back(std::atoi(cur.c_str()));
+            cur.clear();
+        } else {
+            cur += ch;
+        }
+    }
+    if (!cur.empty()) out.push_back(std::atoi(cur.c_str()));
+    return out;
+}
+
+bool looks_libfm(const std::string& path) {
+    std::ifstream f(path);
+    std::string line;
+    while (std::getline(f, line)) {
+        size_t p = line.find_first_not_of(" \t\r");
+        if (p == std::string::npos || line[p] == '#') continue;
+        return line.find(':') != std::string::npos;
+    }
+    return false;
+}
+
+void load(const std::string& path, const std::string& fmt, uint32_t item_offset, sbmf_ratings& r) {
+    const bool libfm = fmt == "libfm" || (fmt == "auto" && looks_libfm(path));
+    const int rc = libfm ? sbmf_load_libfm(path.c_str(), item_offset, &r) : sbmf_load_triples(path.c_str(), &r);
+    if (rc != SBMF_OK) throw std::runtime_error(sbmf_loader_error());
+}
+
+struct RunState {
+    std::string rmse_file;
+    std::ofstream* rlog = nullptr;
+    int verbosity = 0;
+};
+
+int on_sweep(const sbmf_sweep_info* in, void* user) {
+    RunState* rs = static_cast<RunState*>(user);
+    std::cout << "#Iter=" << std::setw(3) << in->sweep << "\tTrain=" << in->rmse_train << "\tTest=" << in->rmse_avg
+              << std::endl;
+    std::ofstream f(rs->rmse_file, std::ios_base::app);
+    f << in->rmse_avg << "\n";
+    if (rs->rlog)
+        *rs->rlog << in->sweep << "\t" << in->rmse_avg << "\t" << in->rmse_this << "\t" << in->rmse_train << "\t"
+                  << in->tau << "\t" << in->ms_sweep << "\t" << in->ms_eval << "\n";
+    if (rs->verbosity > 0)
+        std::cout << "  tau=" << in->tau << " sweep_ms=" << in->ms_sweep << " eval_ms=" << in->ms_eval << std::endl;
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    try {
+        CmdLine cl(argc, argv);
+        std::cout << "----------------------------------------------------------------------------\n"
+                  << "sbmf -- Scalable-BPMF Gibbs sampler for AMD Instinct MI355X (libFM command line)\n"
+                  << "----------------------------------------------------------------------------" << std::endl;
+        // libFM's flags (libfm.cpp:86-111)
+        cl.reg("task", "r=regression [MANDATORY]");
+        cl.reg("meta", "filename for meta information about data set (ignored: one user and one item group)");
+        cl.reg("train", "filename for training data [MANDATORY] (SBPMF triples or libFM text)");
+        cl.reg("test", "filename for test data [MANDATORY]");
+        cl.reg("validation", "unused (SGDA only in libFM)");
+        cl.reg("out", "filename for output: averaged test predictions");
+        cl.reg("dim", "'k0,k1,k2': k0=use bias, k1=use 1-way interactions, k2=dim of 2-way interactions; default=1,1,8");
+        cl.reg("regular", "unused by the Bayesian sampler (SGD/ALS only in libFM)");
+        cl.reg("init_stdev", "stdev for initialization of the factors; default: 1.0 (quirks final) / 0.1 (sbpmf2)");
+        cl.reg("stdev", "unused");
+        cl.reg("iter", "number of collection sweeps; default=100");
+        cl.reg("learn_rate", "unused (SGD only)");
+        cl.reg("method", "learning method: mcmc (SBPMF Gibbs); default=mcmc");
+        cl.reg("verbosity", "how much infos to print; default=0");
+        cl.reg("rlog", "write per-sweep measurements to a TSV file; default=''");
+        cl.reg("seed", "integer seed; default=1 (glibc default seed of the reference samplers)");
+        cl.reg("help", "this screen");
+        cl.reg("relation", "unused (block structure relations)");
+        cl.reg("cache_size", "unused (binary data format)");
+        // sampler settings
+        cl.reg("rng", "ref (reference glibc/Leva/Marsaglia-Tsang stream; default) | philox (in-kernel, throughput)");
+        cl.reg("quirks", "final (gibbs_sbpmf_final.cpp; default) | sbpmf2 | none (stdev = sqrt(variance))");
+        cl.reg("precision", "f64 (default) | f32");
+        cl.reg("burnin", "burn-in sweeps before collection; default=0");
+        cl.reg("format", "auto (default) | triple | libfm");
+        cl.reg("item_offset", "libFM input: item feature id offset; default=0");
+        cl.reg("device", "HIP device ordinal; default=0");
+        cl.reg("recompute_every", "recompute residuals from scratch every n sweeps; default=1");
+        cl.reg("gram_threshold", "rows with more ratings take the Gram route; default=4096");
+        if (cl.has("help") || argc == 1) {
+            cl.print_help();
+            return 0;
+        }
+        cl.check();
+        const std::string task = cl.get("task", "");
+        if (task != "r") throw std::runtime_error("only -task r (regression) is supported by the SBPMF sampler");
+        const std::string method = cl.get("method", "mcmc");
+        if (method != "mcmc")
+            throw std::runtime_error("-method " + method + " is not supported (use mcmc)");
+        if (!cl.has("train") || !cl.has("test")) throw std::runtime_error("-train and -test are mandatory");
+        std::vector<int> dim = split_ints(cl.get("dim", "1,1,8"));
+        if (dim.size() != 3) throw std::runtime_error("dim must have 3 numbers");
+        if (dim[2] <= 0 || dim[2] > 256) throw std::runtime_error("dim k2 must be in [1,256]");
+        if (dim[0] || dim[1])
+            std::cout << "note: bias terms (k0,k1) are not sampled; the reference SBPMF sampler has them compiled "
+                         "out (gibbs_sbpmf_final.cpp:276-295)"
+                      << std::endl;
+
+        sbmf_config cfg;
+        sbmf_config_default(&cfg);
+        cfg.num_factor = (uint32_t)dim[2];
+        cfg.num_iter = (uint32_t)cl.getl("iter", 100);
+        cfg.burnin = (uint32_t)cl.getl("burnin", 0);
+        cfg.seed = (uint64_t)cl.getl("seed", 1);
+        const std::string rng = cl.get("rng", "ref");
+        cfg.rng_mode = rng == "philox" ? SBMF_RNG_PHILOX : SBMF_RNG_REFERENCE;
+        const std::string q = cl.get("quirks", "final");
+        cfg.quirks = q == "sbpmf2" ? SBMF_QUIRKS_SBPMF2 : (q == "none" ? SBMF_QUIRKS_NONE : SBMF_QUIRKS_FINAL);
+        cfg.precision = cl.get("precision", "f64") == "f32" ? SBMF_F32 : SBMF_F64;
+        cfg.device = (int32_t)cl.getl("device", 0);
+        if (cl.has("init_stdev")) cfg.init_stdev = cl.getd("init_stdev", 1.0);
+        cfg.recompute_every = (uint32_t)cl.getl("recompute_every", 1);
+        cfg.gram_threshold = (uint32_t)cl.getl("gram_threshold", 0);
+        cfg.eval_train = 1;
+        cfg.eval_test = 1;
+
+        const std::string fmt = cl.get("format", "auto");
+        const uint32_t off = (uint32_t)cl.getl("item_offset", 0);
+        std::cout << "Loading train...\t" << std::endl;
+        sbmf_ratings tr{}, te{};
+        load(cl.get("train", ""), fmt, off, tr);
+        std::cout << "Loading test... \t" << std::endl;
+        load(cl.get("test", ""), fmt, off, te);
+
+        sbmf_ctx* ctx = nullptr;
+        if (sbmf_create(&cfg, &ctx) != SBMF_OK) throw std::runtime_error(sbmf_last_global_error());
+        auto chk = [&](int rc) {
+            if (rc != SBMF_OK) throw std::runtime_error(sbmf_last_error(ctx));
+        };
+        chk(sbmf_set_train(ctx, tr.n, tr.user, tr.item, tr.rating));
+        chk(sbmf_set_test(ctx, te.n, te.user, te.item, te.rating));
+        chk(sbmf_prepare(ctx));
+        uint32_t nu, ni;
+        uint64_t ntr, nte;
+        chk(sbmf_get_dims(ctx, &nu, &ni, &ntr, &nte));
+        std::cout << "#users=" << nu << "\t#items=" << ni << "\t#train=" << ntr << "\t#test=" << nte << "\tK=" << cfg.num_factor
+                  << std::endl;
+
+        RunState rs;
+        std::ostringstream nm;
+        nm << dim[0] << dim[1] << dim[2];
+        rs.rmse_file = "test_rmse_" + nm.str() + "_" + method;
+        { std::ofstream trunc(rs.rmse_file); }
+        std::ofstream rlog;
+        if (cl.has("rlog") && !cl.get("rlog", "").empty()) {
+            rlog.open(cl.get("rlog", ""));
+            rlog << "iter\trmse\trmse_this\trmse_train\ttau\tms_sweep\tms_eval\n";
+            rs.rlog = &rlog;
+        }
+        rs.verbosity = (int)cl.getl("verbosity", 0);
+        chk(sbmf_run(ctx, cfg.num_iter + cfg.burnin, on_sweep, &rs));
+        if (cl.has("out") && !cl.get("out", "").empty()) {
+            std::vector<double> pred(nte);
+            chk(sbmf_predict(ctx, pred.data()));
+            std::ofstream out(cl.get("out", ""));
+            for (double p : pred) out << p << "\n";
+        }
+        sbmf_destroy(ctx);
+        sbmf_free_ratings(&tr);
+        sbmf_free_ratings(&te);
+    } catch (const std::exception& e) {
+        std::cerr << "ERROR: " << e.what() << std::endl;
+        return 1;
+    }
+    return 0;
+}

@@ -1,0 +1,260 @@
+"""sbmf -- Python mirror of the reference's learner interface over the MI355X C ABI.
+
+The reference's operator API for this path is libFM's ``fm_learn``
+(src/libfm/src/fm_learn.h:38-308): ``init()``, ``learn(train, test)``,
+``predict(data, out)``, ``evaluate(data)``, with the MCMC learner's knobs
+``num_iter`` / ``num_eval_cases`` (fm_learn_mcmc.h:75-93) and the model's
+``num_factor`` (fm_model.h:35-130).  ``FMLearnSBPMF`` keeps those names and
+meanings; the work runs in ``libsbmf.so`` (HIP kernels for gfx950).  Errors
+raise ``SBMFError`` (the reference throws ``std::string``).  There is no CPU
+compute path: without a GPU, ``init()`` raises ``SBMFError`` (SBMF_E_DEVICE).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import (F32, F64, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_DEVICE,
+                   SBMF_OK)
+
+__all__ = ["FMLearnSBPMF", "Data", "SBMFError", "load_triples", "load_libfm", "config_default",
+           "RNG_REFERENCE", "RNG_PHILOX", "QUIRKS_FINAL", "QUIRKS_SBPMF2", "QUIRKS_NONE", "F64", "F32"]
+
+lib = _lib.lib
+
+
+class SBMFError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("sbmf error %d: %s" % (code, msg))
+        self.code = code
+
+
+def _u32(a):
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class Data:
+    """Ratings triples (user, item, rating), 0-based ids; libFM's DataSubset role."""
+
+    def __init__(self, user, item, rating):
+        self.user, self.item, self.rating = _u32(user), _u32(item), _f64(rating)
+        if not (len(self.user) == len(self.item) == len(self.rating)):
+            raise ValueError("user/item/rating length mismatch")
+
+    @property
+    def num_cases(self):
+        return len(self.rating)
+
+    @property
+    def target(self):
+        return self.rating
+
+
+def _from_ratings(r):
+    n = int(r.n)
+    if n == 0:
+        return Data(np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0))
+    u = np.ctypeslib.as_array(r.user, shape=(n,)).copy()
+    i = np.ctypeslib.as_array(r.item, shape=(n,)).copy()
+    v = np.ctypeslib.as_array(r.rating, shape=(n,)).copy()
+    return Data(u, i, v)
+
+
+def load_triples(path):
+    """SBPMF triple file (gibbs_sbpmf_final.cpp:43 acceptance rule)."""
+    r = _lib.Ratings()
+    rc = lib.sbmf_load_triples(str(path).encode(), C.byref(r))
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_loader_error().decode())
+    try:
+        return _from_ratings(r)
+    finally:
+        lib.sbmf_free_ratings(C.byref(r))
+
+
+def load_libfm(path, item_offset=0):
+    """libFM text with one user and one item feature per line (Data.h:192-217)."""
+    r = _lib.Ratings()
+    rc = lib.sbmf_load_libfm(str(path).encode(), item_offset, C.byref(r))
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_loader_error().decode())
+    try:
+        return _from_ratings(r)
+    finally:
+        lib.sbmf_free_ratings(C.byref(r))
+
+
+def config_default():
+    cfg = _lib.Config()
+    lib.sbmf_config_default(C.byref(cfg))
+    return cfg
+
+
+class FMLearnSBPMF:
+    """SBPMF Gibbs learner (fm_learn / fm_learn_mcmc shaped).
+
+    Attributes mirror the reference: ``num_factor`` (K, -dim), ``num_iter``
+    (-iter), ``seed``; plus the sampler's ``rng`` ("ref" | "philox"),
+    ``quirks`` ("final" | "sbpmf2" | "none"), ``precision`` ("f64" | "f32").
+    ``rmse_trajectory`` collects the per-sweep running-mean test RMSE (the
+    reference's ``rmse is`` lines / ``test_rmse_*`` file).
+    """
+
+    _QUIRKS = {"final": QUIRKS_FINAL, "sbpmf2": QUIRKS_SBPMF2, "none": QUIRKS_NONE}
+
+    def __init__(self, num_factor=20, num_iter=100, seed=1, rng="ref", quirks="final", precision="f64", burnin=0,
+                 device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, **hyper):
+        self.cfg = config_default()
+        self.cfg.num_factor = num_factor
+        self.cfg.num_iter = num_iter
+        self.cfg.burnin = burnin
+        self.cfg.seed = seed
+        self.cfg.rng_mode = RNG_PHILOX if rng == "philox" else RNG_REFERENCE
+        self.cfg.quirks = self._QUIRKS[quirks]
+        self.cfg.precision = F32 if precision == "f32" else F64
+        self.cfg.device = device
+        if init_stdev is not None:
+            self.cfg.init_stdev = init_stdev
+        self.cfg.recompute_every = recompute_every
+        self.cfg.eval_train = 1 if eval_train else 0
+        self.cfg.gram_threshold = gram_threshold
+        for k, v in hyper.items():
+            setattr(self.cfg, k, v)
+        self.ctx = None
+        self.history = []
+        self._train = self._test = None
+
+    # -- fm_learn::init (fm_learn.h:80)
+    def init(self, comm=None):
+        if self.ctx is not None:
+            return
+        ctx = C.c_void_p()
+        rc = lib.sbmf_create(C.byref(self.cfg), C.byref(ctx))
+        if rc != SBMF_OK:
+            raise SBMFError(rc, lib.sbmf_last_global_error().decode())
+        self.ctx = ctx
+        if comm is not None:  # (nranks, rank, 128-byte id)
+            nranks, rank, uid = comm
+            buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+            self._check(lib.sbmf_comm_init(self.ctx, nranks, rank, buf))
+
+    def _check(self, rc):
+        if rc != SBMF_OK:
+            raise SBMFError(rc, lib.sbmf_last_error(self.ctx).decode())
+
+    def set_data(self, train, test=None, num_users=0, num_items=0):
+        self.init()
+        self._train, self._test = train, test
+        self._check(lib.sbmf_set_train(self.ctx, train.num_cases, _ptr(train.user, C.c_uint32),
+                                       _ptr(train.item, C.c_uint32), _ptr(train.rating, C.c_double)))
+        if test is not None:
+            self._check(lib.sbmf_set_test(self.ctx, test.num_cases, _ptr(test.user, C.c_uint32),
+                                          _ptr(test.item, C.c_uint32), _ptr(test.rating, C.c_double)))
+        if num_users or num_items:
+            self._check(lib.sbmf_set_dims(self.ctx, num_users, num_items))
+        self._check(lib.sbmf_prepare(self.ctx))
+
+    # -- fm_learn::learn(train, test) (fm_learn.h:150; fm_learn_mcmc.h:1154)
+    def learn(self, train=None, test=None, sweeps=None, callback=None):
+        if train is not None:
+            self.set_data(train, test)
+        n = self.cfg.num_iter + self.cfg.burnin if sweeps is None else sweeps
+
+        def _cb(info_p, _user):
+            info = info_p.contents
+            rec = {f: getattr(info, f) for f, _ in _lib.SweepInfo._fields_}
+            self.history.append(rec)
+            return 1 if (callback is not None and callback(rec)) else 0
+
+        cb = _lib.SWEEP_CB(_cb)
+        self._check(lib.sbmf_run(self.ctx, n, cb, None))
+        return self.history
+
+    @property
+    def rmse_trajectory(self):
+        return np.array([h["rmse_avg"] for h in self.history])
+
+    # -- fm_learn::predict (fm_learn.h:191): averaged clamped predictions of the test set
+    def predict(self):
+        out = np.zeros(self._test.num_cases if self._test is not None else 0)
+        self._check(lib.sbmf_predict(self.ctx, _ptr(out, C.c_double)))
+        return out
+
+    # -- fm_learn::evaluate (fm_learn.h:135): RMSE of the averaged prediction
+    def evaluate(self):
+        p = self.predict()
+        return float(np.sqrt(np.mean((p - self._test.rating) ** 2)))
+
+    def dims(self):
+        nu, ni = C.c_uint32(), C.c_uint32()
+        ntr, nte = C.c_uint64(), C.c_uint64()
+        self._check(lib.sbmf_get_dims(self.ctx, C.byref(nu), C.byref(ni), C.byref(ntr), C.byref(nte)))
+        return nu.value, ni.value, ntr.value, nte.value
+
+    def factors(self):
+        nu, ni, _, _ = self.dims()
+        K = self.cfg.num_factor
+        U = np.zeros((nu, K))
+        V = np.zeros((ni, K))
+        self._check(lib.sbmf_get_factors(self.ctx, _ptr(U, C.c_double), _ptr(V, C.c_double)))
+        return U, V
+
+    def set_factors(self, U, V):
+        U, V = _f64(U), _f64(V)
+        self._check(lib.sbmf_set_factors(self.ctx, _ptr(U, C.c_double), _ptr(V, C.c_double)))
+
+    def hyper(self):
+        K = self.cfg.num_factor
+        h = np.zeros(4 * K)
+        tau = C.c_double()
+        self._check(lib.sbmf_get_hyper(self.ctx, _ptr(h, C.c_double), C.byref(tau)))
+        return {"sigma_u": h[:K], "mu_u": h[K:2 * K], "sigma_v": h[2 * K:3 * K], "mu_v": h[3 * K:], "tau": tau.value}
+
+    def timing(self):
+        t = _lib.Timing()
+        self._check(lib.sbmf_get_timing(self.ctx, C.byref(t)))
+        return t
+
+    def close(self):
+        if self.ctx is not None:
+            lib.sbmf_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id():
+    buf = (C.c_uint8 * 128)()
+    rc = lib.sbmf_comm_unique_id(buf)
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_last_global_error().decode())
+    return bytes(buf)
+
+
+def ref_stream(seed, kind, n, shape=1.0):
+    """Host reference stream: kind 0 rand(), 1 ran_gaussian(), 2 ran_gamma(shape)."""
+    out = np.zeros(n)
+    rc = lib.sbmf_ref_stream(seed, kind, shape, n, _ptr(out, C.c_double))
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_last_global_error().decode())
+    return out
+
+
+def philox_normals(seed, sweep, tag, row, K):
+    out = np.zeros(K)
+    rc = lib.sbmf_philox_normals(seed, sweep, tag, row, K, _ptr(out, C.c_double))
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_last_global_error().decode())
+    return out

@@ -1,0 +1,102 @@
+"""ctypes binding of include/sbmf.h (the drop-in C ABI).
+
+Loads ``../build/libsbmf.so`` (built in-tree by ``csrc/Makefile`` /
+``__graft_entry__.build()``).  There is no pure-Python fallback: if the
+library is missing, importing this module raises.
+"""
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("SBMF_LIB", os.path.join(PKG_DIR, "build", "libsbmf.so"))
+CLI_PATH = os.path.join(PKG_DIR, "build", "sbmf")
+
+SBMF_OK, SBMF_E_ARG, SBMF_E_STATE, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_COMM, SBMF_E_NOMEM = 0, -1, -2, -3, -4, -5, -6
+RNG_REFERENCE, RNG_PHILOX = 0, 1
+QUIRKS_FINAL, QUIRKS_SBPMF2, QUIRKS_NONE = 0, 1, 2
+F64, F32 = 0, 1
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("num_factor", C.c_uint32), ("num_iter", C.c_uint32), ("burnin", C.c_uint32), ("seed", C.c_uint64),
+        ("rng_mode", C.c_int32), ("quirks", C.c_int32), ("precision", C.c_int32), ("device", C.c_int32),
+        ("init_stdev", C.c_double), ("clamp_lo", C.c_double), ("clamp_hi", C.c_double),
+        ("a0", C.c_double), ("b0", C.c_double), ("alpha0", C.c_double), ("beta0", C.c_double),
+        ("nu0", C.c_double), ("mu0", C.c_double),
+        ("recompute_every", C.c_uint32), ("eval_train", C.c_uint32), ("eval_test", C.c_uint32),
+        ("gram_threshold", C.c_uint32), ("reserved", C.c_uint32 * 8),
+    ]
+
+
+class SweepInfo(C.Structure):
+    _fields_ = [
+        ("sweep", C.c_uint32), ("collected", C.c_uint32), ("rmse_avg", C.c_double), ("rmse_this", C.c_double),
+        ("rmse_train", C.c_double), ("tau", C.c_double), ("ms_sweep", C.c_double), ("ms_eval", C.c_double),
+    ]
+
+
+class Timing(C.Structure):
+    _fields_ = [
+        ("ms_user_half", C.c_double), ("ms_item_half", C.c_double), ("ms_hyper", C.c_double),
+        ("ms_eval", C.c_double), ("ms_comm", C.c_double),
+        ("kern_ms", (C.c_double * 5) * 2), ("kern_bytes", (C.c_uint64 * 5) * 2), ("kern_rows", (C.c_uint32 * 5) * 2),
+        ("bytes_algorithmic", C.c_uint64), ("n_launch", C.c_uint32),
+    ]
+
+
+class Ratings(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("user", C.POINTER(C.c_uint32)), ("item", C.POINTER(C.c_uint32)),
+                ("rating", C.POINTER(C.c_double))]
+
+
+SWEEP_CB = C.CFUNCTYPE(C.c_int, C.POINTER(SweepInfo), C.c_void_p)
+
+_P_U32 = C.POINTER(C.c_uint32)
+_P_F64 = C.POINTER(C.c_double)
+_P_U8 = C.POINTER(C.c_uint8)
+
+# name -> (restype, argtypes); every function declared in include/sbmf.h
+SIGNATURES = {
+    "sbmf_config_default": (C.c_int, [C.POINTER(Config)]),
+    "sbmf_create": (C.c_int, [C.POINTER(Config), C.POINTER(C.c_void_p)]),
+    "sbmf_destroy": (None, [C.c_void_p]),
+    "sbmf_last_error": (C.c_char_p, [C.c_void_p]),
+    "sbmf_last_global_error": (C.c_char_p, []),
+    "sbmf_abi_version": (C.c_int, []),
+    "sbmf_set_train": (C.c_int, [C.c_void_p, C.c_uint64, _P_U32, _P_U32, _P_F64]),
+    "sbmf_set_test": (C.c_int, [C.c_void_p, C.c_uint64, _P_U32, _P_U32, _P_F64]),
+    "sbmf_set_dims": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "sbmf_prepare": (C.c_int, [C.c_void_p]),
+    "sbmf_run": (C.c_int, [C.c_void_p, C.c_uint32, SWEEP_CB, C.c_void_p]),
+    "sbmf_predict": (C.c_int, [C.c_void_p, _P_F64]),
+    "sbmf_get_factors": (C.c_int, [C.c_void_p, _P_F64, _P_F64]),
+    "sbmf_set_factors": (C.c_int, [C.c_void_p, _P_F64, _P_F64]),
+    "sbmf_get_hyper": (C.c_int, [C.c_void_p, _P_F64, _P_F64]),
+    "sbmf_get_dims": (C.c_int, [C.c_void_p, _P_U32, _P_U32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "sbmf_get_timing": (C.c_int, [C.c_void_p, C.POINTER(Timing)]),
+    "sbmf_comm_unique_id": (C.c_int, [_P_U8]),
+    "sbmf_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _P_U8]),
+    "sbmf_load_triples": (C.c_int, [C.c_char_p, C.POINTER(Ratings)]),
+    "sbmf_load_libfm": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(Ratings)]),
+    "sbmf_free_ratings": (None, [C.POINTER(Ratings)]),
+    "sbmf_ref_stream": (C.c_int, [C.c_uint32, C.c_int, C.c_double, C.c_uint64, _P_F64]),
+    "sbmf_philox_normals": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P_F64]),
+}
+
+
+def load(path=LIB_PATH):
+    if not os.path.exists(path):
+        raise ImportError("libsbmf.so not built at %s: run __graft_entry__.build() "
+                          "(or make -C scalable-bayesian-matrix-factorization_amd/csrc)" % path)
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    lib.sbmf_loader_error.restype = C.c_char_p
+    lib.sbmf_loader_error.argtypes = []
+    return lib
+
+
+lib = load()

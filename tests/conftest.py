@@ -1,0 +1,69 @@
+import gzip
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "scalable-bayesian-matrix-factorization_amd")
+GOLD = os.path.join(REPO, "tests", "golden")
+for p in (PKG, REPO, os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+def _ensure_built():
+    if not os.path.exists(os.path.join(PKG, "build", "libsbmf.so")):
+        subprocess.run(["make", "-C", os.path.join(PKG, "csrc"), "-j8"], check=True, capture_output=True)
+    if not os.path.exists(os.path.join(REPO, "oracle", "liboracle.so")):
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "all"], check=True, capture_output=True)
+
+
+_ensure_built()
+
+
+def read_triples_text(path):
+    opener = gzip.open if path.endswith(".gz") else open
+    u, i, r = [], [], []
+    with opener(path, "rt") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 3:
+                u.append(int(parts[0]))
+                i.append(int(parts[1]))
+                r.append(float(parts[2]))
+    return np.array(u, np.uint32), np.array(i, np.uint32), np.array(r, np.float64)
+
+
+@pytest.fixture(scope="session")
+def ml100k():
+    tr = read_triples_text(os.path.join(GOLD, "ml100k_train.tsv.gz"))
+    te = read_triples_text(os.path.join(GOLD, "ml100k_test.tsv.gz"))
+    return tr, te
+
+
+@pytest.fixture(scope="session")
+def ragged():
+    tr = read_triples_text(os.path.join(GOLD, "ragged_train.tsv"))
+    te = read_triples_text(os.path.join(GOLD, "ragged_test.tsv"))
+    return tr, te
+
+
+def golden_rmse(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return np.array([float(x) for x in f.read().split()])
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
