@@ -1,0 +1,86 @@
+"""Deterministic synthetic rating sets shaped like the BASELINE configs.
+
+MovieLens files are not available offline, so benchmarks run on planted
+low-rank data with MovieLens-like degree distributions:
+user degrees Pareto (alpha 1.2) with a floor of 20 ratings, item degrees
+log-normal (heavy head, long tail), duplicates removed, ratings
+clip(round(3.5 + u.v + N(0, 0.8)), 1, 5) from a rank-10 model, and a random
+90:10 train/test split.  ML-20M: 138,493 users x 26,744 items, 20.0M ratings
+(median item degree ~18-20, largest item ~67K ratings, largest user ~9K).
+"""
+import numpy as np
+
+SHAPES = {
+    # name: (users, items, total ratings, max user degree, max item degree)
+    "ml-100k": (943, 1682, 100_000, 737, 583),
+    "ml-1m": (6040, 3706, 1_000_209, 2314, 3428),
+    "ml-10m": (69878, 10677, 10_000_054, 7359, 34864),
+    "ml-20m": (138493, 26744, 20_000_263, 9254, 67310),
+    "netflix": (480189, 17770, 100_480_507, 17653, 232944),
+}
+
+
+def _degrees(rng, n, total, dmin, dmax, kind):
+    if kind == "pareto":
+        d = dmin * (1.0 - rng.random(n)) ** (-1.0 / 1.2)
+    else:  # log-normal item popularity
+        d = np.exp(rng.normal(np.log(18.0), 2.3, n))
+    d = np.clip(d, dmin, dmax)
+    # rescale the unclipped middle so the total matches
+    for _ in range(50):
+        s = d.sum()
+        if abs(s - total) < 0.001 * total:
+            break
+        free = (d > dmin) & (d < dmax)
+        f = (total - d[~free].sum()) / max(d[free].sum(), 1.0)
+        d = np.where(free, np.clip(d * f, dmin, dmax), d)
+    d = np.maximum(np.round(d).astype(np.int64), 1)
+    d[np.argmax(d)] = dmax  # pin the head exactly
+    return d
+
+
+def generate(shape="ml-20m", seed=2015, rank=10, noise=0.8, test_frac=0.1):
+    """Returns (train, test, (num_users, num_items)); train/test are
+    (user uint32, item uint32, rating float64) in random file order."""
+    I, J, total, umax, imax = SHAPES[shape]
+    rng = np.random.default_rng(seed)
+    du = _degrees(rng, I, total, min(20, umax), umax, "pareto")
+    di = _degrees(rng, J, total, 1, imax, "lognormal")
+    # Chung-Lu: draw (user, item) pairs with probabilities proportional to
+    # the target degrees, oversample, drop duplicate pairs, keep `total`.
+    pu = du / du.sum()
+    pi = di / di.sum()
+    keys = np.zeros(0, np.int64)
+    m = int(total * 1.3)
+    while True:
+        us = rng.choice(I, m, p=pu).astype(np.int64)
+        its = rng.choice(J, m, p=pi).astype(np.int64)
+        keys = np.concatenate([keys, us * J + its])
+        _, first = np.unique(keys, return_index=True)
+        if len(first) >= total:
+            break
+        m = int((total - len(first)) * 1.5) + 1000
+    key = keys[np.sort(first)][:total]  # first occurrences, draw order = random file order
+    u = (key // J).astype(np.uint32)
+    i = (key % J).astype(np.uint32)
+    P = rng.normal(0.0, (1.0 / rank) ** 0.25, (I, rank))
+    Q = rng.normal(0.0, (1.0 / rank) ** 0.25, (J, rank))
+    r = np.empty(len(u))
+    step = 1 << 22
+    for s in range(0, len(u), step):
+        e = min(len(u), s + step)
+        r[s:e] = 3.5 + np.einsum("nk,nk->n", P[u[s:e]], Q[i[s:e]]) + rng.normal(0.0, noise, e - s)
+    r = np.clip(np.round(r), 1.0, 5.0)
+    nt = int(len(u) * test_frac)
+    test = (u[:nt].copy(), i[:nt].copy(), r[:nt].copy())
+    train = (u[nt:].copy(), i[nt:].copy(), r[nt:].copy())
+    return train, test, (I, J)
+
+
+def describe(train, dims):
+    u, i, _ = train
+    du = np.bincount(u, minlength=dims[0])
+    di = np.bincount(i, minlength=dims[1])
+    q = lambda d: {"mean": float(d.mean()), "median": float(np.median(d)), "max": int(d.max()),
+                   "p99": float(np.percentile(d, 99))}
+    return {"n_train": int(len(u)), "user_deg": q(du), "item_deg": q(di)}
