@@ -30,7 +30,6 @@ sys.path.insert(0, PKG)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BASELINE_RPS = 309e3   # SBMF-P, ML-20M K=100, paper Table 3 derived per-sweep throughput
-KIND_NAMES = ["rows_w2", "rows_w8", "rows_b4", "rows_b8", "gram"]
 
 
 def parse():
@@ -45,6 +44,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--gram-threshold", type=int, default=0)
+    ap.add_argument("--row-kernel", type=int, default=0)
     return ap.parse_args()
 
 
@@ -87,7 +87,8 @@ def device_sync():
 def make_learner(args, world, rank, local, precision, uid):
     from sbmf import Data, FMLearnSBPMF
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=precision, device=local,
-                     recompute_every=0, eval_train=False, gram_threshold=args.gram_threshold)
+                     recompute_every=0, eval_train=False, gram_threshold=args.gram_threshold,
+                     row_kernel=args.row_kernel)
     L.init(comm=(world, rank, uid) if world > 1 else None)
     return L, Data
 
@@ -107,11 +108,12 @@ def measure(args, world, rank, local, precision, train, test, uid, rmse_target=0
     barrier(world)
     device_sync()
     t0 = time.perf_counter()
-    kern_ms = np.zeros((2, 5))
+    from sbmf._lib import NKIND
+    kern_ms = np.zeros((2, NKIND))
     for _ in range(args.steps):
         L.learn(sweeps=1)
         t = L.timing()
-        kern_ms += np.array([[t.kern_ms[s][k] for k in range(5)] for s in range(2)])
+        kern_ms += np.array([[t.kern_ms[s][k] for k in range(NKIND)] for s in range(2)])
         if t_hit is None and L.history[-1]["rmse_avg"] <= rmse_target:
             t_hit = time.time() - t_start
     device_sync()
@@ -119,8 +121,8 @@ def measure(args, world, rank, local, precision, train, test, uid, rmse_target=0
     dt = time.perf_counter() - t0
     dt = max_over_ranks(world, dt)
     t = L.timing()
-    kbytes = np.array([[t.kern_bytes[s][k] for k in range(5)] for s in range(2)], dtype=np.float64)
-    krows = np.array([[t.kern_rows[s][k] for k in range(5)] for s in range(2)])
+    kbytes = np.array([[t.kern_bytes[s][k] for k in range(NKIND)] for s in range(2)], dtype=np.float64)
+    krows = np.array([[t.kern_rows[s][k] for k in range(NKIND)] for s in range(2)])
     res = {
         "seconds": dt, "prep_s": prep_s, "kern_ms": kern_ms / args.steps, "kern_bytes": kbytes, "kern_rows": krows,
         "bytes_alg": t.bytes_algorithmic, "rmse": L.history[-1]["rmse_avg"], "t_hit": t_hit,
@@ -153,6 +155,7 @@ def main():
     args = parse()
     world, rank, local = dist_setup(args)
     from sbmf import comm_unique_id, synth
+    from sbmf._lib import KIND_NAMES, NKIND
     train, test, dims = synth.generate(args.shape)
     uid = None
     if world > 1:
@@ -201,7 +204,7 @@ def main():
                    "ms_user_half": main_res["ms_user"], "ms_item_half": main_res["ms_item"],
                    "ms_hyper": main_res["ms_hyper"], "ms_eval": main_res["ms_eval"], "ms_comm": main_res["ms_comm"],
                    "kernel_ms": {("user_" if s_ == 0 else "item_") + KIND_NAMES[k_]: round(float(km[s_, k_]), 4)
-                                 for s_ in range(2) for k_ in range(5) if km[s_, k_] > 0}},
+                                 for s_ in range(2) for k_ in range(NKIND) if km[s_, k_] > 0}},
         "roofline": {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_launch": float(main_res["kern_bytes"][s, k]),

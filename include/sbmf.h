@@ -31,6 +31,7 @@ extern "C" {
 #endif
 
 #define SBMF_ABI_VERSION 1
+#define SBMF_NKIND 11 /* kernel kinds reported by sbmf_get_timing */
 
 enum sbmf_status {
     SBMF_OK = 0,
@@ -78,7 +79,11 @@ typedef struct sbmf_config {
     uint32_t eval_train;      /* 1: compute train RMSE of the current sample each sweep          */
     uint32_t eval_test;       /* 1: test prediction + running-mean RMSE each sweep (:539-563)    */
     uint32_t gram_threshold;  /* rows with more ratings use the Gram route (0 = default)         */
-    uint32_t reserved[8];
+    uint32_t row_kernel;      /* 0: MFMA Gram-block kernels (default); 1: per-coordinate
+                                 wave-reduction kernels + Gram route                             */
+    uint32_t stream_threshold;/* row_kernel 0: rows with more ratings use the streaming
+                                 Gram-block kernel (0 = default 512)                             */
+    uint32_t reserved[6];
 } sbmf_config;
 
 /* Per-sweep report passed to the run callback. */
@@ -142,17 +147,21 @@ int sbmf_get_dims(sbmf_ctx* ctx, uint32_t* num_users, uint32_t* num_items, uint6
 
 /* --- measurement --------------------------------------------------------------------------- */
 /* Device times of the last sweep (HIP events on the context's stream).
- * kern_*[side][kind]: side 0 = user half, 1 = item half; kind 0..3 = the
- * row-kernel bins (1 wave / row with 2 or 8 rating slots per lane, 4 or 8
- * waves / row), 4 = Gram route (all its launches).  kern_bytes is the
+ * kern_*[side][kind]: side 0 = user half, 1 = item half; kind =
+ *   0..4  MFMA Gram-block row kernels (1 wave/row <=16 and <=64 ratings,
+ *         2 / 4 / 8 waves/row <=128 / 256 / 512 ratings),
+ *   5     streaming MFMA Gram-block kernel (one 8-wave workgroup per row, any length),
+ *   6..9  per-coordinate wave-reduction row kernels (1 wave/row <=128 and
+ *         <=512, 4 / 8 waves/row <=2048 / 4096),
+ *   10    Gram route (all its launches).  kern_bytes is the
  * algorithmic traffic of that launch per SURVEY.md §8(d): per rating
  * s*K (partner row) + 4 (partner id) + s (residual), per row 2*s*K (own row
  * read + write), s = 4 (f32) or 8 (f64). */
 typedef struct sbmf_timing {
     double ms_user_half, ms_item_half, ms_hyper, ms_eval, ms_comm;
-    double kern_ms[2][5];
-    uint64_t kern_bytes[2][5];
-    uint32_t kern_rows[2][5];
+    double kern_ms[2][SBMF_NKIND];
+    uint64_t kern_bytes[2][SBMF_NKIND];
+    uint32_t kern_rows[2][SBMF_NKIND];
     uint64_t bytes_algorithmic;  /* whole sweep, both halves                                    */
     uint32_t n_launch;           /* kernel launches in the last sweep                           */
 } sbmf_timing;

@@ -51,6 +51,17 @@ struct GramRow {
 enum RowKernelKind { RK_W2 = 0, RK_W8 = 1, RK_B4 = 2, RK_B8 = 3, RK_NUM = 4 };
 static const uint32_t RK_MAXDEG[RK_NUM] = {128, 512, 2048, 4096};
 
+// Gram-block (MFMA) row kernels: max ratings per row for each kind.
+enum GblockKind { GK_W4 = 0, GK_W16 = 1, GK_B2 = 2, GK_B4 = 3, GK_B8 = 4, GK_NUM = 5 };
+static const uint32_t GK_MAXDEG[GK_NUM] = {16, 64, 128, 256, 512};
+
+template <typename T>
+hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
+
+// Streaming Gram-block kernel: one 512-thread workgroup per row, any length.
+template <typename T>
+hipError_t launch_gstream(const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
+
 template <typename T>
 hipError_t launch_rows(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
 

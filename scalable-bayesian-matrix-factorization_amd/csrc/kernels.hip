@@ -301,6 +301,489 @@ __global__ __launch_bounds__(64 * NW * RPB) void k_rows(const uint32_t* __restri
     }
 }
 
+// ------------------------------------------------------------ Gram-block rows (MFMA)
+// Layout: 16 lanes per rating, 4 ratings per 64-lane vector; lane (r = l>>4,
+// i = l&15) holds s = partner[j_r][16b + i] of k-block b -- one 128-byte line
+// per rating per block (f64), fully coalesced.  Per block:
+//   G_B = S_B^T S_B   one MFMA 16x16x4 per vector (A = B = the same register:
+//                     lane l supplies S[l>>4][l&15], verified by
+//                     tests/hip/mfma_layout.hip),
+//   c_B = S_B^T e     one FMA per vector (e replicated over the rating's
+//                     16 lanes) + a cross-row reduction,
+//   16 draws          lane c holds row c of G_B (LDS transpose); for step j:
+//                     new = A + Bq q, D = new - old, q_c -= G[c][j] D_j
+//                     (Q_k = c_k + G_kk u_k - sum_{l<k} G_kl D_l, exact),
+//   e -= S_B D_B      16-lane DPP rotate-reduce per vector.
+// A row is handled by one wave (RPW rows per block) or by NW waves (one row
+// per block, per-wave partials summed in LDS in wave order).
+template <typename T>
+struct MfmaT;
+template <>
+struct MfmaT<double> {
+    typedef double acc_t __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ acc_t mfma(double a, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, a, c, 0, 0, 0);
+    }
+    // C/D map: col = l&15, row = (l>>4) + 4j
+    static __device__ __forceinline__ int row(int l, int j) { return (l >> 4) + 4 * j; }
+};
+template <>
+struct MfmaT<float> {
+    typedef float acc_t __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ acc_t mfma(float a, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, c, 0, 0, 0);
+    }
+    // C/D map: col = l&15, row = 4*(l>>4) + j
+    static __device__ __forceinline__ int row(int l, int j) { return 4 * (l >> 4) + j; }
+};
+
+// sum over the 16 lanes of each DPP row, result in every lane of the row
+template <typename T>
+__device__ __forceinline__ T row16_sum(T x) {
+    x += dpp<0x121, 0xf>(x);  // row_ror:1
+    x += dpp<0x122, 0xf>(x);  // row_ror:2
+    x += dpp<0x124, 0xf>(x);  // row_ror:4
+    x += dpp<0x128, 0xf>(x);  // row_ror:8
+    return x;
+}
+__device__ __forceinline__ float shfl_xor_t(float v, int m) { return __shfl_xor(v, m); }
+__device__ __forceinline__ double shfl_xor_t(double v, int m) { return __shfl_xor(v, m); }
+__device__ __forceinline__ float shfl_t(float v, int src) { return __shfl(v, src); }
+__device__ __forceinline__ double shfl_t(double v, int src) { return __shfl(v, src); }
+
+constexpr int GB = 16;      // k per block
+constexpr int GLD = GB + 1; // padded LDS row (conflict-free row reads)
+
+template <typename T, int V, int NW, int RPW>
+__global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW)) void k_gblock(const uint32_t* __restrict__ rows,
+                                                                     uint32_t nrows, HalfArgs<T> a) {
+    typedef typename MfmaT<T>::acc_t acc_t;
+    constexpr int NWAVE = NW > 1 ? NW : RPW;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int wr = NW > 1 ? wv : 0;           // wave within the row
+    const uint32_t ri = NW > 1 ? blockIdx.x : blockIdx.x * RPW + wv;
+    if (ri >= nrows) return;                  // NW>1: whole block; RPW: this wave only (no block barriers)
+    const uint32_t row = rows[ri];
+    const uint32_t beg = a.ptr[row];
+    const uint32_t n = a.ptr[row + 1] - beg;
+    const uint32_t K = a.K, Kp = a.Kp;
+    const int ci = lane & 15;                 // k within block / solve row
+    const int rr = lane >> 4;                 // rating within vector
+
+    __shared__ T Gs[NWAVE][GB][GLD];
+    __shared__ T Cs[NWAVE][GB];
+    const int ws = NW > 1 ? 0 : wv;           // LDS slot holding this row's reduced G / c / D
+
+    // per-row normals: lane l holds z for k = 2l, 2l+1 (zA) and 128+2l, 129+2l (zB)
+    T zA0, zA1, zB0 = T(0), zB1 = T(0);
+    if (a.zbuf) {
+        const uint32_t i0 = 2 * lane;
+        zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
+        zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
+        if (K > 128) {
+            zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
+            zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
+        }
+    } else {
+        double z0, z1;
+        philox_normal_pair(a.seed, row, a.sweep, a.tag, lane, z0, z1);
+        zA0 = (T)z0;
+        zA1 = (T)z1;
+        if (K > 128) {
+            philox_normal_pair(a.seed, row, a.sweep, a.tag, 64 + lane, z0, z1);
+            zB0 = (T)z0;
+            zB1 = (T)z1;
+        }
+    }
+
+    // ratings of this wave: vector v covers ratings q = (wr*V + v)*4 + rr
+    uint32_t pj[V];
+    T e[V];
+    bool ok[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
+        ok[v] = q < n;
+        pj[v] = ok[v] ? a.part[beg + q] : 0u;
+        e[v] = T(0);
+    }
+    if (a.e_from_dot) {
+        T dot[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) dot[v] = T(0);
+        for (uint32_t k0 = 0; k0 < K; k0 += GB) {
+            const uint32_t kk = k0 + ci;
+            const T o = kk < K ? a.own[(size_t)row * Kp + kk] : T(0);
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (ok[v] && kk < K) dot[v] += a.partner[(size_t)pj[v] * Kp + kk] * o;
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const T d = row16_sum(dot[v]);
+            const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
+            e[v] = ok[v] ? a.r_this[beg + q] - d : T(0);
+        }
+    } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
+            e[v] = ok[v] ? a.E_in[a.perm[beg + q]] : T(0);
+        }
+    }
+
+    const T tau = a.tau;
+    // software pipeline: block b+1's slices and own/sigma/mu values are in
+    // flight while block b is reduced, solved and applied
+    T s[V], sn[V];
+    T oldc, sgc, muc;
+    {
+        const uint32_t kk = ci;
+        const bool kin = kk < K;
+#pragma unroll
+        for (int v = 0; v < V; ++v) s[v] = (ok[v] && kin) ? a.partner[(size_t)pj[v] * Kp + kk] : T(0);
+        oldc = kin ? a.own[(size_t)row * Kp + kk] : T(0);
+        sgc = kin ? a.sig[kk] : T(0);
+        muc = kin ? a.mu[kk] : T(0);
+    }
+    for (uint32_t b0 = 0; b0 < K; b0 += GB) {
+        const uint32_t kk = b0 + ci;
+        const bool kin = kk < K;
+        const uint32_t kn = kk + GB;
+        const bool nin = kn < K;
+        const T oldn = nin ? a.own[(size_t)row * Kp + kn] : T(0);
+        const T sgn = nin ? a.sig[kn] : T(0);
+        const T mun = nin ? a.mu[kn] : T(0);
+#pragma unroll
+        for (int v = 0; v < V; ++v) sn[v] = (ok[v] && nin) ? a.partner[(size_t)pj[v] * Kp + kn] : T(0);
+        acc_t g = {T(0), T(0), T(0), T(0)};
+        T cc = T(0);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            g = MfmaT<T>::mfma(s[v], g);
+            cc += s[v] * e[v];
+        }
+        cc += shfl_xor_t(cc, 16);
+        cc += shfl_xor_t(cc, 32);
+        // ---- 2. G, c -> LDS (row layout); multi-wave rows sum in wave order
+        if constexpr (NW > 1) {
+            __syncthreads();  // previous block's readers of Gs are done
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Gs[wr][MfmaT<T>::row(lane, j)][ci] = g[j];
+            if (lane < GB) Cs[wr][lane] = cc;
+            __syncthreads();
+            for (int x = threadIdx.x; x < GB * GB; x += 64 * NW) {
+                const int r0 = x >> 4, c0 = x & 15;
+                T sum = Gs[0][r0][c0];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) sum += Gs[w][r0][c0];
+                Gs[0][r0][c0] = sum;  // each entry owned by one thread: read-then-write is safe
+                if (x < GB) {
+                    T cs = Cs[0][x];
+#pragma unroll
+                    for (int w = 1; w < NW; ++w) cs += Cs[w][x];
+                    Cs[0][x] = cs;
+                }
+            }
+            __syncthreads();
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Gs[ws][MfmaT<T>::row(lane, j)][ci] = g[j];
+            if (lane < GB) Cs[ws][lane] = cc;
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own LDS writes visible to own reads
+            __builtin_amdgcn_wave_barrier();
+        }
+        // ---- 3. the 16 sequential draws (every wave redundantly for NW>1: no extra barrier)
+        T Grow[GB];
+#pragma unroll
+        for (int j = 0; j < GB; ++j) Grow[j] = Gs[ws][ci][j];
+        const T P = Gs[ws][ci][ci];
+        const T old = oldc, sg = sgc, mu = muc;
+        // z_kk lives in lane (kk>>1)&63 of zA (kk<128) or zB
+        const int zl = (int)((kk >> 1) & 63);
+        // shuffle both registers, then pick by this lane's own parity (the
+        // source lane's select would use the source lane's k)
+        const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
+        T z = (kk & 1) ? za1 : za0;
+        if (K > 128) {
+            const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
+            z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
+        }
+        const T var = kin ? T(1) / (sg + tau * P) : T(0);
+        const T sd = a.sd_is_var ? var : tsqrt(var);
+        const T A = var * sg * mu + sd * z;
+        const T Bq = var * tau;
+        T q = Cs[ws][ci] + P * old;
+        T nwv = old, dlt = T(0);
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+            const T nw = A + Bq * q;
+            const T d = nw - old;  // lanes with k >= K have var = 0 and q-terms 0: d = -old = 0
+            const T dj = readlane(d, j);
+            q -= Grow[j] * dj;
+            nwv = (ci == j) ? nw : nwv;
+            dlt = (ci == j) ? d : dlt;
+        }
+        if (wr == 0 && lane < GB && kin) a.own[(size_t)row * Kp + kk] = nwv;
+        // ---- 4. e -= S_B D_B   (lane (r,i) holds D_i after the solve: dlt of lane i)
+        const T Dl = shfl_t(dlt, ci);
+#pragma unroll
+        for (int v = 0; v < V; ++v) e[v] -= row16_sum(s[v] * Dl);
+#pragma unroll
+        for (int v = 0; v < V; ++v) s[v] = sn[v];
+        oldc = oldn;
+        sgc = sgn;
+        muc = mun;
+    }
+
+    // ---- epilogue: residuals out, per-row partial sums
+    T sq = T(0), trs = T(0);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
+        if (ok[v] && ci == 0) {
+            a.E_out[beg + q] = e[v];
+            sq += e[v] * e[v];
+            if (a.row_tr) {
+                const T r = a.r_this[beg + q];
+                T pr = r - e[v];
+                pr = (pr < a.hi) ? pr : a.hi;
+                pr = (a.lo < pr) ? pr : a.lo;
+                trs += (pr - r) * (pr - r);
+            }
+        }
+    }
+    if (a.row_sq || a.row_tr) {
+        double dsq = wave_sum((double)sq);
+        double dtr = wave_sum((double)trs);
+        if constexpr (NW > 1) {
+            __shared__ double red2[NW][2];
+            if (lane == 0) {
+                red2[wr][0] = dsq;
+                red2[wr][1] = dtr;
+            }
+            __syncthreads();
+            dsq = 0.0;
+            dtr = 0.0;
+            for (int w = 0; w < NW; ++w) {
+                dsq += red2[w][0];
+                dtr += red2[w][1];
+            }
+        }
+        if (wr == 0 && lane == 0) {
+            if (a.row_sq) a.row_sq[row] = dsq;
+            if (a.row_tr) a.row_tr[row] = dtr;
+        }
+    }
+}
+
+// ------------------------------------------------------------ streaming Gram-block rows
+// Rows of any length: one workgroup (NW waves) per row.  Residuals live in
+// the row's own slice of E_out (L2-resident), so there is no register limit
+// on the row length and no inter-workgroup synchronisation.  Per 16-wide
+// k-block: pass A gathers the slices (whole 128-byte lines) and accumulates
+// G_B = S^T S (MFMA) and c_B = S^T e; the 16 draws run as in k_gblock; pass
+// B re-reads the slices (L2 hits) and applies e -= S D.  Wave w owns vectors
+// w, w+NW, ... in both passes, so every residual is read back by the wave
+// (and lanes) that wrote it.
+template <typename T, int NW, int UNR>
+__global__ __launch_bounds__(64 * NW) void k_gstream(const uint32_t* __restrict__ rows, uint32_t nrows,
+                                                     HalfArgs<T> a) {
+    typedef typename MfmaT<T>::acc_t acc_t;
+    const int lane = threadIdx.x & 63;
+    const int wr = threadIdx.x >> 6;
+    if (blockIdx.x >= nrows) return;
+    const uint32_t row = rows[blockIdx.x];
+    const uint32_t beg = a.ptr[row];
+    const uint32_t n = a.ptr[row + 1] - beg;
+    const uint32_t nvec = (n + 3) / 4;
+    const uint32_t K = a.K, Kp = a.Kp;
+    const int ci = lane & 15;
+    const int rr = lane >> 4;
+    __shared__ T Gs[NW][GB][GLD];
+    __shared__ T Cs[NW][GB];
+    __shared__ double red2[NW][2];
+
+    T zA0, zA1, zB0 = T(0), zB1 = T(0);
+    if (a.zbuf) {
+        const uint32_t i0 = 2 * lane;
+        zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
+        zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
+        if (K > 128) {
+            zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
+            zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
+        }
+    } else {
+        double z0, z1;
+        philox_normal_pair(a.seed, row, a.sweep, a.tag, lane, z0, z1);
+        zA0 = (T)z0;
+        zA1 = (T)z1;
+        if (K > 128) {
+            philox_normal_pair(a.seed, row, a.sweep, a.tag, 64 + lane, z0, z1);
+            zB0 = (T)z0;
+            zB1 = (T)z1;
+        }
+    }
+
+    // ---- initial residuals of this row -> E_out (own order)
+    if (a.e_from_dot) {
+        for (uint32_t v = wr; v < nvec; v += NW) {
+            const uint32_t q = 4 * v + rr;
+            const bool ok = q < n;
+            const uint32_t pj = ok ? a.part[beg + q] : 0u;
+            T d = T(0);
+            for (uint32_t k0 = 0; k0 < K; k0 += GB) {
+                const uint32_t kk = k0 + ci;
+                if (ok && kk < K) d += a.partner[(size_t)pj * Kp + kk] * a.own[(size_t)row * Kp + kk];
+            }
+            d = row16_sum(d);
+            if (ok && ci == 0) a.E_out[beg + q] = a.r_this[beg + q] - d;
+        }
+    } else {
+        for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) a.E_out[beg + x] = a.E_in[a.perm[beg + x]];
+    }
+    __threadfence_block();
+    __syncthreads();
+
+    const T tau = a.tau;
+    double sq = 0.0, trs = 0.0;
+    for (uint32_t b0 = 0; b0 < K; b0 += GB) {
+        const uint32_t kk = b0 + ci;
+        const bool kin = kk < K;
+        // ---- pass A
+        acc_t g = {T(0), T(0), T(0), T(0)};
+        T cc = T(0);
+        for (uint32_t v0 = wr; v0 < nvec; v0 += NW * UNR) {
+            T s[UNR], e[UNR];
+            uint32_t pj[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const uint32_t q = 4 * (v0 + u * NW) + rr;
+                pj[u] = q < n ? a.part[beg + q] : 0u;
+                e[u] = q < n ? a.E_out[beg + q] : T(0);
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const uint32_t q = 4 * (v0 + u * NW) + rr;
+                s[u] = (q < n && kin) ? a.partner[(size_t)pj[u] * Kp + kk] : T(0);
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                g = MfmaT<T>::mfma(s[u], g);
+                cc += s[u] * e[u];
+            }
+        }
+        cc += shfl_xor_t(cc, 16);
+        cc += shfl_xor_t(cc, 32);
+        __syncthreads();  // previous block's solve reads of Gs[0] are done
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Gs[wr][MfmaT<T>::row(lane, j)][ci] = g[j];
+        if (lane < GB) Cs[wr][lane] = cc;
+        __syncthreads();
+        for (int x = threadIdx.x; x < GB * GB; x += 64 * NW) {
+            const int r0 = x >> 4, c0 = x & 15;
+            T sum = Gs[0][r0][c0];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) sum += Gs[w][r0][c0];
+            Gs[0][r0][c0] = sum;
+            if (x < GB) {
+                T cs = Cs[0][x];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) cs += Cs[w][x];
+                Cs[0][x] = cs;
+            }
+        }
+        __syncthreads();
+        // ---- the 16 draws (every wave, identical inputs -> identical results)
+        T Grow[GB];
+#pragma unroll
+        for (int j = 0; j < GB; ++j) Grow[j] = Gs[0][ci][j];
+        const T P = Gs[0][ci][ci];
+        const T old = kin ? a.own[(size_t)row * Kp + kk] : T(0);
+        const T sg = kin ? a.sig[kk] : T(0);
+        const T mu = kin ? a.mu[kk] : T(0);
+        const int zl = (int)((kk >> 1) & 63);
+        const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
+        T z = (kk & 1) ? za1 : za0;
+        if (K > 128) {
+            const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
+            z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
+        }
+        const T var = kin ? T(1) / (sg + tau * P) : T(0);
+        const T sd = a.sd_is_var ? var : tsqrt(var);
+        const T A = var * sg * mu + sd * z;
+        const T Bq = var * tau;
+        T q = Cs[0][ci] + P * old;
+        T nwv = old, dlt = T(0);
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+            const T nw = A + Bq * q;
+            const T d = nw - old;
+            const T dj = readlane(d, j);
+            q -= Grow[j] * dj;
+            nwv = (ci == j) ? nw : nwv;
+            dlt = (ci == j) ? d : dlt;
+        }
+        if (wr == 0 && lane < GB && kin) a.own[(size_t)row * Kp + kk] = nwv;
+        const T Dl = shfl_t(dlt, ci);
+        const bool last = b0 + GB >= K;
+        // ---- pass B: e -= S D   (slices re-read from L2)
+        for (uint32_t v0 = wr; v0 < nvec; v0 += NW * UNR) {
+            T s[UNR], e[UNR];
+            bool okv[UNR];
+            uint32_t pj[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const uint32_t q = 4 * (v0 + u * NW) + rr;
+                okv[u] = q < n;
+                pj[u] = okv[u] ? a.part[beg + q] : 0u;
+                e[u] = okv[u] ? a.E_out[beg + q] : T(0);
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) s[u] = (okv[u] && kin) ? a.partner[(size_t)pj[u] * Kp + kk] : T(0);
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const T ev = e[u] - row16_sum(s[u] * Dl);
+                const uint32_t q = 4 * (v0 + u * NW) + rr;
+                if (okv[u] && ci == 0) {
+                    a.E_out[beg + q] = ev;
+                    if (last) {
+                        sq += (double)(ev * ev);
+                        if (a.row_tr) {
+                            const T r = a.r_this[beg + q];
+                            T pr = r - ev;
+                            pr = (pr < a.hi) ? pr : a.hi;
+                            pr = (a.lo < pr) ? pr : a.lo;
+                            trs += (double)((pr - r) * (pr - r));
+                        }
+                    }
+                }
+            }
+        }
+        __threadfence_block();  // this wave's residual stores precede its next pass-A reads
+    }
+    if (a.row_sq || a.row_tr) {
+        double dsq = wave_sum(sq);
+        double dtr = wave_sum(trs);
+        if (lane == 0) {
+            red2[wr][0] = dsq;
+            red2[wr][1] = dtr;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            dsq = 0.0;
+            dtr = 0.0;
+            for (int w = 0; w < NW; ++w) {
+                dsq += red2[w][0];
+                dtr += red2[w][1];
+            }
+            if (a.row_sq) a.row_sq[row] = dsq;
+            if (a.row_tr) a.row_tr[row] = dtr;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ Gram route
 constexpr int GT = 128;  // Gram tile edge (K padded to 16 inside)
 constexpr int GSUB = 32; // ratings staged per LDS sub-chunk
@@ -540,6 +1023,8 @@ __global__ __launch_bounds__(64) void k_gram_rowsum(const GramRow* __restrict__ 
 }
 
 // ------------------------------------------------------------------ residual recompute
+// One wave per row; 16 lanes per rating (lane (r = l>>4, i = l&15) covers
+// k = 16b + i), so each partner row is read as whole 128-byte lines.
 template <typename T>
 __global__ __launch_bounds__(256) void k_resid(const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ part,
                                                 const T* __restrict__ r, const T* __restrict__ own,
@@ -548,16 +1033,32 @@ __global__ __launch_bounds__(256) void k_resid(const uint32_t* __restrict__ ptr,
     const uint32_t row = r0 + blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= r1) return;
+    const int ci = lane & 15, rr = lane >> 4;
     const uint32_t beg = ptr[row], end = ptr[row + 1];
     const T* o = own + (size_t)row * Kp;
+    T ov[16];  // own row, this lane's k values (k = 16b + ci)
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        const uint32_t kk = 16 * b + ci;
+        ov[b] = kk < K ? o[kk] : T(0);
+    }
     double sq = 0.0;
-    for (uint32_t idx = beg + lane; idx < end; idx += 64) {
-        const T* src = partner + (size_t)part[idx] * Kp;
+    for (uint32_t i0 = beg; i0 < end; i0 += 4) {
+        const uint32_t idx = i0 + rr;
+        const bool ok = idx < end;
+        const T* src = partner + (size_t)(ok ? part[idx] : 0u) * Kp;
         T d = T(0);
-        for (uint32_t k = 0; k < K; ++k) d += o[k] * src[k];
-        const T e = r[idx] - d;
-        E[idx] = e;
-        sq += (double)(e * e);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+            const uint32_t kk = 16 * b + ci;
+            if (16 * b < (int)K && ok && kk < K) d += ov[b] * src[kk];
+        }
+        d = row16_sum(d);
+        if (ok && ci == 0) {
+            const T e = r[idx] - d;
+            E[idx] = e;
+            sq += (double)(e * e);
+        }
     }
     sq = wave_sum(sq);
     if (lane == 0) row_sq[row] = sq;
@@ -583,37 +1084,49 @@ __global__ __launch_bounds__(256) void k_colstats(const T* __restrict__ tab, uin
 }
 
 // ------------------------------------------------------------------ test evaluation
+// 256 test ratings per block; each wave takes 4 at a time with 16 lanes per
+// rating (coalesced 128-byte reads of both factor rows).
 template <typename T>
 __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ti,
                                                const double* __restrict__ tr, uint64_t t0, uint64_t t1,
                                                const T* __restrict__ U, const T* __restrict__ V, uint32_t K,
                                                uint32_t Kp, T lo, T hi, int collect, double div,
                                                double* __restrict__ sum, double* __restrict__ part) {
-    const uint64_t t = t0 + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ci = lane & 15, rr = lane >> 4;
+    const uint64_t base = t0 + (uint64_t)blockIdx.x * 256 + (uint64_t)w * 64;
     double a2 = 0.0, t2 = 0.0;
-    if (t < t1) {
-        const T* u = U + (size_t)tu[t] * Kp;
-        const T* v = V + (size_t)ti[t] * Kp;
+    for (int it = 0; it < 16; ++it) {
+        const uint64_t t = base + it * 4 + rr;
+        const bool ok = t < t1;
+        const T* u = U + (size_t)(ok ? tu[t] : 0u) * Kp;
+        const T* v = V + (size_t)(ok ? ti[t] : 0u) * Kp;
         T p = T(0);
-        for (uint32_t k = 0; k < K; ++k) p += u[k] * v[k];
-        p = (p < hi) ? p : hi;
-        p = (lo < p) ? p : lo;
-        double s = sum[t];
-        if (collect) {
-            s += (double)p;
-            sum[t] = s;
+        for (uint32_t k0 = 0; k0 < K; k0 += 16) {
+            const uint32_t kk = k0 + ci;
+            if (ok && kk < K) p += u[kk] * v[kk];
         }
-        const double d = tr[t] - s / div;
-        a2 = d * d;
-        const double dt = tr[t] - (double)p;
-        t2 = dt * dt;
+        p = row16_sum(p);
+        if (ok && ci == 0) {
+            p = (p < hi) ? p : hi;
+            p = (lo < p) ? p : lo;
+            double s = sum[t];
+            if (collect) {
+                s += (double)p;
+                sum[t] = s;
+            }
+            const double d = tr[t] - s / div;
+            a2 += d * d;
+            const double dt = tr[t] - (double)p;
+            t2 += dt * dt;
+        }
     }
     __shared__ double red[4][2];
     a2 = wave_sum(a2);
     t2 = wave_sum(t2);
-    if ((threadIdx.x & 63) == 0) {
-        red[threadIdx.x >> 6][0] = a2;
-        red[threadIdx.x >> 6][1] = t2;
+    if (lane == 0) {
+        red[w][0] = a2;
+        red[w][1] = t2;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -695,6 +1208,43 @@ hipError_t launch_rows(int kind, const uint32_t* rows, uint32_t nrows, const Hal
     if (a.K <= 128) return launch_rows_ks<T, 2>(kind, rows, nrows, a, st);
     if (a.K <= 256) return launch_rows_ks<T, 4>(kind, rows, nrows, a, st);
     return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st) {
+    if (nrows == 0) return hipSuccess;
+    if (a.K > 256) return hipErrorInvalidValue;
+    switch (kind) {
+        case GK_W4:  // 1 wave / row, <= 16 ratings, 4 rows / block
+            k_gblock<T, 4, 1, 4><<<(nrows + 3) / 4, 256, 0, st>>>(rows, nrows, a);
+            break;
+        case GK_W16:  // 1 wave / row, <= 64 ratings
+            k_gblock<T, 16, 1, 4><<<(nrows + 3) / 4, 256, 0, st>>>(rows, nrows, a);
+            break;
+        case GK_B2:  // 2 waves / row, <= 128 ratings
+            k_gblock<T, 16, 2, 1><<<nrows, 128, 0, st>>>(rows, nrows, a);
+            break;
+        case GK_B4:  // 4 waves / row, <= 256 ratings
+            k_gblock<T, 16, 4, 1><<<nrows, 256, 0, st>>>(rows, nrows, a);
+            break;
+        case GK_B8:  // 8 waves / row, <= 512 ratings
+            k_gblock<T, 16, 8, 1><<<nrows, 512, 0, st>>>(rows, nrows, a);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_gstream(const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st) {
+    if (nrows == 0) return hipSuccess;
+    if (a.K > 256) return hipErrorInvalidValue;
+    // 8 waves x 8 vectors in flight per wave.  NOTE: the same kernel with
+    // 16 waves (1024 threads) returned wrong, run-to-run different results
+    // on gfx950 (tests/dbg_gs.py); unexplained, kept out until understood.
+    k_gstream<T, 8, 8><<<nrows, 512, 0, st>>>(rows, nrows, a);
+    return hipGetLastError();
 }
 
 template <typename T>
@@ -786,6 +1336,8 @@ hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint
 
 #define SBMF_INST(T)                                                                                                 \
     template hipError_t launch_rows<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);            \
+    template hipError_t launch_gblock<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);          \
+    template hipError_t launch_gstream<T>(const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);              \
     template hipError_t launch_gram<T>(const GramItem*, uint32_t, const GramRow*, uint32_t, double*, T*, double*,   \
                                        double*, const HalfArgs<T>&, hipStream_t);                                    \
     template hipError_t launch_resid<T>(const uint32_t*, const uint32_t*, const T*, const T*, const T*, uint32_t,     \

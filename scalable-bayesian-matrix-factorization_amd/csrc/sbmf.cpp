@@ -102,7 +102,7 @@ struct Side {
     std::vector<double> r;              // [N] ratings
     uint32_t r0 = 0, r1 = 0;            // owned row range (multi-GPU)
     std::vector<uint64_t> bounds;       // [nranks+1] row ranges of every rank
-    std::vector<uint32_t> bin_rows[RK_NUM];
+    std::vector<uint32_t> bin_rows[SBMF_NKIND - 1];  // kinds: GK_* (0..4), KIND_STREAM (5), KIND_RK0 + RK_* (6..9)
     std::vector<GramItem> gitems;
     std::vector<GramRow> grows;
 };
@@ -143,7 +143,11 @@ static void partition(Side& s, int nranks, int rank) {
     s.r1 = (uint32_t)s.bounds[rank + 1];
 }
 
-static void build_bins(Side& s, uint32_t gram_thr) {
+static const int KIND_STREAM = GK_NUM;       // 5
+static const int KIND_RK0 = GK_NUM + 1;       // 6..9
+static const int KIND_GRAM = SBMF_NKIND - 1;  // 10
+
+static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr) {
     for (auto& b : s.bin_rows) b.clear();
     s.gitems.clear();
     s.grows.clear();
@@ -156,6 +160,10 @@ static void build_bins(Side& s, uint32_t gram_thr) {
     const uint32_t chunk = 2048;
     for (uint32_t r : order) {
         const uint32_t d = deg(r);
+        if (row_kernel == 0 && d > stream_thr && d <= gram_thr) {
+            s.bin_rows[KIND_STREAM].push_back(r);
+            continue;
+        }
         if (d > gram_thr || d > RK_MAXDEG[RK_NUM - 1]) {
             GramRow gr{r, (uint32_t)s.gitems.size(), 0};
             for (uint32_t o = 0; o < d; o += chunk) {
@@ -165,9 +173,15 @@ static void build_bins(Side& s, uint32_t gram_thr) {
             s.grows.push_back(gr);
             continue;
         }
+        if (row_kernel == 0) {
+            int kind = GK_W4;
+            while (d > GK_MAXDEG[kind]) ++kind;
+            s.bin_rows[kind].push_back(r);
+            continue;
+        }
         int kind = RK_W2;
         while (d > RK_MAXDEG[kind]) ++kind;
-        s.bin_rows[kind].push_back(r);
+        s.bin_rows[KIND_RK0 + kind].push_back(r);
     }
 }
 
@@ -203,11 +217,11 @@ struct sbmf_ctx {
     // device
     hipStream_t st = nullptr;
     hipEvent_t ev[8] = {};
-    hipEvent_t kev[2][5][2] = {};
+    hipEvent_t kev[2][SBMF_NKIND][2] = {};
     DBuf d_uptr, d_upart, d_uperm, d_ur, d_vptr, d_vpart, d_vperm, d_vr;
     DBuf d_U, d_V, d_Eu, d_Ev, d_zU, d_zV, d_hyper;
     DBuf d_rowsq_u, d_rowtr_u, d_rowsq_v, d_rowtr_v;
-    DBuf d_bins_u[RK_NUM], d_bins_v[RK_NUM];
+    DBuf d_bins_u[SBMF_NKIND - 1], d_bins_v[SBMF_NKIND - 1];
     DBuf d_gitems_u, d_grows_u, d_gitems_v, d_grows_v, d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
     DBuf d_colpart, d_res, d_scratch;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
@@ -276,7 +290,7 @@ static void prepare_T(sbmf_ctx* c) {
     if (c->I == 0 || c->J == 0) fail(SBMF_E_STATE, "no ratings: call sbmf_set_train first");
     if (N >= 0xffffffffull) fail(SBMF_E_ARG, "more than 2^32-1 ratings are not supported");
     c->K = cf.num_factor;
-    c->Kp = (c->K + (uint32_t)(32 / sizeof(T)) - 1) / (uint32_t)(32 / sizeof(T)) * (uint32_t)(32 / sizeof(T));
+    c->Kp = (c->K + 15) / 16 * 16;  // k-blocks of 16 start on 128-byte (f64) / 64-byte (f32) boundaries
 
     std::vector<uint32_t> pos_u, pos_v;
     build_side(N, c->tu.data(), c->ti.data(), c->tr.data(), c->I, c->users, pos_u);
@@ -289,9 +303,18 @@ static void prepare_T(sbmf_ctx* c) {
     }
     partition(c->users, c->nranks, c->rank);
     partition(c->items, c->nranks, c->rank);
-    const uint32_t thr = cf.gram_threshold ? std::min(cf.gram_threshold, RK_MAXDEG[RK_NUM - 1]) : RK_MAXDEG[RK_NUM - 1];
-    build_bins(c->users, thr);
-    build_bins(c->items, thr);
+    // row_kernel 0: Gram-block kernels for rows <= stream threshold, the
+    // streaming kernel above it, the Gram route only if a threshold is set.
+    // row_kernel 1: per-coordinate kernels up to 4096 ratings, Gram route above.
+    const uint32_t sthr = std::min<uint32_t>(cf.stream_threshold ? cf.stream_threshold : GK_MAXDEG[GK_NUM - 1],
+                                             GK_MAXDEG[GK_NUM - 1]);
+    uint32_t thr;
+    if (cf.row_kernel == 0)
+        thr = cf.gram_threshold ? cf.gram_threshold : 0xffffffffu;
+    else
+        thr = cf.gram_threshold ? std::min(cf.gram_threshold, RK_MAXDEG[RK_NUM - 1]) : RK_MAXDEG[RK_NUM - 1];
+    build_bins(c->users, thr, (int)cf.row_kernel, sthr);
+    build_bins(c->items, thr, (int)cf.row_kernel, sthr);
     {  // test split in 256-aligned blocks
         const uint64_t T_ = c->su.size(), nb = (T_ + 255) / 256;
         c->tbounds.assign(c->nranks + 1, 0);
@@ -313,7 +336,7 @@ static void prepare_T(sbmf_ctx* c) {
     upload(c->d_vpart, c->items.part, st);
     upload(c->d_vperm, c->items.perm, st);
     upload(c->d_vr, to_T<T>(c->items.r), st);
-    for (int k = 0; k < RK_NUM; ++k) {
+    for (int k = 0; k < SBMF_NKIND - 1; ++k) {
         upload(c->d_bins_u[k], c->users.bin_rows[k], st);
         upload(c->d_bins_v[k], c->items.bin_rows[k], st);
     }
@@ -480,18 +503,23 @@ static void run_half(sbmf_ctx* c, bool users) {
     DBuf* bins = users ? c->d_bins_u : c->d_bins_v;
     const int sd = users ? 0 : 1;
     if (!s.gitems.empty()) {
-        HIPCHK(hipEventRecord(c->kev[sd][4][0], st));
+        HIPCHK(hipEventRecord(c->kev[sd][KIND_GRAM][0], st));
         HIPCHK(launch_gram<T>((users ? c->d_gitems_u : c->d_gitems_v).as<GramItem>(), (uint32_t)s.gitems.size(),
                               (users ? c->d_grows_u : c->d_grows_v).as<GramRow>(), (uint32_t)s.grows.size(),
                               c->d_slabs.as<double>(), c->d_delta.as<T>(), c->d_chunk_sq.as<double>(),
                               a.row_tr ? c->d_chunk_tr.as<double>() : nullptr, a, st));
-        HIPCHK(hipEventRecord(c->kev[sd][4][1], st));
+        HIPCHK(hipEventRecord(c->kev[sd][KIND_GRAM][1], st));
         c->timing.n_launch += 4;
     }
-    for (int k = RK_NUM - 1; k >= 0; --k) {
+    for (int k = SBMF_NKIND - 2; k >= 0; --k) {
         if (s.bin_rows[k].empty()) continue;
         HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
-        HIPCHK(launch_rows<T>(k, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
+        if (k < GK_NUM)
+            HIPCHK(launch_gblock<T>(k, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
+        else if (k == KIND_STREAM)
+            HIPCHK(launch_gstream<T>(bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
+        else
+            HIPCHK(launch_rows<T>(k - KIND_RK0, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
         HIPCHK(hipEventRecord(c->kev[sd][k][1], st));
         c->timing.n_launch++;
     }
@@ -507,14 +535,14 @@ static void fill_kernel_bytes(sbmf_ctx* c) {
     const uint64_t tsz = tsize(c);
     for (int sd = 0; sd < 2; ++sd) {
         const Side& s = sd == 0 ? c->users : c->items;
-        for (int k = 0; k < RK_NUM; ++k) {
+        for (int k = 0; k < SBMF_NKIND - 1; ++k) {
             c->timing.kern_bytes[sd][k] = alg_bytes(s, s.bin_rows[k], c->K, tsz);
             c->timing.kern_rows[sd][k] = (uint32_t)s.bin_rows[k].size();
         }
         std::vector<uint32_t> gr;
         for (const GramRow& g : s.grows) gr.push_back(g.row);
-        c->timing.kern_bytes[sd][4] = alg_bytes(s, gr, c->K, tsz);
-        c->timing.kern_rows[sd][4] = (uint32_t)gr.size();
+        c->timing.kern_bytes[sd][KIND_GRAM] = alg_bytes(s, gr, c->K, tsz);
+        c->timing.kern_rows[sd][KIND_GRAM] = (uint32_t)gr.size();
     }
 }
 
@@ -650,8 +678,8 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         c->timing.ms_eval = ev_ms(c->ev[5], c->ev[6]);
         for (int sd = 0; sd < 2; ++sd) {
             const Side& sdd = sd == 0 ? c->users : c->items;
-            for (int k = 0; k < 5; ++k) {
-                const bool ran = k < RK_NUM ? !sdd.bin_rows[k].empty() : !sdd.gitems.empty();
+            for (int k = 0; k < SBMF_NKIND; ++k) {
+                const bool ran = k < KIND_GRAM ? !sdd.bin_rows[k].empty() : !sdd.gitems.empty();
                 c->timing.kern_ms[sd][k] = ran ? ev_ms(c->kev[sd][k][0], c->kev[sd][k][1]) : 0.0;
             }
         }

@@ -165,7 +165,9 @@ int main(int argc, char** argv) {
         cl.reg("item_offset", "libFM input: item feature id offset; default=0");
         cl.reg("device", "HIP device ordinal; default=0");
         cl.reg("recompute_every", "recompute residuals from scratch every n sweeps; default=1");
-        cl.reg("gram_threshold", "rows with more ratings take the Gram route; default=4096");
+        cl.reg("gram_threshold", "rows with more ratings take the Gram route; default: never (row_kernel 0)");
+        cl.reg("stream_threshold", "rows with more ratings take the streaming kernel; default=512");
+        cl.reg("row_kernel", "0: MFMA Gram-block kernels (default) | 1: per-coordinate wave-reduction kernels");
         if (cl.has("help") || argc == 1) {
             cl.print_help();
             return 0;
@@ -200,6 +202,8 @@ int main(int argc, char** argv) {
         if (cl.has("init_stdev")) cfg.init_stdev = cl.getd("init_stdev", 1.0);
         cfg.recompute_every = (uint32_t)cl.getl("recompute_every", 1);
         cfg.gram_threshold = (uint32_t)cl.getl("gram_threshold", 0);
+        cfg.stream_threshold = (uint32_t)cl.getl("stream_threshold", 0);
+        cfg.row_kernel = (uint32_t)cl.getl("row_kernel", 0);
         cfg.eval_train = 1;
         cfg.eval_test = 1;
 

@@ -111,7 +111,8 @@ class FMLearnSBPMF:
     _QUIRKS = {"final": QUIRKS_FINAL, "sbpmf2": QUIRKS_SBPMF2, "none": QUIRKS_NONE}
 
     def __init__(self, num_factor=20, num_iter=100, seed=1, rng="ref", quirks="final", precision="f64", burnin=0,
-                 device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, **hyper):
+                 device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, row_kernel=0,
+                 stream_threshold=0, **hyper):
         self.cfg = config_default()
         self.cfg.num_factor = num_factor
         self.cfg.num_iter = num_iter
@@ -126,6 +127,8 @@ class FMLearnSBPMF:
         self.cfg.recompute_every = recompute_every
         self.cfg.eval_train = 1 if eval_train else 0
         self.cfg.gram_threshold = gram_threshold
+        self.cfg.row_kernel = row_kernel
+        self.cfg.stream_threshold = stream_threshold
         for k, v in hyper.items():
             setattr(self.cfg, k, v)
         self.ctx = None

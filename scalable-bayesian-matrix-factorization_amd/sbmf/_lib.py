@@ -15,6 +15,9 @@ SBMF_OK, SBMF_E_ARG, SBMF_E_STATE, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_COMM, SBMF_E
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 QUIRKS_FINAL, QUIRKS_SBPMF2, QUIRKS_NONE = 0, 1, 2
 F64, F32 = 0, 1
+NKIND = 11  # SBMF_NKIND
+KIND_NAMES = ['gblock_w4', 'gblock_w16', 'gblock_b2', 'gblock_b4', 'gblock_b8', 'gstream', 'rows_w2', 'rows_w8',
+              'rows_b4', 'rows_b8', 'gram']
 
 
 class Config(C.Structure):
@@ -25,7 +28,8 @@ class Config(C.Structure):
         ("a0", C.c_double), ("b0", C.c_double), ("alpha0", C.c_double), ("beta0", C.c_double),
         ("nu0", C.c_double), ("mu0", C.c_double),
         ("recompute_every", C.c_uint32), ("eval_train", C.c_uint32), ("eval_test", C.c_uint32),
-        ("gram_threshold", C.c_uint32), ("reserved", C.c_uint32 * 8),
+        ("gram_threshold", C.c_uint32), ("row_kernel", C.c_uint32), ("stream_threshold", C.c_uint32),
+        ("reserved", C.c_uint32 * 6),
     ]
 
 
@@ -40,7 +44,8 @@ class Timing(C.Structure):
     _fields_ = [
         ("ms_user_half", C.c_double), ("ms_item_half", C.c_double), ("ms_hyper", C.c_double),
         ("ms_eval", C.c_double), ("ms_comm", C.c_double),
-        ("kern_ms", (C.c_double * 5) * 2), ("kern_bytes", (C.c_uint64 * 5) * 2), ("kern_rows", (C.c_uint32 * 5) * 2),
+        ("kern_ms", (C.c_double * NKIND) * 2), ("kern_bytes", (C.c_uint64 * NKIND) * 2),
+        ("kern_rows", (C.c_uint32 * NKIND) * 2),
         ("bytes_algorithmic", C.c_uint64), ("n_launch", C.c_uint32),
     ]
 

@@ -38,10 +38,12 @@ def test_f64_ref_stream_tracks_reference_100_sweeps(ml100k, seed):
     assert err.max() < 1e-6
 
 
-def test_f64_factors_match_oracle_after_5_sweeps(ml100k):
+@pytest.mark.parametrize("row_kernel", [0, 1])
+def test_f64_factors_match_oracle_after_5_sweeps(ml100k, row_kernel):
+    """row_kernel 0: MFMA Gram-block kernels; 1: per-coordinate wave-reduction kernels."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=20, iters=5, seed=1)
-    L = _run(tr, te, 5, num_factor=20, seed=1)
+    L = _run(tr, te, 5, num_factor=20, seed=1, row_kernel=row_kernel)
     U, V = L.factors()
     h = L.hyper()
     assert np.abs(U - o["U"]).max() < 1e-7
@@ -68,34 +70,50 @@ def test_ragged_edge_cases_track_reference(ragged, name, quirks, seed):
     assert np.abs(L.rmse_trajectory - gold).max() < 1e-6
 
 
-def test_f32_ref_stream_within_north_star_tolerance(ml100k):
+@pytest.mark.parametrize("row_kernel", [0, 1])
+def test_f32_ref_stream_within_north_star_tolerance(ml100k, row_kernel):
     tr, te = ml100k
     gold = golden_rmse("ref_final_ml100k_k20_s1.txt")
-    L = _run(tr, te, 100, num_factor=20, seed=1, precision="f32")
+    L = _run(tr, te, 100, num_factor=20, seed=1, precision="f32", row_kernel=row_kernel)
     err = np.abs(L.rmse_trajectory - gold)
     print("f32 max |dRMSE| = %.3e" % err.max())
     assert err.max() < 1e-3
 
 
+@pytest.mark.parametrize("row_kernel", [0, 1])
 @pytest.mark.parametrize("thr", [16, 64, 300])
-def test_gram_route_matches_oracle(ml100k, thr):
+def test_gram_route_matches_oracle(ml100k, thr, row_kernel):
     """Force rows above `thr` ratings onto the Gram route (G = S^T S, exact
     K-step recurrence) and compare with the sequential oracle."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=20, iters=5, seed=1)
-    L = _run(tr, te, 5, num_factor=20, seed=1, gram_threshold=thr)
+    L = _run(tr, te, 5, num_factor=20, seed=1, gram_threshold=thr, row_kernel=row_kernel)
     U, V = L.factors()
     assert np.abs(U - o["U"]).max() < 1e-7
     assert np.abs(V - o["V"]).max() < 1e-7
     np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("thr", [1, 40, 200])
+@pytest.mark.parametrize("K", [20, 100, 200])
+def test_streaming_kernel_matches_oracle(ml100k, thr, K):
+    """Rows above `thr` ratings through the streaming Gram-block kernel."""
+    tr, te = ml100k
+    o = oracle.run(tr, te, K=K, iters=3, seed=5)
+    L = _run(tr, te, 3, num_factor=K, seed=5, stream_threshold=thr)
+    U, V = L.factors()
+    assert np.abs(U - o["U"]).max() < 1e-7
+    assert np.abs(V - o["V"]).max() < 1e-7
+    np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("row_kernel", [0, 1])
 @pytest.mark.parametrize("K", [8, 50, 100, 130, 200])
-def test_factor_counts_match_oracle(ml100k, K):
-    """K spanning 1..4 register slots of 64 and the padded tails."""
+def test_factor_counts_match_oracle(ml100k, K, row_kernel):
+    """K spanning 1..4 register slots of 64, partial 16-wide k-blocks and padded tails."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=K, iters=3, seed=3)
-    L = _run(tr, te, 3, num_factor=K, seed=3)
+    L = _run(tr, te, 3, num_factor=K, seed=3, row_kernel=row_kernel)
     U, V = L.factors()
     assert np.abs(U - o["U"]).max() < 1e-7
     assert np.abs(V - o["V"]).max() < 1e-7
