@@ -190,6 +190,12 @@ int sbmf_load_triples(const char* path, sbmf_ratings* out);
 int sbmf_load_libfm(const char* path, uint32_t item_offset, sbmf_ratings* out);
 void sbmf_free_ratings(sbmf_ratings* r);
 
+/* --- multi-GPU layout (host only) ---------------------------------------------------------- */
+/* The row partition every rank uses: contiguous row blocks balanced by
+ * ratings (ptr = CSR/CSC offsets [R+1]), boundaries rounded to 256 rows.
+ * bounds: [nranks+1]; rank k owns rows [bounds[k], bounds[k+1]). */
+int sbmf_partition_rows(const uint32_t* ptr, uint32_t R, int nranks, uint64_t* bounds);
+
 /* --- test hooks ---------------------------------------------------------------------------- */
 /* The host glibc-compatible stream (reference mode): n values of rand(),
  * ran_gaussian() and ran_gamma(shape) for seed. */

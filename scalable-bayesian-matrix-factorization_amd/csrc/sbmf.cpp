@@ -126,19 +126,21 @@ static void build_side(uint64_t N, const uint32_t* key, const uint32_t* other, c
 }
 
 // nnz-balanced contiguous partition, boundaries aligned to 256 rows.
-static void partition(Side& s, int nranks, int rank) {
-    const std::vector<uint32_t>& ptr = s.ptr;
-    const uint32_t R = (uint32_t)ptr.size() - 1;
-    s.bounds.assign(nranks + 1, 0);
+static void partition_bounds(const uint32_t* ptr, uint32_t R, int nranks, uint64_t* bounds) {
+    bounds[0] = 0;
     for (int k = 1; k <= nranks; ++k) {
         uint32_t row = R;
         if (k < nranks) {
             const double target = (double)ptr[R] * k / nranks;
-            row = (uint32_t)(std::lower_bound(ptr.begin(), ptr.end(), (uint32_t)std::llround(target)) - ptr.begin());
+            row = (uint32_t)(std::lower_bound(ptr, ptr + R + 1, (uint32_t)std::llround(target)) - ptr);
             row = std::min((row + 128) / 256 * 256, R);
         }
-        s.bounds[k] = std::max<uint64_t>(s.bounds[k - 1], row);
+        bounds[k] = std::max<uint64_t>(bounds[k - 1], row);
     }
+}
+static void partition(Side& s, int nranks, int rank) {
+    s.bounds.assign(nranks + 1, 0);
+    partition_bounds(s.ptr.data(), (uint32_t)s.ptr.size() - 1, nranks, s.bounds.data());
     s.r0 = (uint32_t)s.bounds[rank];
     s.r1 = (uint32_t)s.bounds[rank + 1];
 }
@@ -965,6 +967,14 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
     ctx->nranks = nranks;
     ctx->rank = rank;
     if (nranks > 1) ctx->comm.init(nranks, rank, id);
+    API_END(ctx)
+}
+
+int sbmf_partition_rows(const uint32_t* ptr, uint32_t R, int nranks, uint64_t* bounds) {
+    sbmf_ctx* ctx = nullptr;
+    API_BEGIN
+    if (!ptr || !bounds || nranks < 1) sbmf::fail(SBMF_E_ARG, "bad arguments");
+    sbmf::partition_bounds(ptr, R, nranks, bounds);
     API_END(ctx)
 }
 

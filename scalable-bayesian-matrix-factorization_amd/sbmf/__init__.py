@@ -14,8 +14,8 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import (F32, F64, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_DEVICE,
-                   SBMF_OK)
+from ._lib import (F32, F64, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
+                   SBMF_E_COMM, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_NOMEM, SBMF_E_STATE, SBMF_OK)
 
 __all__ = ["FMLearnSBPMF", "Data", "SBMFError", "load_triples", "load_libfm", "config_default",
            "RNG_REFERENCE", "RNG_PHILOX", "QUIRKS_FINAL", "QUIRKS_SBPMF2", "QUIRKS_NONE", "F64", "F32"]
@@ -250,6 +250,16 @@ def ref_stream(seed, kind, n, shape=1.0):
     """Host reference stream: kind 0 rand(), 1 ran_gaussian(), 2 ran_gamma(shape)."""
     out = np.zeros(n)
     rc = lib.sbmf_ref_stream(seed, kind, shape, n, _ptr(out, C.c_double))
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_last_global_error().decode())
+    return out
+
+
+def partition_rows(ptr, nranks):
+    """Row blocks [bounds[k], bounds[k+1]) of every rank (host-only, as the library partitions)."""
+    ptr = _u32(ptr)
+    out = np.zeros(nranks + 1, dtype=np.uint64)
+    rc = lib.sbmf_partition_rows(_ptr(ptr, C.c_uint32), len(ptr) - 1, nranks, _ptr(out, C.c_uint64))
     if rc != SBMF_OK:
         raise SBMFError(rc, lib.sbmf_last_global_error().decode())
     return out

@@ -1,0 +1,81 @@
+"""The drop-in C ABI: library loads, exports every function include/sbmf.h
+declares, ctypes struct layouts match the C compiler's, defaults match the
+reference constants, and compute entry points fail loudly without a GPU."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import PKG, REPO, gpu_available
+import sbmf
+from sbmf import _lib
+
+HEADER = os.path.join(REPO, "include", "sbmf.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sbmf_[a-z_0-9]+)\s*\(", text)) - {"sbmf_sweep_cb"})
+
+
+def test_every_declared_symbol_is_exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (sbmf_\w+)", out))
+    missing = [f for f in declared_functions() if f not in exported]
+    assert not missing, missing
+    assert set(_lib.SIGNATURES) <= exported
+
+
+def test_ctypes_signatures_cover_header():
+    assert set(declared_functions()) <= set(_lib.SIGNATURES) | {"sbmf_loader_error"}
+
+
+def test_struct_layouts_match_c(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "sbmf.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(sbmf_config), sizeof(sbmf_sweep_info), sizeof(sbmf_timing),
+         sizeof(sbmf_ratings), offsetof(sbmf_config, init_stdev), offsetof(sbmf_config, recompute_every),
+         offsetof(sbmf_timing, bytes_algorithmic));
+  return 0; }''')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    import ctypes as C
+    want = [C.sizeof(_lib.Config), C.sizeof(_lib.SweepInfo), C.sizeof(_lib.Timing), C.sizeof(_lib.Ratings),
+            _lib.Config.init_stdev.offset, _lib.Config.recompute_every.offset, _lib.Timing.bytes_algorithmic.offset]
+    assert got == want
+
+
+def test_defaults_are_the_reference_constants():
+    c = sbmf.config_default()
+    # gibbs_sbpmf_final.cpp:218 (D=20), :256-269 (hyperpriors), :299-300 (100 sweeps, no burn-in)
+    assert (c.num_factor, c.num_iter, c.burnin) == (20, 100, 0)
+    assert (c.a0, c.b0, c.alpha0, c.beta0, c.nu0, c.mu0) == (1, 1, 1, 1, 1, 0)
+    assert c.clamp_hi == 5.0 and c.rng_mode == sbmf.RNG_REFERENCE and c.quirks == sbmf.QUIRKS_FINAL
+    assert c.precision == sbmf.F64
+    assert _lib.lib.sbmf_abi_version() == 1
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure path")
+def test_no_cpu_fallback_without_gpu():
+    L = sbmf.FMLearnSBPMF()
+    with pytest.raises(sbmf.SBMFError) as ei:
+        L.init()
+    assert ei.value.code == sbmf.SBMF_E_DEVICE
+    assert "no HIP device" in str(ei.value)
+
+
+def test_bad_config_rejected_before_device():
+    import ctypes as C
+    cfg = sbmf.config_default()
+    cfg.num_factor = 0
+    ctx = C.c_void_p()
+    assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG
+    cfg.num_factor = 300
+    assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG

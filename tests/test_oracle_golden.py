@@ -1,0 +1,27 @@
+"""The oracle (CPU restatement, oracle/sbpmf_oracle.c) against the reference's
+own outputs: per-sweep test RMSE trajectories produced by the compiled,
+unmodified reference samplers (tests/golden/, oracle/make_golden.py).  Bit-exact:
+every one of the 100 "%.17g" values must be identical."""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden_rmse
+
+
+@pytest.mark.parametrize("variant,data,seed", [("final", "ml100k", 1), ("final", "ml100k", 7),
+                                               ("sbpmf2", "ml100k", 1), ("final", "ragged", 1),
+                                               ("sbpmf2", "ragged", 5)])
+def test_oracle_bitwise_equals_reference(variant, data, seed, ml100k, ragged):
+    tr, te = ml100k if data == "ml100k" else ragged
+    gold = golden_rmse("ref_%s_%s_k20_s%d.txt" % (variant, data, seed))
+    o = oracle.run(tr, te, K=20, iters=100, seed=seed, quirks=variant, want_factors=False)
+    assert np.array_equal(o["rmse"], gold), np.abs(o["rmse"] - gold).max()
+
+
+def test_oracle_dims_follow_reference_rule(ragged):
+    """num_users/items = max id + 1 over train AND test (gibbs_sbpmf_final.cpp:146-148)."""
+    tr, te = ragged
+    o = oracle.run(tr, te, K=4, iters=1, seed=1, want_factors=False)
+    assert o["num_users"] == max(tr[0].max(), te[0].max()) + 1
+    assert o["num_items"] == max(tr[1].max(), te[1].max()) + 1
