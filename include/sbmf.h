@@ -82,8 +82,11 @@ typedef struct sbmf_config {
     uint32_t row_kernel;      /* 0: MFMA Gram-block kernels (default); 1: per-coordinate
                                  wave-reduction kernels + Gram route                             */
     uint32_t stream_threshold;/* row_kernel 0: rows with more ratings use the streaming
-                                 Gram-block kernel (0 = default 512)                             */
-    uint32_t reserved[6];
+                                 Gram-block kernel (0 = default: 256 f64 / 512 f32)              */
+    uint32_t split_chunk;     /* rows longer than this are split over several co-resident
+                                 workgroups (largest first, as residency allows; 0 = 4096;
+                                 0xffffffff = never split)                                       */
+    uint32_t reserved[5];
 } sbmf_config;
 
 /* Per-sweep report passed to the run callback. */
@@ -148,9 +151,10 @@ int sbmf_get_dims(sbmf_ctx* ctx, uint32_t* num_users, uint32_t* num_items, uint6
 /* --- measurement --------------------------------------------------------------------------- */
 /* Device times of the last sweep (HIP events on the context's stream).
  * kern_*[side][kind]: side 0 = user half, 1 = item half; kind =
- *   0..4  MFMA Gram-block row kernels (1 wave/row <=16 and <=64 ratings,
- *         2 / 4 / 8 waves/row <=128 / 256 / 512 ratings),
- *   5     streaming MFMA Gram-block kernel (one 8-wave workgroup per row, any length),
+ *   0..4  MFMA Gram-block row kernels: 1 wave/row (two sizes), 2 / 4 / 8
+ *         waves/row; up to 8/32/64/128/256 ratings (f64), 16/64/128/256/512 (f32),
+ *   5     streaming MFMA Gram-block kernel (one 8-wave workgroup per row or per
+ *         chunk of a row split over co-resident workgroups),
  *   6..9  per-coordinate wave-reduction row kernels (1 wave/row <=128 and
  *         <=512, 4 / 8 waves/row <=2048 / 4096),
  *   10    Gram route (all its launches).  kern_bytes is the

@@ -51,16 +51,53 @@ struct GramRow {
 enum RowKernelKind { RK_W2 = 0, RK_W8 = 1, RK_B4 = 2, RK_B8 = 3, RK_NUM = 4 };
 static const uint32_t RK_MAXDEG[RK_NUM] = {128, 512, 2048, 4096};
 
-// Gram-block (MFMA) row kernels: max ratings per row for each kind.
+// Gram-block (MFMA) row kernels.  Max ratings per row for each kind: f64
+// holds 8 vectors (32 ratings) per wave, f32 16 (64 ratings).
 enum GblockKind { GK_W4 = 0, GK_W16 = 1, GK_B2 = 2, GK_B4 = 3, GK_B8 = 4, GK_NUM = 5 };
-static const uint32_t GK_MAXDEG[GK_NUM] = {16, 64, 128, 256, 512};
+inline uint32_t gk_maxdeg(int kind, bool f64) {
+    static const uint32_t waves4[GK_NUM] = {1, 4, 8, 16, 32};  // (waves x vectors) / V*4 ratings
+    const uint32_t per_wave = f64 ? 32 : 64;
+    return kind == GK_W4 ? per_wave / 4 : per_wave * waves4[kind] / 4;
+}
 
 template <typename T>
 hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
 
-// Streaming Gram-block kernel: one 512-thread workgroup per row, any length.
+// Streaming Gram-block kernel: one 512-thread workgroup per task (a whole
+// row, or one chunk of a row split over several co-resident workgroups).
+struct SplitTask {
+    uint32_t row;    // global row id
+    uint32_t beg;    // first rating of the chunk (absolute index)
+    uint32_t len;    // ratings in the chunk
+    uint32_t nch;    // chunks of the row (1 = whole row, no exchange)
+    uint32_t chunk;  // chunk index within the row
+    uint32_t slab0;  // split rows: first chunk slab of the row (also its new-own slot)
+    uint32_t cnt0;   // split rows: first block counter of the row
+    uint32_t pad;
+};
+struct SplitRow {
+    uint32_t row, slab0, nch, pad;
+};
+struct SplitSync {
+    double* slabs;       // [nchunk_total][nblk][16*16+16]
+    uint32_t* counters;  // [nsplit_rows * nblk], zeroed per launch
+    uint32_t ncounters;
+    uint32_t nblk;       // ceil(K/16)
+    double* chunk_sq;    // [nchunk_total]
+    double* chunk_tr;    // [nchunk_total]
+    void* newown;        // [nsplit_rows][Kp] (T)
+    uint32_t* timeout;   // set to 1 if a spin gave up
+};
 template <typename T>
-hipError_t launch_gstream(const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
+hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, const HalfArgs<T>& a, const SplitSync& sy,
+                          hipStream_t st);
+// Co-resident k_gstream workgroups per CU (occupancy API).
+template <typename T>
+int gstream_blocks_per_cu();
+// Rows split over several workgroups (cooperative launch; grid <= residency).
+template <typename T>
+hipError_t launch_gsplit(const SplitTask* tasks, uint32_t ntask, const SplitRow* srows, uint32_t nsrow,
+                         const HalfArgs<T>& a, const SplitSync& sy, hipStream_t st);
 
 template <typename T>
 hipError_t launch_rows(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);

@@ -105,6 +105,9 @@ struct Side {
     std::vector<uint32_t> bin_rows[SBMF_NKIND - 1];  // kinds: GK_* (0..4), KIND_STREAM (5), KIND_RK0 + RK_* (6..9)
     std::vector<GramItem> gitems;
     std::vector<GramRow> grows;
+    std::vector<SplitTask> stasks;   // streaming kernel: whole rows (nch = 1)
+    std::vector<SplitTask> xtasks;   // streaming kernel: chunks of split rows
+    std::vector<SplitRow> xrows;
 };
 
 static void build_side(uint64_t N, const uint32_t* key, const uint32_t* other, const double* rat, uint32_t R,
@@ -149,7 +152,7 @@ static const int KIND_STREAM = GK_NUM;       // 5
 static const int KIND_RK0 = GK_NUM + 1;       // 6..9
 static const int KIND_GRAM = SBMF_NKIND - 1;  // 10
 
-static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr) {
+static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr, bool f64) {
     for (auto& b : s.bin_rows) b.clear();
     s.gitems.clear();
     s.grows.clear();
@@ -177,7 +180,7 @@ static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stre
         }
         if (row_kernel == 0) {
             int kind = GK_W4;
-            while (d > GK_MAXDEG[kind]) ++kind;
+            while (d > gk_maxdeg(kind, f64)) ++kind;
             s.bin_rows[kind].push_back(r);
             continue;
         }
@@ -226,6 +229,8 @@ struct sbmf_ctx {
     DBuf d_bins_u[SBMF_NKIND - 1], d_bins_v[SBMF_NKIND - 1];
     DBuf d_gitems_u, d_grows_u, d_gitems_v, d_grows_v, d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
     DBuf d_colpart, d_res, d_scratch;
+    DBuf d_stasks_u, d_stasks_v, d_xtasks_u, d_xtasks_v, d_xrows_u, d_xrows_v;
+    DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
     std::vector<double> h_res;
     double* h_pinned = nullptr;  // pinned staging for z streams
@@ -271,6 +276,7 @@ static void ensure_pinned(sbmf_ctx* c, size_t bytes) {
 }
 
 static void fill_kernel_bytes(sbmf_ctx* c);
+static void build_stream_tasks(Side& s, uint32_t chunk, uint32_t gres, uint32_t nblk);
 
 // ------------------------------------------------------------------ prepare
 template <typename T>
@@ -308,15 +314,26 @@ static void prepare_T(sbmf_ctx* c) {
     // row_kernel 0: Gram-block kernels for rows <= stream threshold, the
     // streaming kernel above it, the Gram route only if a threshold is set.
     // row_kernel 1: per-coordinate kernels up to 4096 ratings, Gram route above.
-    const uint32_t sthr = std::min<uint32_t>(cf.stream_threshold ? cf.stream_threshold : GK_MAXDEG[GK_NUM - 1],
-                                             GK_MAXDEG[GK_NUM - 1]);
+    const bool f64 = sizeof(T) == 8;
+    const uint32_t gkmax = gk_maxdeg(GK_NUM - 1, f64);
+    const uint32_t sthr = std::min<uint32_t>(cf.stream_threshold ? cf.stream_threshold : gkmax, gkmax);
     uint32_t thr;
     if (cf.row_kernel == 0)
         thr = cf.gram_threshold ? cf.gram_threshold : 0xffffffffu;
     else
         thr = cf.gram_threshold ? std::min(cf.gram_threshold, RK_MAXDEG[RK_NUM - 1]) : RK_MAXDEG[RK_NUM - 1];
-    build_bins(c->users, thr, (int)cf.row_kernel, sthr);
-    build_bins(c->items, thr, (int)cf.row_kernel, sthr);
+    build_bins(c->users, thr, (int)cf.row_kernel, sthr, f64);
+    build_bins(c->items, thr, (int)cf.row_kernel, sthr, f64);
+    const uint32_t nblk = (c->K + 15) / 16;
+    {
+        int dev_cus = 0;
+        HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, cf.device));
+        const int per_cu = std::max(1, std::min(2, gstream_blocks_per_cu<T>()));
+        const uint32_t gres = (uint32_t)(dev_cus * per_cu);
+        const uint32_t chunk = cf.split_chunk ? cf.split_chunk : 4096;
+        build_stream_tasks(c->users, chunk, gres, nblk);
+        build_stream_tasks(c->items, chunk, gres, nblk);
+    }
     {  // test split in 256-aligned blocks
         const uint64_t T_ = c->su.size(), nb = (T_ + 255) / 256;
         c->tbounds.assign(c->nranks + 1, 0);
@@ -341,6 +358,24 @@ static void prepare_T(sbmf_ctx* c) {
     for (int k = 0; k < SBMF_NKIND - 1; ++k) {
         upload(c->d_bins_u[k], c->users.bin_rows[k], st);
         upload(c->d_bins_v[k], c->items.bin_rows[k], st);
+    }
+    upload(c->d_stasks_u, c->users.stasks, st);
+    upload(c->d_stasks_v, c->items.stasks, st);
+    upload(c->d_xtasks_u, c->users.xtasks, st);
+    upload(c->d_xtasks_v, c->items.xtasks, st);
+    upload(c->d_xrows_u, c->users.xrows, st);
+    upload(c->d_xrows_v, c->items.xrows, st);
+    {
+        const size_t nx = std::max(c->users.xtasks.size(), c->items.xtasks.size());
+        const size_t nr = std::max(c->users.xrows.size(), c->items.xrows.size());
+        c->d_xslabs.alloc(std::max<size_t>(nx, 1) * nblk * (16 * 16 + 16) * sizeof(double));
+        c->d_xcnt.alloc(std::max<size_t>(nr, 1) * nblk * sizeof(uint32_t));
+        c->d_xchunk_sq.alloc(std::max<size_t>(nx, 1) * sizeof(double));
+        c->d_xchunk_tr.alloc(std::max<size_t>(nx, 1) * sizeof(double));
+        HIPCHK(hipMemsetAsync(c->d_xchunk_tr.p, 0, c->d_xchunk_tr.bytes, st));
+        c->d_xnewown.alloc(std::max<size_t>(nx, 1) * c->Kp * sizeof(T));
+        c->d_xtimeout.alloc(sizeof(uint32_t));
+        HIPCHK(hipMemsetAsync(c->d_xtimeout.p, 0, sizeof(uint32_t), st));
     }
     upload(c->d_gitems_u, c->users.gitems, st);
     upload(c->d_grows_u, c->users.grows, st);
@@ -416,6 +451,34 @@ static void prepare_T(sbmf_ctx* c) {
     c->collected = 0;
     fill_kernel_bytes(c);
     c->prepared = true;
+}
+
+// Streaming-kernel tasks.  Largest rows first: a row longer than `chunk` is
+// split into ceil(n/chunk) equal chunks as long as all split chunks of the
+// half-sweep fit the co-resident grid (gres); the rest run whole.
+static void build_stream_tasks(Side& s, uint32_t chunk, uint32_t gres, uint32_t nblk) {
+    s.stasks.clear();
+    s.xtasks.clear();
+    s.xrows.clear();
+    const std::vector<uint32_t>& rows = s.bin_rows[KIND_STREAM];  // degree-descending
+    uint32_t used = 0;
+    for (uint32_t r : rows) {
+        const uint32_t n = s.ptr[r + 1] - s.ptr[r];
+        const uint32_t nch = chunk == 0xffffffffu ? 1 : (n + chunk - 1) / chunk;
+        if (nch > 1 && used + nch <= gres) {
+            const uint32_t slab0 = (uint32_t)s.xtasks.size();
+            const uint32_t cnt0 = (uint32_t)s.xrows.size() * nblk;
+            const uint32_t per = (n + nch - 1) / nch;
+            for (uint32_t c = 0; c < nch; ++c) {
+                const uint32_t b = c * per, e = std::min(n, b + per);
+                s.xtasks.push_back(SplitTask{r, s.ptr[r] + b, e - b, nch, c, slab0, cnt0, 0});
+            }
+            s.xrows.push_back(SplitRow{r, slab0, nch, 0});
+            used += nch;
+        } else {
+            s.stasks.push_back(SplitTask{r, s.ptr[r], n, 1, 0, 0, 0, 0});
+        }
+    }
 }
 
 // ------------------------------------------------------------------ one sweep
@@ -518,8 +581,23 @@ static void run_half(sbmf_ctx* c, bool users) {
         HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
         if (k < GK_NUM)
             HIPCHK(launch_gblock<T>(k, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
-        else if (k == KIND_STREAM)
-            HIPCHK(launch_gstream<T>(bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
+        else if (k == KIND_STREAM) {
+            SplitSync sy{};
+            sy.slabs = c->d_xslabs.as<double>();
+            sy.counters = c->d_xcnt.as<uint32_t>();
+            sy.nblk = (c->K + 15) / 16;
+            sy.ncounters = (uint32_t)s.xrows.size() * sy.nblk;
+            sy.chunk_sq = c->d_xchunk_sq.as<double>();
+            sy.chunk_tr = c->d_xchunk_tr.as<double>();
+            sy.newown = c->d_xnewown.p;
+            sy.timeout = c->d_xtimeout.as<uint32_t>();
+            if (!s.xtasks.empty())
+                HIPCHK(launch_gsplit<T>((users ? c->d_xtasks_u : c->d_xtasks_v).as<SplitTask>(), (uint32_t)s.xtasks.size(),
+                                        (users ? c->d_xrows_u : c->d_xrows_v).as<SplitRow>(), (uint32_t)s.xrows.size(),
+                                        a, sy, st));
+            HIPCHK(launch_gstream<T>((users ? c->d_stasks_u : c->d_stasks_v).as<SplitTask>(),
+                                     (uint32_t)s.stasks.size(), a, sy, st));
+        }
         else
             HIPCHK(launch_rows<T>(k - KIND_RK0, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
         HIPCHK(hipEventRecord(c->kev[sd][k][1], st));
@@ -770,8 +848,10 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     if (cfg->quirks < 0 || cfg->quirks > 2) sbmf::fail(SBMF_E_ARG, "bad quirks");
     if (cfg->precision != SBMF_F64 && cfg->precision != SBMF_F32) sbmf::fail(SBMF_E_ARG, "bad precision");
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-        sbmf::fail(SBMF_E_DEVICE, "no HIP device available (this library has no CPU fallback)");
+    const hipError_t derr = hipGetDeviceCount(&ndev);
+    if (derr != hipSuccess || ndev <= 0)
+        sbmf::fail(SBMF_E_DEVICE, "no HIP device available (%s; this library has no CPU fallback)",
+                   derr != hipSuccess ? hipGetErrorString(derr) : "0 devices");
     if (cfg->device < 0 || cfg->device >= ndev) sbmf::fail(SBMF_E_DEVICE, "device %d out of range (%d)", cfg->device, ndev);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, cfg->device));

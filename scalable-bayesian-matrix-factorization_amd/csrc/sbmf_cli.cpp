@@ -167,6 +167,7 @@ int main(int argc, char** argv) {
         cl.reg("recompute_every", "recompute residuals from scratch every n sweeps; default=1");
         cl.reg("gram_threshold", "rows with more ratings take the Gram route; default: never (row_kernel 0)");
         cl.reg("stream_threshold", "rows with more ratings take the streaming kernel; default=512");
+        cl.reg("split_chunk", "rows longer than this are split over several workgroups; default=4096");
         cl.reg("row_kernel", "0: MFMA Gram-block kernels (default) | 1: per-coordinate wave-reduction kernels");
         if (cl.has("help") || argc == 1) {
             cl.print_help();
@@ -204,6 +205,7 @@ int main(int argc, char** argv) {
         cfg.gram_threshold = (uint32_t)cl.getl("gram_threshold", 0);
         cfg.stream_threshold = (uint32_t)cl.getl("stream_threshold", 0);
         cfg.row_kernel = (uint32_t)cl.getl("row_kernel", 0);
+        cfg.split_chunk = (uint32_t)cl.getl("split_chunk", 0);
         cfg.eval_train = 1;
         cfg.eval_test = 1;
 

@@ -8,6 +8,12 @@ The reference's operator API for this path is libFM's ``fm_learn``
 meanings; the work runs in ``libsbmf.so`` (HIP kernels for gfx950).  Errors
 raise ``SBMFError`` (the reference throws ``std::string``).  There is no CPU
 compute path: without a GPU, ``init()`` raises ``SBMFError`` (SBMF_E_DEVICE).
+
+Runtime note: libsbmf binds ROCm's ``libamdhip64.so.7``.  PyTorch wheels ship
+their own copy under the same soname; if torch is imported first, libsbmf
+shares torch's runtime (fine).  If sbmf is imported first, create the learner
+(``init()``) before the first ``torch.cuda`` call -- a second HSA runtime
+initialised after the first one sees no device.
 """
 import ctypes as C
 
@@ -112,7 +118,7 @@ class FMLearnSBPMF:
 
     def __init__(self, num_factor=20, num_iter=100, seed=1, rng="ref", quirks="final", precision="f64", burnin=0,
                  device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, row_kernel=0,
-                 stream_threshold=0, **hyper):
+                 stream_threshold=0, split_chunk=0, **hyper):
         self.cfg = config_default()
         self.cfg.num_factor = num_factor
         self.cfg.num_iter = num_iter
@@ -129,6 +135,7 @@ class FMLearnSBPMF:
         self.cfg.gram_threshold = gram_threshold
         self.cfg.row_kernel = row_kernel
         self.cfg.stream_threshold = stream_threshold
+        self.cfg.split_chunk = split_chunk
         for k, v in hyper.items():
             setattr(self.cfg, k, v)
         self.ctx = None

@@ -29,7 +29,7 @@ class Config(C.Structure):
         ("nu0", C.c_double), ("mu0", C.c_double),
         ("recompute_every", C.c_uint32), ("eval_train", C.c_uint32), ("eval_test", C.c_uint32),
         ("gram_threshold", C.c_uint32), ("row_kernel", C.c_uint32), ("stream_threshold", C.c_uint32),
-        ("reserved", C.c_uint32 * 6),
+        ("split_chunk", C.c_uint32), ("reserved", C.c_uint32 * 5),
     ]
 
 

@@ -62,8 +62,14 @@ def golden_rmse(name):
 
 
 def gpu_available():
+    """Device probe through the HIP runtime libsbmf is bound to (not torch's:
+    initialising torch's bundled runtime first leaves a second HSA runtime in
+    the process that then sees no device)."""
+    import ctypes
+    from sbmf import _lib  # noqa: F401  (binds libamdhip64.so.7 first)
     try:
-        import torch
-        return torch.cuda.is_available()
-    except Exception:
+        hip = ctypes.CDLL("libamdhip64.so.7")
+    except OSError:
         return False
+    n = ctypes.c_int(0)
+    return hip.hipGetDeviceCount(ctypes.byref(n)) == 0 and n.value > 0

@@ -107,6 +107,28 @@ def test_streaming_kernel_matches_oracle(ml100k, thr, K):
     np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("chunk", [16, 64, 150])
+@pytest.mark.parametrize("K", [20, 100])
+def test_split_rows_match_oracle(ml100k, chunk, K):
+    """Long rows split over several co-resident workgroups that exchange their
+    per-block (G, c) partials through global memory (cooperative launch)."""
+    tr, te = ml100k
+    o = oracle.run(tr, te, K=K, iters=3, seed=9)
+    L = _run(tr, te, 3, num_factor=K, seed=9, stream_threshold=40, split_chunk=chunk)
+    U, V = L.factors()
+    assert np.abs(U - o["U"]).max() < 1e-7
+    assert np.abs(V - o["V"]).max() < 1e-7
+    np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
+
+
+def test_split_rows_deterministic(ml100k):
+    tr, te = ml100k
+    a = _run(tr, te, 3, num_factor=32, seed=2, rng="philox", stream_threshold=40, split_chunk=50)
+    b = _run(tr, te, 3, num_factor=32, seed=2, rng="philox", stream_threshold=40, split_chunk=50)
+    for x, y in zip(a.factors(), b.factors()):
+        assert np.array_equal(x, y)
+
+
 @pytest.mark.parametrize("row_kernel", [0, 1])
 @pytest.mark.parametrize("K", [8, 50, 100, 130, 200])
 def test_factor_counts_match_oracle(ml100k, K, row_kernel):
