@@ -1,0 +1,32 @@
+#!/bin/bash
+# One measurement pass on a 1-GPU MI355X box (run from the repo root via gpurun):
+#   bash profiles/collect.sh <tag> bench   default bench line (f64 + f32 + CPU baseline + time-to-RMSE)
+#   bash profiles/collect.sh <tag> trace   rocprofv3 --kernel-trace --stats of a bench run
+#   bash profiles/collect.sh <tag> fetch   --pmc FETCH_SIZE      (each counter pass on its own,
+#   bash profiles/collect.sh <tag> write   --pmc WRITE_SIZE       never combined with other
+#   bash profiles/collect.sh <tag> l2      --pmc TCC_HIT/MISS     tracing domains)
+# Outputs land in gpurun_out/<tag>_<pass>*.  Under rocprofv3 (ROCm 7.2) the
+# HIP runtime's exit-time teardown segfaults after the profiler has written
+# its files, so each rocprofv3 pass is the last GPU step of its gpurun call.
+set -euo pipefail
+TAG=${1:-r01}
+PASS=${2:-bench}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p "$O"
+cd /tmp && export TMPDIR=/tmp
+BENCH="$R/bench.py"
+SHORT="--no-cpu --no-f32 --no-ttr"
+case "$PASS" in
+  bench) timeout -k 10 500 python3 "$BENCH" > "$O/${TAG}_bench.json" 2> "$O/${TAG}_bench.err" ;;
+  trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${TAG}_trace" -o "$TAG" -- \
+           python3 "$BENCH" --steps 10 --warmup 2 $SHORT > "$O/${TAG}_trace.log" 2>&1 ;;
+  fetch) timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d "$O/${TAG}_pmc_fetch" -o "$TAG" -- \
+           python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_fetch.log" 2>&1 ;;
+  write) timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d "$O/${TAG}_pmc_write" -o "$TAG" -- \
+           python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_write.log" 2>&1 ;;
+  l2)    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc TCC_HIT_sum TCC_MISS_sum -d "$O/${TAG}_pmc_l2" -o "$TAG" -- \
+           python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_l2.log" 2>&1 ;;
+  *) echo "unknown pass $PASS" >&2; exit 2 ;;
+esac
+echo "collect.sh $TAG $PASS done"

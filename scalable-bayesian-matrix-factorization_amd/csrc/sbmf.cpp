@@ -94,6 +94,8 @@ static void upload(DBuf& d, const std::vector<U>& h, hipStream_t st) {
 
 // ------------------------------------------------------------------ host layout
 // One orientation: users (CSR by user, partner = item) or items (CSC).
+static const int NBIN = 10;  // row bins (kinds 0..9)
+
 struct Side {
     uint32_t R = 0;                     // rows
     std::vector<uint32_t> ptr;          // [R+1]
@@ -102,7 +104,7 @@ struct Side {
     std::vector<double> r;              // [N] ratings
     uint32_t r0 = 0, r1 = 0;            // owned row range (multi-GPU)
     std::vector<uint64_t> bounds;       // [nranks+1] row ranges of every rank
-    std::vector<uint32_t> bin_rows[SBMF_NKIND - 1];  // kinds: GK_* (0..4), KIND_STREAM (5), KIND_RK0 + RK_* (6..9)
+    std::vector<uint32_t> bin_rows[NBIN];  // kinds: GK_* (0..4), KIND_STREAM (5), KIND_RK0 + RK_* (6..9)
     std::vector<GramItem> gitems;
     std::vector<GramRow> grows;
     std::vector<SplitTask> stasks;   // streaming kernel: whole rows (nch = 1)
@@ -148,9 +150,10 @@ static void partition(Side& s, int nranks, int rank) {
     s.r1 = (uint32_t)s.bounds[rank + 1];
 }
 
-static const int KIND_STREAM = GK_NUM;       // 5
-static const int KIND_RK0 = GK_NUM + 1;       // 6..9
-static const int KIND_GRAM = SBMF_NKIND - 1;  // 10
+static const int KIND_STREAM = GK_NUM;  // 5: streaming kernel, whole rows (row bin: every streaming row)
+static const int KIND_RK0 = GK_NUM + 1;  // 6..9
+static const int KIND_GRAM = 10;         // Gram route
+static const int KIND_SPLIT = 11;        // streaming kernel, rows split over workgroups (timing only)
 
 static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr, bool f64) {
     for (auto& b : s.bin_rows) b.clear();
@@ -226,7 +229,7 @@ struct sbmf_ctx {
     DBuf d_uptr, d_upart, d_uperm, d_ur, d_vptr, d_vpart, d_vperm, d_vr;
     DBuf d_U, d_V, d_Eu, d_Ev, d_zU, d_zV, d_hyper;
     DBuf d_rowsq_u, d_rowtr_u, d_rowsq_v, d_rowtr_v;
-    DBuf d_bins_u[SBMF_NKIND - 1], d_bins_v[SBMF_NKIND - 1];
+    DBuf d_bins_u[NBIN], d_bins_v[NBIN];
     DBuf d_gitems_u, d_grows_u, d_gitems_v, d_grows_v, d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
     DBuf d_colpart, d_res, d_scratch;
     DBuf d_stasks_u, d_stasks_v, d_xtasks_u, d_xtasks_v, d_xrows_u, d_xrows_v;
@@ -355,7 +358,7 @@ static void prepare_T(sbmf_ctx* c) {
     upload(c->d_vpart, c->items.part, st);
     upload(c->d_vperm, c->items.perm, st);
     upload(c->d_vr, to_T<T>(c->items.r), st);
-    for (int k = 0; k < SBMF_NKIND - 1; ++k) {
+    for (int k = 0; k < NBIN; ++k) {
         upload(c->d_bins_u[k], c->users.bin_rows[k], st);
         upload(c->d_bins_v[k], c->items.bin_rows[k], st);
     }
@@ -576,9 +579,9 @@ static void run_half(sbmf_ctx* c, bool users) {
         HIPCHK(hipEventRecord(c->kev[sd][KIND_GRAM][1], st));
         c->timing.n_launch += 4;
     }
-    for (int k = SBMF_NKIND - 2; k >= 0; --k) {
+    for (int k = NBIN - 1; k >= 0; --k) {
         if (s.bin_rows[k].empty()) continue;
-        HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
+        if (k != KIND_STREAM) HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
         if (k < GK_NUM)
             HIPCHK(launch_gblock<T>(k, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
         else if (k == KIND_STREAM) {
@@ -591,10 +594,15 @@ static void run_half(sbmf_ctx* c, bool users) {
             sy.chunk_tr = c->d_xchunk_tr.as<double>();
             sy.newown = c->d_xnewown.p;
             sy.timeout = c->d_xtimeout.as<uint32_t>();
-            if (!s.xtasks.empty())
+            if (!s.xtasks.empty()) {
+                HIPCHK(hipEventRecord(c->kev[sd][KIND_SPLIT][0], st));
                 HIPCHK(launch_gsplit<T>((users ? c->d_xtasks_u : c->d_xtasks_v).as<SplitTask>(), (uint32_t)s.xtasks.size(),
                                         (users ? c->d_xrows_u : c->d_xrows_v).as<SplitRow>(), (uint32_t)s.xrows.size(),
                                         a, sy, st));
+                HIPCHK(hipEventRecord(c->kev[sd][KIND_SPLIT][1], st));
+                c->timing.n_launch++;
+            }
+            HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
             HIPCHK(launch_gstream<T>((users ? c->d_stasks_u : c->d_stasks_v).as<SplitTask>(),
                                      (uint32_t)s.stasks.size(), a, sy, st));
         }
@@ -615,10 +623,18 @@ static void fill_kernel_bytes(sbmf_ctx* c) {
     const uint64_t tsz = tsize(c);
     for (int sd = 0; sd < 2; ++sd) {
         const Side& s = sd == 0 ? c->users : c->items;
-        for (int k = 0; k < SBMF_NKIND - 1; ++k) {
+        for (int k = 0; k < NBIN; ++k) {
             c->timing.kern_bytes[sd][k] = alg_bytes(s, s.bin_rows[k], c->K, tsz);
             c->timing.kern_rows[sd][k] = (uint32_t)s.bin_rows[k].size();
         }
+        // streaming rows: whole rows (kind 5) and split rows (kind 11) are separate launches
+        std::vector<uint32_t> xr, whole;
+        for (const SplitRow& x : s.xrows) xr.push_back(x.row);
+        for (const SplitTask& t : s.stasks) whole.push_back(t.row);
+        c->timing.kern_bytes[sd][KIND_STREAM] = alg_bytes(s, whole, c->K, tsz);
+        c->timing.kern_rows[sd][KIND_STREAM] = (uint32_t)whole.size();
+        c->timing.kern_bytes[sd][KIND_SPLIT] = alg_bytes(s, xr, c->K, tsz);
+        c->timing.kern_rows[sd][KIND_SPLIT] = (uint32_t)xr.size();
         std::vector<uint32_t> gr;
         for (const GramRow& g : s.grows) gr.push_back(g.row);
         c->timing.kern_bytes[sd][KIND_GRAM] = alg_bytes(s, gr, c->K, tsz);
@@ -742,7 +758,12 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         if (cf.eval_train) HIPCHK(launch_sum(c->d_rowtr_v.as<double>(), c->J, d_res + RES_TRSQ, scratch, st));
         HIPCHK(hipEventRecord(c->ev[6], st));
         HIPCHK(hipMemcpyAsync(c->h_res.data(), d_res, 8 * sizeof(double), hipMemcpyDeviceToHost, st));
+        uint32_t split_timeout = 0;
+        if (c->d_xtimeout.p)
+            HIPCHK(hipMemcpyAsync(&split_timeout, c->d_xtimeout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        if (split_timeout)  // a bounded spin in k_gstream gave up: the sweep's results are not valid
+            fail(SBMF_E_STATE, "sweep %u: split-row hand-off timed out (workgroups not co-resident)", c->sweep);
 
         sbmf_sweep_info info{};
         info.sweep = c->sweep;
@@ -759,7 +780,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         for (int sd = 0; sd < 2; ++sd) {
             const Side& sdd = sd == 0 ? c->users : c->items;
             for (int k = 0; k < SBMF_NKIND; ++k) {
-                const bool ran = k < KIND_GRAM ? !sdd.bin_rows[k].empty() : !sdd.gitems.empty();
+                const bool ran = k == KIND_GRAM    ? !sdd.gitems.empty()
+                                 : k == KIND_SPLIT ? !sdd.xrows.empty()
+                                 : k == KIND_STREAM ? !sdd.stasks.empty()
+                                                    : !sdd.bin_rows[k].empty();
                 c->timing.kern_ms[sd][k] = ran ? ev_ms(c->kev[sd][k][0], c->kev[sd][k][1]) : 0.0;
             }
         }

@@ -15,9 +15,9 @@ SBMF_OK, SBMF_E_ARG, SBMF_E_STATE, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_COMM, SBMF_E
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 QUIRKS_FINAL, QUIRKS_SBPMF2, QUIRKS_NONE = 0, 1, 2
 F64, F32 = 0, 1
-NKIND = 11  # SBMF_NKIND
+NKIND = 12  # SBMF_NKIND
 KIND_NAMES = ['gblock_w4', 'gblock_w16', 'gblock_b2', 'gblock_b4', 'gblock_b8', 'gstream', 'rows_w2', 'rows_w8',
-              'rows_b4', 'rows_b8', 'gram']
+              'rows_b4', 'rows_b8', 'gram', 'gsplit']
 
 
 class Config(C.Structure):
@@ -106,3 +106,15 @@ def load(path=LIB_PATH):
 
 
 lib = load()
+
+
+def unload():
+    """dlclose libsbmf so its HIP module destructor (fat-binary unregistration)
+    runs now, while the HIP runtime is fully alive, instead of from exit()
+    handlers after tools such as rocprofv3 have finalised (which segfaults in
+    ROCm 7.2).  Every learner must be closed first; the module is unusable after."""
+    global lib
+    import _ctypes
+    if lib is not None:
+        _ctypes.dlclose(lib._handle)
+        lib = None
