@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--gram-threshold", type=int, default=0)
     ap.add_argument("--row-kernel", type=int, default=0)
     ap.add_argument("--no-ttr", action="store_true", help="skip the time-to-RMSE runs")
+    ap.add_argument("--tune", type=int, default=0, help="kernel-variant bits (sbmf_config.tune)")
+    ap.add_argument("--split-chunk", type=int, default=0, help="streaming task size (0 = LDS capacity)")
     return ap.parse_args()
 
 
@@ -97,7 +99,7 @@ def make_learner(args, world, rank, local, precision, uid):
     from sbmf import Data, FMLearnSBPMF
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=precision, device=local,
                      recompute_every=0, eval_train=False, gram_threshold=args.gram_threshold,
-                     row_kernel=args.row_kernel)
+                     row_kernel=args.row_kernel, tune=args.tune, split_chunk=args.split_chunk)
     L.init(comm=(world, rank, uid) if world > 1 else None)
     return L, Data
 
@@ -143,7 +145,8 @@ def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85
     # burn-in 50 (paper protocol): average over the collected sweeps only
     # (quirks "none"), since the reference's divisor counts burn-in sweeps too.
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=args.precision, device=local,
-                     recompute_every=0, burnin=burnin, row_kernel=args.row_kernel,
+                     recompute_every=0, burnin=burnin, row_kernel=args.row_kernel, tune=args.tune,
+                     split_chunk=args.split_chunk,
                      quirks="final" if burnin == 0 else "none")
     L.init(comm=(world, rank, uid) if world > 1 else None)
     L.set_data(Data(*train), Data(*test))

@@ -31,7 +31,7 @@ extern "C" {
 #endif
 
 #define SBMF_ABI_VERSION 1
-#define SBMF_NKIND 12 /* kernel kinds reported by sbmf_get_timing */
+#define SBMF_NKIND 11 /* kernel kinds reported by sbmf_get_timing */
 
 enum sbmf_status {
     SBMF_OK = 0,
@@ -83,10 +83,13 @@ typedef struct sbmf_config {
                                  wave-reduction kernels + Gram route                             */
     uint32_t stream_threshold;/* row_kernel 0: rows with more ratings use the streaming
                                  Gram-block kernel (0 = default: 256 f64 / 512 f32)              */
-    uint32_t split_chunk;     /* rows longer than this are split over several co-resident
-                                 workgroups (largest first, as residency allows; 0 = 4096;
-                                 0xffffffff = never split)                                       */
-    uint32_t reserved[5];
+    uint32_t split_chunk;     /* streaming-kernel task size: rows longer than this are split
+                                 into chunks on co-resident workgroups (0 = the LDS capacity,
+                                 1792 f64 / 3584 f32; larger values are capped to it)            */
+    uint32_t tune;            /* kernel-variant bits for experiments (0 = tuned defaults):
+                                 bit 0 = residual update of the Gram-block kernels on MFMA,
+                                 bit 1 = streaming kernel in 4-wave workgroups (4 per CU)        */
+    uint32_t reserved[4];
 } sbmf_config;
 
 /* Per-sweep report passed to the run callback. */
@@ -153,12 +156,13 @@ int sbmf_get_dims(sbmf_ctx* ctx, uint32_t* num_users, uint32_t* num_items, uint6
  * kern_*[side][kind]: side 0 = user half, 1 = item half; kind =
  *   0..4  MFMA Gram-block row kernels: 1 wave/row (two sizes), 2 / 4 / 8
  *         waves/row; up to 8/32/64/128/256 ratings (f64), 16/64/128/256/512 (f32),
- *   5     streaming MFMA Gram-block kernel, whole rows (one 8-wave workgroup per row),
+ *   5     streaming MFMA Gram-block kernel: one persistent cooperative launch
+ *         over tasks of <= 1792 (f64) / 3584 (f32) ratings -- whole rows, or
+ *         chunks of longer rows on co-resident workgroups -- plus the publish
+ *         of split rows,
  *   6..9  per-coordinate wave-reduction row kernels (1 wave/row <=128 and
  *         <=512, 4 / 8 waves/row <=2048 / 4096),
- *   10    Gram route (all its launches),
- *   11    streaming kernel over rows split into chunks on co-resident
- *         workgroups (cooperative launch + publish).  kern_bytes is the
+ *   10    Gram route (all its launches).  kern_bytes is the
  * algorithmic traffic of that launch per SURVEY.md §8(d): per rating
  * s*K (partner row) + 4 (partner id) + s (residual), per row 2*s*K (own row
  * read + write), s = 4 (f32) or 8 (f64). */

@@ -27,6 +27,10 @@ case "$PASS" in
            python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_write.log" 2>&1 ;;
   l2)    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc TCC_HIT_sum TCC_MISS_sum -d "$O/${TAG}_pmc_l2" -o "$TAG" -- \
            python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_l2.log" 2>&1 ;;
+  sq)    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d "$O/${TAG}_pmc_sq" -o "$TAG" -- \
+           python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_sq.log" 2>&1 ;;
+  sq2)   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM -d "$O/${TAG}_pmc_sq2" -o "$TAG" -- \
+           python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_sq2.log" 2>&1 ;;
   *) echo "unknown pass $PASS" >&2; exit 2 ;;
 esac
 echo "collect.sh $TAG $PASS done"

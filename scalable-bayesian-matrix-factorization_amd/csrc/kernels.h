@@ -17,9 +17,10 @@ struct HalfArgs {
     T* E_out;              // [N] residuals in this orientation's order
     const T* r_this;       // [N] ratings in this order (E_FROM_DOT, train RMSE, Gram update)
     T* own;                // [R][Kp]
-    const T* partner;      // [P][Kp]
-    const T* sig;          // [K] precision hyperparameter of this side
-    const T* mu;           // [K] mean hyperparameter of this side
+    const T* partner;      // [P+2][Kp]: row P is all zeros (sentinel), row P+1 slack
+    const T* sig;          // [Kp] precision hyperparameter of this side (zero padded)
+    const T* mu;           // [Kp] mean hyperparameter of this side (zero padded)
+    uint32_t zrow;         // P: the partner table's zero row (ratings past a row's end point here)
     const T* zbuf;         // reference mode: [R][K] N(0,1) variates; nullptr -> Philox
     T tau;
     uint32_t K, Kp;
@@ -30,6 +31,7 @@ struct HalfArgs {
     double* row_tr;        // [R] per-row train squared error of the clamped sample (or null)
     T lo, hi;
     int e_from_dot;        // 1: e0 = r - own.partner (no gather; multi-GPU)
+    uint32_t tune;         // kernel variant bits (sbmf_config.tune): bit 0 = residual update on MFMA
 };
 
 // Heavy-row (Gram route) work description.
@@ -65,6 +67,9 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
 
 // Streaming Gram-block kernel: one 512-thread workgroup per task (a whole
 // row, or one chunk of a row split over several co-resident workgroups).
+// Streaming-kernel task: at most `cmax` ratings of one row (the whole row,
+// or one chunk of a row split over `nch` co-resident workgroups).  A task
+// with len == 0 is an empty slot (round padding).
 struct SplitTask {
     uint32_t row;    // global row id
     uint32_t beg;    // first rating of the chunk (absolute index)
@@ -85,19 +90,27 @@ struct SplitSync {
     uint32_t nblk;       // ceil(K/16)
     double* chunk_sq;    // [nchunk_total]
     double* chunk_tr;    // [nchunk_total]
-    void* newown;        // [nsplit_rows][Kp] (T)
+    void* newown;        // [nchunk_total][Kp] (T), slot slab0 of each split row
     uint32_t* timeout;   // set to 1 if a spin gave up
+    uint32_t cmax;       // ratings per task (LDS-resident partner ids and residuals)
 };
+// Largest task (ratings) the streaming kernel keeps in LDS with two
+// workgroups per CU, for the kernel variant `tune`.
 template <typename T>
-hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, const HalfArgs<T>& a, const SplitSync& sy,
-                          hipStream_t st);
-// Co-resident k_gstream workgroups per CU (occupancy API).
+uint32_t gstream_cmax(uint32_t tune);
+// Workgroups per CU the streaming kernel variant `tune` is sized for.
+int gstream_wg_target(uint32_t tune);
+// Co-resident k_gstream workgroups per CU at the given task capacity (occupancy API).
 template <typename T>
-int gstream_blocks_per_cu();
-// Rows split over several workgroups (cooperative launch; grid <= residency).
+int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune);
+// All streaming tasks of a half-sweep in one cooperative persistent launch of
+// `grid` (<= residency) workgroups; workgroup w runs tasks w, w+grid, ...
+// Tasks are laid out in rounds of `grid` slots and every split row's chunks
+// share a round, so chunk hand-offs only wait on co-resident peers.  Split
+// rows are then published by k_split_finish.
 template <typename T>
-hipError_t launch_gsplit(const SplitTask* tasks, uint32_t ntask, const SplitRow* srows, uint32_t nsrow,
-                         const HalfArgs<T>& a, const SplitSync& sy, hipStream_t st);
+hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid, const SplitRow* srows, uint32_t nsrow,
+                          const HalfArgs<T>& a, const SplitSync& sy, hipStream_t st);
 
 template <typename T>
 hipError_t launch_rows(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);

@@ -324,6 +324,9 @@ struct MfmaT<double> {
     static __device__ __forceinline__ acc_t mfma(double a, acc_t c) {
         return __builtin_amdgcn_mfma_f64_16x16x4f64(a, a, c, 0, 0, 0);
     }
+    static __device__ __forceinline__ acc_t mfma2(double a, double b, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
     // C/D map: col = l&15, row = (l>>4) + 4j
     static __device__ __forceinline__ int row(int l, int j) { return (l >> 4) + 4 * j; }
 };
@@ -332,6 +335,9 @@ struct MfmaT<float> {
     typedef float acc_t __attribute__((ext_vector_type(4)));
     static __device__ __forceinline__ acc_t mfma(float a, acc_t c) {
         return __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ acc_t mfma2(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
     }
     // C/D map: col = l&15, row = 4*(l>>4) + j
     static __device__ __forceinline__ int row(int l, int j) { return 4 * (l >> 4) + j; }
@@ -363,7 +369,63 @@ __device__ __forceinline__ void lds_barrier() {
 constexpr int GB = 16;      // k per block
 constexpr int GLD = GB + 1; // padded LDS row (conflict-free row reads)
 
-template <typename T, int V, int NW, int RPW>
+// e -= S D for 4 vectors (16 ratings) on the matrix cores.  Lane l = 16r'+i
+// holds s[v][l] = S[rating (v, r')][i].  The tile goes through LDS (one
+// 16 x GLD buffer per wave, `tile`) into the MFMA A layout, A[m][kk] =
+// S[m][4q+kk] with tile row m = MfmaT::row(l, v) -- the accumulator row that
+// lane l reads back in register v -- and B[kk][n] = D[4q+kk] (bD[q], the same
+// for every n).  After 4 MFMAs lane l's register v holds (S D) of rating
+// (v, r').  LDS ops of one wave execute in order, so the buffer can be
+// rewritten right after it is read.  nv < 4: the unused tile rows are never
+// read back (an MFMA output row only depends on its own A row).
+template <typename T, int NV>
+__device__ __forceinline__ void e_update_mfma(T* __restrict__ tile, const T (&s)[NV], const T (&bD)[4], T (&e)[NV],
+                                              int lane) {
+    typedef typename MfmaT<T>::acc_t acc_t;
+    const int ci = lane & 15, rr = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < (NV + 3) / 4; ++t) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            if (4 * t + v < NV) tile[MfmaT<T>::row(lane, v) * GLD + ci] = s[4 * t + v];
+        acc_t y = {T(0), T(0), T(0), T(0)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y = MfmaT<T>::mfma2(tile[ci * GLD + 4 * q + rr], bD[q], y);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            if (4 * t + v < NV) e[4 * t + v] -= y[v];
+    }
+}
+
+// The 16 draws of a block in "gamma form": with H[c][l] = Bq_c G[c][l] for
+// l < c (0 otherwise) and gamma_c = A_c - old_c + Bq_c (c_c + P_c old_c),
+// step j reads d_j = gamma_j (final: it only receives corrections from
+// l < j) and applies gamma_c -= H[c][j] d_j.  After 16 steps lane c holds
+// d_c = new_c - old_c.  Same arithmetic as q_c -= G[c][j] d_j followed by
+// new = A + Bq q, with a 2-instruction dependency chain per step.
+template <typename T>
+__device__ __forceinline__ T gblock_solve(const T (&H)[GB], T gam) {
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+        const T dj = readlane(gam, j);
+        gam -= H[j] * dj;
+    }
+    return gam;
+}
+
+// Same recurrence with the H row read from LDS (row `hrow`, scaled by Bq)
+// step by step, for kernels without the registers to hold it.
+template <typename T>
+__device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, T gam) {
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+        const T dj = readlane(gam, j);
+        gam -= (Bq * hrow[j]) * dj;
+    }
+    return gam;
+}
+
+template <typename T, int V, int NW, int RPW, bool EM>
 __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const uint32_t* __restrict__ rows,
                                                                      uint32_t nrows, HalfArgs<T> a) {
     typedef typename MfmaT<T>::acc_t acc_t;
@@ -380,10 +442,13 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
     const int ci = lane & 15;                 // k within block / solve row
     const int rr = lane >> 4;                 // rating within vector
 
-    __shared__ T Gs[NWAVE][GB][GLD];
-    __shared__ T Cs[NWAVE][GB];
+    __shared__ T Ls[NWAVE][GB][GLD];          // strictly lower part of G_B (row layout)
+    __shared__ T Ps[NWAVE][GB];               // diagonal of G_B
+    __shared__ T Cs[NWAVE][GB];               // c_B
     __shared__ T newS[NW > 1 ? 256 : 1];
-    const int ws = NW > 1 ? 0 : wv;           // LDS slot holding this row's reduced G / c / D
+    __shared__ T Ts[EM ? NWAVE : 1][GB * GLD];  // per-wave S tile for the MFMA residual update
+    __shared__ T Ds[EM ? NWAVE : 1][GB];        // per-wave copy of the block's D
+    const int ws = NW > 1 ? 0 : wv;           // LDS slot holding this row's reduced G / c
 
     // per-row normals: lane l holds z for k = 2l, 2l+1 (zA) and 128+2l, 129+2l (zB)
     T zA0, zA1, zB0 = T(0), zB1 = T(0);
@@ -407,66 +472,57 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
         }
     }
 
-    // ratings of this wave: vector v covers ratings q = (wr*V + v)*4 + rr
-    uint32_t pj[V];
+    // ratings of this wave: vector v covers ratings q = (wr*V + v)*4 + rr;
+    // slots past the row's end gather the partner table's zero row
+    const T* __restrict__ prow[V];
     T e[V];
-    bool ok[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-        ok[v] = q < n;
-        pj[v] = ok[v] ? a.part[beg + q] : 0u;
-        e[v] = T(0);
+        const uint32_t pj = q < n ? a.part[beg + q] : a.zrow;
+        prow[v] = a.partner + (size_t)pj * Kp + ci;
     }
     if (a.e_from_dot) {
         T dot[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) dot[v] = T(0);
         for (uint32_t k0 = 0; k0 < K; k0 += GB) {
-            const uint32_t kk = k0 + ci;
-            const T o = kk < K ? a.own[(size_t)row * Kp + kk] : T(0);
+            const T o = a.own[(size_t)row * Kp + k0 + ci];  // padding columns are zero
 #pragma unroll
-            for (int v = 0; v < V; ++v)
-                if (ok[v] && kk < K) dot[v] += a.partner[(size_t)pj[v] * Kp + kk] * o;
+            for (int v = 0; v < V; ++v) dot[v] += prow[v][k0] * o;
         }
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             const T d = row16_sum(dot[v]);
             const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-            e[v] = ok[v] ? a.r_this[beg + q] - d : T(0);
+            e[v] = q < n ? a.r_this[beg + q] - d : T(0);
         }
     } else {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-            e[v] = ok[v] ? a.E_in[a.perm[beg + q]] : T(0);
+            e[v] = q < n ? a.E_in[a.perm[beg + q]] : T(0);
         }
     }
 
     const T tau = a.tau;
+    const T* __restrict__ orow = a.own + (size_t)row * Kp + ci;
     // software pipeline: block b+1's slices and own/sigma/mu values are in
-    // flight while block b is reduced, solved and applied
+    // flight while block b is reduced, solved and applied.  The prefetch past
+    // the last block stays inside the tables (slack row / padding).
     T s[V], sn[V];
-    T oldc, sgc, muc;
-    {
-        const uint32_t kk = ci;
-        const bool kin = kk < K;
 #pragma unroll
-        for (int v = 0; v < V; ++v) s[v] = (ok[v] && kin) ? a.partner[(size_t)pj[v] * Kp + kk] : T(0);
-        oldc = kin ? a.own[(size_t)row * Kp + kk] : T(0);
-        sgc = kin ? a.sig[kk] : T(0);
-        muc = kin ? a.mu[kk] : T(0);
-    }
+    for (int v = 0; v < V; ++v) s[v] = prow[v][0];
+    T oldc = orow[0], sgc = a.sig[ci], muc = a.mu[ci];
     for (uint32_t b0 = 0; b0 < K; b0 += GB) {
         const uint32_t kk = b0 + ci;
         const bool kin = kk < K;
-        const uint32_t kn = kk + GB;
-        const bool nin = kn < K;
-        const T oldn = nin ? a.own[(size_t)row * Kp + kn] : T(0);
-        const T sgn = nin ? a.sig[kn] : T(0);
-        const T mun = nin ? a.mu[kn] : T(0);
+        const uint32_t kn = b0 + GB;
+        const T oldn = orow[kn];
+        const T sgn = a.sig[kn + ci];
+        const T mun = a.mu[kn + ci];
 #pragma unroll
-        for (int v = 0; v < V; ++v) sn[v] = (ok[v] && nin) ? a.partner[(size_t)pj[v] * Kp + kn] : T(0);
+        for (int v = 0; v < V; ++v) sn[v] = prow[v][kn];
         acc_t g = {T(0), T(0), T(0), T(0)};
         T cc = T(0);
 #pragma unroll
@@ -476,39 +532,43 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
         }
         cc += shfl_xor_t(cc, 16);
         cc += shfl_xor_t(cc, 32);
-        // ---- 2. G, c -> LDS (row layout); multi-wave rows sum in wave order
-        if constexpr (NW > 1) {
-            lds_barrier();  // previous block's readers of Gs are done
+        // ---- 2. G (strictly lower + diagonal), c -> LDS; multi-wave rows sum in wave order
+        if constexpr (NW > 1) lds_barrier();  // previous block's readers of Ls are done
 #pragma unroll
-            for (int j = 0; j < 4; ++j) Gs[wr][MfmaT<T>::row(lane, j)][ci] = g[j];
-            if (lane < GB) Cs[wr][lane] = cc;
+        for (int j = 0; j < 4; ++j) {
+            const int r = MfmaT<T>::row(lane, j);
+            Ls[NW > 1 ? wr : ws][r][ci] = ci < r ? g[j] : T(0);
+            if (r == ci) Ps[NW > 1 ? wr : ws][ci] = g[j];
+        }
+        if (lane < GB) Cs[NW > 1 ? wr : ws][lane] = cc;
+        if constexpr (NW > 1) {
             lds_barrier();
             for (int x = threadIdx.x; x < GB * GB; x += 64 * NW) {
                 const int r0 = x >> 4, c0 = x & 15;
-                T sum = Gs[0][r0][c0];
+                if (c0 < r0) {
+                    T sum = Ls[0][r0][c0];
 #pragma unroll
-                for (int w = 1; w < NW; ++w) sum += Gs[w][r0][c0];
-                Gs[0][r0][c0] = sum;  // each entry owned by one thread: read-then-write is safe
+                    for (int w = 1; w < NW; ++w) sum += Ls[w][r0][c0];
+                    Ls[0][r0][c0] = sum;  // each entry owned by one thread: read-then-write is safe
+                }
                 if (x < GB) {
-                    T cs = Cs[0][x];
+                    T cs = Cs[0][x], ps = Ps[0][x];
 #pragma unroll
-                    for (int w = 1; w < NW; ++w) cs += Cs[w][x];
+                    for (int w = 1; w < NW; ++w) {
+                        cs += Cs[w][x];
+                        ps += Ps[w][x];
+                    }
                     Cs[0][x] = cs;
+                    Ps[0][x] = ps;
                 }
             }
             lds_barrier();
         } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) Gs[ws][MfmaT<T>::row(lane, j)][ci] = g[j];
-            if (lane < GB) Cs[ws][lane] = cc;
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own LDS writes visible to own reads
             __builtin_amdgcn_wave_barrier();
         }
         // ---- 3. the 16 sequential draws (every wave redundantly for NW>1: no extra barrier)
-        T Grow[GB];
-#pragma unroll
-        for (int j = 0; j < GB; ++j) Grow[j] = Gs[ws][ci][j];
-        const T P = Gs[ws][ci][ci];
+        const T P = Ps[ws][ci];
         const T old = oldc, sg = sgc, mu = muc;
         // z_kk lives in lane (kk>>1)&63 of zA (kk<128) or zB
         const int zl = (int)((kk >> 1) & 63);
@@ -520,21 +580,15 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
             const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
             z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
         }
-        const T var = kin ? T(1) / (sg + tau * P) : T(0);
+        const T var = kin ? T(1) / (sg + tau * P) : T(0);  // k >= K: var = 0 -> d = -old = 0
         const T sd = a.sd_is_var ? var : tsqrt(var);
         const T A = var * sg * mu + sd * z;
         const T Bq = var * tau;
-        T q = Cs[ws][ci] + P * old;
-        T nwv = old, dlt = T(0);
+        T H[GB];
 #pragma unroll
-        for (int j = 0; j < GB; ++j) {
-            const T nw = A + Bq * q;
-            const T d = nw - old;  // lanes with k >= K have var = 0 and q-terms 0: d = -old = 0
-            const T dj = readlane(d, j);
-            q -= Grow[j] * dj;
-            nwv = (ci == j) ? nw : nwv;
-            dlt = (ci == j) ? d : dlt;
-        }
+        for (int j = 0; j < GB; ++j) H[j] = Bq * Ls[ws][ci][j];
+        const T dlt = gblock_solve(H, A - old + Bq * (Cs[ws][ci] + P * old));
+        const T nwv = old + dlt;
         if constexpr (NW > 1) {
             // staged in LDS, written after the last barrier: no wave of this
             // row can still have a load of the same own value in flight
@@ -542,10 +596,17 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
         } else {
             if (lane < GB && kin) a.own[(size_t)row * Kp + kk] = nwv;  // one wave: program order
         }
-        // ---- 4. e -= S_B D_B   (lane (r,i) holds D_i after the solve: dlt of lane i)
-        const T Dl = shfl_t(dlt, ci);
+        // ---- 4. e -= S_B D_B (every 16-lane group computed the same d: lane (r,i) holds D_i)
+        if constexpr (EM) {  // on the matrix cores
+            if (lane < GB) Ds[wv][lane] = dlt;
+            T bD[4];
 #pragma unroll
-        for (int v = 0; v < V; ++v) e[v] -= row16_sum(s[v] * Dl);
+            for (int q = 0; q < 4; ++q) bD[q] = Ds[wv][4 * q + rr];
+            e_update_mfma<T, V>(Ts[wv], s, bD, e, lane);
+        } else {  // 16-lane DPP row sums
+#pragma unroll
+            for (int v = 0; v < V; ++v) e[v] -= row16_sum(s[v] * dlt);
+        }
 #pragma unroll
         for (int v = 0; v < V; ++v) s[v] = sn[v];
         oldc = oldn;
@@ -562,7 +623,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-        if (ok[v] && ci == 0) {
+        if (q < n && ci == 0) {
             a.E_out[beg + q] = e[v];
             sq += e[v] * e[v];
             if (a.row_tr) {
@@ -599,259 +660,298 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
 }
 
 // ------------------------------------------------------------ streaming Gram-block rows
-// Long rows: one workgroup (NW waves) per task.  A task is a whole row, or
-// one chunk of a row split over `nch` workgroups (SplitTask).  Residuals
-// live in the task's slice of E_out (L2-resident), so there is no register
-// limit on the length.  Per 16-wide k-block: pass A gathers the slices
-// (whole 128-byte lines) and accumulates G_B = S^T S (MFMA) and c_B = S^T e;
-// split rows exchange their (G_B, c_B) partials through global slabs (plain
+// Long rows (and their chunks): one 8-wave workgroup per task of at most
+// cmax ratings, in one persistent cooperative launch per half-sweep.  The
+// task's partner ids and residuals are staged in LDS once, so every later
+// traversal issues its partner-slice loads straight from LDS addresses (no
+// dependent global id load) and updates residuals on-chip.  Traversal t
+// applies block t-1 (e -= S_{t-1} D_{t-1}) and accumulates block t
+// (G_t = S^T S by MFMA, c_t = S^T e) in one pass over the task's ratings.
+// Split rows exchange their (G_B, c_B) partials through global slabs (plain
 // stores -> agent release -> counter; poll -> agent acquire -> loads, the
-// CDNA guide's G16 hand-off) and every chunk sums them in chunk order, so
-// all chunks draw identical coordinates; the 16 draws run as in k_gblock;
-// pass B re-reads the slices (L2) and applies e -= S D.  Wave w owns
-// vectors w, w+NW, ... in both passes.
-template <typename T, int NW, int UNR>
+// CDNA guide's G16 hand-off); every chunk sums them in chunk order, so all
+// chunks draw identical coordinates.  Wave w owns vectors w, w+NW, ...
+constexpr uint32_t GSTREAM_PAD = 4 * 8 * 8;  // traversal stride of k_gstream<T, 8, 8> (ratings)
+// dynamic LDS: [cmax+pad] partner ids, then (16-byte aligned) [cmax+pad] residuals
+__host__ __device__ constexpr size_t gstream_ids_bytes(uint32_t cmax) {
+    return ((size_t)(cmax + GSTREAM_PAD) * sizeof(uint32_t) + 15) / 16 * 16;
+}
+
+template <typename T, int NW, int UNR, bool EM>
 __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restrict__ tasks, uint32_t ntask,
                                                      HalfArgs<T> a, SplitSync sy) {
     typedef typename MfmaT<T>::acc_t acc_t;
     const int lane = threadIdx.x & 63;
     const int wr = threadIdx.x >> 6;
-    if (blockIdx.x >= ntask) return;
-    const SplitTask tk = tasks[blockIdx.x];
-    const uint32_t row = tk.row;
-    const uint32_t beg = tk.beg;
-    const uint32_t n = tk.len;
-    const uint32_t nch = tk.nch;
-    const uint32_t nvec = (n + 3) / 4;
     const uint32_t K = a.K, Kp = a.Kp;
     const int ci = lane & 15;
     const int rr = lane >> 4;
     constexpr int SL = GB * GB + GB;  // slab doubles per (chunk, block)
-    __shared__ T Gs[NW][GB][GLD];
+    __shared__ T Ls[NW][GB][GLD];     // strictly lower part of G_B
+    __shared__ T Ps[NW][GB];          // diagonal of G_B
     __shared__ T Cs[NW][GB];
     __shared__ double red2[NW][2];
-
-    T zA0, zA1, zB0 = T(0), zB1 = T(0);
-    if (a.zbuf) {
-        const uint32_t i0 = 2 * lane;
-        zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
-        zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
-        if (K > 128) {
-            zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
-            zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
-        }
-    } else {
-        double z0, z1;
-        philox_normal_pair(a.seed, row, a.sweep, a.tag, lane, z0, z1);
-        zA0 = (T)z0;
-        zA1 = (T)z1;
-        if (K > 128) {
-            philox_normal_pair(a.seed, row, a.sweep, a.tag, 64 + lane, z0, z1);
-            zB0 = (T)z0;
-            zB1 = (T)z1;
-        }
-    }
-
-    // ---- initial residuals of this task -> E_out (own order)
-    if (a.e_from_dot) {
-        for (uint32_t v = wr; v < nvec; v += NW) {
-            const uint32_t q = 4 * v + rr;
-            const bool ok = q < n;
-            const uint32_t pj = ok ? a.part[beg + q] : 0u;
-            T d = T(0);
-            for (uint32_t k0 = 0; k0 < K; k0 += GB) {
-                const uint32_t kk = k0 + ci;
-                if (ok && kk < K) d += a.partner[(size_t)pj * Kp + kk] * a.own[(size_t)row * Kp + kk];
-            }
-            d = row16_sum(d);
-            if (ok && ci == 0) a.E_out[beg + q] = a.r_this[beg + q] - d;
-        }
-    } else {
-        for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) a.E_out[beg + x] = a.E_in[a.perm[beg + x]];
-    }
-    __threadfence_block();
-    __syncthreads();
-
+    __shared__ T newS[256];           // new own values of the row, written once at the end
+    __shared__ T Ts[EM ? NW : 1][GB * GLD];  // per-wave S tile for the MFMA residual update
+    __shared__ T Ds[EM ? NW : 1][GB];        // per-wave copy of the previous block's D
+    extern __shared__ unsigned char dyn_lds[];
+    uint32_t* pjL = reinterpret_cast<uint32_t*>(dyn_lds);  // [cmax+pad] partner ids
+    T* eL = reinterpret_cast<T*>(dyn_lds + gstream_ids_bytes(sy.cmax));  // [cmax+pad] residuals
     const T tau = a.tau;
-    double sq = 0.0, trs = 0.0;
     const uint32_t nblk = (K + GB - 1) / GB;
-    __shared__ T newS[256];  // new own values of this row, written once at the end
-    T Dl = T(0);             // D of the previous block, lane (r,i) holds D_i
-    T oldn = (uint32_t)ci < K ? a.own[(size_t)row * Kp + ci] : T(0);  // block 0's old values
-    // Traversal t applies block t-1 (e -= S_{t-1} D_{t-1}) and accumulates
-    // block t (G_t, c_t) in one pass over the task's ratings.
-    for (uint32_t t = 0; t <= nblk; ++t) {
-        const bool app = t > 0, acc = t < nblk;
-        const uint32_t kp = (t - 1) * GB + ci, kc = t * GB + ci;
-        const bool pin = app && kp < K, cin = acc && kc < K;
-        const bool last = t == nblk;
-        acc_t g = {T(0), T(0), T(0), T(0)};
-        T cc = T(0);
-        for (uint32_t v0 = wr; v0 < nvec; v0 += NW * UNR) {
-            T sp[UNR], sc[UNR], e[UNR];
-            uint32_t pj[UNR];
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                const uint32_t q = 4 * (v0 + u * NW) + rr;
-                pj[u] = q < n ? a.part[beg + q] : 0u;
-                e[u] = q < n ? a.E_out[beg + q] : T(0);
+
+    for (uint32_t ti = blockIdx.x; ti < ntask; ti += gridDim.x) {
+        const SplitTask tk = tasks[ti];
+        const uint32_t n = tk.len;
+        if (n == 0) continue;  // empty round slot (uniform)
+        const uint32_t row = tk.row;
+        const uint32_t beg = tk.beg;
+        const uint32_t nch = tk.nch;
+        const uint32_t nvec = (n + 3) / 4;
+
+        T zA0, zA1, zB0 = T(0), zB1 = T(0);
+        if (a.zbuf) {
+            const uint32_t i0 = 2 * lane;
+            zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
+            zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
+            if (K > 128) {
+                zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
+                zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
             }
-#pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                const uint32_t q = 4 * (v0 + u * NW) + rr;
-                const T* src = a.partner + (size_t)pj[u] * Kp;
-                sp[u] = (q < n && pin) ? src[kp] : T(0);
-                sc[u] = (q < n && cin) ? src[kc] : T(0);
+        } else {
+            double z0, z1;
+            philox_normal_pair(a.seed, row, a.sweep, a.tag, lane, z0, z1);
+            zA0 = (T)z0;
+            zA1 = (T)z1;
+            if (K > 128) {
+                philox_normal_pair(a.seed, row, a.sweep, a.tag, 64 + lane, z0, z1);
+                zB0 = (T)z0;
+                zB1 = (T)z1;
             }
+        }
+
+        // ---- stage the task's partner ids and initial residuals in LDS; the
+        // slots up to the traversal stride (4*NW*UNR ratings) hold the zero
+        // row and zero residuals, so the traversal needs no per-rating masks
+        const uint32_t npad = (n + 4 * NW * UNR - 1) / (4 * NW * UNR) * (4 * NW * UNR);
+        for (uint32_t x = threadIdx.x; x < npad; x += 64 * NW) pjL[x] = x < n ? a.part[beg + x] : a.zrow;
+        for (uint32_t x = n + threadIdx.x; x < npad; x += 64 * NW) eL[x] = T(0);
+        if (a.e_from_dot) {
+            __syncthreads();
+            for (uint32_t v = wr; v < nvec; v += NW) {
+                const uint32_t q = 4 * v + rr;
+                const uint32_t pj = q < n ? pjL[q] : a.zrow;
+                T d = T(0);
+                for (uint32_t k0 = 0; k0 < K; k0 += GB)  // padding columns are zero
+                    d += a.partner[(size_t)pj * Kp + k0 + ci] * a.own[(size_t)row * Kp + k0 + ci];
+                d = row16_sum(d);
+                if (q < n && ci == 0) eL[q] = a.r_this[beg + q] - d;
+            }
+        } else {
+            for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) eL[x] = a.E_in[a.perm[beg + x]];
+        }
+        __syncthreads();
+
+        double sq = 0.0, trs = 0.0;
+        T Dl = T(0);  // (DPP path) D of the previous block, lane (r,i) holds D_i
+        T oldn = a.own[(size_t)row * Kp + ci];  // block 0's old values (padding columns are zero)
+        for (uint32_t t = 0; t <= nblk; ++t) {
+            const bool app = t > 0, acc = t < nblk;
+            const uint32_t kp = (t - 1) * GB + ci, kc = t * GB + ci;
+            const bool last = t == nblk;
+            acc_t g = {T(0), T(0), T(0), T(0)};
+            T cc = T(0);
+            T bD[4];  // (MFMA path) B operand of the residual update: D_{t-1}[4q + (lane>>4)]
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                const uint32_t q = 4 * (v0 + u * NW) + rr;
+            for (int q = 0; q < 4; ++q) bD[q] = (EM && app) ? Ds[EM ? wr : 0][4 * q + rr] : T(0);
+            for (uint32_t v0 = wr; v0 < nvec; v0 += NW * UNR) {
+                T sp[UNR], sc[UNR], e[UNR];
+                uint32_t pj[UNR];
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    const uint32_t q = 4 * (v0 + u * NW) + rr;  // < npad: padded slots
+                    pj[u] = pjL[q];
+                    e[u] = eL[q];
+                }
+#pragma unroll
+                for (int u = 0; u < UNR; ++u) {
+                    // zero row / zero padding columns / slack row: no per-lane masks
+                    const T* src = a.partner + (size_t)pj[u] * Kp;
+                    sp[u] = app ? src[kp] : T(0);
+                    sc[u] = acc ? src[kc] : T(0);
+                }
                 if (app) {
-                    e[u] -= row16_sum(sp[u] * Dl);
-                    if (q < n && ci == 0) {
-                        a.E_out[beg + q] = e[u];
-                        if (last) {
-                            sq += (double)(e[u] * e[u]);
-                            if (a.row_tr) {
-                                const T r = a.r_this[beg + q];
-                                T pr = r - e[u];
-                                pr = (pr < a.hi) ? pr : a.hi;
-                                pr = (a.lo < pr) ? pr : a.lo;
-                                trs += (double)((pr - r) * (pr - r));
+                    if constexpr (EM) {
+                        e_update_mfma<T, UNR>(Ts[wr], sp, bD, e, lane);
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < UNR; ++u) e[u] -= row16_sum(sp[u] * Dl);
+                    }
+                    if (ci == 0) {
+#pragma unroll
+                        for (int u = 0; u < UNR; ++u)  // the same lanes of the same wave read it next traversal
+                            eL[4 * (v0 + u * NW) + rr] = e[u];
+                    }
+                    if (last) {
+#pragma unroll
+                        for (int u = 0; u < UNR; ++u) {
+                            const uint32_t q = 4 * (v0 + u * NW) + rr;
+                            if (q < n && ci == 0) {
+                                a.E_out[beg + q] = e[u];
+                                sq += (double)(e[u] * e[u]);
+                                if (a.row_tr) {
+                                    const T r = a.r_this[beg + q];
+                                    T pr = r - e[u];
+                                    pr = (pr < a.hi) ? pr : a.hi;
+                                    pr = (a.lo < pr) ? pr : a.lo;
+                                    trs += (double)((pr - r) * (pr - r));
+                                }
                             }
                         }
                     }
                 }
                 if (acc) {
-                    g = MfmaT<T>::mfma(sc[u], g);
-                    cc += sc[u] * e[u];
-                }
-            }
-        }
-        __threadfence_block();  // this wave's residual stores precede its next reads
-        if (!acc) break;
-        const T old = oldn;     // loaded before this block's barriers: never sees the new value
-        const uint32_t kk = kc;
-        const bool kin = cin;
-        if (t + 1 < nblk) oldn = (kk + GB < K) ? a.own[(size_t)row * Kp + kk + GB] : T(0);
-        cc += shfl_xor_t(cc, 16);
-        cc += shfl_xor_t(cc, 32);
-        __syncthreads();  // previous block's solve reads of Gs[0] are done
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Gs[wr][MfmaT<T>::row(lane, j)][ci] = g[j];
-        if (lane < GB) Cs[wr][lane] = cc;
-        __syncthreads();
-        for (int x = threadIdx.x; x < GB * GB; x += 64 * NW) {
-            const int r0 = x >> 4, c0 = x & 15;
-            T sum = Gs[0][r0][c0];
-#pragma unroll
-            for (int w = 1; w < NW; ++w) sum += Gs[w][r0][c0];
-            Gs[0][r0][c0] = sum;
-            if (x < GB) {
-                T cs = Cs[0][x];
-#pragma unroll
-                for (int w = 1; w < NW; ++w) cs += Cs[w][x];
-                Cs[0][x] = cs;
-            }
-        }
-        __syncthreads();
-        if (nch > 1) {
-            // ---- cross-workgroup reduction of (G_B, c_B) over the row's chunks
-            double* myslab = sy.slabs + ((size_t)(tk.slab0 + tk.chunk) * sy.nblk + t) * SL;
-            for (int x = threadIdx.x; x < SL; x += 64 * NW)
-                myslab[x] = x < GB * GB ? (double)Gs[0][x >> 4][x & 15] : (double)Cs[0][x - GB * GB];
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            uint32_t* cnt = sy.counters + (size_t)tk.cnt0 + t;
-            if (threadIdx.x == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                uint32_t spins = 0;
-                while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > (1u << 26)) {  // give up: flag, never hang the device
-                        __hip_atomic_store(sy.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
+                    for (int u = 0; u < UNR; ++u) {
+                        g = MfmaT<T>::mfma(sc[u], g);
+                        cc += sc[u] * e[u];
                     }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            if (!acc) break;
+            const T old = oldn;  // loaded before this block's barriers: never sees the new value
+            const uint32_t kk = kc;
+            const bool kin = kk < K;
+            if (t + 1 < nblk) oldn = a.own[(size_t)row * Kp + kk + GB];  // padding columns are zero
+            cc += shfl_xor_t(cc, 16);
+            cc += shfl_xor_t(cc, 32);
+            __syncthreads();  // previous block's solve reads of Ls/Ps/Cs[0] are done
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = MfmaT<T>::row(lane, j);
+                Ls[wr][r][ci] = ci < r ? g[j] : T(0);
+                if (r == ci) Ps[wr][ci] = g[j];
+            }
+            if (lane < GB) Cs[wr][lane] = cc;
+            __syncthreads();
+            for (int x = threadIdx.x; x < GB * GB; x += 64 * NW) {
+                const int r0 = x >> 4, c0 = x & 15;
+                if (c0 < r0) {
+                    T sum = Ls[0][r0][c0];
+#pragma unroll
+                    for (int w = 1; w < NW; ++w) sum += Ls[w][r0][c0];
+                    Ls[0][r0][c0] = sum;
+                }
+                if (x < GB) {
+                    T cs = Cs[0][x], ps = Ps[0][x];
+#pragma unroll
+                    for (int w = 1; w < NW; ++w) {
+                        cs += Cs[w][x];
+                        ps += Ps[w][x];
+                    }
+                    Cs[0][x] = cs;
+                    Ps[0][x] = ps;
+                }
+            }
+            __syncthreads();
+            if (nch > 1) {
+                // ---- cross-workgroup reduction of (G_B, c_B) over the row's chunks
+                // slab: [lower part + diagonal as a 16x16 image | c]
+                double* myslab = sy.slabs + ((size_t)(tk.slab0 + tk.chunk) * sy.nblk + t) * SL;
+                for (int x = threadIdx.x; x < SL; x += 64 * NW) {
+                    const int r0 = (x >> 4) & 15, c0 = x & 15;
+                    myslab[x] = x < GB * GB ? (double)(r0 == c0 ? Ps[0][r0] : Ls[0][r0][c0]) : (double)Cs[0][x - GB * GB];
+                }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                uint32_t* cnt = sy.counters + (size_t)tk.cnt0 + t;
+                if (threadIdx.x == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    uint32_t spins = 0;
+                    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++spins > (1u << 26)) {  // give up: flag, never hang the device
+                            __hip_atomic_store(sy.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __syncthreads();
+                const double* slab0 = sy.slabs + ((size_t)tk.slab0 * sy.nblk + t) * SL;
+                for (int x = threadIdx.x; x < SL; x += 64 * NW) {
+                    double sum = 0.0;
+                    for (uint32_t c = 0; c < nch; ++c) sum += slab0[(size_t)c * sy.nblk * SL + x];
+                    if (x < GB * GB) {
+                        const int r0 = x >> 4, c0 = x & 15;
+                        if (r0 == c0)
+                            Ps[0][r0] = (T)sum;
+                        else
+                            Ls[0][r0][c0] = (T)sum;  // upper entries stay 0 in every chunk
+                    } else {
+                        Cs[0][x - GB * GB] = (T)sum;
+                    }
+                }
+                __syncthreads();
             }
-            __syncthreads();
-            const double* slab0 = sy.slabs + ((size_t)tk.slab0 * sy.nblk + t) * SL;
-            for (int x = threadIdx.x; x < SL; x += 64 * NW) {
-                double sum = 0.0;
-                for (uint32_t c = 0; c < nch; ++c) sum += slab0[(size_t)c * sy.nblk * SL + x];
-                if (x < GB * GB)
-                    Gs[0][x >> 4][x & 15] = (T)sum;
+            // ---- the 16 draws (every wave of every chunk: identical inputs -> identical results)
+            const T P = Ps[0][ci];
+            const T sg = a.sig[kk];  // zero padded
+            const T mu = a.mu[kk];
+            const int zl = (int)((kk >> 1) & 63);
+            const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
+            T z = (kk & 1) ? za1 : za0;
+            if (K > 128) {
+                const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
+                z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
+            }
+            const T var = kin ? T(1) / (sg + tau * P) : T(0);
+            const T sd = a.sd_is_var ? var : tsqrt(var);
+            const T A = var * sg * mu + sd * z;
+            const T Bq = var * tau;
+            const T dlt = gblock_solve_lds(&Ls[0][ci][0], Bq, A - old + Bq * (Cs[0][ci] + P * old));
+            if (wr == 0 && lane < GB && kin) newS[kk] = old + dlt;
+            if constexpr (EM) {
+                if (lane < GB) Ds[wr][lane] = dlt;  // every wave solved identically: its own copy
+            } else {
+                Dl = dlt;  // every 16-lane group solved identically: lane (r,i) holds D_i
+            }
+        }
+        __syncthreads();
+        // ---- new own row: whole rows write it, split rows stage it (k_split_finish publishes)
+        if (tk.chunk == 0)
+            for (uint32_t k = threadIdx.x; k < K; k += 64 * NW) {
+                if (nch > 1)
+                    static_cast<T*>(sy.newown)[(size_t)tk.slab0 * Kp + k] = newS[k];
                 else
-                    Cs[0][x - GB * GB] = (T)sum;
+                    a.own[(size_t)row * Kp + k] = newS[k];
             }
-            __syncthreads();
+        double dsq = wave_sum(sq);
+        double dtr = wave_sum(trs);
+        if (lane == 0) {
+            red2[wr][0] = dsq;
+            red2[wr][1] = dtr;
         }
-        // ---- the 16 draws (every wave of every chunk: identical inputs -> identical results)
-        T Grow[GB];
-#pragma unroll
-        for (int j = 0; j < GB; ++j) Grow[j] = Gs[0][ci][j];
-        const T P = Gs[0][ci][ci];
-        const T sg = kin ? a.sig[kk] : T(0);
-        const T mu = kin ? a.mu[kk] : T(0);
-        const int zl = (int)((kk >> 1) & 63);
-        const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
-        T z = (kk & 1) ? za1 : za0;
-        if (K > 128) {
-            const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
-            z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            dsq = 0.0;
+            dtr = 0.0;
+            for (int w = 0; w < NW; ++w) {
+                dsq += red2[w][0];
+                dtr += red2[w][1];
+            }
+            if (nch > 1) {
+                sy.chunk_sq[tk.slab0 + tk.chunk] = dsq;
+                sy.chunk_tr[tk.slab0 + tk.chunk] = dtr;
+            } else {
+                if (a.row_sq) a.row_sq[row] = dsq;
+                if (a.row_tr) a.row_tr[row] = dtr;
+            }
         }
-        const T var = kin ? T(1) / (sg + tau * P) : T(0);
-        const T sd = a.sd_is_var ? var : tsqrt(var);
-        const T A = var * sg * mu + sd * z;
-        const T Bq = var * tau;
-        T q = Cs[0][ci] + P * old;
-        T nwv = old, dlt = T(0);
-#pragma unroll
-        for (int j = 0; j < GB; ++j) {
-            const T nw = A + Bq * q;
-            const T d = nw - old;
-            const T dj = readlane(d, j);
-            q -= Grow[j] * dj;
-            nwv = (ci == j) ? nw : nwv;
-            dlt = (ci == j) ? d : dlt;
-        }
-        if (wr == 0 && lane < GB && kin) newS[kk] = nwv;
-        Dl = shfl_t(dlt, ci);
-    }
-    __syncthreads();
-    // ---- new own row: whole rows write it, split rows stage it (k_split_finish publishes)
-    if (tk.chunk == 0)
-        for (uint32_t k = threadIdx.x; k < K; k += 64 * NW) {
-            if (nch > 1)
-                static_cast<T*>(sy.newown)[(size_t)tk.slab0 * Kp + k] = newS[k];
-            else
-                a.own[(size_t)row * Kp + k] = newS[k];
-        }
-    double dsq = wave_sum(sq);
-    double dtr = wave_sum(trs);
-    if (lane == 0) {
-        red2[wr][0] = dsq;
-        red2[wr][1] = dtr;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        dsq = 0.0;
-        dtr = 0.0;
-        for (int w = 0; w < NW; ++w) {
-            dsq += red2[w][0];
-            dtr += red2[w][1];
-        }
-        if (nch > 1) {
-            sy.chunk_sq[tk.slab0 + tk.chunk] = dsq;
-            sy.chunk_tr[tk.slab0 + tk.chunk] = dtr;
-        } else {
-            if (a.row_sq) a.row_sq[row] = dsq;
-            if (a.row_tr) a.row_tr[row] = dtr;
-        }
+        __syncthreads();  // LDS (ids, residuals, newS, red2) is reused by the next task
     }
 }
 
@@ -1310,64 +1410,95 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
     if (a.K > 256) return hipErrorInvalidValue;
     // f64: 8 vectors (32 ratings) per wave; f32: 16 vectors (64 ratings) per wave
     constexpr int V = sizeof(T) == 8 ? 8 : 16;
+    const bool em = a.tune & 1u;
+#define SBMF_GBLOCK(V_, NW_, RPW_, GRID_, THR_)                                                  \
+    if (em)                                                                                      \
+        k_gblock<T, V_, NW_, RPW_, true><<<GRID_, THR_, 0, st>>>(rows, nrows, a);                \
+    else                                                                                         \
+        k_gblock<T, V_, NW_, RPW_, false><<<GRID_, THR_, 0, st>>>(rows, nrows, a);
     switch (kind) {
         case GK_W4:  // 1 wave / row, V/4 vectors, 4 rows / block
-            k_gblock<T, V / 4, 1, 4><<<(nrows + 3) / 4, 256, 0, st>>>(rows, nrows, a);
+            SBMF_GBLOCK(V / 4, 1, 4, (nrows + 3) / 4, 256);
             break;
         case GK_W16:  // 1 wave / row
-            k_gblock<T, V, 1, 4><<<(nrows + 3) / 4, 256, 0, st>>>(rows, nrows, a);
+            SBMF_GBLOCK(V, 1, 4, (nrows + 3) / 4, 256);
             break;
         case GK_B2:  // 2 waves / row
-            k_gblock<T, V, 2, 1><<<nrows, 128, 0, st>>>(rows, nrows, a);
+            SBMF_GBLOCK(V, 2, 1, nrows, 128);
             break;
         case GK_B4:  // 4 waves / row
-            k_gblock<T, V, 4, 1><<<nrows, 256, 0, st>>>(rows, nrows, a);
+            SBMF_GBLOCK(V, 4, 1, nrows, 256);
             break;
         case GK_B8:  // 8 waves / row
-            k_gblock<T, V, 8, 1><<<nrows, 512, 0, st>>>(rows, nrows, a);
+            SBMF_GBLOCK(V, 8, 1, nrows, 512);
             break;
         default:
             return hipErrorInvalidValue;
     }
+#undef SBMF_GBLOCK
     return hipGetLastError();
 }
 
+// tune bit 0: residual update on MFMA; bit 1: 4-wave workgroups (4 per CU)
+// instead of 8-wave workgroups (2 per CU).
+static int gstream_nw(uint32_t tune) { return (tune & 2u) ? 4 : 8; }
+int gstream_wg_target(uint32_t tune) { return (tune & 2u) ? 4 : 2; }
+
 template <typename T>
-hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, const HalfArgs<T>& a, const SplitSync& sy,
-                          hipStream_t st) {
-    if (ntask == 0) return hipSuccess;
-    if (a.K > 256) return hipErrorInvalidValue;
-    // 8 waves x 8 vectors in flight per wave.  NOTE: the same kernel with
-    // 16 waves (1024 threads) returned wrong, run-to-run different results
-    // on gfx950; kept out until understood.
-    k_gstream<T, 8, 8><<<ntask, 512, 0, st>>>(tasks, ntask, a, sy);
-    return hipGetLastError();
+static const void* gstream_fn(uint32_t tune) {
+    if (tune & 2u)
+        return (tune & 1u) ? (const void*)k_gstream<T, 4, 8, true> : (const void*)k_gstream<T, 4, 8, false>;
+    return (tune & 1u) ? (const void*)k_gstream<T, 8, 8, true> : (const void*)k_gstream<T, 8, 8, false>;
 }
 
 template <typename T>
-int gstream_blocks_per_cu() {
+uint32_t gstream_cmax(uint32_t tune) {
+    hipFuncAttributes fa{};
+    int dev = 0, lds_cu = 65536;
+    if (hipFuncGetAttributes(&fa, gstream_fn<T>(tune)) != hipSuccess) return 1024;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
+    // gstream_wg_target workgroups per CU: static + [ids | residuals] each
+    const long per_wg = lds_cu / gstream_wg_target(tune) - (long)fa.sharedSizeBytes - 16;
+    const long c = per_wg / (long)(sizeof(uint32_t) + sizeof(T)) - (long)GSTREAM_PAD;
+    const long cap = sizeof(T) == 8 ? 4096 : 8192;
+    return (uint32_t)std::max(256L, std::min(cap, c) / 64 * 64);
+}
+
+template <typename T>
+int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gstream<T, 8, 8>, 512, 0) != hipSuccess) return 1;
+    const size_t dyn = gstream_ids_bytes(cmax) + (size_t)(cmax + GSTREAM_PAD) * sizeof(T);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gstream_fn<T>(tune), 64 * gstream_nw(tune), dyn) != hipSuccess)
+        return 1;
     return n;
 }
 
 template <typename T>
-hipError_t launch_gsplit(const SplitTask* tasks, uint32_t ntask, const SplitRow* srows, uint32_t nsrow,
-                         const HalfArgs<T>& a, const SplitSync& sy, hipStream_t st) {
+hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid, const SplitRow* srows, uint32_t nsrow,
+                          const HalfArgs<T>& a, const SplitSync& sy, hipStream_t st) {
     if (ntask == 0) return hipSuccess;
-    if (a.K > 256) return hipErrorInvalidValue;
-    hipError_t err = hipMemsetAsync(sy.counters, 0, (size_t)sy.ncounters * sizeof(uint32_t), st);
-    if (err != hipSuccess) return err;
-    // all chunks of a row must be resident together: the cooperative launch
-    // checks that the whole grid fits (host side sizes it to <= residency)
+    if (a.K > 256 || sy.cmax == 0 || grid == 0) return hipErrorInvalidValue;
+    hipError_t err;
+    if (nsrow) {
+        err = hipMemsetAsync(sy.counters, 0, (size_t)sy.ncounters * sizeof(uint32_t), st);
+        if (err != hipSuccess) return err;
+    }
+    // all chunks of a split row must be resident together: the cooperative
+    // launch checks that the whole grid fits (the host sizes it to residency)
     const SplitTask* tp = tasks;
     HalfArgs<T> ap = a;
     SplitSync syp = sy;
     void* args[] = {(void*)&tp, (void*)&ntask, (void*)&ap, (void*)&syp};
-    err = hipLaunchCooperativeKernel((const void*)k_gstream<T, 8, 8>, dim3(ntask), dim3(512), args, 0, st);
+    const size_t dyn = gstream_ids_bytes(sy.cmax) + (size_t)(sy.cmax + GSTREAM_PAD) * sizeof(T);
+    err = hipLaunchCooperativeKernel(gstream_fn<T>(a.tune), dim3(std::min(grid, ntask)), dim3(64 * gstream_nw(a.tune)),
+                                     args, (unsigned)dyn, st);
     if (err != hipSuccess) return err;
-    k_split_finish<T><<<nsrow, 64, 0, st>>>(srows, nsrow, a, sy);
-    return hipGetLastError();
+    if (nsrow) {
+        k_split_finish<T><<<nsrow, 64, 0, st>>>(srows, nsrow, a, sy);
+        return hipGetLastError();
+    }
+    return hipSuccess;
 }
 
 template <typename T>
@@ -1460,11 +1591,10 @@ hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint
 #define SBMF_INST(T)                                                                                                 \
     template hipError_t launch_rows<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);            \
     template hipError_t launch_gblock<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);          \
-    template hipError_t launch_gstream<T>(const SplitTask*, uint32_t, const HalfArgs<T>&, const SplitSync&,          \
-                                          hipStream_t);                                                              \
-    template int gstream_blocks_per_cu<T>();                                                                        \
-    template hipError_t launch_gsplit<T>(const SplitTask*, uint32_t, const SplitRow*, uint32_t, const HalfArgs<T>&,  \
-                                         const SplitSync&, hipStream_t);                                             \
+    template hipError_t launch_gstream<T>(const SplitTask*, uint32_t, uint32_t, const SplitRow*, uint32_t,           \
+                                          const HalfArgs<T>&, const SplitSync&, hipStream_t);                        \
+    template int gstream_blocks_per_cu<T>(uint32_t, uint32_t);                                                      \
+    template uint32_t gstream_cmax<T>(uint32_t);                                                                    \
     template hipError_t launch_gram<T>(const GramItem*, uint32_t, const GramRow*, uint32_t, double*, T*, double*,   \
                                        double*, const HalfArgs<T>&, hipStream_t);                                    \
     template hipError_t launch_resid<T>(const uint32_t*, const uint32_t*, const T*, const T*, const T*, uint32_t,     \

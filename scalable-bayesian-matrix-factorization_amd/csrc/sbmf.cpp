@@ -107,9 +107,10 @@ struct Side {
     std::vector<uint32_t> bin_rows[NBIN];  // kinds: GK_* (0..4), KIND_STREAM (5), KIND_RK0 + RK_* (6..9)
     std::vector<GramItem> gitems;
     std::vector<GramRow> grows;
-    std::vector<SplitTask> stasks;   // streaming kernel: whole rows (nch = 1)
-    std::vector<SplitTask> xtasks;   // streaming kernel: chunks of split rows
-    std::vector<SplitRow> xrows;
+    std::vector<SplitTask> stasks;   // streaming kernel tasks, in rounds of `sgrid` slots
+    std::vector<SplitRow> xrows;     // rows split over several tasks
+    uint32_t nxchunk = 0;            // tasks belonging to split rows (slab / staging slots)
+    uint32_t sgrid = 0;              // persistent grid of the streaming launch
 };
 
 static void build_side(uint64_t N, const uint32_t* key, const uint32_t* other, const double* rat, uint32_t R,
@@ -153,7 +154,6 @@ static void partition(Side& s, int nranks, int rank) {
 static const int KIND_STREAM = GK_NUM;  // 5: streaming kernel, whole rows (row bin: every streaming row)
 static const int KIND_RK0 = GK_NUM + 1;  // 6..9
 static const int KIND_GRAM = 10;         // Gram route
-static const int KIND_SPLIT = 11;        // streaming kernel, rows split over workgroups (timing only)
 
 static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr, bool f64) {
     for (auto& b : s.bin_rows) b.clear();
@@ -232,7 +232,8 @@ struct sbmf_ctx {
     DBuf d_bins_u[NBIN], d_bins_v[NBIN];
     DBuf d_gitems_u, d_grows_u, d_gitems_v, d_grows_v, d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
     DBuf d_colpart, d_res, d_scratch;
-    DBuf d_stasks_u, d_stasks_v, d_xtasks_u, d_xtasks_v, d_xrows_u, d_xrows_v;
+    uint32_t cmax = 0;  // streaming-kernel task capacity (ratings)
+    DBuf d_stasks_u, d_stasks_v, d_xrows_u, d_xrows_v;
     DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
     std::vector<double> h_res;
@@ -331,11 +332,14 @@ static void prepare_T(sbmf_ctx* c) {
     {
         int dev_cus = 0;
         HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, cf.device));
-        const int per_cu = std::max(1, std::min(2, gstream_blocks_per_cu<T>()));
+        // task capacity: the LDS-resident maximum, or smaller if split_chunk asks
+        c->cmax = gstream_cmax<T>(cf.tune);
+        if (cf.split_chunk) c->cmax = std::min(c->cmax, std::max(cf.split_chunk, 1u));
+        const int per_cu =
+            std::max(1, std::min(gstream_wg_target(cf.tune), gstream_blocks_per_cu<T>(c->cmax, cf.tune)));
         const uint32_t gres = (uint32_t)(dev_cus * per_cu);
-        const uint32_t chunk = cf.split_chunk ? cf.split_chunk : 4096;
-        build_stream_tasks(c->users, chunk, gres, nblk);
-        build_stream_tasks(c->items, chunk, gres, nblk);
+        build_stream_tasks(c->users, c->cmax, gres, nblk);
+        build_stream_tasks(c->items, c->cmax, gres, nblk);
     }
     {  // test split in 256-aligned blocks
         const uint64_t T_ = c->su.size(), nb = (T_ + 255) / 256;
@@ -364,12 +368,10 @@ static void prepare_T(sbmf_ctx* c) {
     }
     upload(c->d_stasks_u, c->users.stasks, st);
     upload(c->d_stasks_v, c->items.stasks, st);
-    upload(c->d_xtasks_u, c->users.xtasks, st);
-    upload(c->d_xtasks_v, c->items.xtasks, st);
     upload(c->d_xrows_u, c->users.xrows, st);
     upload(c->d_xrows_v, c->items.xrows, st);
     {
-        const size_t nx = std::max(c->users.xtasks.size(), c->items.xtasks.size());
+        const size_t nx = std::max(c->users.nxchunk, c->items.nxchunk);
         const size_t nr = std::max(c->users.xrows.size(), c->items.xrows.size());
         c->d_xslabs.alloc(std::max<size_t>(nx, 1) * nblk * (16 * 16 + 16) * sizeof(double));
         c->d_xcnt.alloc(std::max<size_t>(nr, 1) * nblk * sizeof(uint32_t));
@@ -393,8 +395,11 @@ static void prepare_T(sbmf_ctx* c) {
     c->d_chunk_sq.alloc(std::max<size_t>(nslab, 1) * sizeof(double));
     c->d_chunk_tr.alloc(std::max<size_t>(nslab, 1) * sizeof(double));
 
-    c->d_U.alloc((size_t)c->I * c->Kp * sizeof(T));
-    c->d_V.alloc((size_t)c->J * c->Kp * sizeof(T));
+    // factor tables [rows + 2][Kp]: row `rows` stays zero (the sentinel partner of
+    // padded rating slots), row `rows + 1` is slack for the next-block prefetch
+    // past the last column block; padding columns K..Kp-1 stay zero.
+    c->d_U.alloc((size_t)(c->I + 2) * c->Kp * sizeof(T));
+    c->d_V.alloc((size_t)(c->J + 2) * c->Kp * sizeof(T));
     HIPCHK(hipMemsetAsync(c->d_U.p, 0, c->d_U.bytes, st));
     HIPCHK(hipMemsetAsync(c->d_V.p, 0, c->d_V.bytes, st));
     c->d_Eu.alloc(std::max<uint64_t>(N, 1) * sizeof(T));
@@ -407,7 +412,8 @@ static void prepare_T(sbmf_ctx* c) {
     c->d_rowtr_v.alloc((size_t)c->J * sizeof(double));
     HIPCHK(hipMemsetAsync(c->d_rowsq_v.p, 0, c->d_rowsq_v.bytes, st));
     HIPCHK(hipMemsetAsync(c->d_rowtr_v.p, 0, c->d_rowtr_v.bytes, st));
-    c->d_hyper.alloc(4 * (size_t)c->K * sizeof(T));
+    // [sig_u | mu_u | sig_v | mu_v], each Kp long and zero padded, + 16 slack for prefetch
+    c->d_hyper.alloc((4 * (size_t)c->Kp + 16) * sizeof(T));
     HIPCHK(hipMemsetAsync(c->d_hyper.p, 0, c->d_hyper.bytes, st));
     const uint32_t nchunk = (std::max(c->I, c->J) + 255) / 256;
     c->d_colpart.alloc((size_t)nchunk * 2 * c->K * sizeof(double));
@@ -456,31 +462,50 @@ static void prepare_T(sbmf_ctx* c) {
     c->prepared = true;
 }
 
-// Streaming-kernel tasks.  Largest rows first: a row longer than `chunk` is
-// split into ceil(n/chunk) equal chunks as long as all split chunks of the
-// half-sweep fit the co-resident grid (gres); the rest run whole.
-static void build_stream_tasks(Side& s, uint32_t chunk, uint32_t gres, uint32_t nblk) {
+// Streaming-kernel tasks (at most `cmax` ratings each: a whole row, or the
+// equal chunks of a longer row) laid out in rounds of `gres` slots, largest
+// rows first; a split row's chunks always share a round, so its workgroups
+// are co-resident (workgroup w runs slot w of every round).  Rounds alternate
+// direction so no slot always gets the largest task.
+static void build_stream_tasks(Side& s, uint32_t cmax, uint32_t gres, uint32_t nblk) {
     s.stasks.clear();
-    s.xtasks.clear();
     s.xrows.clear();
+    s.nxchunk = 0;
+    s.sgrid = 0;
     const std::vector<uint32_t>& rows = s.bin_rows[KIND_STREAM];  // degree-descending
-    uint32_t used = 0;
+    if (rows.empty()) return;
+    std::vector<std::vector<SplitTask>> rounds;
+    uint32_t fill = gres;
     for (uint32_t r : rows) {
         const uint32_t n = s.ptr[r + 1] - s.ptr[r];
-        const uint32_t nch = chunk == 0xffffffffu ? 1 : (n + chunk - 1) / chunk;
-        if (nch > 1 && used + nch <= gres) {
-            const uint32_t slab0 = (uint32_t)s.xtasks.size();
+        const uint32_t nch = (n + cmax - 1) / cmax;
+        if (nch > gres)
+            fail(SBMF_E_ARG, "row %u has %u ratings: more than %u co-resident chunks of %u", r, n, gres, cmax);
+        if (fill + nch > gres) {
+            rounds.emplace_back();
+            fill = 0;
+        }
+        if (nch == 1) {
+            rounds.back().push_back(SplitTask{r, s.ptr[r], n, 1, 0, 0, 0, 0});
+        } else {
+            const uint32_t slab0 = s.nxchunk;
             const uint32_t cnt0 = (uint32_t)s.xrows.size() * nblk;
             const uint32_t per = (n + nch - 1) / nch;
             for (uint32_t c = 0; c < nch; ++c) {
                 const uint32_t b = c * per, e = std::min(n, b + per);
-                s.xtasks.push_back(SplitTask{r, s.ptr[r] + b, e - b, nch, c, slab0, cnt0, 0});
+                rounds.back().push_back(SplitTask{r, s.ptr[r] + b, e - b, nch, c, slab0, cnt0, 0});
             }
             s.xrows.push_back(SplitRow{r, slab0, nch, 0});
-            used += nch;
-        } else {
-            s.stasks.push_back(SplitTask{r, s.ptr[r], n, 1, 0, 0, 0, 0});
+            s.nxchunk += nch;
         }
+        fill += nch;
+    }
+    s.sgrid = rounds.size() > 1 ? gres : (uint32_t)rounds[0].size();
+    for (size_t k = 0; k < rounds.size(); ++k) {
+        std::vector<SplitTask>& rd = rounds[k];
+        if (k + 1 < rounds.size()) rd.resize(gres, SplitTask{0, 0, 0, 1, 0, 0, 0, 0});  // empty slots
+        if (k & 1) std::reverse(rd.begin(), rd.end());
+        s.stasks.insert(s.stasks.end(), rd.begin(), rd.end());
     }
 }
 
@@ -530,7 +555,8 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
         a.own = c->d_U.as<T>();
         a.partner = c->d_V.as<T>();
         a.sig = c->d_hyper.as<T>();
-        a.mu = c->d_hyper.as<T>() + c->K;
+        a.mu = c->d_hyper.as<T>() + c->Kp;
+        a.zrow = c->J;
         a.zbuf = c->cfg.rng_mode == SBMF_RNG_REFERENCE ? c->d_zU.as<T>() : nullptr;
         a.tag = TAG_USERS;
         a.row_sq = nullptr;
@@ -544,13 +570,15 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
         a.r_this = c->d_vr.as<T>();
         a.own = c->d_V.as<T>();
         a.partner = c->d_U.as<T>();
-        a.sig = c->d_hyper.as<T>() + 2 * c->K;
-        a.mu = c->d_hyper.as<T>() + 3 * c->K;
+        a.sig = c->d_hyper.as<T>() + 2 * c->Kp;
+        a.mu = c->d_hyper.as<T>() + 3 * c->Kp;
+        a.zrow = c->I;
         a.zbuf = c->cfg.rng_mode == SBMF_RNG_REFERENCE ? c->d_zV.as<T>() : nullptr;
         a.tag = TAG_ITEMS;
         a.row_sq = c->d_rowsq_v.as<double>();
         a.row_tr = c->cfg.eval_train ? c->d_rowtr_v.as<double>() : nullptr;
     }
+    a.tune = c->cfg.tune;
     a.tau = (T)c->tau;
     a.K = c->K;
     a.Kp = c->Kp;
@@ -581,7 +609,7 @@ static void run_half(sbmf_ctx* c, bool users) {
     }
     for (int k = NBIN - 1; k >= 0; --k) {
         if (s.bin_rows[k].empty()) continue;
-        if (k != KIND_STREAM) HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
+        HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
         if (k < GK_NUM)
             HIPCHK(launch_gblock<T>(k, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
         else if (k == KIND_STREAM) {
@@ -594,17 +622,10 @@ static void run_half(sbmf_ctx* c, bool users) {
             sy.chunk_tr = c->d_xchunk_tr.as<double>();
             sy.newown = c->d_xnewown.p;
             sy.timeout = c->d_xtimeout.as<uint32_t>();
-            if (!s.xtasks.empty()) {
-                HIPCHK(hipEventRecord(c->kev[sd][KIND_SPLIT][0], st));
-                HIPCHK(launch_gsplit<T>((users ? c->d_xtasks_u : c->d_xtasks_v).as<SplitTask>(), (uint32_t)s.xtasks.size(),
-                                        (users ? c->d_xrows_u : c->d_xrows_v).as<SplitRow>(), (uint32_t)s.xrows.size(),
-                                        a, sy, st));
-                HIPCHK(hipEventRecord(c->kev[sd][KIND_SPLIT][1], st));
-                c->timing.n_launch++;
-            }
-            HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
-            HIPCHK(launch_gstream<T>((users ? c->d_stasks_u : c->d_stasks_v).as<SplitTask>(),
-                                     (uint32_t)s.stasks.size(), a, sy, st));
+            sy.cmax = c->cmax;
+            HIPCHK(launch_gstream<T>((users ? c->d_stasks_u : c->d_stasks_v).as<SplitTask>(), (uint32_t)s.stasks.size(),
+                                     s.sgrid, (users ? c->d_xrows_u : c->d_xrows_v).as<SplitRow>(),
+                                     (uint32_t)s.xrows.size(), a, sy, st));
         }
         else
             HIPCHK(launch_rows<T>(k - KIND_RK0, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
@@ -627,14 +648,6 @@ static void fill_kernel_bytes(sbmf_ctx* c) {
             c->timing.kern_bytes[sd][k] = alg_bytes(s, s.bin_rows[k], c->K, tsz);
             c->timing.kern_rows[sd][k] = (uint32_t)s.bin_rows[k].size();
         }
-        // streaming rows: whole rows (kind 5) and split rows (kind 11) are separate launches
-        std::vector<uint32_t> xr, whole;
-        for (const SplitRow& x : s.xrows) xr.push_back(x.row);
-        for (const SplitTask& t : s.stasks) whole.push_back(t.row);
-        c->timing.kern_bytes[sd][KIND_STREAM] = alg_bytes(s, whole, c->K, tsz);
-        c->timing.kern_rows[sd][KIND_STREAM] = (uint32_t)whole.size();
-        c->timing.kern_bytes[sd][KIND_SPLIT] = alg_bytes(s, xr, c->K, tsz);
-        c->timing.kern_rows[sd][KIND_SPLIT] = (uint32_t)xr.size();
         std::vector<uint32_t> gr;
         for (const GramRow& g : s.grows) gr.push_back(g.row);
         c->timing.kern_bytes[sd][KIND_GRAM] = alg_bytes(s, gr, c->K, tsz);
@@ -681,9 +694,9 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // ---- column statistics with the current mu (:378-381, :397-401)
         const T* hyp = c->d_hyper.as<T>();
         double* colpart = c->d_colpart.as<double>();
-        HIPCHK(launch_colstats<T>(c->d_U.as<T>(), K, c->Kp, 0, c->I, hyp + K, colpart, st));
+        HIPCHK(launch_colstats<T>(c->d_U.as<T>(), K, c->Kp, 0, c->I, hyp + c->Kp, colpart, st));
         HIPCHK(launch_sum_cols(colpart, (c->I + 255) / 256, 2 * K, d_res + RES_COL, st));
-        HIPCHK(launch_colstats<T>(c->d_V.as<T>(), K, c->Kp, 0, c->J, hyp + 3 * K, colpart, st));
+        HIPCHK(launch_colstats<T>(c->d_V.as<T>(), K, c->Kp, 0, c->J, hyp + 3 * c->Kp, colpart, st));
         HIPCHK(launch_sum_cols(colpart, (c->J + 255) / 256, 2 * K, d_res + RES_COL + 2 * K, st));
         c->timing.n_launch += 5;
         HIPCHK(hipMemcpyAsync(c->h_res.data(), d_res, c->h_res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -713,12 +726,13 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             c->mu_v[k] = mv_star + sd(sv_star) * hs.z_mv[k];
         }
         {
-            std::vector<T> h(4 * (size_t)K);
+            const size_t Kp = c->Kp;
+            std::vector<T> h(4 * Kp, T(0));
             for (uint32_t k = 0; k < K; ++k) {
                 h[k] = (T)c->sig_u[k];
-                h[K + k] = (T)c->mu_u[k];
-                h[2 * K + k] = (T)c->sig_v[k];
-                h[3 * K + k] = (T)c->mu_v[k];
+                h[Kp + k] = (T)c->mu_u[k];
+                h[2 * Kp + k] = (T)c->sig_v[k];
+                h[3 * Kp + k] = (T)c->mu_v[k];
             }
             HIPCHK(hipMemcpyAsync(c->d_hyper.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st));
             if (ref) {  // user variates then item variates (:485 then :529)
@@ -780,10 +794,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         for (int sd = 0; sd < 2; ++sd) {
             const Side& sdd = sd == 0 ? c->users : c->items;
             for (int k = 0; k < SBMF_NKIND; ++k) {
-                const bool ran = k == KIND_GRAM    ? !sdd.gitems.empty()
-                                 : k == KIND_SPLIT ? !sdd.xrows.empty()
-                                 : k == KIND_STREAM ? !sdd.stasks.empty()
-                                                    : !sdd.bin_rows[k].empty();
+                const bool ran = k == KIND_GRAM ? !sdd.gitems.empty() : !sdd.bin_rows[k].empty();
                 c->timing.kern_ms[sd][k] = ran ? ev_ms(c->kev[sd][k][0], c->kev[sd][k][1]) : 0.0;
             }
         }

@@ -118,7 +118,7 @@ class FMLearnSBPMF:
 
     def __init__(self, num_factor=20, num_iter=100, seed=1, rng="ref", quirks="final", precision="f64", burnin=0,
                  device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, row_kernel=0,
-                 stream_threshold=0, split_chunk=0, **hyper):
+                 stream_threshold=0, split_chunk=0, tune=0, **hyper):
         self.cfg = config_default()
         self.cfg.num_factor = num_factor
         self.cfg.num_iter = num_iter
@@ -136,6 +136,7 @@ class FMLearnSBPMF:
         self.cfg.row_kernel = row_kernel
         self.cfg.stream_threshold = stream_threshold
         self.cfg.split_chunk = split_chunk
+        self.cfg.tune = tune
         for k, v in hyper.items():
             setattr(self.cfg, k, v)
         self.ctx = None

@@ -15,9 +15,9 @@ SBMF_OK, SBMF_E_ARG, SBMF_E_STATE, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_COMM, SBMF_E
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 QUIRKS_FINAL, QUIRKS_SBPMF2, QUIRKS_NONE = 0, 1, 2
 F64, F32 = 0, 1
-NKIND = 12  # SBMF_NKIND
+NKIND = 11  # SBMF_NKIND
 KIND_NAMES = ['gblock_w4', 'gblock_w16', 'gblock_b2', 'gblock_b4', 'gblock_b8', 'gstream', 'rows_w2', 'rows_w8',
-              'rows_b4', 'rows_b8', 'gram', 'gsplit']
+              'rows_b4', 'rows_b8', 'gram']
 
 
 class Config(C.Structure):
@@ -29,7 +29,7 @@ class Config(C.Structure):
         ("nu0", C.c_double), ("mu0", C.c_double),
         ("recompute_every", C.c_uint32), ("eval_train", C.c_uint32), ("eval_test", C.c_uint32),
         ("gram_threshold", C.c_uint32), ("row_kernel", C.c_uint32), ("stream_threshold", C.c_uint32),
-        ("split_chunk", C.c_uint32), ("reserved", C.c_uint32 * 5),
+        ("split_chunk", C.c_uint32), ("tune", C.c_uint32), ("reserved", C.c_uint32 * 4),
     ]
 
 

@@ -42,7 +42,23 @@ def _degrees(rng, n, total, dmin, dmax, kind):
 
 def generate(shape="ml-20m", seed=2015, rank=10, noise=0.5, test_frac=0.1):
     """Returns (train, test, (num_users, num_items)); train/test are
-    (user uint32, item uint32, rating float64) in random file order."""
+    (user uint32, item uint32, rating float64) in random file order.
+    With $SBMF_SYNTH_CACHE set, the arrays are cached there as .npz."""
+    import os
+    cache = os.environ.get("SBMF_SYNTH_CACHE")
+    if cache:
+        path = os.path.join(cache, "synth_%s_s%d_r%d_n%g_t%g.npz" % (shape, seed, rank, noise, test_frac))
+        if os.path.exists(path):
+            z = np.load(path)
+            return ((z["tu"], z["ti"], z["tr"]), (z["su"], z["si"], z["sr"]), (int(z["I"]), int(z["J"])))
+        train, test, dims = _generate(shape, seed, rank, noise, test_frac)
+        os.makedirs(cache, exist_ok=True)
+        np.savez(path, tu=train[0], ti=train[1], tr=train[2], su=test[0], si=test[1], sr=test[2], I=dims[0], J=dims[1])
+        return train, test, dims
+    return _generate(shape, seed, rank, noise, test_frac)
+
+
+def _generate(shape, seed, rank, noise, test_frac):
     I, J, total, umax, imax = SHAPES[shape]
     rng = np.random.default_rng(seed)
     du = _degrees(rng, I, total, min(20, umax), umax, "pareto")

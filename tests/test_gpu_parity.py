@@ -121,6 +121,20 @@ def test_split_rows_match_oracle(ml100k, chunk, K):
     np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("tune", [0, 1, 2, 3])
+def test_kernel_variants_match_oracle(ml100k, tune):
+    """Kernel variants (sbmf_config.tune): residual update by 16-lane DPP sums
+    (bit 0 clear) or on the matrix cores through an LDS transpose (bit 0 set),
+    streaming kernel in 8-wave (bit 1 clear) or 4-wave workgroups (bit 1 set)."""
+    tr, te = ml100k
+    o = oracle.run(tr, te, K=50, iters=3, seed=4)
+    for kw in ({}, {"stream_threshold": 40, "split_chunk": 64}):
+        L = _run(tr, te, 3, num_factor=50, seed=4, tune=tune, **kw)
+        U, V = L.factors()
+        assert np.abs(U - o["U"]).max() < 1e-7
+        assert np.abs(V - o["V"]).max() < 1e-7
+
+
 def test_split_rows_deterministic(ml100k):
     tr, te = ml100k
     a = _run(tr, te, 3, num_factor=32, seed=2, rng="philox", stream_threshold=40, split_chunk=50)
