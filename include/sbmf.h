@@ -87,8 +87,8 @@ typedef struct sbmf_config {
                                  into chunks on co-resident workgroups (0 = the LDS capacity,
                                  1792 f64 / 3584 f32; larger values are capped to it)            */
     uint32_t tune;            /* kernel-variant bits for experiments (0 = tuned defaults):
-                                 bit 0 = residual update of the Gram-block kernels on MFMA,
-                                 bit 1 = streaming kernel in 4-wave workgroups (4 per CU)        */
+                                 bit 0 = block solve replicated in every wave of a row
+                                 (default: one wave solves, D shared through LDS)                */
     uint32_t reserved[4];
 } sbmf_config;
 

@@ -12,16 +12,16 @@ template <typename T>
 struct HalfArgs {
     const uint32_t* ptr;   // [R+1] rating offsets of this orientation
     const uint32_t* part;  // [N] partner row id per rating
-    const uint32_t* perm;  // [N] position of the rating in the other orientation (E gather)
-    const T* E_in;         // [N] residuals in the other orientation's order
-    T* E_out;              // [N] residuals in this orientation's order
+    const uint32_t* perm;  // [N] position of the rating in the other orientation's order
+    const T* E_this;       // [N] residuals in this orientation's order (read sequentially)
+    T* E_other;            // [N] residuals in the other orientation's order: E_other[perm[q]] (scatter)
     const T* r_this;       // [N] ratings in this order (E_FROM_DOT, train RMSE, Gram update)
     T* own;                // [R][Kp]
     const T* partner;      // [P+2][Kp]: row P is all zeros (sentinel), row P+1 slack
     const T* sig;          // [Kp] precision hyperparameter of this side (zero padded)
     const T* mu;           // [Kp] mean hyperparameter of this side (zero padded)
     uint32_t zrow;         // P: the partner table's zero row (ratings past a row's end point here)
-    const T* zbuf;         // reference mode: [R][K] N(0,1) variates; nullptr -> Philox
+    const T* zbuf;         // [R][K] N(0,1) variates of this half (host reference stream or launch_philox_fill)
     T tau;
     uint32_t K, Kp;
     int sd_is_var;         // quirk FINAL/SBPMF2: posterior variance used as stdev
@@ -31,7 +31,7 @@ struct HalfArgs {
     double* row_tr;        // [R] per-row train squared error of the clamped sample (or null)
     T lo, hi;
     int e_from_dot;        // 1: e0 = r - own.partner (no gather; multi-GPU)
-    uint32_t tune;         // kernel variant bits (sbmf_config.tune): bit 0 = residual update on MFMA
+    uint32_t tune;         // kernel variant bits (sbmf_config.tune): bit 0 = replicated block solve
 };
 
 // Heavy-row (Gram route) work description.
@@ -93,6 +93,7 @@ struct SplitSync {
     void* newown;        // [nchunk_total][Kp] (T), slot slab0 of each split row
     uint32_t* timeout;   // set to 1 if a spin gave up
     uint32_t cmax;       // ratings per task (LDS-resident partner ids and residuals)
+    unsigned long long* prof;  // [8] phase cycles of wave 0 (SBMF_KPROF diagnostics) or null
 };
 // Largest task (ratings) the streaming kernel keeps in LDS with two
 // workgroups per CU, for the kernel variant `tune`.
@@ -123,8 +124,9 @@ hipError_t launch_gram(const GramItem* items, uint32_t nitems, const GramRow* gr
 // E = r - dot(own, partner) over all ratings of the orientation (row-major
 // walk; one wave per row) + per-row sum of squares.  own rows [r0,r1).
 template <typename T>
-hipError_t launch_resid(const uint32_t* ptr, const uint32_t* part, const T* r, const T* own, const T* partner,
-                        uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, T* E, double* row_sq, hipStream_t st);
+hipError_t launch_resid(const uint32_t* ptr, const uint32_t* part, const uint32_t* perm, const T* r, const T* own,
+                        const T* partner, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, T* E_other,
+                        double* row_sq, hipStream_t st);
 
 // Column partials over table rows [r0,r1): out[c][0..K) = sum (x-mu)^2,
 // out[c][K..2K) = sum x, c = chunk of 256 rows (global chunk index).
@@ -146,6 +148,11 @@ hipError_t launch_sum(const double* in, uint64_t n, double* out, double* scratch
 hipError_t launch_sum_cols(const double* in, uint32_t nchunk, uint32_t width, double* out, hipStream_t st);
 
 // Philox init: tab[r][k] = sd * z(seed, sweep=0xffffffff, tag, r, k), rows [r0,r1).
+// z[row][k] = N(0,1) Philox normal (seed, sweep, tag, row, pair k/2) for rows [r0, r1):
+// the per-half variates of throughput mode, the same stream the kernels drew inline.
+template <typename T>
+hipError_t launch_philox_fill(T* z, uint32_t K, uint32_t r0, uint32_t r1, uint64_t seed, uint32_t sweep, uint32_t tag,
+                              hipStream_t st);
 template <typename T>
 hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, double sd, uint64_t seed,
                               uint32_t tag, hipStream_t st);

@@ -136,14 +136,10 @@ __global__ __launch_bounds__(64 * NW * RPB) void k_rows(const uint32_t* __restri
 #pragma unroll
     for (int zs = 0; zs < ZS; ++zs) {
         const uint32_t i0 = 128 * zs + 2 * lane;
-        if (a.zbuf) {
+        {  // per-half normals (host reference stream or launch_philox_fill)
             z_r[zs][0] = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
             z_r[zs][1] = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
-        } else {
-            double z0, z1;
-            philox_normal_pair(a.seed, row, a.sweep, a.tag, 64 * zs + lane, z0, z1);
-            z_r[zs][0] = (T)z0;
-            z_r[zs][1] = (T)z1;
+
         }
     }
 
@@ -188,7 +184,7 @@ __global__ __launch_bounds__(64 * NW * RPB) void k_rows(const uint32_t* __restri
     } else {
 #pragma unroll
         for (int t = 0; t < MMAX; ++t)
-            if (ok[t]) e[t] = a.E_in[a.perm[beg + g + t * G]];
+            if (ok[t]) e[t] = a.E_this[beg + g + t * G];
     }
 
     __shared__ T red[NW > 1 ? 2 : 1][NW][2];
@@ -266,7 +262,7 @@ __global__ __launch_bounds__(64 * NW * RPB) void k_rows(const uint32_t* __restri
     for (int t = 0; t < MMAX; ++t) {
         if (ok[t]) {
             const uint32_t idx = beg + g + t * G;
-            a.E_out[idx] = e[t];
+            a.E_other[a.perm[idx]] = e[t];
             sq += e[t] * e[t];
             if (a.row_tr) {
                 const T r = a.r_this[idx];
@@ -369,34 +365,6 @@ __device__ __forceinline__ void lds_barrier() {
 constexpr int GB = 16;      // k per block
 constexpr int GLD = GB + 1; // padded LDS row (conflict-free row reads)
 
-// e -= S D for 4 vectors (16 ratings) on the matrix cores.  Lane l = 16r'+i
-// holds s[v][l] = S[rating (v, r')][i].  The tile goes through LDS (one
-// 16 x GLD buffer per wave, `tile`) into the MFMA A layout, A[m][kk] =
-// S[m][4q+kk] with tile row m = MfmaT::row(l, v) -- the accumulator row that
-// lane l reads back in register v -- and B[kk][n] = D[4q+kk] (bD[q], the same
-// for every n).  After 4 MFMAs lane l's register v holds (S D) of rating
-// (v, r').  LDS ops of one wave execute in order, so the buffer can be
-// rewritten right after it is read.  nv < 4: the unused tile rows are never
-// read back (an MFMA output row only depends on its own A row).
-template <typename T, int NV>
-__device__ __forceinline__ void e_update_mfma(T* __restrict__ tile, const T (&s)[NV], const T (&bD)[4], T (&e)[NV],
-                                              int lane) {
-    typedef typename MfmaT<T>::acc_t acc_t;
-    const int ci = lane & 15, rr = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < (NV + 3) / 4; ++t) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-            if (4 * t + v < NV) tile[MfmaT<T>::row(lane, v) * GLD + ci] = s[4 * t + v];
-        acc_t y = {T(0), T(0), T(0), T(0)};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) y = MfmaT<T>::mfma2(tile[ci * GLD + 4 * q + rr], bD[q], y);
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-            if (4 * t + v < NV) e[4 * t + v] -= y[v];
-    }
-}
-
 // The 16 draws of a block in "gamma form": with H[c][l] = Bq_c G[c][l] for
 // l < c (0 otherwise) and gamma_c = A_c - old_c + Bq_c (c_c + P_c old_c),
 // step j reads d_j = gamma_j (final: it only receives corrections from
@@ -425,7 +393,7 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
     return gam;
 }
 
-template <typename T, int V, int NW, int RPW, bool EM>
+template <typename T, int V, int NW, int RPW, bool SW>
 __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const uint32_t* __restrict__ rows,
                                                                      uint32_t nrows, HalfArgs<T> a) {
     typedef typename MfmaT<T>::acc_t acc_t;
@@ -446,29 +414,18 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
     __shared__ T Ps[NWAVE][GB];               // diagonal of G_B
     __shared__ T Cs[NWAVE][GB];               // c_B
     __shared__ T newS[NW > 1 ? 256 : 1];
-    __shared__ T Ts[EM ? NWAVE : 1][GB * GLD];  // per-wave S tile for the MFMA residual update
-    __shared__ T Ds[EM ? NWAVE : 1][GB];        // per-wave copy of the block's D
+    __shared__ T Dsh[GB];                     // SW: the block's D from the solving wave
     const int ws = NW > 1 ? 0 : wv;           // LDS slot holding this row's reduced G / c
 
     // per-row normals: lane l holds z for k = 2l, 2l+1 (zA) and 128+2l, 129+2l (zB)
     T zA0, zA1, zB0 = T(0), zB1 = T(0);
-    if (a.zbuf) {
+    {  // per-half normals (host reference stream or launch_philox_fill)
         const uint32_t i0 = 2 * lane;
         zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
         zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
         if (K > 128) {
             zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
             zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
-        }
-    } else {
-        double z0, z1;
-        philox_normal_pair(a.seed, row, a.sweep, a.tag, lane, z0, z1);
-        zA0 = (T)z0;
-        zA1 = (T)z1;
-        if (K > 128) {
-            philox_normal_pair(a.seed, row, a.sweep, a.tag, 64 + lane, z0, z1);
-            zB0 = (T)z0;
-            zB1 = (T)z1;
         }
     }
 
@@ -501,7 +458,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-            e[v] = q < n ? a.E_in[a.perm[beg + q]] : T(0);
+            e[v] = q < n ? a.E_this[beg + q] : T(0);
         }
     }
 
@@ -567,46 +524,48 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own LDS writes visible to own reads
             __builtin_amdgcn_wave_barrier();
         }
-        // ---- 3. the 16 sequential draws (every wave redundantly for NW>1: no extra barrier)
-        const T P = Ps[ws][ci];
-        const T old = oldc, sg = sgc, mu = muc;
-        // z_kk lives in lane (kk>>1)&63 of zA (kk<128) or zB
-        const int zl = (int)((kk >> 1) & 63);
-        // shuffle both registers, then pick by this lane's own parity (the
-        // source lane's select would use the source lane's k)
-        const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
-        T z = (kk & 1) ? za1 : za0;
-        if (K > 128) {
-            const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
-            z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
-        }
-        const T var = kin ? T(1) / (sg + tau * P) : T(0);  // k >= K: var = 0 -> d = -old = 0
-        const T sd = a.sd_is_var ? var : tsqrt(var);
-        const T A = var * sg * mu + sd * z;
-        const T Bq = var * tau;
-        T H[GB];
+        // ---- 3. the 16 sequential draws: every wave of the row redundantly
+        // (no barrier), or -- SW, multi-wave rows -- wave 0 alone, handing D
+        // to the others through LDS (their issue slots go to other rows)
+        T dlt = T(0);
+        if (!(SW && NW > 1) || wr == 0) {
+            const T P = Ps[ws][ci];
+            const T old = oldc, sg = sgc, mu = muc;
+            // z_kk lives in lane (kk>>1)&63 of zA (kk<128) or zB
+            const int zl = (int)((kk >> 1) & 63);
+            // shuffle both registers, then pick by this lane's own parity (the
+            // source lane's select would use the source lane's k)
+            const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
+            T z = (kk & 1) ? za1 : za0;
+            if (K > 128) {
+                const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
+                z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
+            }
+            const T var = kin ? T(1) / (sg + tau * P) : T(0);  // k >= K: var = 0 -> d = -old = 0
+            const T sd = a.sd_is_var ? var : tsqrt(var);
+            const T A = var * sg * mu + sd * z;
+            const T Bq = var * tau;
+            T H[GB];
 #pragma unroll
-        for (int j = 0; j < GB; ++j) H[j] = Bq * Ls[ws][ci][j];
-        const T dlt = gblock_solve(H, A - old + Bq * (Cs[ws][ci] + P * old));
-        const T nwv = old + dlt;
-        if constexpr (NW > 1) {
-            // staged in LDS, written after the last barrier: no wave of this
-            // row can still have a load of the same own value in flight
-            if (wr == 0 && lane < GB && kin) newS[kk] = nwv;
-        } else {
-            if (lane < GB && kin) a.own[(size_t)row * Kp + kk] = nwv;  // one wave: program order
+            for (int j = 0; j < GB; ++j) H[j] = Bq * Ls[ws][ci][j];
+            dlt = gblock_solve(H, A - old + Bq * (Cs[ws][ci] + P * old));
+            const T nwv = old + dlt;
+            if constexpr (NW > 1) {
+                // staged in LDS, written after the last barrier: no wave of this
+                // row can still have a load of the same own value in flight
+                if (wr == 0 && lane < GB && kin) newS[kk] = nwv;
+                if (SW && lane < GB) Dsh[lane] = dlt;
+            } else {
+                if (lane < GB && kin) a.own[(size_t)row * Kp + kk] = nwv;  // one wave: program order
+            }
         }
-        // ---- 4. e -= S_B D_B (every 16-lane group computed the same d: lane (r,i) holds D_i)
-        if constexpr (EM) {  // on the matrix cores
-            if (lane < GB) Ds[wv][lane] = dlt;
-            T bD[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bD[q] = Ds[wv][4 * q + rr];
-            e_update_mfma<T, V>(Ts[wv], s, bD, e, lane);
-        } else {  // 16-lane DPP row sums
-#pragma unroll
-            for (int v = 0; v < V; ++v) e[v] -= row16_sum(s[v] * dlt);
+        if constexpr (SW && NW > 1) {
+            lds_barrier();
+            dlt = Dsh[ci];
         }
+        // ---- 4. e -= S_B D_B (lane (r,i) holds D_i): 16-lane DPP row sums
+#pragma unroll
+        for (int v = 0; v < V; ++v) e[v] -= row16_sum(s[v] * dlt);
 #pragma unroll
         for (int v = 0; v < V; ++v) s[v] = sn[v];
         oldc = oldn;
@@ -624,7 +583,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
         if (q < n && ci == 0) {
-            a.E_out[beg + q] = e[v];
+            a.E_other[a.perm[beg + q]] = e[v];
             sq += e[v] * e[v];
             if (a.row_tr) {
                 const T r = a.r_this[beg + q];
@@ -671,13 +630,22 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
 // stores -> agent release -> counter; poll -> agent acquire -> loads, the
 // CDNA guide's G16 hand-off); every chunk sums them in chunk order, so all
 // chunks draw identical coordinates.  Wave w owns vectors w, w+NW, ...
-constexpr uint32_t GSTREAM_PAD = 4 * 8 * 8;  // traversal stride of k_gstream<T, 8, 8> (ratings)
-// dynamic LDS: [cmax+pad] partner ids, then (16-byte aligned) [cmax+pad] residuals
+// Padding of a task's LDS arrays: two traversal strides (4*NW*UNR <= 256
+// ratings) -- the task rounded up to a stride, plus the group a prefetching
+// traversal reads past its end.  The residual array is followed by 8 x 64
+// per-lane sink slots for masked-off stores.
+constexpr uint32_t GSTREAM_PAD = 2 * 4 * 8 * 8;
+constexpr uint32_t GSTREAM_SINK = 8 * 64;
+// dynamic LDS: [cmax+pad] partner ids, then (16-byte aligned) [cmax+pad+sink] residuals
 __host__ __device__ constexpr size_t gstream_ids_bytes(uint32_t cmax) {
     return ((size_t)(cmax + GSTREAM_PAD) * sizeof(uint32_t) + 15) / 16 * 16;
 }
+template <typename T>
+__host__ __device__ constexpr size_t gstream_dyn_bytes(uint32_t cmax) {
+    return gstream_ids_bytes(cmax) + (size_t)(cmax + GSTREAM_PAD + GSTREAM_SINK) * sizeof(T);
+}
 
-template <typename T, int NW, int UNR, bool EM>
+template <typename T, int NW, int UNR, bool SW>
 __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restrict__ tasks, uint32_t ntask,
                                                      HalfArgs<T> a, SplitSync sy) {
     typedef typename MfmaT<T>::acc_t acc_t;
@@ -692,8 +660,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
     __shared__ T Cs[NW][GB];
     __shared__ double red2[NW][2];
     __shared__ T newS[256];           // new own values of the row, written once at the end
-    __shared__ T Ts[EM ? NW : 1][GB * GLD];  // per-wave S tile for the MFMA residual update
-    __shared__ T Ds[EM ? NW : 1][GB];        // per-wave copy of the previous block's D
+    __shared__ T Dsh[GB];             // SW: the block's D from the solving wave
     extern __shared__ unsigned char dyn_lds[];
     uint32_t* pjL = reinterpret_cast<uint32_t*>(dyn_lds);  // [cmax+pad] partner ids
     T* eL = reinterpret_cast<T*>(dyn_lds + gstream_ids_bytes(sy.cmax));  // [cmax+pad] residuals
@@ -710,7 +677,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
         const uint32_t nvec = (n + 3) / 4;
 
         T zA0, zA1, zB0 = T(0), zB1 = T(0);
-        if (a.zbuf) {
+        {  // per-half normals (host reference stream or launch_philox_fill)
             const uint32_t i0 = 2 * lane;
             zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
             zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
@@ -718,22 +685,21 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
                 zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
                 zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
             }
-        } else {
-            double z0, z1;
-            philox_normal_pair(a.seed, row, a.sweep, a.tag, lane, z0, z1);
-            zA0 = (T)z0;
-            zA1 = (T)z1;
-            if (K > 128) {
-                philox_normal_pair(a.seed, row, a.sweep, a.tag, 64 + lane, z0, z1);
-                zB0 = (T)z0;
-                zB1 = (T)z1;
-            }
         }
 
+        // optional phase profile (SBMF_KPROF): wave 0's cycles per phase
+        unsigned long long tp = (sy.prof && threadIdx.x == 0) ? clock64() : 0ull;
+        auto stamp = [&](int ph) {
+            if (sy.prof && threadIdx.x == 0) {
+                const unsigned long long now = clock64();
+                atomicAdd(&sy.prof[ph], now - tp);
+                tp = now;
+            }
+        };
         // ---- stage the task's partner ids and initial residuals in LDS; the
         // slots up to the traversal stride (4*NW*UNR ratings) hold the zero
         // row and zero residuals, so the traversal needs no per-rating masks
-        const uint32_t npad = (n + 4 * NW * UNR - 1) / (4 * NW * UNR) * (4 * NW * UNR);
+        const uint32_t npad = (n + 4 * NW * UNR - 1) / (4 * NW * UNR) * (4 * NW * UNR) + 4 * NW * UNR;
         for (uint32_t x = threadIdx.x; x < npad; x += 64 * NW) pjL[x] = x < n ? a.part[beg + x] : a.zrow;
         for (uint32_t x = n + threadIdx.x; x < npad; x += 64 * NW) eL[x] = T(0);
         if (a.e_from_dot) {
@@ -748,56 +714,67 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
                 if (q < n && ci == 0) eL[q] = a.r_this[beg + q] - d;
             }
         } else {
-            for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) eL[x] = a.E_in[a.perm[beg + x]];
+            for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) eL[x] = a.E_this[beg + x];
         }
         __syncthreads();
+        stamp(0);  // staging
 
         double sq = 0.0, trs = 0.0;
-        T Dl = T(0);  // (DPP path) D of the previous block, lane (r,i) holds D_i
+        T Dl = T(0);  // D of the previous block, lane (r,i) holds D_i
         T oldn = a.own[(size_t)row * Kp + ci];  // block 0's old values (padding columns are zero)
+        // Traversal over the task's padded vectors, specialised by phase so
+        // the group body is straight-line code (a branch around a load makes
+        // the compiler drain every outstanding load at the join):
+        //   PH 0: t = 0     accumulate block 0 only
+        //   PH 1: 0<t<nblk  apply block t-1, accumulate block t
+        //   PH 2: t = nblk  apply the last block, emit residuals
+        // All loads are unconditional: the unused slice of phases 0 / 2 reads
+        // a valid column (padding / slack row) and is ignored.
+        T* const eDummy = eL + (size_t)(sy.cmax + GSTREAM_PAD) + 64 * wr;  // per-lane sink of masked stores
         for (uint32_t t = 0; t <= nblk; ++t) {
             const bool app = t > 0, acc = t < nblk;
-            const uint32_t kp = (t - 1) * GB + ci, kc = t * GB + ci;
-            const bool last = t == nblk;
+            const uint32_t kc = t * GB + ci;
+            const uint32_t kp = app ? kc - GB : kc;
             acc_t g = {T(0), T(0), T(0), T(0)};
             T cc = T(0);
-            T bD[4];  // (MFMA path) B operand of the residual update: D_{t-1}[4q + (lane>>4)]
+            auto traverse = [&](auto phase) {
+                constexpr int PH = decltype(phase)::value;
+                auto load = [&](uint32_t v0, T (&sp)[UNR], T (&sc)[UNR], T (&e)[UNR]) {
+                    uint32_t pj[UNR];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) bD[q] = (EM && app) ? Ds[EM ? wr : 0][4 * q + rr] : T(0);
-            for (uint32_t v0 = wr; v0 < nvec; v0 += NW * UNR) {
-                T sp[UNR], sc[UNR], e[UNR];
-                uint32_t pj[UNR];
+                    for (int u = 0; u < UNR; ++u) {
+                        const uint32_t q = 4 * (v0 + u * NW) + rr;  // < npad: padded slots
+                        pj[u] = pjL[q];
+                        e[u] = eL[q];
+                    }
 #pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    const uint32_t q = 4 * (v0 + u * NW) + rr;  // < npad: padded slots
-                    pj[u] = pjL[q];
-                    e[u] = eL[q];
-                }
-#pragma unroll
-                for (int u = 0; u < UNR; ++u) {
-                    // zero row / zero padding columns / slack row: no per-lane masks
-                    const T* src = a.partner + (size_t)pj[u] * Kp;
-                    sp[u] = app ? src[kp] : T(0);
-                    sc[u] = acc ? src[kc] : T(0);
-                }
-                if (app) {
-                    if constexpr (EM) {
-                        e_update_mfma<T, UNR>(Ts[wr], sp, bD, e, lane);
-                    } else {
+                    for (int u = 0; u < UNR; ++u) {
+                        const T* src = a.partner + (size_t)pj[u] * Kp;
+                        if constexpr (PH != 0) sp[u] = src[kp];
+                        if constexpr (PH != 2) sc[u] = src[kc];
+                    }
+                };
+                auto proc = [&](uint32_t v0, const T (&sp)[UNR], const T (&sc)[UNR], T (&e)[UNR]) {
+                    if constexpr (PH != 0) {
 #pragma unroll
                         for (int u = 0; u < UNR; ++u) e[u] -= row16_sum(sp[u] * Dl);
                     }
-                    if (ci == 0) {
+                    if constexpr (PH == 1) {
+                        // lane ci == 0 of each rating writes its residual back (the
+                        // same lanes of the same wave read it next traversal); the
+                        // other lanes write a private dummy slot: no branch
 #pragma unroll
-                        for (int u = 0; u < UNR; ++u)  // the same lanes of the same wave read it next traversal
-                            eL[4 * (v0 + u * NW) + rr] = e[u];
+                        for (int u = 0; u < UNR; ++u) {
+                            T* dst = ci == 0 ? &eL[4 * (v0 + u * NW) + rr] : &eDummy[lane];
+                            *dst = e[u];
+                        }
                     }
-                    if (last) {
+                    if constexpr (PH == 2) {
 #pragma unroll
                         for (int u = 0; u < UNR; ++u) {
                             const uint32_t q = 4 * (v0 + u * NW) + rr;
                             if (q < n && ci == 0) {
-                                a.E_out[beg + q] = e[u];
+                                a.E_other[a.perm[beg + q]] = e[u];
                                 sq += (double)(e[u] * e[u]);
                                 if (a.row_tr) {
                                     const T r = a.r_this[beg + q];
@@ -809,15 +786,27 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
                             }
                         }
                     }
-                }
-                if (acc) {
+                    if constexpr (PH != 2) {
 #pragma unroll
-                    for (int u = 0; u < UNR; ++u) {
-                        g = MfmaT<T>::mfma(sc[u], g);
-                        cc += sc[u] * e[u];
+                        for (int u = 0; u < UNR; ++u) {
+                            g = MfmaT<T>::mfma(sc[u], g);
+                            cc += sc[u] * e[u];
+                        }
                     }
+                };
+                for (uint32_t v0 = wr; v0 < nvec; v0 += NW * UNR) {
+                    T sp[UNR], sc[UNR], e[UNR];
+                    load(v0, sp, sc, e);
+                    proc(v0, sp, sc, e);
                 }
-            }
+            };
+            if (t == 0)
+                traverse(std::integral_constant<int, 0>{});
+            else if (t < nblk)
+                traverse(std::integral_constant<int, 1>{});
+            else
+                traverse(std::integral_constant<int, 2>{});
+            stamp(1);  // traversal
             if (!acc) break;
             const T old = oldn;  // loaded before this block's barriers: never sees the new value
             const uint32_t kk = kc;
@@ -826,6 +815,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
             cc += shfl_xor_t(cc, 16);
             cc += shfl_xor_t(cc, 32);
             __syncthreads();  // previous block's solve reads of Ls/Ps/Cs[0] are done
+            stamp(2);  // wait for the workgroup's other waves
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int r = MfmaT<T>::row(lane, j);
@@ -854,6 +844,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
                 }
             }
             __syncthreads();
+            stamp(3);  // G / c partials and their cross-wave reduction
             if (nch > 1) {
                 // ---- cross-workgroup reduction of (G_B, c_B) over the row's chunks
                 // slab: [lower part + diagonal as a 16x16 image | c]
@@ -897,28 +888,35 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
                 }
                 __syncthreads();
             }
-            // ---- the 16 draws (every wave of every chunk: identical inputs -> identical results)
-            const T P = Ps[0][ci];
-            const T sg = a.sig[kk];  // zero padded
-            const T mu = a.mu[kk];
-            const int zl = (int)((kk >> 1) & 63);
-            const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
-            T z = (kk & 1) ? za1 : za0;
-            if (K > 128) {
-                const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
-                z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
+            stamp(4);  // split-row exchange
+            // ---- the 16 draws: every wave of every chunk (identical inputs ->
+            // identical results), or -- SW -- wave 0 alone, D handed over in LDS
+            T dlt = T(0);
+            if (!SW || wr == 0) {
+                const T P = Ps[0][ci];
+                const T sg = a.sig[kk];  // zero padded
+                const T mu = a.mu[kk];
+                const int zl = (int)((kk >> 1) & 63);
+                const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
+                T z = (kk & 1) ? za1 : za0;
+                if (K > 128) {
+                    const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
+                    z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
+                }
+                const T var = kin ? T(1) / (sg + tau * P) : T(0);
+                const T sd = a.sd_is_var ? var : tsqrt(var);
+                const T A = var * sg * mu + sd * z;
+                const T Bq = var * tau;
+                dlt = gblock_solve_lds(&Ls[0][ci][0], Bq, A - old + Bq * (Cs[0][ci] + P * old));
+                if (wr == 0 && lane < GB && kin) newS[kk] = old + dlt;
+                if (SW && lane < GB) Dsh[lane] = dlt;
             }
-            const T var = kin ? T(1) / (sg + tau * P) : T(0);
-            const T sd = a.sd_is_var ? var : tsqrt(var);
-            const T A = var * sg * mu + sd * z;
-            const T Bq = var * tau;
-            const T dlt = gblock_solve_lds(&Ls[0][ci][0], Bq, A - old + Bq * (Cs[0][ci] + P * old));
-            if (wr == 0 && lane < GB && kin) newS[kk] = old + dlt;
-            if constexpr (EM) {
-                if (lane < GB) Ds[wr][lane] = dlt;  // every wave solved identically: its own copy
-            } else {
-                Dl = dlt;  // every 16-lane group solved identically: lane (r,i) holds D_i
+            if constexpr (SW) {
+                __syncthreads();
+                dlt = Dsh[ci];
             }
+            Dl = dlt;  // lane (r,i) holds D_i
+            stamp(5);  // solve
         }
         __syncthreads();
         // ---- new own row: whole rows write it, split rows stage it (k_split_finish publishes)
@@ -952,6 +950,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
             }
         }
         __syncthreads();  // LDS (ids, residuals, newS, red2) is reused by the next task
+        stamp(6);  // task epilogue
     }
 }
 
@@ -1032,7 +1031,7 @@ __global__ __launch_bounds__(256) void k_gram_partial(const GramItem* __restrict
                     for (uint32_t k = 0; k < K; ++k) d += src[k] * ownS[k];
                     ev = a.r_this[idx] - d;
                 } else {
-                    ev = a.E_in[a.perm[idx]];
+                    ev = a.E_this[idx];
                 }
             }
             es[r] = ev;
@@ -1106,14 +1105,10 @@ __global__ __launch_bounds__(256) void k_gram_solve(const GramRow* __restrict__ 
 #pragma unroll
     for (int zs = 0; zs < ZS; ++zs) {
         const uint32_t i0 = 128 * zs + 2 * lane;
-        if (a.zbuf) {
+        {  // per-half normals (host reference stream or launch_philox_fill)
             z_r[zs][0] = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
             z_r[zs][1] = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
-        } else {
-            double z0, z1;
-            philox_normal_pair(a.seed, row, a.sweep, a.tag, 64 * zs + lane, z0, z1);
-            z_r[zs][0] = (T)z0;
-            z_r[zs][1] = (T)z1;
+
         }
     }
     const double* bvec = Gs + (size_t)Kt * Kt;
@@ -1171,7 +1166,7 @@ __global__ __launch_bounds__(256) void k_gram_update(const GramItem* __restrict_
         for (uint32_t k = 0; k < K; ++k) d += src[k] * ownS[k];
         const T r = a.r_this[idx];
         const T e = r - d;
-        a.E_out[idx] = e;
+        a.E_other[a.perm[idx]] = e;
         sq += (double)(e * e);
         if (chunk_tr) {
             T pr = d;
@@ -1216,9 +1211,10 @@ __global__ __launch_bounds__(64) void k_gram_rowsum(const GramRow* __restrict__ 
 // k = 16b + i), so each partner row is read as whole 128-byte lines.
 template <typename T>
 __global__ __launch_bounds__(256) void k_resid(const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ part,
-                                                const T* __restrict__ r, const T* __restrict__ own,
-                                                const T* __restrict__ partner, uint32_t K, uint32_t Kp, uint32_t r0,
-                                                uint32_t r1, T* __restrict__ E, double* __restrict__ row_sq) {
+                                                const uint32_t* __restrict__ perm, const T* __restrict__ r,
+                                                const T* __restrict__ own, const T* __restrict__ partner, uint32_t K,
+                                                uint32_t Kp, uint32_t r0, uint32_t r1, T* __restrict__ E_other,
+                                                double* __restrict__ row_sq) {
     const uint32_t row = r0 + blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= r1) return;
@@ -1245,7 +1241,7 @@ __global__ __launch_bounds__(256) void k_resid(const uint32_t* __restrict__ ptr,
         d = row16_sum(d);
         if (ok && ci == 0) {
             const T e = r[idx] - d;
-            E[idx] = e;
+            E_other[perm[idx]] = e;
             sq += (double)(e * e);
         }
     }
@@ -1355,6 +1351,21 @@ __global__ __launch_bounds__(256) void k_sum_cols(const double* __restrict__ in,
     if (threadIdx.x == 0) out[w] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
+// Per-half normals in throughput mode: z[row][2p + j] = pair p of the Philox
+// stream (seed, row, sweep, tag) -- one thread per pair.
+template <typename T>
+__global__ __launch_bounds__(256) void k_philox_fill(T* __restrict__ z, uint32_t K, uint32_t r0, uint32_t r1,
+                                                     uint64_t seed, uint32_t sweep, uint32_t tag) {
+    const uint32_t npair = (K + 1) / 2;
+    const uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t row = r0 + (uint32_t)(x / npair), p = (uint32_t)(x % npair);
+    if (row >= r1) return;
+    double z0, z1;
+    philox_normal_pair(seed, row, sweep, tag, p, z0, z1);
+    z[(size_t)row * K + 2 * p] = (T)z0;
+    if (2 * p + 1 < K) z[(size_t)row * K + 2 * p + 1] = (T)z1;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_init_philox(T* __restrict__ tab, uint32_t K, uint32_t Kp, uint32_t r0,
                                                       uint32_t r1, double sd, uint64_t seed, uint32_t tag) {
@@ -1410,9 +1421,9 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
     if (a.K > 256) return hipErrorInvalidValue;
     // f64: 8 vectors (32 ratings) per wave; f32: 16 vectors (64 ratings) per wave
     constexpr int V = sizeof(T) == 8 ? 8 : 16;
-    const bool em = a.tune & 1u;
+    const bool sw = !(a.tune & 1u);
 #define SBMF_GBLOCK(V_, NW_, RPW_, GRID_, THR_)                                                  \
-    if (em)                                                                                      \
+    if (sw)                                                                                      \
         k_gblock<T, V_, NW_, RPW_, true><<<GRID_, THR_, 0, st>>>(rows, nrows, a);                \
     else                                                                                         \
         k_gblock<T, V_, NW_, RPW_, false><<<GRID_, THR_, 0, st>>>(rows, nrows, a);
@@ -1439,16 +1450,14 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
     return hipGetLastError();
 }
 
-// tune bit 0: residual update on MFMA; bit 1: 4-wave workgroups (4 per CU)
-// instead of 8-wave workgroups (2 per CU).
-static int gstream_nw(uint32_t tune) { return (tune & 2u) ? 4 : 8; }
-int gstream_wg_target(uint32_t tune) { return (tune & 2u) ? 4 : 2; }
+// Default: the block solve by one wave, D handed to the others in LDS;
+// tune bit 0: every wave solves redundantly (no extra barrier).
+static int gstream_nw(uint32_t) { return 8; }
+int gstream_wg_target(uint32_t) { return 2; }
 
 template <typename T>
 static const void* gstream_fn(uint32_t tune) {
-    if (tune & 2u)
-        return (tune & 1u) ? (const void*)k_gstream<T, 4, 8, true> : (const void*)k_gstream<T, 4, 8, false>;
-    return (tune & 1u) ? (const void*)k_gstream<T, 8, 8, true> : (const void*)k_gstream<T, 8, 8, false>;
+    return (tune & 1u) ? (const void*)k_gstream<T, 8, 8, false> : (const void*)k_gstream<T, 8, 8, true>;
 }
 
 template <typename T>
@@ -1460,7 +1469,7 @@ uint32_t gstream_cmax(uint32_t tune) {
     (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
     // gstream_wg_target workgroups per CU: static + [ids | residuals] each
     const long per_wg = lds_cu / gstream_wg_target(tune) - (long)fa.sharedSizeBytes - 16;
-    const long c = per_wg / (long)(sizeof(uint32_t) + sizeof(T)) - (long)GSTREAM_PAD;
+    const long c = (per_wg - (long)(GSTREAM_SINK * sizeof(T))) / (long)(sizeof(uint32_t) + sizeof(T)) - (long)GSTREAM_PAD;
     const long cap = sizeof(T) == 8 ? 4096 : 8192;
     return (uint32_t)std::max(256L, std::min(cap, c) / 64 * 64);
 }
@@ -1468,7 +1477,7 @@ uint32_t gstream_cmax(uint32_t tune) {
 template <typename T>
 int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune) {
     int n = 0;
-    const size_t dyn = gstream_ids_bytes(cmax) + (size_t)(cmax + GSTREAM_PAD) * sizeof(T);
+    const size_t dyn = gstream_dyn_bytes<T>(cmax);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gstream_fn<T>(tune), 64 * gstream_nw(tune), dyn) != hipSuccess)
         return 1;
     return n;
@@ -1490,7 +1499,7 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     HalfArgs<T> ap = a;
     SplitSync syp = sy;
     void* args[] = {(void*)&tp, (void*)&ntask, (void*)&ap, (void*)&syp};
-    const size_t dyn = gstream_ids_bytes(sy.cmax) + (size_t)(sy.cmax + GSTREAM_PAD) * sizeof(T);
+    const size_t dyn = gstream_dyn_bytes<T>(sy.cmax);
     err = hipLaunchCooperativeKernel(gstream_fn<T>(a.tune), dim3(std::min(grid, ntask)), dim3(64 * gstream_nw(a.tune)),
                                      args, (unsigned)dyn, st);
     if (err != hipSuccess) return err;
@@ -1530,10 +1539,11 @@ hipError_t launch_gram(const GramItem* items, uint32_t nitems, const GramRow* gr
 }
 
 template <typename T>
-hipError_t launch_resid(const uint32_t* ptr, const uint32_t* part, const T* r, const T* own, const T* partner,
-                        uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, T* E, double* row_sq, hipStream_t st) {
+hipError_t launch_resid(const uint32_t* ptr, const uint32_t* part, const uint32_t* perm, const T* r, const T* own,
+                        const T* partner, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, T* E_other,
+                        double* row_sq, hipStream_t st) {
     if (r1 <= r0) return hipSuccess;
-    k_resid<T><<<(r1 - r0 + 3) / 4, 256, 0, st>>>(ptr, part, r, own, partner, K, Kp, r0, r1, E, row_sq);
+    k_resid<T><<<(r1 - r0 + 3) / 4, 256, 0, st>>>(ptr, part, perm, r, own, partner, K, Kp, r0, r1, E_other, row_sq);
     return hipGetLastError();
 }
 
@@ -1581,6 +1591,15 @@ hipError_t launch_sum_cols(const double* in, uint32_t nchunk, uint32_t width, do
 }
 
 template <typename T>
+hipError_t launch_philox_fill(T* z, uint32_t K, uint32_t r0, uint32_t r1, uint64_t seed, uint32_t sweep, uint32_t tag,
+                              hipStream_t st) {
+    if (r1 <= r0 || K == 0) return hipSuccess;
+    const uint64_t n = (uint64_t)(r1 - r0) * ((K + 1) / 2);
+    k_philox_fill<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(z, K, r0, r1, seed, sweep, tag);
+    return hipGetLastError();
+}
+
+template <typename T>
 hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, double sd, uint64_t seed,
                               uint32_t tag, hipStream_t st) {
     if (r1 <= r0) return hipSuccess;
@@ -1597,8 +1616,10 @@ hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint
     template uint32_t gstream_cmax<T>(uint32_t);                                                                    \
     template hipError_t launch_gram<T>(const GramItem*, uint32_t, const GramRow*, uint32_t, double*, T*, double*,   \
                                        double*, const HalfArgs<T>&, hipStream_t);                                    \
-    template hipError_t launch_resid<T>(const uint32_t*, const uint32_t*, const T*, const T*, const T*, uint32_t,     \
-                                        uint32_t, uint32_t, uint32_t, T*, double*, hipStream_t);                     \
+    template hipError_t launch_resid<T>(const uint32_t*, const uint32_t*, const uint32_t*, const T*, const T*,       \
+                                        const T*, uint32_t, uint32_t, uint32_t, uint32_t, T*, double*, hipStream_t); \
+    template hipError_t launch_philox_fill<T>(T*, uint32_t, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t,        \
+                                              hipStream_t);                                                          \
     template hipError_t launch_colstats<T>(const T*, uint32_t, uint32_t, uint32_t, uint32_t, const T*, double*,     \
                                            hipStream_t);                                                             \
     template hipError_t launch_test<T>(const uint32_t*, const uint32_t*, const double*, uint64_t, uint64_t,         \

@@ -233,6 +233,8 @@ struct sbmf_ctx {
     DBuf d_gitems_u, d_grows_u, d_gitems_v, d_grows_v, d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
     DBuf d_colpart, d_res, d_scratch;
     uint32_t cmax = 0;  // streaming-kernel task capacity (ratings)
+    bool kprof = false; // SBMF_KPROF=1: streaming-kernel phase cycles printed per sweep
+    DBuf d_kprof;
     DBuf d_stasks_u, d_stasks_v, d_xrows_u, d_xrows_v;
     DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
@@ -430,7 +432,7 @@ static void prepare_T(sbmf_ctx* c) {
     HIPCHK(hipMemsetAsync(c->d_tsum.p, 0, c->d_tsum.bytes, st));
     c->d_tpart.alloc(((T_ + 255) / 256 + 1) * 2 * sizeof(double));
     HIPCHK(hipMemsetAsync(c->d_tpart.p, 0, c->d_tpart.bytes, st));
-    if (cf.rng_mode == SBMF_RNG_REFERENCE) {
+    {  // per-half normals: host reference stream, or launch_philox_fill in throughput mode
         c->d_zU.alloc((size_t)c->I * c->K * sizeof(T));
         c->d_zV.alloc((size_t)c->J * c->K * sizeof(T));
     }
@@ -456,6 +458,11 @@ static void prepare_T(sbmf_ctx* c) {
         HIPCHK(launch_init_philox<T>(c->d_V.as<T>(), c->K, c->Kp, 0, c->J, c->init_sd, cf.seed, TAG_INIT_V, st));
     }
     HIPCHK(hipStreamSynchronize(st));
+    c->kprof = std::getenv("SBMF_KPROF") && std::atoi(std::getenv("SBMF_KPROF")) > 0;
+    if (c->kprof) {
+        c->d_kprof.alloc(16 * sizeof(unsigned long long));
+        HIPCHK(hipMemset(c->d_kprof.p, 0, 16 * sizeof(unsigned long long)));
+    }
     c->sweep = 0;
     c->collected = 0;
     fill_kernel_bytes(c);
@@ -549,15 +556,15 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
         a.ptr = c->d_uptr.as<uint32_t>();
         a.part = c->d_upart.as<uint32_t>();
         a.perm = c->d_uperm.as<uint32_t>();
-        a.E_in = c->d_Ev.as<T>();
-        a.E_out = c->d_Eu.as<T>();
+        a.E_this = c->d_Eu.as<T>();   // user order
+        a.E_other = c->d_Ev.as<T>();  // item order
         a.r_this = c->d_ur.as<T>();
         a.own = c->d_U.as<T>();
         a.partner = c->d_V.as<T>();
         a.sig = c->d_hyper.as<T>();
         a.mu = c->d_hyper.as<T>() + c->Kp;
         a.zrow = c->J;
-        a.zbuf = c->cfg.rng_mode == SBMF_RNG_REFERENCE ? c->d_zU.as<T>() : nullptr;
+        a.zbuf = c->d_zU.as<T>();
         a.tag = TAG_USERS;
         a.row_sq = nullptr;
         a.row_tr = nullptr;
@@ -565,15 +572,15 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
         a.ptr = c->d_vptr.as<uint32_t>();
         a.part = c->d_vpart.as<uint32_t>();
         a.perm = c->d_vperm.as<uint32_t>();
-        a.E_in = c->d_Eu.as<T>();
-        a.E_out = c->d_Ev.as<T>();
+        a.E_this = c->d_Ev.as<T>();   // item order
+        a.E_other = c->d_Eu.as<T>();  // user order
         a.r_this = c->d_vr.as<T>();
         a.own = c->d_V.as<T>();
         a.partner = c->d_U.as<T>();
         a.sig = c->d_hyper.as<T>() + 2 * c->Kp;
         a.mu = c->d_hyper.as<T>() + 3 * c->Kp;
         a.zrow = c->I;
-        a.zbuf = c->cfg.rng_mode == SBMF_RNG_REFERENCE ? c->d_zV.as<T>() : nullptr;
+        a.zbuf = c->d_zV.as<T>();
         a.tag = TAG_ITEMS;
         a.row_sq = c->d_rowsq_v.as<double>();
         a.row_tr = c->cfg.eval_train ? c->d_rowtr_v.as<double>() : nullptr;
@@ -623,6 +630,7 @@ static void run_half(sbmf_ctx* c, bool users) {
             sy.newown = c->d_xnewown.p;
             sy.timeout = c->d_xtimeout.as<uint32_t>();
             sy.cmax = c->cmax;
+            sy.prof = c->kprof ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
             HIPCHK(launch_gstream<T>((users ? c->d_stasks_u : c->d_stasks_v).as<SplitTask>(), (uint32_t)s.stasks.size(),
                                      s.sgrid, (users ? c->d_xrows_u : c->d_xrows_v).as<SplitRow>(),
                                      (uint32_t)s.xrows.size(), a, sy, st));
@@ -684,8 +692,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // ---- 1. residual sum of squares (E recompute at sweep start, :317-334)
         const bool recompute = c->sweep == 0 || (cf.recompute_every && c->sweep % cf.recompute_every == 0);
         if (recompute) {
-            HIPCHK(launch_resid<T>(c->d_vptr.as<uint32_t>(), c->d_vpart.as<uint32_t>(), c->d_vr.as<T>(), c->d_V.as<T>(),
-                                   c->d_U.as<T>(), K, c->Kp, c->items.r0, c->items.r1, c->d_Ev.as<T>(),
+            // residuals of every rating, scattered into user order for the user half
+            HIPCHK(launch_resid<T>(c->d_vptr.as<uint32_t>(), c->d_vpart.as<uint32_t>(), c->d_vperm.as<uint32_t>(),
+                                   c->d_vr.as<T>(), c->d_V.as<T>(), c->d_U.as<T>(), K, c->Kp, c->items.r0,
+                                   c->items.r1, c->d_Eu.as<T>(),
                                    c->d_rowsq_v.as<double>(), st));
             c->timing.n_launch++;
             if (c->nranks > 1) c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
@@ -742,12 +752,16 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(hipStreamSynchronize(st));
         }
         HIPCHK(hipEventRecord(c->ev[1], st));
-        // ---- 3. user half-sweep
+        // ---- 3. user half-sweep (throughput mode: this half's normals first)
+        if (!ref)
+            HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep, TAG_USERS, st));
         run_half<T>(c, true);
         HIPCHK(hipEventRecord(c->ev[2], st));
         if (c->nranks > 1) c->comm.bcast_ranges(c->d_U.p, c->Kp * sizeof(T), c->users.bounds, st);
         HIPCHK(hipEventRecord(c->ev[3], st));
         // ---- 4. item half-sweep
+        if (!ref)
+            HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep, TAG_ITEMS, st));
         run_half<T>(c, false);
         HIPCHK(hipEventRecord(c->ev[4], st));
         if (c->nranks > 1) {
@@ -776,6 +790,24 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         if (c->d_xtimeout.p)
             HIPCHK(hipMemcpyAsync(&split_timeout, c->d_xtimeout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        if (c->kprof) {
+            unsigned long long h[16];
+            HIPCHK(hipMemcpy(h, c->d_kprof.p, sizeof(h), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemset(c->d_kprof.p, 0, sizeof(h)));
+            static const char* nm[7] = {"stage", "traverse", "wg-wait", "reduce", "split-xchg", "solve", "epilogue"};
+            for (int sd = 0; sd < 2; ++sd) {
+                const Side& S = sd ? c->items : c->users;
+                double tot = 0;
+                for (int k = 0; k < 7; ++k) tot += (double)h[8 * sd + k];
+                if (tot == 0) continue;
+                std::fprintf(stderr, "[kprof] sweep %u %s gstream (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep,
+                             sd ? "items" : "users", S.sgrid, S.stasks.size());
+                for (int k = 0; k < 7; ++k)
+                    std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.sgrid / 1e6,
+                                 100.0 * (double)h[8 * sd + k] / tot);
+                std::fprintf(stderr, "\n");
+            }
+        }
         if (split_timeout)  // a bounded spin in k_gstream gave up: the sweep's results are not valid
             fail(SBMF_E_STATE, "sweep %u: split-row hand-off timed out (workgroups not co-resident)", c->sweep);
 
