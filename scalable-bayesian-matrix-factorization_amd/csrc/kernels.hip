@@ -645,7 +645,9 @@ __host__ __device__ constexpr size_t gstream_dyn_bytes(uint32_t cmax) {
     return gstream_ids_bytes(cmax) + (size_t)(cmax + GSTREAM_PAD + GSTREAM_SINK) * sizeof(T);
 }
 
-template <typename T, int NW, int UNR, bool SW>
+// SIDE (0 users, 1 items) only names the instantiation, so profiles tell the
+// two half-sweeps apart.
+template <typename T, int NW, int UNR, bool SW, int SIDE>
 __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restrict__ tasks, uint32_t ntask,
                                                      HalfArgs<T> a, SplitSync sy) {
     typedef typename MfmaT<T>::acc_t acc_t;
@@ -1456,8 +1458,10 @@ static int gstream_nw(uint32_t) { return 8; }
 int gstream_wg_target(uint32_t) { return 2; }
 
 template <typename T>
-static const void* gstream_fn(uint32_t tune) {
-    return (tune & 1u) ? (const void*)k_gstream<T, 8, 8, false> : (const void*)k_gstream<T, 8, 8, true>;
+static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
+    if (side)
+        return (tune & 1u) ? (const void*)k_gstream<T, 8, 8, false, 1> : (const void*)k_gstream<T, 8, 8, true, 1>;
+    return (tune & 1u) ? (const void*)k_gstream<T, 8, 8, false, 0> : (const void*)k_gstream<T, 8, 8, true, 0>;
 }
 
 template <typename T>
@@ -1500,7 +1504,8 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     SplitSync syp = sy;
     void* args[] = {(void*)&tp, (void*)&ntask, (void*)&ap, (void*)&syp};
     const size_t dyn = gstream_dyn_bytes<T>(sy.cmax);
-    err = hipLaunchCooperativeKernel(gstream_fn<T>(a.tune), dim3(std::min(grid, ntask)), dim3(64 * gstream_nw(a.tune)),
+    err = hipLaunchCooperativeKernel(gstream_fn<T>(a.tune, a.tag == TAG_ITEMS ? 1u : 0u), dim3(std::min(grid, ntask)),
+                                     dim3(64 * gstream_nw(a.tune)),
                                      args, (unsigned)dyn, st);
     if (err != hipSuccess) return err;
     if (nsrow) {
