@@ -48,13 +48,17 @@ def parse():
     ap.add_argument("--no-ttr", action="store_true", help="skip the time-to-RMSE runs")
     ap.add_argument("--tune", type=int, default=0, help="kernel-variant bits (sbmf_config.tune)")
     ap.add_argument("--split-chunk", type=int, default=0, help="streaming task size (0 = LDS capacity)")
+    ap.add_argument("--stream-threshold", type=int, default=0, help="rows above this use the streaming kernel")
+    ap.add_argument("--device", type=int, default=-1,
+                    help="HIP device for every rank (testing only; default: LOCAL_RANK)")
+    ap.add_argument("--shape-override", default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) if args.device < 0 else args.device
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -99,7 +103,8 @@ def make_learner(args, world, rank, local, precision, uid):
     from sbmf import Data, FMLearnSBPMF
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=precision, device=local,
                      recompute_every=0, eval_train=False, gram_threshold=args.gram_threshold,
-                     row_kernel=args.row_kernel, tune=args.tune, split_chunk=args.split_chunk)
+                     row_kernel=args.row_kernel, tune=args.tune, split_chunk=args.split_chunk,
+                     stream_threshold=args.stream_threshold)
     L.init(comm=(world, rank, uid) if world > 1 else None)
     return L, Data
 
@@ -137,7 +142,7 @@ def measure(args, world, rank, local, precision, train, test, uid):
     return res
 
 
-def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85, max_sweeps=400, max_s=60.0):
+def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85, max_sweeps=400):
     """Wall-clock from the end of data load to the first sweep whose running-mean
     test RMSE <= target, with the reference's averaging rule."""
     from sbmf import Data, FMLearnSBPMF
@@ -146,14 +151,16 @@ def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85
     # (quirks "none"), since the reference's divisor counts burn-in sweeps too.
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=args.precision, device=local,
                      recompute_every=0, burnin=burnin, row_kernel=args.row_kernel, tune=args.tune,
-                     split_chunk=args.split_chunk,
+                     split_chunk=args.split_chunk, stream_threshold=args.stream_threshold,
                      quirks="final" if burnin == 0 else "none")
     L.init(comm=(world, rank, uid) if world > 1 else None)
     L.set_data(Data(*train), Data(*test))
     barrier(world)
     t0 = time.perf_counter()
     hit = None
-    while len(L.history) < max_sweeps and time.perf_counter() - t0 < max_s:
+    # stop rule depends only on the (rank-identical) running-mean RMSE and the
+    # sweep count, so every rank leaves the loop after the same sweep
+    while len(L.history) < max_sweeps:
         L.learn(sweeps=1)
         if L.history[-1]["sweep"] >= burnin and L.history[-1]["rmse_avg"] <= target:
             hit = time.perf_counter() - t0
@@ -223,13 +230,16 @@ def main():
         except Exception:
             traffic = None
     out = {
-        "metric": "ratings/sec per Gibbs sweep, ML-20M K=100",
+        "metric": "ratings/sec per Gibbs sweep, %s K=%d" % ({"ml-20m": "ML-20M", "ml-10m": "ML-10M", "ml-1m": "ML-1M",
+                                                             "ml-100k": "ML-100k", "netflix": "Netflix"}[args.shape],
+                                                            args.K),
         "value": value, "unit": "ratings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": value / BASELINE_RPS,
         "dtype": args.precision,
         "data": "synthetic ML-20M-shaped (sbmf/synth.py: planted rank-10, Pareto users, log-normal items)",
-        "config": {"workload": "ML-20M K=100 SBPMF Gibbs sweep (user+item half-sweeps, hyperparameters, test RMSE)",
+        "config": {"workload": "%s K=%d SBPMF Gibbs sweep (user+item half-sweeps, hyperparameters, test RMSE)"
+                               % (args.shape, args.K),
                    "num_users": dims[0], "num_items": dims[1], "n_train": n_train, "n_test": len(test[0]),
                    "K": args.K, "rng": "philox", "quirks": "final",
                    "parallelism": "rows x%d (RCCL block broadcast)" % world,

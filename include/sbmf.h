@@ -88,7 +88,8 @@ typedef struct sbmf_config {
                                  1792 f64 / 3584 f32; larger values are capped to it)            */
     uint32_t tune;            /* kernel-variant bits for experiments (0 = tuned defaults):
                                  bit 0 = block solve replicated in every wave of a row
-                                 (default: one wave solves, D shared through LDS)                */
+                                 (default: one wave solves, D shared through LDS),
+                                 bit 1 = residuals from r - own.partner as on several GPUs       */
     uint32_t reserved[4];
 } sbmf_config;
 

@@ -3,38 +3,132 @@
 
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <random>
+#include <stdexcept>
 #include <string>
 
 namespace sbmf {
 
 [[noreturn]] void comm_fail(const char* what, ncclResult_t r);
 
+namespace {
+const char kHostMagic[8] = {'S', 'B', 'M', 'F', 'H', 'O', 'S', 'T'};
+constexpr size_t kHostHeader = 128;         // barrier counters
+constexpr size_t kHostWindow = 64ull << 20;  // bytes exchanged per round
+struct HostBarrier {
+    std::atomic<int> count;
+    std::atomic<int> sense;
+};
+std::string host_name(const uint8_t id[128]) {
+    uint64_t tok;
+    std::memcpy(&tok, id + 8, 8);
+    return "/sbmf_" + std::to_string(tok);
+}
+}  // namespace
+
 Comm::~Comm() {
     if (comm_) (void)ncclCommDestroy((ncclComm_t)comm_);
+    if (shm_) munmap(shm_, shm_bytes_);
 }
 
 void Comm::unique_id(uint8_t id[128]) {
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    const char* mode = std::getenv("SBMF_COMM");
+    if (mode && std::string(mode) == "host") {
+        std::memset(id, 0, 128);
+        std::memcpy(id, kHostMagic, 8);
+        std::random_device rd;
+        const uint64_t tok = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)getpid() ^
+                             (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+        std::memcpy(id + 8, &tok, 8);
+        return;
+    }
     ncclUniqueId u;
     ncclResult_t r = ncclGetUniqueId(&u);
     if (r != ncclSuccess) comm_fail("ncclGetUniqueId", r);
     std::memcpy(id, &u, 128);
 }
 
+void Comm::host_barrier() {
+    HostBarrier* b = reinterpret_cast<HostBarrier*>(shm_);
+    sense_ ^= 1;
+    if (b->count.fetch_add(1) == nranks_ - 1) {
+        b->count.store(0);
+        b->sense.store(sense_);
+    } else {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (b->sense.load() != sense_) {
+            sched_yield();
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+                throw std::runtime_error("host comm barrier timed out (a rank is gone)");
+        }
+    }
+}
+
 void Comm::init(int nranks, int rank, const uint8_t id[128]) {
+    nranks_ = nranks;
+    rank_ = rank;
+    if (std::memcmp(id, kHostMagic, 8) == 0) {
+        const std::string name = host_name(id);
+        shm_bytes_ = kHostHeader + kHostWindow;
+        const int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
+        if (fd < 0) throw std::runtime_error("shm_open " + name + " failed");
+        if (ftruncate(fd, (off_t)shm_bytes_) != 0) {
+            close(fd);
+            throw std::runtime_error("ftruncate of the host comm segment failed");
+        }
+        void* p = mmap(nullptr, shm_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (p == MAP_FAILED) throw std::runtime_error("mmap of the host comm segment failed");
+        shm_ = static_cast<unsigned char*>(p);
+        host_barrier();  // every rank has mapped the segment: the name can go
+        if (rank_ == 0) shm_unlink(name.c_str());
+        return;
+    }
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
     ncclComm_t c;
     ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
     if (r != ncclSuccess) comm_fail("ncclCommInitRank", r);
     comm_ = c;
-    nranks_ = nranks;
-    rank_ = rank;
 }
 
 void Comm::bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_t>& bounds, hipStream_t st) {
-    if (!comm_ || nranks_ <= 1) return;
+    if (nranks_ <= 1) return;
+    if (shm_) {  // host backend: windows of the whole range through the segment
+        if (hipStreamSynchronize(st) != hipSuccess) throw std::runtime_error("hipStreamSynchronize failed");
+        unsigned char* win = shm_ + kHostHeader;
+        const size_t lo = (size_t)bounds[0] * unit_bytes, hi = (size_t)bounds[nranks_] * unit_bytes;
+        const size_t mlo = (size_t)bounds[rank_] * unit_bytes, mhi = (size_t)bounds[rank_ + 1] * unit_bytes;
+        char* dev = static_cast<char*>(base);
+        for (size_t w0 = lo; w0 < hi; w0 += kHostWindow) {
+            const size_t w1 = std::min(hi, w0 + kHostWindow);
+            const size_t a = std::max(w0, mlo), b = std::min(w1, mhi);
+            if (a < b && hipMemcpy(win + (a - w0), dev + a, b - a, hipMemcpyDeviceToHost) != hipSuccess)
+                throw std::runtime_error("host comm: D2H failed");
+            host_barrier();
+            if (a < b) {
+                if (w0 < a && hipMemcpy(dev + w0, win, a - w0, hipMemcpyHostToDevice) != hipSuccess)
+                    throw std::runtime_error("host comm: H2D failed");
+                if (b < w1 && hipMemcpy(dev + b, win + (b - w0), w1 - b, hipMemcpyHostToDevice) != hipSuccess)
+                    throw std::runtime_error("host comm: H2D failed");
+            } else if (hipMemcpy(dev + w0, win, w1 - w0, hipMemcpyHostToDevice) != hipSuccess) {
+                throw std::runtime_error("host comm: H2D failed");
+            }
+            host_barrier();
+        }
+        return;
+    }
+    if (!comm_) return;
     ncclResult_t r = ncclGroupStart();
     if (r != ncclSuccess) comm_fail("ncclGroupStart", r);
     for (int k = 0; k < nranks_; ++k) {

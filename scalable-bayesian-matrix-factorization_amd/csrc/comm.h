@@ -11,6 +11,10 @@
 
 namespace sbmf {
 
+// Test-only alternative (SBMF_COMM=host when the id is made): the same
+// exchange through a POSIX shared-memory segment and a process-shared
+// barrier, so the multi-rank sampler can run as several processes on ONE GPU
+// (RCCL rejects two ranks on one device).  Synchronous; not a product path.
 class Comm {
   public:
     Comm() = default;
@@ -19,13 +23,17 @@ class Comm {
     Comm& operator=(const Comm&) = delete;
     static void unique_id(uint8_t id[128]);
     void init(int nranks, int rank, const uint8_t id[128]);
-    bool active() const { return comm_ != nullptr; }
+    bool active() const { return comm_ != nullptr || shm_ != nullptr; }
     // Rank k owns units [bounds[k], bounds[k+1]) of unit_bytes each, starting
     // at base; after the call every rank holds every rank's units.
     void bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_t>& bounds, hipStream_t st);
 
   private:
+    void host_barrier();
     void* comm_ = nullptr;  // ncclComm_t
+    unsigned char* shm_ = nullptr;  // host backend: [barrier header | window]
+    size_t shm_bytes_ = 0;
+    int sense_ = 0;
     int nranks_ = 1, rank_ = 0;
 };
 

@@ -594,7 +594,8 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     a.sweep = c->sweep;
     a.lo = (T)c->lo;
     a.hi = (T)c->hi;
-    a.e_from_dot = md ? 1 : 0;
+    // multi-GPU: residuals from r - own.partner (tune bit 1 forces it on one GPU, for validation)
+    a.e_from_dot = (md || (c->cfg.tune & 2u)) ? 1 : 0;
     return a;
 }
 

@@ -1,0 +1,60 @@
+"""Several ranks on one GPU (host comm backend instead of RCCL, which refuses
+two ranks on one device): the row-block partition, the per-half block
+exchange, the rank-local residual form and the fixed-order partial sums must
+reproduce a single-rank run bit for bit."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from sbmf import Data, FMLearnSBPMF, comm_unique_id
+
+pytestmark = pytest.mark.gpu
+WORKER = os.path.join(REPO, "tests", "workers", "multirank_worker.py")
+
+
+@pytest.mark.parametrize("nranks,rng", [(2, "ref"), (3, "philox")])
+def test_ranks_on_one_gpu_match_single_rank(ml100k, tmp_path, nranks, rng):
+    K, sweeps, seed = 30, 3, 6
+    tr, te = ml100k
+    # single rank, same residual form as every rank of a multi-rank run (tune bit 1)
+    L = FMLearnSBPMF(num_factor=K, seed=seed, rng=rng, tune=2)
+    L.set_data(Data(*tr), Data(*te))
+    L.learn(sweeps=sweeps)
+    U1, V1 = L.factors()
+    rmse1 = L.rmse_trajectory
+    L.close()
+
+    old = os.environ.get("SBMF_COMM")
+    os.environ["SBMF_COMM"] = "host"
+    try:
+        uid = comm_unique_id()
+    finally:
+        if old is None:
+            del os.environ["SBMF_COMM"]
+        else:
+            os.environ["SBMF_COMM"] = old
+    outs = [str(tmp_path / ("r%d.npz" % r)) for r in range(nranks)]
+    procs = [subprocess.Popen([sys.executable, WORKER, str(r), str(nranks), uid.hex(), outs[r], str(K), str(sweeps),
+                               str(seed), rng], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(nranks)]
+    logs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        logs.append(o.decode(errors="replace"))
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-2000:]
+    for r in range(nranks):
+        z = np.load(outs[r])
+        # every rank ends with the full, identical factor tables
+        assert np.array_equal(z["U"], U1) and np.array_equal(z["V"], V1), \
+            (r, np.abs(z["U"] - U1).max(), np.abs(z["V"] - V1).max())
+        assert np.array_equal(z["rmse"], rmse1)

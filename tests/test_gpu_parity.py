@@ -134,6 +134,20 @@ def test_kernel_variants_match_oracle(ml100k, tune):
         assert np.abs(V - o["V"]).max() < 1e-7
 
 
+@pytest.mark.parametrize("kw", [{}, {"stream_threshold": 40, "split_chunk": 64}, {"row_kernel": 1},
+                                {"gram_threshold": 64}])
+def test_multigpu_residual_mode_matches_oracle(ml100k, kw):
+    """The residual form every rank uses with several GPUs (e0 = r - own.partner
+    recomputed per row instead of carried), forced on one GPU (tune bit 1)."""
+    tr, te = ml100k
+    o = oracle.run(tr, te, K=30, iters=3, seed=6)
+    L = _run(tr, te, 3, num_factor=30, seed=6, tune=2, **kw)
+    U, V = L.factors()
+    assert np.abs(U - o["U"]).max() < 1e-7
+    assert np.abs(V - o["V"]).max() < 1e-7
+    np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
+
+
 def test_split_rows_deterministic(ml100k):
     tr, te = ml100k
     a = _run(tr, te, 3, num_factor=32, seed=2, rng="philox", stream_threshold=40, split_chunk=50)

@@ -1,0 +1,45 @@
+"""One rank of the multi-rank sampler (spawned by tests/test_gpu_multirank.py).
+
+usage: python multirank_worker.py <rank> <nranks> <id-hex> <out.npz> <K> <sweeps> <seed> <rng>
+The ranks share one GPU and exchange their row blocks through the host comm
+backend (the id was made with SBMF_COMM=host); the result must equal a
+single-rank run in the same residual form.
+"""
+import gzip
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "scalable-bayesian-matrix-factorization_amd"))
+
+
+def read(path):
+    u, i, r = [], [], []
+    with gzip.open(path, "rt") as f:
+        for line in f:
+            p = line.split()
+            if len(p) >= 3:
+                u.append(int(p[0]))
+                i.append(int(p[1]))
+                r.append(float(p[2]))
+    return np.array(u, np.uint32), np.array(i, np.uint32), np.array(r)
+
+
+def main():
+    rank, nranks, idhex, out, K, sweeps, seed, rng = sys.argv[1:9]
+    from sbmf import Data, FMLearnSBPMF
+    g = os.path.join(REPO, "tests", "golden")
+    tr, te = read(os.path.join(g, "ml100k_train.tsv.gz")), read(os.path.join(g, "ml100k_test.tsv.gz"))
+    L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0)
+    L.init(comm=(int(nranks), int(rank), bytes.fromhex(idhex)))
+    L.set_data(Data(*tr), Data(*te))
+    L.learn(sweeps=int(sweeps))
+    U, V = L.factors()
+    np.savez(out, U=U, V=V, rmse=L.rmse_trajectory, tau=np.array([h["tau"] for h in L.history]))
+    L.close()
+
+
+if __name__ == "__main__":
+    main()
