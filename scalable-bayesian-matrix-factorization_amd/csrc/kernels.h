@@ -121,12 +121,18 @@ hipError_t launch_gram(const GramItem* items, uint32_t nitems, const GramRow* gr
                        double* slabs, T* delta, double* chunk_sq, double* chunk_tr, const HalfArgs<T>& a,
                        hipStream_t st);
 
-// E = r - dot(own, partner) over all ratings of the orientation (row-major
-// walk; one wave per row) + per-row sum of squares.  own rows [r0,r1).
+// Full residual recompute over rows [r0, r1) of one orientation, split into
+// tasks of <= RESID_CHUNK ratings (one wave each): e = r - own.partner is
+// scattered into the other orientation's order (E_other[perm[q]]), each task
+// writes its sum of squares, and row_sq[row] folds the row's tasks in order.
+constexpr uint32_t RESID_CHUNK = 1024;
+struct ResidTask {
+    uint32_t row, beg, len, pad;
+};
 template <typename T>
-hipError_t launch_resid(const uint32_t* ptr, const uint32_t* part, const uint32_t* perm, const T* r, const T* own,
-                        const T* partner, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, T* E_other,
-                        double* row_sq, hipStream_t st);
+hipError_t launch_resid(const ResidTask* tasks, uint32_t ntask, const uint32_t* tptr, uint32_t r0, uint32_t r1,
+                        const uint32_t* part, const uint32_t* perm, const T* r, const T* own, const T* partner,
+                        uint32_t K, uint32_t Kp, T* E_other, double* task_sq, double* row_sq, hipStream_t st);
 
 // Column partials over table rows [r0,r1): out[c][0..K) = sum (x-mu)^2,
 // out[c][K..2K) = sum x, c = chunk of 256 rows (global chunk index).

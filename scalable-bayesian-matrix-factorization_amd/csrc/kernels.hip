@@ -1212,34 +1212,30 @@ __global__ __launch_bounds__(64) void k_gram_rowsum(const GramRow* __restrict__ 
 // One wave per row; 16 lanes per rating (lane (r = l>>4, i = l&15) covers
 // k = 16b + i), so each partner row is read as whole 128-byte lines.
 template <typename T>
-__global__ __launch_bounds__(256) void k_resid(const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ part,
-                                                const uint32_t* __restrict__ perm, const T* __restrict__ r,
-                                                const T* __restrict__ own, const T* __restrict__ partner, uint32_t K,
-                                                uint32_t Kp, uint32_t r0, uint32_t r1, T* __restrict__ E_other,
-                                                double* __restrict__ row_sq) {
-    const uint32_t row = r0 + blockIdx.x * 4 + (threadIdx.x >> 6);
+__global__ __launch_bounds__(256) void k_resid(const ResidTask* __restrict__ tasks, uint32_t ntask,
+                                                const uint32_t* __restrict__ part, const uint32_t* __restrict__ perm,
+                                                const T* __restrict__ r, const T* __restrict__ own,
+                                                const T* __restrict__ partner, uint32_t K, uint32_t Kp,
+                                                T* __restrict__ E_other, double* __restrict__ task_sq) {
+    const uint32_t ti = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (row >= r1) return;
+    if (ti >= ntask) return;
+    const ResidTask tk = tasks[ti];
     const int ci = lane & 15, rr = lane >> 4;
-    const uint32_t beg = ptr[row], end = ptr[row + 1];
-    const T* o = own + (size_t)row * Kp;
-    T ov[16];  // own row, this lane's k values (k = 16b + ci)
+    const T* o = own + (size_t)tk.row * Kp;
+    T ov[16];  // own row, this lane's k values (k = 16b + ci); padding columns are zero
 #pragma unroll
-    for (int b = 0; b < 16; ++b) {
-        const uint32_t kk = 16 * b + ci;
-        ov[b] = kk < K ? o[kk] : T(0);
-    }
+    for (int b = 0; b < 16; ++b) ov[b] = 16 * b < (int)Kp ? o[16 * b + ci] : T(0);
     double sq = 0.0;
-    for (uint32_t i0 = beg; i0 < end; i0 += 4) {
+    const uint32_t end = tk.beg + tk.len;
+    for (uint32_t i0 = tk.beg; i0 < end; i0 += 4) {
         const uint32_t idx = i0 + rr;
         const bool ok = idx < end;
-        const T* src = partner + (size_t)(ok ? part[idx] : 0u) * Kp;
+        const T* src = partner + (size_t)part[ok ? idx : tk.beg] * Kp;
         T d = T(0);
 #pragma unroll
-        for (int b = 0; b < 16; ++b) {
-            const uint32_t kk = 16 * b + ci;
-            if (16 * b < (int)K && ok && kk < K) d += ov[b] * src[kk];
-        }
+        for (int b = 0; b < 16; ++b)
+            if (16 * b < (int)Kp) d += ov[b] * src[16 * b + ci];
         d = row16_sum(d);
         if (ok && ci == 0) {
             const T e = r[idx] - d;
@@ -1248,7 +1244,17 @@ __global__ __launch_bounds__(256) void k_resid(const uint32_t* __restrict__ ptr,
         }
     }
     sq = wave_sum(sq);
-    if (lane == 0) row_sq[row] = sq;
+    if (lane == 0) task_sq[ti] = sq;
+}
+
+// row_sq[row] = the row's task partials in task order (deterministic)
+__global__ __launch_bounds__(256) void k_resid_rows(const uint32_t* __restrict__ tptr, uint32_t r0, uint32_t r1,
+                                                     const double* __restrict__ task_sq, double* __restrict__ row_sq) {
+    const uint32_t row = r0 + blockIdx.x * 256 + threadIdx.x;
+    if (row >= r1) return;
+    double s = 0.0;
+    for (uint32_t t = tptr[row - r0]; t < tptr[row - r0 + 1]; ++t) s += task_sq[t];
+    row_sq[row] = s;
 }
 
 // ------------------------------------------------------------------ column statistics
@@ -1544,11 +1550,14 @@ hipError_t launch_gram(const GramItem* items, uint32_t nitems, const GramRow* gr
 }
 
 template <typename T>
-hipError_t launch_resid(const uint32_t* ptr, const uint32_t* part, const uint32_t* perm, const T* r, const T* own,
-                        const T* partner, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, T* E_other,
-                        double* row_sq, hipStream_t st) {
+hipError_t launch_resid(const ResidTask* tasks, uint32_t ntask, const uint32_t* tptr, uint32_t r0, uint32_t r1,
+                        const uint32_t* part, const uint32_t* perm, const T* r, const T* own, const T* partner,
+                        uint32_t K, uint32_t Kp, T* E_other, double* task_sq, double* row_sq, hipStream_t st) {
     if (r1 <= r0) return hipSuccess;
-    k_resid<T><<<(r1 - r0 + 3) / 4, 256, 0, st>>>(ptr, part, perm, r, own, partner, K, Kp, r0, r1, E_other, row_sq);
+    if (Kp > 256) return hipErrorInvalidValue;
+    if (ntask) k_resid<T><<<(ntask + 3) / 4, 256, 0, st>>>(tasks, ntask, part, perm, r, own, partner, K, Kp, E_other,
+                                                          task_sq);
+    k_resid_rows<<<(r1 - r0 + 255) / 256, 256, 0, st>>>(tptr, r0, r1, task_sq, row_sq);
     return hipGetLastError();
 }
 
@@ -1621,8 +1630,9 @@ hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint
     template uint32_t gstream_cmax<T>(uint32_t);                                                                    \
     template hipError_t launch_gram<T>(const GramItem*, uint32_t, const GramRow*, uint32_t, double*, T*, double*,   \
                                        double*, const HalfArgs<T>&, hipStream_t);                                    \
-    template hipError_t launch_resid<T>(const uint32_t*, const uint32_t*, const uint32_t*, const T*, const T*,       \
-                                        const T*, uint32_t, uint32_t, uint32_t, uint32_t, T*, double*, hipStream_t); \
+    template hipError_t launch_resid<T>(const ResidTask*, uint32_t, const uint32_t*, uint32_t, uint32_t,              \
+                                        const uint32_t*, const uint32_t*, const T*, const T*, const T*, uint32_t,     \
+                                        uint32_t, T*, double*, double*, hipStream_t);                                \
     template hipError_t launch_philox_fill<T>(T*, uint32_t, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t,        \
                                               hipStream_t);                                                          \
     template hipError_t launch_colstats<T>(const T*, uint32_t, uint32_t, uint32_t, uint32_t, const T*, double*,     \

@@ -109,6 +109,8 @@ struct Side {
     std::vector<GramRow> grows;
     std::vector<SplitTask> stasks;   // streaming kernel tasks, in rounds of `sgrid` slots
     std::vector<SplitRow> xrows;     // rows split over several tasks
+    std::vector<ResidTask> rtasks;   // residual recompute: own rows in chunks of <= RESID_CHUNK
+    std::vector<uint32_t> rtptr;     // [r1-r0+1] first task of each own row
     uint32_t nxchunk = 0;            // tasks belonging to split rows (slab / staging slots)
     uint32_t sgrid = 0;              // persistent grid of the streaming launch
 };
@@ -236,6 +238,7 @@ struct sbmf_ctx {
     bool kprof = false; // SBMF_KPROF=1: streaming-kernel phase cycles printed per sweep
     DBuf d_kprof;
     DBuf d_stasks_u, d_stasks_v, d_xrows_u, d_xrows_v;
+    DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
     DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
     std::vector<double> h_res;
@@ -367,6 +370,19 @@ static void prepare_T(sbmf_ctx* c) {
     for (int k = 0; k < NBIN; ++k) {
         upload(c->d_bins_u[k], c->users.bin_rows[k], st);
         upload(c->d_bins_v[k], c->items.bin_rows[k], st);
+    }
+    {  // residual recompute tasks over the own item rows
+        Side& s = c->items;
+        s.rtasks.clear();
+        s.rtptr.assign(1, 0);
+        for (uint32_t r = s.r0; r < s.r1; ++r) {
+            for (uint32_t b = s.ptr[r]; b < s.ptr[r + 1]; b += RESID_CHUNK)
+                s.rtasks.push_back(ResidTask{r, b, std::min<uint32_t>(RESID_CHUNK, s.ptr[r + 1] - b), 0});
+            s.rtptr.push_back((uint32_t)s.rtasks.size());
+        }
+        upload(c->d_rtasks, s.rtasks, st);
+        upload(c->d_rtptr, s.rtptr, st);
+        c->d_rtsq.alloc(std::max<size_t>(s.rtasks.size(), 1) * sizeof(double));
     }
     upload(c->d_stasks_u, c->users.stasks, st);
     upload(c->d_stasks_v, c->items.stasks, st);
@@ -694,10 +710,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         const bool recompute = c->sweep == 0 || (cf.recompute_every && c->sweep % cf.recompute_every == 0);
         if (recompute) {
             // residuals of every rating, scattered into user order for the user half
-            HIPCHK(launch_resid<T>(c->d_vptr.as<uint32_t>(), c->d_vpart.as<uint32_t>(), c->d_vperm.as<uint32_t>(),
-                                   c->d_vr.as<T>(), c->d_V.as<T>(), c->d_U.as<T>(), K, c->Kp, c->items.r0,
-                                   c->items.r1, c->d_Eu.as<T>(),
-                                   c->d_rowsq_v.as<double>(), st));
+            HIPCHK(launch_resid<T>(c->d_rtasks.as<ResidTask>(), (uint32_t)c->items.rtasks.size(),
+                                   c->d_rtptr.as<uint32_t>(), c->items.r0, c->items.r1, c->d_vpart.as<uint32_t>(),
+                                   c->d_vperm.as<uint32_t>(), c->d_vr.as<T>(), c->d_V.as<T>(), c->d_U.as<T>(), K,
+                                   c->Kp, c->d_Eu.as<T>(), c->d_rtsq.as<double>(), c->d_rowsq_v.as<double>(), st));
             c->timing.n_launch++;
             if (c->nranks > 1) c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
         }
