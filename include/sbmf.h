@@ -89,7 +89,11 @@ typedef struct sbmf_config {
     uint32_t tune;            /* kernel-variant bits for experiments (0 = tuned defaults):
                                  bit 0 = block solve replicated in every wave of a row
                                  (default: one wave solves, D shared through LDS),
-                                 bit 1 = residuals from r - own.partner as on several GPUs       */
+                                 bit 1 = residuals from r - own.partner as on several GPUs,
+                                 bit 2 = power-of-two waves per Gram-block row (2/4/8) instead
+                                         of ceil(ratings / ratings-per-wave),
+                                 bit 3 = f64 rows of 33..64 ratings on two 8-vector waves instead
+                                         of one 16-vector wave                                   */
     uint32_t reserved[4];
 } sbmf_config;
 
@@ -155,8 +159,9 @@ int sbmf_get_dims(sbmf_ctx* ctx, uint32_t* num_users, uint32_t* num_items, uint6
 /* --- measurement --------------------------------------------------------------------------- */
 /* Device times of the last sweep (HIP events on the context's stream).
  * kern_*[side][kind]: side 0 = user half, 1 = item half; kind =
- *   0..4  MFMA Gram-block row kernels: 1 wave/row (two sizes), 2 / 4 / 8
- *         waves/row; up to 8/32/64/128/256 ratings (f64), 16/64/128/256/512 (f32),
+ *   0..4  MFMA Gram-block row kernels: 1 wave/row (two sizes), then 2..8
+ *         waves/row (ceil(ratings/32) f64, /64 f32) timed in three groups; up to
+ *         8/64/64/128/256 ratings (f64), 16/64/128/256/512 (f32),
  *   5     streaming MFMA Gram-block kernel: one persistent cooperative launch
  *         over tasks of <= 1792 (f64) / 3584 (f32) ratings -- whole rows, or
  *         chunks of longer rows on co-resident workgroups -- plus the publish

@@ -32,6 +32,7 @@ struct HalfArgs {
     T lo, hi;
     int e_from_dot;        // 1: e0 = r - own.partner (no gather; multi-GPU)
     uint32_t tune;         // kernel variant bits (sbmf_config.tune): bit 0 = replicated block solve
+    unsigned long long* prof;  // [8] phase cycles of wave 0 (SBMF_KPROF diagnostics) or null
 };
 
 // Heavy-row (Gram route) work description.
@@ -56,12 +57,17 @@ static const uint32_t RK_MAXDEG[RK_NUM] = {128, 512, 2048, 4096};
 // Gram-block (MFMA) row kernels.  Max ratings per row for each kind: f64
 // holds 8 vectors (32 ratings) per wave, f32 16 (64 ratings).
 enum GblockKind { GK_W4 = 0, GK_W16 = 1, GK_B2 = 2, GK_B4 = 3, GK_B8 = 4, GK_NUM = 5 };
-inline uint32_t gk_maxdeg(int kind, bool f64) {
+inline uint32_t gk_maxdeg(int kind, bool f64, bool wide = false) {
     static const uint32_t waves4[GK_NUM] = {1, 4, 8, 16, 32};  // (waves x vectors) / V*4 ratings
     const uint32_t per_wave = f64 ? 32 : 64;
+    // wide (f64 default; tune bit 3 turns it off): the 1-wave kind holds 16 vectors (64 ratings)
+    if (wide && f64 && (kind == GK_W16 || kind == GK_B2)) return 64;
     return kind == GK_W4 ? per_wave / 4 : per_wave * waves4[kind] / 4;
 }
 
+// Multi-wave Gram-block rows with exactly `nw` (2..8) waves per row.
+template <typename T>
+hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
 template <typename T>
 hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
 

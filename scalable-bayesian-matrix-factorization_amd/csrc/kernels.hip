@@ -393,8 +393,15 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
     return gam;
 }
 
+// Occupancy (waves/SIMD): 4 for 8 f64 vectors per wave (<= 128 VGPRs; tune
+// bit 4 -> 3), 3 for 16 f32 vectors, 2 for the 16-vector f64 kind.  Partner
+// rows are kept as 32-bit ids and the block solve reads its H row from LDS.
+#ifndef SBMF_GBLOCK_OCC64
+#define SBMF_GBLOCK_OCC64 4
+#endif
+#define GBLOCK_OCC(T, V) ((V) * sizeof(T) > 64 ? 2 : (sizeof(T) == 8 ? SBMF_GBLOCK_OCC64 : 3))
 template <typename T, int V, int NW, int RPW, bool SW>
-__global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const uint32_t* __restrict__ rows,
+__global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_gblock(const uint32_t* __restrict__ rows,
                                                                      uint32_t nrows, HalfArgs<T> a) {
     typedef typename MfmaT<T>::acc_t acc_t;
     constexpr int NWAVE = NW > 1 ? NW : RPW;
@@ -403,6 +410,20 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
     const int wr = NW > 1 ? wv : 0;           // wave within the row
     const uint32_t ri = NW > 1 ? blockIdx.x : blockIdx.x * RPW + wv;
     if (ri >= nrows) return;                  // NW>1: whole block; RPW: this wave only (no block barriers)
+    // optional phase profile (build with KPROF=1, run with SBMF_KPROF=1;
+    // multi-wave rows): wave 0's cycles per phase
+#ifdef SBMF_KPROF_BUILD
+    unsigned long long tp = (a.prof && threadIdx.x == 0) ? clock64() : 0ull;
+    auto stamp = [&](int ph) {
+        if (NW > 1 && a.prof && threadIdx.x == 0) {
+            const unsigned long long now = clock64();
+            atomicAdd(&a.prof[ph], now - tp);
+            tp = now;
+        }
+    };
+#else
+    auto stamp = [](int) {};
+#endif
     const uint32_t row = rows[ri];
     const uint32_t beg = a.ptr[row];
     const uint32_t n = a.ptr[row + 1] - beg;
@@ -431,14 +452,17 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
 
     // ratings of this wave: vector v covers ratings q = (wr*V + v)*4 + rr;
     // slots past the row's end gather the partner table's zero row
-    const T* __restrict__ prow[V];
+    uint32_t pj[V];  // partner rows (the zero row past the row's end)
     T e[V];
+    uint32_t pm[V];  // residual scatter targets, loaded now so the epilogue stores do not wait
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-        const uint32_t pj = q < n ? a.part[beg + q] : a.zrow;
-        prow[v] = a.partner + (size_t)pj * Kp + ci;
+        pj[v] = q < n ? a.part[beg + q] : a.zrow;
+        pm[v] = q < n ? a.perm[beg + q] : 0u;
     }
+    const T* __restrict__ pbase = a.partner + ci;
+#define PROW(v) (pbase + (size_t)pj[v] * Kp)
     if (a.e_from_dot) {
         T dot[V];
 #pragma unroll
@@ -446,7 +470,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
         for (uint32_t k0 = 0; k0 < K; k0 += GB) {
             const T o = a.own[(size_t)row * Kp + k0 + ci];  // padding columns are zero
 #pragma unroll
-            for (int v = 0; v < V; ++v) dot[v] += prow[v][k0] * o;
+            for (int v = 0; v < V; ++v) dot[v] += PROW(v)[k0] * o;
         }
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -464,12 +488,13 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
 
     const T tau = a.tau;
     const T* __restrict__ orow = a.own + (size_t)row * Kp + ci;
+    stamp(0);  // row setup (ids, residuals, normals)
     // software pipeline: block b+1's slices and own/sigma/mu values are in
     // flight while block b is reduced, solved and applied.  The prefetch past
     // the last block stays inside the tables (slack row / padding).
     T s[V], sn[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) s[v] = prow[v][0];
+    for (int v = 0; v < V; ++v) s[v] = PROW(v)[0];
     T oldc = orow[0], sgc = a.sig[ci], muc = a.mu[ci];
     for (uint32_t b0 = 0; b0 < K; b0 += GB) {
         const uint32_t kk = b0 + ci;
@@ -479,7 +504,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
         const T sgn = a.sig[kn + ci];
         const T mun = a.mu[kn + ci];
 #pragma unroll
-        for (int v = 0; v < V; ++v) sn[v] = prow[v][kn];
+        for (int v = 0; v < V; ++v) sn[v] = PROW(v)[kn];
         acc_t g = {T(0), T(0), T(0), T(0)};
         T cc = T(0);
 #pragma unroll
@@ -489,8 +514,10 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
         }
         cc += shfl_xor_t(cc, 16);
         cc += shfl_xor_t(cc, 32);
+        stamp(1);  // slice loads + G / c
         // ---- 2. G (strictly lower + diagonal), c -> LDS; multi-wave rows sum in wave order
         if constexpr (NW > 1) lds_barrier();  // previous block's readers of Ls are done
+        stamp(2);  // barrier: other waves
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int r = MfmaT<T>::row(lane, j);
@@ -520,6 +547,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
                 }
             }
             lds_barrier();
+            stamp(3);  // cross-wave reduction
         } else {
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own LDS writes visible to own reads
             __builtin_amdgcn_wave_barrier();
@@ -545,10 +573,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
             const T sd = a.sd_is_var ? var : tsqrt(var);
             const T A = var * sg * mu + sd * z;
             const T Bq = var * tau;
-            T H[GB];
-#pragma unroll
-            for (int j = 0; j < GB; ++j) H[j] = Bq * Ls[ws][ci][j];
-            dlt = gblock_solve(H, A - old + Bq * (Cs[ws][ci] + P * old));
+            dlt = gblock_solve_lds(&Ls[ws][ci][0], Bq, A - old + Bq * (Cs[ws][ci] + P * old));
             const T nwv = old + dlt;
             if constexpr (NW > 1) {
                 // staged in LDS, written after the last barrier: no wave of this
@@ -563,9 +588,11 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
             lds_barrier();
             dlt = Dsh[ci];
         }
+        stamp(4);  // solve + D hand-off
         // ---- 4. e -= S_B D_B (lane (r,i) holds D_i): 16-lane DPP row sums
 #pragma unroll
         for (int v = 0; v < V; ++v) e[v] -= row16_sum(s[v] * dlt);
+        stamp(5);  // residual update
 #pragma unroll
         for (int v = 0; v < V; ++v) s[v] = sn[v];
         oldc = oldn;
@@ -583,7 +610,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
         if (q < n && ci == 0) {
-            a.E_other[a.perm[beg + q]] = e[v];
+            a.E_other[pm[v]] = e[v];
             sq += e[v] * e[v];
             if (a.row_tr) {
                 const T r = a.r_this[beg + q];
@@ -616,6 +643,8 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), 3) void k_gblock(const ui
             if (a.row_tr) a.row_tr[row] = dtr;
         }
     }
+    stamp(6);  // epilogue
+#undef PROW
 }
 
 // ------------------------------------------------------------ streaming Gram-block rows
@@ -689,7 +718,8 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
             }
         }
 
-        // optional phase profile (SBMF_KPROF): wave 0's cycles per phase
+        // optional phase profile (build with KPROF=1, run with SBMF_KPROF=1): wave 0's cycles per phase
+#ifdef SBMF_KPROF_BUILD
         unsigned long long tp = (sy.prof && threadIdx.x == 0) ? clock64() : 0ull;
         auto stamp = [&](int ph) {
             if (sy.prof && threadIdx.x == 0) {
@@ -698,6 +728,9 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
                 tp = now;
             }
         };
+#else
+        auto stamp = [](int) {};
+#endif
         // ---- stage the task's partner ids and initial residuals in LDS; the
         // slots up to the traversal stride (4*NW*UNR ratings) hold the zero
         // row and zero residuals, so the traversal needs no per-rating masks
@@ -741,6 +774,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
             T cc = T(0);
             auto traverse = [&](auto phase) {
                 constexpr int PH = decltype(phase)::value;
+                uint32_t pm[UNR];  // PH 2: residual scatter targets, in flight with the slices
                 auto load = [&](uint32_t v0, T (&sp)[UNR], T (&sc)[UNR], T (&e)[UNR]) {
                     uint32_t pj[UNR];
 #pragma unroll
@@ -748,6 +782,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
                         const uint32_t q = 4 * (v0 + u * NW) + rr;  // < npad: padded slots
                         pj[u] = pjL[q];
                         e[u] = eL[q];
+                        if constexpr (PH == 2) pm[u] = q < n ? a.perm[beg + q] : 0u;
                     }
 #pragma unroll
                     for (int u = 0; u < UNR; ++u) {
@@ -776,7 +811,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
                         for (int u = 0; u < UNR; ++u) {
                             const uint32_t q = 4 * (v0 + u * NW) + rr;
                             if (q < n && ci == 0) {
-                                a.E_other[a.perm[beg + q]] = e[u];
+                                a.E_other[pm[u]] = e[u];
                                 sq += (double)(e[u] * e[u]);
                                 if (a.row_tr) {
                                     const T r = a.r_this[beg + q];
@@ -1440,7 +1475,11 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
             SBMF_GBLOCK(V / 4, 1, 4, (nrows + 3) / 4, 256);
             break;
         case GK_W16:  // 1 wave / row
-            SBMF_GBLOCK(V, 1, 4, (nrows + 3) / 4, 256);
+            if (sizeof(T) == 8 && !(a.tune & 8u)) {  // wide (default): 16 vectors (64 ratings), 2 waves/SIMD
+                SBMF_GBLOCK(16, 1, 2, (nrows + 1) / 2, 128);
+            } else {
+                SBMF_GBLOCK(V, 1, 4, (nrows + 3) / 4, 256);
+            }
             break;
         case GK_B2:  // 2 waves / row
             SBMF_GBLOCK(V, 2, 1, nrows, 128);
@@ -1462,6 +1501,33 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
 // tune bit 0: every wave solves redundantly (no extra barrier).
 static int gstream_nw(uint32_t) { return 8; }
 int gstream_wg_target(uint32_t) { return 2; }
+
+template <typename T>
+hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st) {
+    if (nrows == 0) return hipSuccess;
+    constexpr int V = sizeof(T) == 8 ? 8 : 16;
+    const bool sw = !(a.tune & 1u);
+#define SBMF_GB_NW(NW_)                                                                          \
+    case NW_:                                                                                    \
+        if (sw)                                                                                  \
+            k_gblock<T, V, NW_, 1, true><<<nrows, 64 * NW_, 0, st>>>(rows, nrows, a);            \
+        else                                                                                     \
+            k_gblock<T, V, NW_, 1, false><<<nrows, 64 * NW_, 0, st>>>(rows, nrows, a);           \
+        break;
+    switch (nw) {
+        SBMF_GB_NW(2)
+        SBMF_GB_NW(3)
+        SBMF_GB_NW(4)
+        SBMF_GB_NW(5)
+        SBMF_GB_NW(6)
+        SBMF_GB_NW(7)
+        SBMF_GB_NW(8)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef SBMF_GB_NW
+    return hipGetLastError();
+}
 
 template <typename T>
 static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
@@ -1624,6 +1690,7 @@ hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint
 #define SBMF_INST(T)                                                                                                 \
     template hipError_t launch_rows<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);            \
     template hipError_t launch_gblock<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);          \
+    template hipError_t launch_gblock_nw<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);       \
     template hipError_t launch_gstream<T>(const SplitTask*, uint32_t, uint32_t, const SplitRow*, uint32_t,           \
                                           const HalfArgs<T>&, const SplitSync&, hipStream_t);                        \
     template int gstream_blocks_per_cu<T>(uint32_t, uint32_t);                                                      \

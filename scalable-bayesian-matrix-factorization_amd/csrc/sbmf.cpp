@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -109,6 +110,7 @@ struct Side {
     std::vector<GramRow> grows;
     std::vector<SplitTask> stasks;   // streaming kernel tasks, in rounds of `sgrid` slots
     std::vector<SplitRow> xrows;     // rows split over several tasks
+    std::vector<std::array<uint32_t, 3>> gsub[GK_NUM];  // multi-wave bins: (waves, offset, count) sub-ranges
     std::vector<ResidTask> rtasks;   // residual recompute: own rows in chunks of <= RESID_CHUNK
     std::vector<uint32_t> rtptr;     // [r1-r0+1] first task of each own row
     uint32_t nxchunk = 0;            // tasks belonging to split rows (slab / staging slots)
@@ -157,7 +159,7 @@ static const int KIND_STREAM = GK_NUM;  // 5: streaming kernel, whole rows (row 
 static const int KIND_RK0 = GK_NUM + 1;  // 6..9
 static const int KIND_GRAM = 10;         // Gram route
 
-static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr, bool f64) {
+static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr, bool f64, bool wide) {
     for (auto& b : s.bin_rows) b.clear();
     s.gitems.clear();
     s.grows.clear();
@@ -185,7 +187,7 @@ static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stre
         }
         if (row_kernel == 0) {
             int kind = GK_W4;
-            while (d > gk_maxdeg(kind, f64)) ++kind;
+            while (d > gk_maxdeg(kind, f64, wide)) ++kind;
             s.bin_rows[kind].push_back(r);
             continue;
         }
@@ -331,8 +333,27 @@ static void prepare_T(sbmf_ctx* c) {
         thr = cf.gram_threshold ? cf.gram_threshold : 0xffffffffu;
     else
         thr = cf.gram_threshold ? std::min(cf.gram_threshold, RK_MAXDEG[RK_NUM - 1]) : RK_MAXDEG[RK_NUM - 1];
-    build_bins(c->users, thr, (int)cf.row_kernel, sthr, f64);
-    build_bins(c->items, thr, (int)cf.row_kernel, sthr, f64);
+    const bool wide = !(cf.tune & 8u);  // f64 rows <= 64 ratings on one wave (default)
+    build_bins(c->users, thr, (int)cf.row_kernel, sthr, f64, wide);
+    build_bins(c->items, thr, (int)cf.row_kernel, sthr, f64, wide);
+    // multi-wave Gram-block bins: ceil(deg / ratings-per-wave) waves per row,
+    // contiguous sub-ranges since each bin is degree-descending
+    for (Side* sd : {&c->users, &c->items})
+        for (int k = GK_B2; k < GK_NUM; ++k) {
+            sd->gsub[k].clear();
+            const std::vector<uint32_t>& rows = sd->bin_rows[k];
+            const uint32_t per_wave = f64 ? 32 : 64;
+            for (uint32_t i = 0; i < rows.size();) {
+                const uint32_t d = sd->ptr[rows[i] + 1] - sd->ptr[rows[i]];
+                const uint32_t nw = std::max(2u, (d + per_wave - 1) / per_wave);
+                uint32_t j = i;
+                while (j < rows.size() &&
+                       std::max(2u, (sd->ptr[rows[j] + 1] - sd->ptr[rows[j]] + per_wave - 1) / per_wave) == nw)
+                    ++j;
+                sd->gsub[k].push_back({nw, i, j - i});
+                i = j;
+            }
+        }
     const uint32_t nblk = (c->K + 15) / 16;
     {
         int dev_cus = 0;
@@ -476,8 +497,8 @@ static void prepare_T(sbmf_ctx* c) {
     HIPCHK(hipStreamSynchronize(st));
     c->kprof = std::getenv("SBMF_KPROF") && std::atoi(std::getenv("SBMF_KPROF")) > 0;
     if (c->kprof) {
-        c->d_kprof.alloc(16 * sizeof(unsigned long long));
-        HIPCHK(hipMemset(c->d_kprof.p, 0, 16 * sizeof(unsigned long long)));
+        c->d_kprof.alloc(32 * sizeof(unsigned long long));
+        HIPCHK(hipMemset(c->d_kprof.p, 0, 32 * sizeof(unsigned long long)));
     }
     c->sweep = 0;
     c->collected = 0;
@@ -602,6 +623,7 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
         a.row_tr = c->cfg.eval_train ? c->d_rowtr_v.as<double>() : nullptr;
     }
     a.tune = c->cfg.tune;
+    a.prof = c->kprof ? c->d_kprof.as<unsigned long long>() + 16 + 8 * (users ? 0 : 1) : nullptr;
     a.tau = (T)c->tau;
     a.K = c->K;
     a.Kp = c->Kp;
@@ -634,7 +656,10 @@ static void run_half(sbmf_ctx* c, bool users) {
     for (int k = NBIN - 1; k >= 0; --k) {
         if (s.bin_rows[k].empty()) continue;
         HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
-        if (k < GK_NUM)
+        if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
+            for (const auto& g : s.gsub[k])
+                HIPCHK(launch_gblock_nw<T>((int)g[0], bins[k].as<uint32_t>() + g[1], g[2], a, st));
+        } else if (k < GK_NUM)
             HIPCHK(launch_gblock<T>(k, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
         else if (k == KIND_STREAM) {
             SplitSync sy{};
@@ -808,9 +833,22 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(hipMemcpyAsync(&split_timeout, c->d_xtimeout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (c->kprof) {
-            unsigned long long h[16];
+            unsigned long long h[32];
             HIPCHK(hipMemcpy(h, c->d_kprof.p, sizeof(h), hipMemcpyDeviceToHost));
             HIPCHK(hipMemset(c->d_kprof.p, 0, sizeof(h)));
+            static const char* gn[7] = {"setup", "load+mfma", "barrier", "reduce", "solve+handoff", "e-update",
+                                        "epilogue"};
+            for (int sd = 0; sd < 2; ++sd) {
+                double tot = 0;
+                for (int k = 0; k < 7; ++k) tot += (double)h[16 + 8 * sd + k];
+                if (tot == 0) continue;
+                std::fprintf(stderr, "[kprof] sweep %u %s gblock multi-wave rows (wave-0 Gcycles total):", c->sweep,
+                             sd ? "items" : "users");
+                for (int k = 0; k < 7; ++k)
+                    std::fprintf(stderr, " %s %.3f (%.0f%%)", gn[k], (double)h[16 + 8 * sd + k] / 1e9,
+                                 100.0 * (double)h[16 + 8 * sd + k] / tot);
+                std::fprintf(stderr, "\n");
+            }
             static const char* nm[7] = {"stage", "traverse", "wg-wait", "reduce", "split-xchg", "solve", "epilogue"};
             for (int sd = 0; sd < 2; ++sd) {
                 const Side& S = sd ? c->items : c->users;

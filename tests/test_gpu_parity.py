@@ -121,7 +121,7 @@ def test_split_rows_match_oracle(ml100k, chunk, K):
     np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("tune", [0, 1])
+@pytest.mark.parametrize("tune", [0, 1, 4, 8, 13])
 def test_kernel_variants_match_oracle(ml100k, tune):
     """Kernel variants (sbmf_config.tune): block solve by one wave that hands D
     over in LDS (default, bit 0 clear) or by every wave of a row (bit 0 set)."""
