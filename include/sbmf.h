@@ -85,7 +85,7 @@ typedef struct sbmf_config {
                                  Gram-block kernel (0 = default: 256 f64 / 512 f32)              */
     uint32_t split_chunk;     /* streaming-kernel task size: rows longer than this are split
                                  into chunks on co-resident workgroups (0 = the LDS capacity,
-                                 1792 f64 / 3584 f32; larger values are capped to it)            */
+                                 4096 f64 / ~8K f32, sized to LDS; larger values are capped to it)            */
     uint32_t tune;            /* kernel-variant bits for experiments (0 = tuned defaults):
                                  bit 0 = block solve replicated in every wave of a row
                                  (default: one wave solves, D shared through LDS),
@@ -163,7 +163,7 @@ int sbmf_get_dims(sbmf_ctx* ctx, uint32_t* num_users, uint32_t* num_items, uint6
  *         waves/row (ceil(ratings/32) f64, /64 f32) timed in three groups; up to
  *         8/64/64/128/256 ratings (f64), 16/64/128/256/512 (f32),
  *   5     streaming MFMA Gram-block kernel: one persistent cooperative launch
- *         over tasks of <= 1792 (f64) / 3584 (f32) ratings -- whole rows, or
+ *         over tasks of <= 4096 (f64) / ~8K (f32) ratings (LDS capacity) -- whole rows, or
  *         chunks of longer rows on co-resident workgroups -- plus the publish
  *         of split rows,
  *   6..9  per-coordinate wave-reduction row kernels (1 wave/row <=128 and

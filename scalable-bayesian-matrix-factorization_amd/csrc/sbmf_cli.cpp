@@ -167,7 +167,7 @@ int main(int argc, char** argv) {
         cl.reg("recompute_every", "recompute residuals from scratch every n sweeps; default=1");
         cl.reg("gram_threshold", "rows with more ratings take the Gram route; default: never (row_kernel 0)");
         cl.reg("stream_threshold", "rows with more ratings take the streaming kernel; default=256 (f64) / 512 (f32)");
-        cl.reg("split_chunk", "streaming task size; longer rows are split over co-resident workgroups; default=1792 (f64) / 3584 (f32)");
+        cl.reg("split_chunk", "streaming task size; longer rows are split over co-resident workgroups; default: LDS capacity (4096 f64 / ~8K f32)");
         cl.reg("row_kernel", "0: MFMA Gram-block kernels (default) | 1: per-coordinate wave-reduction kernels");
         if (cl.has("help") || argc == 1) {
             cl.print_help();
