@@ -9,6 +9,4 @@ run() {
 import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print('%.3f G/s %.2f ms user %.2f item %.2f' % (d['value']/1e9, d['ms_per_step'], c['ms_user_half'], c['ms_item_half'])); print({k: v for k, v in c['kernel_ms'].items() if v > 0.1})"
 }
 run X=0 --tune 0
-run X=0 --tune 0 --stream-threshold 192
-run X=0 --tune 0 --stream-threshold 128
-run X=0 --tune 0 --stream-threshold 64
+run X=0 --tune 0 --precision f32

@@ -35,7 +35,12 @@ namespace {
 // ------------------------------------------------------------------ wave64 helpers
 template <int CTRL, int ROWM>
 __device__ __forceinline__ int dpp_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWM, 0xf, false);
+    // quad_perm (0x00-0xff), row_ror (0x121-0x12f) and the row mirrors over all rows write
+    // every lane: no "old" value to materialise (saves a v_mov per DPP)
+    if constexpr (ROWM == 0xf && (CTRL <= 0xff || (CTRL >= 0x121 && CTRL <= 0x12f) || CTRL == 0x140 || CTRL == 0x141))
+        return __builtin_amdgcn_mov_dpp(v, CTRL, ROWM, 0xf, false);
+    else
+        return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWM, 0xf, false);
 }
 template <int CTRL, int ROWM>
 __device__ __forceinline__ float dpp(float v) {
@@ -459,6 +464,9 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
         pj[v] = q < n ? a.part[beg + q] : a.zrow;
+#ifdef SBMF_KPROF_BUILD
+        if (a.tune & 0x100u) pj[v] = 0;  // ablation (wrong results): every gather hits one cached row
+#endif
         pm[v] = q < n ? a.perm[beg + q] : 0u;
     }
     const T* __restrict__ pbase = a.partner + ci;
@@ -495,8 +503,27 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     T s[V], sn[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) s[v] = PROW(v)[0];
+    // ratings for the train error, parked in LDS (read back by the same lanes
+    // in the epilogue) so the epilogue waits on no global load
+    __shared__ T Rs[NWAVE * V * 4];
+    const bool want_r = a.row_tr != nullptr;
+    if (want_r && ci == 0) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
+            Rs[(wv * V + v) * 4 + rr] = q < n ? a.r_this[beg + q] : T(0);
+        }
+    }
     T oldc = orow[0], sgc = a.sig[ci], muc = a.mu[ci];
+#ifdef SBMF_KPROF_BUILD
+    // ablation (wrong results): tune 0x800 runs the block loop twice (block index wraps)
+    const uint32_t Kr = (K + GB - 1) / GB * GB;
+    const uint32_t KL = (a.tune & 0x800u) ? 2 * Kr : K;
+    for (uint32_t bl = 0; bl < KL; bl += GB) {
+        const uint32_t b0 = bl % Kr;
+#else
     for (uint32_t b0 = 0; b0 < K; b0 += GB) {
+#endif
         const uint32_t kk = b0 + ci;
         const bool kin = kk < K;
         const uint32_t kn = b0 + GB;
@@ -509,6 +536,11 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         T cc = T(0);
 #pragma unroll
         for (int v = 0; v < V; ++v) {
+#ifdef SBMF_KPROF_BUILD
+            if (a.tune & 0x1000u)  // ablation (wrong results): no MFMA
+                g[v & 3] += s[v];
+            else
+#endif
             g = MfmaT<T>::mfma(s[v], g);
             cc += s[v] * e[v];
         }
@@ -573,6 +605,11 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             const T sd = a.sd_is_var ? var : tsqrt(var);
             const T A = var * sg * mu + sd * z;
             const T Bq = var * tau;
+#ifdef SBMF_KPROF_BUILD
+            if (a.tune & 0x200u)  // ablation (wrong results): no 16-step recurrence
+                dlt = A - old + Bq * (Cs[ws][ci] + P * old);
+            else
+#endif
             dlt = gblock_solve_lds(&Ls[ws][ci][0], Bq, A - old + Bq * (Cs[ws][ci] + P * old));
             const T nwv = old + dlt;
             if constexpr (NW > 1) {
@@ -590,6 +627,12 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         }
         stamp(4);  // solve + D hand-off
         // ---- 4. e -= S_B D_B (lane (r,i) holds D_i): 16-lane DPP row sums
+#ifdef SBMF_KPROF_BUILD
+        if (a.tune & 0x400u) {  // ablation (wrong results): residual update without the row sums
+#pragma unroll
+            for (int v = 0; v < V; ++v) e[v] -= s[v] * dlt;
+        } else
+#endif
 #pragma unroll
         for (int v = 0; v < V; ++v) e[v] -= row16_sum(s[v] * dlt);
         stamp(5);  // residual update
@@ -612,8 +655,8 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         if (q < n && ci == 0) {
             a.E_other[pm[v]] = e[v];
             sq += e[v] * e[v];
-            if (a.row_tr) {
-                const T r = a.r_this[beg + q];
+            if (want_r) {
+                const T r = Rs[(wv * V + v) * 4 + rr];
                 T pr = r - e[v];
                 pr = (pr < a.hi) ? pr : a.hi;
                 pr = (a.lo < pr) ? pr : a.lo;
@@ -630,7 +673,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
                 red2[wr][0] = dsq;
                 red2[wr][1] = dtr;
             }
-            __syncthreads();
+            lds_barrier();  // LDS only: the residual scatter stores stay in flight
             dsq = 0.0;
             dtr = 0.0;
             for (int w = 0; w < NW; ++w) {
