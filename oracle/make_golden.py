@@ -5,15 +5,18 @@ Runs the reference itself (oracle/_ref/, compiled unmodified from
 /root/reference by `make -C oracle ref`) and stores its outputs as small
 fixtures.  The reference samplers read their inputs from the hard-coded
 relative paths ../../data/m100k/{train_sbpmf,test_sbpmf} (final,
-gibbs_sbpmf_final.cpp:33,96) and ../../data/m100k/{train,test} (sbpmf2,
-gibbs_sbpmf2.cpp:33,96), with D=20 factors and 100 sweeps baked in
-(:218, :299).  We satisfy those paths with a scratch directory tree in /tmp
+gibbs_sbpmf_final.cpp:33,96), ../../data/m100k/{train,test} (sbpmf2,
+gibbs_sbpmf2.cpp:33,96), ../../data/ra.{train,test}_sbpmf (the biased
+sampler at the top level, gibbs_sbpmf2.cpp:32,98; D=20) and
+../../data/m1m/{train,test}_sbpmf (src/libfm/gibbs_sbpmf22.cpp:33,74; D=100),
+with 100 sweeps baked in.  We satisfy those paths with a scratch directory tree in /tmp
 so any triple file can be fed in without touching the sources.
 
 Fixtures written (all data, no reference source):
   ml100k_train.tsv.gz / ml100k_test.tsv.gz   inputs (copy of data/m100k/*_sbpmf)
   ragged_train.tsv / ragged_test.tsv          synthetic edge-case inputs
-  ref_<variant>_<data>_k20_s<seed>.txt        100 lines "%.17g" test RMSE
+  ref_<variant>_<data>_k<K>_s<seed>.txt       100 lines "%.17g" test RMSE
+                                              (variants final, sbpmf2, bias2, bias22)
   ref_rng_s<seed>.txt                         rand / ran_gaussian / ran_gamma
 Only runnable in the build container (needs /root/reference).
 """
@@ -35,19 +38,28 @@ def run_ref(binary, train_path, test_path, seed):
     """Run a reference sampler with its hard-coded relative input paths."""
     root = "/tmp/sbmf_refrun_%d" % os.getpid()
     cwd = os.path.join(root, "a", "b")
-    data = os.path.join(root, "data", "m100k")
     os.makedirs(cwd, exist_ok=True)
-    os.makedirs(data, exist_ok=True)
-    for name, src in (("train_sbpmf", train_path), ("test_sbpmf", test_path),
-                      ("train", train_path), ("test", test_path)):
-        dst = os.path.join(data, name)
+    links = [("m100k/train_sbpmf", train_path), ("m100k/test_sbpmf", test_path), ("m100k/train", train_path),
+             ("m100k/test", test_path), ("ra.train_sbpmf", train_path), ("ra.test_sbpmf", test_path),
+             ("m1m/train_sbpmf", train_path), ("m1m/test_sbpmf", test_path)]
+    for name, src in links:
+        dst = os.path.join(root, "data", name)
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
         if os.path.lexists(dst):
             os.remove(dst)
         os.symlink(os.path.abspath(src), dst)
     env = dict(os.environ, SBMF_REF_SEED=str(seed))
-    out = subprocess.run([binary], cwd=cwd, env=env, capture_output=True, text=True, check=True).stdout
+    p = subprocess.run([binary], cwd=cwd, env=env, capture_output=True, text=True)
     shutil.rmtree(root)
-    return [l.split()[-1] for l in out.splitlines() if l.startswith("rmse is")]
+    vals = [l.split()[-1] for l in p.stdout.splitlines() if l.startswith("rmse is")]
+    # The top-level biased sampler dies in its exit cleanup when a user or item
+    # id has no training ratings: the b_i / b_j step's `user_item_count[i]`
+    # (gibbs_sbpmf2.cpp:520,568) inserts the id into the map, and the cleanup
+    # (:651-667) then deletes an R[i] / R_t[j] that was never allocated.  Every
+    # "rmse is" line is printed before that, so the trajectory is complete.
+    if p.returncode != 0 and not (len(vals) == 100 and p.returncode == -11):
+        raise RuntimeError("%s exited with %d" % (binary, p.returncode))
+    return vals
 
 
 def ragged_dataset(seed=3):
@@ -94,12 +106,15 @@ def main():
 
     runs = [("final", "ml100k", ml_train, ml_test, 1), ("final", "ml100k", ml_train, ml_test, 7),
             ("sbpmf2", "ml100k", ml_train, ml_test, 1), ("final", "ragged", rtrain_p, rtest_p, 1),
-            ("sbpmf2", "ragged", rtrain_p, rtest_p, 5)]
+            ("sbpmf2", "ragged", rtrain_p, rtest_p, 5), ("bias2", "ml100k", ml_train, ml_test, 1),
+            ("bias2", "ragged", rtrain_p, rtest_p, 3), ("bias22", "ml100k", ml_train, ml_test, 1)]
+    binaries = {"final": ("gibbs_sbpmf_final", 20), "sbpmf2": ("gibbs_sbpmf2", 20),
+                "bias2": ("gibbs_sbpmf2_bias", 20), "bias22": ("gibbs_sbpmf22", 100)}
     for variant, dname, tr, te, seed in runs:
-        binary = os.path.join(HERE, "_ref", "gibbs_sbpmf_final" if variant == "final" else "gibbs_sbpmf2")
-        vals = run_ref(binary, tr, te, seed)
+        binary, K = binaries[variant]
+        vals = run_ref(os.path.join(HERE, "_ref", binary), tr, te, seed)
         assert len(vals) == 100, (variant, dname, len(vals))
-        with open(os.path.join(GOLD, "ref_%s_%s_k20_s%d.txt" % (variant, dname, seed)), "w") as f:
+        with open(os.path.join(GOLD, "ref_%s_%s_k%d_s%d.txt" % (variant, dname, K, seed)), "w") as f:
             f.write("\n".join(vals) + "\n")
         print("golden", variant, dname, seed, vals[0], vals[-1])
     for seed in (1, 7):

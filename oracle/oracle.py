@@ -10,7 +10,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
-QUIRKS = {"final": 0, "sbpmf2": 1, "none": 2}
+QUIRKS = {"final": 0, "sbpmf2": 1, "none": 2, "bias2": 3, "bias22": 4}
 
 
 class OracleConfig(C.Structure):
@@ -24,7 +24,8 @@ class OracleResult(C.Structure):
                 ("tau", C.POINTER(C.c_double)), ("rmse_cap", C.c_uint32),
                 ("U", C.POINTER(C.c_double)), ("V", C.POINTER(C.c_double)), ("hyper", C.POINTER(C.c_double)),
                 ("pred_sum", C.POINTER(C.c_double)), ("num_users", C.c_uint32), ("num_items", C.c_uint32),
-                ("sweeps_done", C.c_uint32), ("seconds", C.c_double)]
+                ("sweeps_done", C.c_uint32), ("seconds", C.c_double), ("bu", C.POINTER(C.c_double)),
+                ("bv", C.POINTER(C.c_double)), ("b0", C.c_double)]
 
 
 def build():
@@ -64,7 +65,8 @@ def run(train, test, K=20, iters=100, seed=1, quirks="final", burnin=0, num_user
         seconds_limit=0.0, want_factors=True):
     """train/test: (user, item, rating) arrays.  Returns dict with per-sweep
     'rmse' (running mean, the reference's "rmse is"), 'rmse_this', 'tau',
-    final 'U' [I][K], 'V' [J][K], 'hyper', 'pred_sum', 'seconds'."""
+    final 'U' [I][K], 'V' [J][K], 'hyper', 'pred_sum', 'seconds', and for the
+    biased samplers (quirks bias2 / bias22) 'bu', 'bv', 'b0'."""
     L = lib()
     cfg = OracleConfig()
     L.oracle_config_default(C.byref(cfg))
@@ -88,6 +90,8 @@ def run(train, test, K=20, iters=100, seed=1, quirks="final", burnin=0, num_user
     res.hyper = _p(hyper, C.c_double)
     ps = np.zeros(max(len(sr), 1))
     res.pred_sum = _p(ps, C.c_double)
+    bu, bv = np.zeros(I), np.zeros(J)
+    res.bu, res.bv = _p(bu, C.c_double), _p(bv, C.c_double)
     rc = L.oracle_run_arrays(C.byref(cfg), C.c_uint64(len(tr)), _p(tu, C.c_uint32), _p(ti, C.c_uint32),
                              _p(tr, C.c_double), C.c_uint64(len(sr)), _p(su, C.c_uint32), _p(si, C.c_uint32),
                              _p(sr, C.c_double), C.c_uint32(num_users), C.c_uint32(num_items), C.byref(res))
@@ -95,7 +99,7 @@ def run(train, test, K=20, iters=100, seed=1, quirks="final", burnin=0, num_user
     n = res.sweeps_done
     return {"rmse": rm[:n], "rmse_this": rt[:n], "tau": ta[:n], "U": U, "V": V, "hyper": hyper,
             "pred_sum": ps[:len(sr)], "seconds": res.seconds, "sweeps": n, "num_users": res.num_users,
-            "num_items": res.num_items}
+            "num_items": res.num_items, "bu": bu, "bv": bv, "b0": res.b0}
 
 
 def stream(seed, kind, n, shape=1.0):

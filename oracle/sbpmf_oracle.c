@@ -28,6 +28,9 @@
  *   user half-sweep   :453-491
  *   item half-sweep   :495-535
  *   test RMSE         :539-563 (running mean of clamped predictions)
+ * and the biased sampler (quirks BIAS2 / BIAS22, run_bias below):
+ * /root/reference/gibbs_sbpmf2.cpp (top level) = src/libfm/gibbs_sbpmf22.cpp
+ * up to init scale, test clamp and D.
  * The floating-point operation order of every expression follows the
  * reference so that a gcc -O3 build (SSE2, no FMA contraction) reproduces
  * it bit for bit.
@@ -183,6 +186,193 @@ static double now_s(void) {
     return ts.tv_sec + 1e-9 * ts.tv_nsec;
 }
 
+/* ------------------------------------------------------- biased sampler --- */
+/* /root/reference/gibbs_sbpmf2.cpp (top level; BIAS2) and the same algorithm
+ * in src/libfm/gibbs_sbpmf22.cpp (BIAS22).  Line numbers: top-level file
+ * first, then gibbs_sbpmf22.cpp.  Global bias b_0 with a Normal-Gamma prior,
+ * per-user / per-item biases b_i, b_j each with its own (sigma, mu) pair drawn
+ * every sweep, tau named alpha with shape a0' + N and rate b0' + sum E^2, and
+ * factor hyperparameters with shape alpha + I (not (I+1)/2).  All six prior
+ * groups use alpha = beta = sigma = 1, mu = 0 (:284-318 / :290-325). */
+static int run_bias(const oracle_config *cfg, uint64_t n_train, const uint32_t *tu, const uint32_t *ti,
+                    const double *tr, uint64_t n_test, const uint32_t *su, const uint32_t *si, const double *sr,
+                    uint32_t I, uint32_t J, oracle_result *res) {
+    const uint32_t D = cfg->K;
+    const int top = cfg->quirks == ORACLE_QUIRKS_BIAS2;
+    const double init_scale = cfg->init_stdev >= 0 ? cfg->init_stdev : (top ? 0.1 : 1.0); /* :242 / :186 */
+    const double lo = cfg->clamp_lo >= 0 ? cfg->clamp_lo : (top ? 0.5 : 1.0);            /* :628 / :578 */
+    const double hi = cfg->clamp_hi;
+    lists R, Rt;
+    build_lists(n_train, tu, ti, I, &R);
+    build_lists(n_train, ti, tu, J, &Rt);
+
+    srand(cfg->seed);
+    double *U = malloc((size_t)I * D * sizeof(double));
+    double *V = malloc((size_t)D * J * sizeof(double));
+    for (uint32_t i = 0; i < I; i++) /* :240-244 */
+        for (uint32_t k = 0; k < D; k++) U[(size_t)i * D + k] = init_scale * o_gaussian(0.0, 1.0);
+    for (uint32_t k = 0; k < D; k++) /* :246-250 */
+        for (uint32_t j = 0; j < J; j++) V[(size_t)k * J + j] = init_scale * o_gaussian(0.0, 1.0);
+    double *sigma_u = calloc(D, sizeof(double)), *mu_u = calloc(D, sizeof(double));
+    double *sigma_v = calloc(D, sizeof(double)), *mu_v = calloc(D, sizeof(double));
+    double *b_i = calloc(I ? I : 1, sizeof(double)), *mu_b_i = calloc(I ? I : 1, sizeof(double));
+    double *sigma_b_i = calloc(I ? I : 1, sizeof(double));
+    double *b_j = calloc(J ? J : 1, sizeof(double)), *mu_b_j = calloc(J ? J : 1, sizeof(double));
+    double *sigma_b_j = calloc(J ? J : 1, sizeof(double));
+    const double ag = 1.0, bg = 1.0, sg = 1.0, mg = 0.0; /* alpha_k, beta_k, sigma_k, mu_k of every group */
+    double mu_b_0 = 0.0, sigma_b_0 = 0.0, b_0 = 0.0, alpha = 0.0; /* :315-318 */
+
+    double *E = calloc(n_train ? n_train : 1, sizeof(double));
+    double *sum = calloc(n_test ? n_test : 1, sizeof(double));
+    const uint32_t iters = cfg->iters; /* burn_iter = 0 (:323) */
+    double t_start = now_s();
+    res->sweeps_done = 0;
+    for (uint32_t iter = 0; iter < iters; iter++) {
+        /* E recompute, sum E, sum E^2 :342-359 */
+        double es = 0.0, esq = 0.0;
+        for (uint64_t c = 0; c < n_train; c++) {
+            uint32_t user = tu[c], item = ti[c];
+            double temp = 0.0;
+            for (uint32_t k = 0; k < D; k++) temp += U[(size_t)user * D + k] * V[(size_t)k * J + item];
+            E[c] = tr[c] - (b_0 + b_i[user] + b_j[item] + temp);
+            es += E[c];
+            esq += (E[c] * E[c]);
+        }
+        /* alpha :366-372 */
+        alpha = o_gamma(1.0 + n_train, 1.0 + esq);
+        /* sigma_b_0, mu_b_0, b_0 :376-410 */
+        sigma_b_0 = o_gamma(ag + 1, bg + (0.5 * (b_0 - mu_b_0) * (b_0 - mu_b_0)));
+        double s0 = 1.0 / (sg + sigma_b_0);
+        mu_b_0 = o_gaussian(s0 * ((sg * mg) + b_0 * sigma_b_0), s0);
+        double sb0 = 1 / (sigma_b_0 + alpha * n_train);
+        double mb0 = sb0 * (sigma_b_0 * mu_b_0 + alpha * (es + n_train * b_0));
+        double old_b0 = b_0;
+        b_0 = o_gaussian(mb0, sb0);
+        for (uint64_t c = 0; c < n_train; c++) E[c] += (old_b0 - b_0);
+        /* factor hyperparameters :415-467 */
+        for (uint32_t k = 0; k < D; k++) {
+            double temp = 0.0, temp2 = 0.0;
+            for (uint32_t i = 0; i < I; i++) {
+                double x = U[(size_t)i * D + k];
+                temp += (x - mu_u[k]) * (x - mu_u[k]);
+                temp2 += x;
+            }
+            sigma_u[k] = o_gamma(ag + I, bg + (0.5) * temp);
+            double s2 = 1 / (sg + sigma_u[k] * I);
+            mu_u[k] = o_gaussian(s2 * (sg * mg + sigma_u[k] * temp2), s2);
+            temp = 0.0;
+            temp2 = 0.0;
+            for (uint32_t j = 0; j < J; j++) {
+                double x = V[(size_t)k * J + j];
+                temp += (x - mu_v[k]) * (x - mu_v[k]);
+                temp2 += x;
+            }
+            sigma_v[k] = o_gamma(ag + J, bg + (0.5) * temp);
+            double s1 = 1 / (sg + sigma_v[k] * J);
+            mu_v[k] = o_gaussian(s1 * (sg * mg + sigma_v[k] * temp2), s1);
+        }
+        /* per-row bias hyperparameters: users :470-489, items :492-511 */
+        for (uint32_t i = 0; i < I; i++) {
+            sigma_b_i[i] = o_gamma(ag + 1, bg + (0.5 * (b_i[i] - mu_b_i[i]) * (b_i[i] - mu_b_i[i])));
+            double s4 = 1.0 / (sg + sigma_b_i[i]);
+            mu_b_i[i] = o_gaussian(s4 * ((sg * mg) + b_i[i] * sigma_b_i[i]), s4);
+        }
+        for (uint32_t j = 0; j < J; j++) {
+            sigma_b_j[j] = o_gamma(ag + 1, bg + (0.5 * (b_j[j] - mu_b_j[j]) * (b_j[j] - mu_b_j[j])));
+            double s5 = 1.0 / (sg + sigma_b_j[j]);
+            mu_b_j[j] = o_gaussian(s5 * ((sg * mg) + b_j[j] * sigma_b_j[j]), s5);
+        }
+        /* users: b_i then the k-loop :515-558 */
+        for (uint32_t i = 0; i < I; i++) {
+            uint32_t b = R.ptr[i], e = R.ptr[i + 1];
+            double sbi = 1 / (sigma_b_i[i] + (alpha * (e - b)));
+            double temp = 0.0;
+            for (uint32_t p = b; p < e; p++) temp += (E[R.cas[p]] + b_i[i]);
+            double mbi = sbi * ((sigma_b_i[i] * mu_b_i[i]) + alpha * temp);
+            double old = b_i[i];
+            b_i[i] = o_gaussian(mbi, sbi);
+            for (uint32_t p = b; p < e; p++) E[R.cas[p]] += (old - b_i[i]);
+            for (uint32_t k = 0; k < D; k++) {
+                const double *Vk = V + (size_t)k * J;
+                double t1 = 0.0, t2 = 0.0;
+                double *Uik = &U[(size_t)i * D + k];
+                for (uint32_t p = b; p < e; p++) {
+                    double v = Vk[R.oth[p]];
+                    t1 += (v * v);
+                    t2 += (v * (E[R.cas[p]] + v * *Uik));
+                }
+                double s_star = 1 / (sigma_u[k] + (alpha * t1));
+                double m_star = s_star * (alpha * t2 + sigma_u[k] * mu_u[k]);
+                double ou = *Uik;
+                *Uik = o_gaussian(m_star, s_star);
+                for (uint32_t p = b; p < e; p++) E[R.cas[p]] += Vk[R.oth[p]] * (ou - *Uik);
+            }
+        }
+        /* items: b_j then the k-loop :563-606 */
+        for (uint32_t j = 0; j < J; j++) {
+            uint32_t b = Rt.ptr[j], e = Rt.ptr[j + 1];
+            double sbj = 1 / (sigma_b_j[j] + (alpha * (e - b)));
+            double temp = 0.0;
+            for (uint32_t p = b; p < e; p++) temp += (E[Rt.cas[p]] + b_j[j]);
+            double mbj = sbj * ((sigma_b_j[j] * mu_b_j[j]) + alpha * temp);
+            double old = b_j[j];
+            b_j[j] = o_gaussian(mbj, sbj);
+            for (uint32_t p = b; p < e; p++) E[Rt.cas[p]] += (old - b_j[j]);
+            for (uint32_t k = 0; k < D; k++) {
+                double t1 = 0.0, t2 = 0.0;
+                double *Vjk = &V[(size_t)k * J + j];
+                for (uint32_t p = b; p < e; p++) {
+                    double u = U[(size_t)Rt.oth[p] * D + k];
+                    t1 += (u * u);
+                    t2 += (u * (E[Rt.cas[p]] + *Vjk * u));
+                }
+                double s_star = 1 / (sigma_v[k] + (alpha * t1));
+                double m_star = s_star * (alpha * t2 + sigma_v[k] * mu_v[k]);
+                double ov = *Vjk;
+                *Vjk = o_gaussian(m_star, s_star);
+                for (uint32_t p = b; p < e; p++) E[Rt.cas[p]] += U[(size_t)Rt.oth[p] * D + k] * (ov - *Vjk);
+            }
+        }
+        /* test RMSE of the running mean :610-636 (every sweep, divides by iter+1) */
+        double diff = 0.0, diff_this = 0.0;
+        for (uint64_t t = 0; t < n_test; t++) {
+            uint32_t user = su[t], item = si[t];
+            double temp = b_0 + b_i[user] + b_j[item];
+            for (uint32_t k = 0; k < D; k++) temp += U[(size_t)user * D + k] * V[(size_t)k * J + item];
+            temp = (temp < hi) ? temp : hi;
+            temp = (lo < temp) ? temp : lo;
+            sum[t] += temp;
+            diff += (sr[t] - ((double)sum[t] / (iter + 1))) * (sr[t] - ((double)sum[t] / (iter + 1)));
+            diff_this += (sr[t] - temp) * (sr[t] - temp);
+        }
+        if (res->rmse && iter < res->rmse_cap) res->rmse[iter] = sqrt(diff / n_test);
+        if (res->rmse_this && iter < res->rmse_cap) res->rmse_this[iter] = sqrt(diff_this / n_test);
+        if (res->tau && iter < res->rmse_cap) res->tau[iter] = alpha;
+        res->sweeps_done = iter + 1;
+        if (cfg->sweep_seconds_limit > 0 && now_s() - t_start > cfg->sweep_seconds_limit) break;
+    }
+    res->seconds = now_s() - t_start;
+    if (res->U) memcpy(res->U, U, (size_t)I * D * sizeof(double));
+    if (res->V)
+        for (uint32_t j = 0; j < J; j++)
+            for (uint32_t k = 0; k < D; k++) res->V[(size_t)j * D + k] = V[(size_t)k * J + j];
+    if (res->hyper) {
+        memcpy(res->hyper, sigma_u, D * sizeof(double));
+        memcpy(res->hyper + D, mu_u, D * sizeof(double));
+        memcpy(res->hyper + 2 * D, sigma_v, D * sizeof(double));
+        memcpy(res->hyper + 3 * D, mu_v, D * sizeof(double));
+    }
+    if (res->pred_sum && n_test) memcpy(res->pred_sum, sum, n_test * sizeof(double));
+    if (res->bu) memcpy(res->bu, b_i, (size_t)I * sizeof(double));
+    if (res->bv) memcpy(res->bv, b_j, (size_t)J * sizeof(double));
+    res->b0 = b_0;
+    free(U); free(V); free(sigma_u); free(mu_u); free(sigma_v); free(mu_v);
+    free(b_i); free(mu_b_i); free(sigma_b_i); free(b_j); free(mu_b_j); free(sigma_b_j);
+    free(E); free(sum);
+    free_lists(&R); free_lists(&Rt);
+    return 0;
+}
+
 int oracle_run_arrays(const oracle_config *cfg, uint64_t n_train, const uint32_t *tu, const uint32_t *ti,
                       const double *tr, uint64_t n_test, const uint32_t *su, const uint32_t *si,
                       const double *sr, uint32_t num_users, uint32_t num_items, oracle_result *res) {
@@ -208,6 +398,8 @@ int oracle_run_arrays(const oracle_config *cfg, uint64_t n_train, const uint32_t
     }
     res->num_users = I;
     res->num_items = J;
+    if (cfg->quirks == ORACLE_QUIRKS_BIAS2 || cfg->quirks == ORACLE_QUIRKS_BIAS22)
+        return run_bias(cfg, n_train, tu, ti, tr, n_test, su, si, sr, I, J, res);
 
     lists R, Rt;
     build_lists(n_train, tu, ti, I, &R);  /* R[u] = {case, item}  :204-205 */
@@ -365,11 +557,11 @@ int oracle_load_triples(const char *path, uint64_t *n, uint32_t **u, uint32_t **
 void oracle_free(void *p) { free(p); }
 
 #ifdef ORACLE_MAIN
-/* CLI: sbpmf_oracle TRAIN TEST K ITERS SEED [final|sbpmf2|none]
+/* CLI: sbpmf_oracle TRAIN TEST K ITERS SEED [final|sbpmf2|none|bias2|bias22]
  * prints "rmse is %.17g" per collection sweep, like gibbs_sbpmf_final.cpp:562 */
 int main(int argc, char **argv) {
     if (argc < 6) {
-        fprintf(stderr, "usage: %s TRAIN TEST K ITERS SEED [final|sbpmf2|none]\n", argv[0]);
+        fprintf(stderr, "usage: %s TRAIN TEST K ITERS SEED [final|sbpmf2|none|bias2|bias22]\n", argv[0]);
         return 2;
     }
     oracle_config cfg;
@@ -380,6 +572,8 @@ int main(int argc, char **argv) {
     if (argc > 6) {
         if (!strcmp(argv[6], "sbpmf2")) cfg.quirks = ORACLE_QUIRKS_SBPMF2;
         else if (!strcmp(argv[6], "none")) cfg.quirks = ORACLE_QUIRKS_NONE;
+        else if (!strcmp(argv[6], "bias2")) cfg.quirks = ORACLE_QUIRKS_BIAS2;
+        else if (!strcmp(argv[6], "bias22")) cfg.quirks = ORACLE_QUIRKS_BIAS22;
     }
     uint64_t n, nt;
     uint32_t *u, *i, *su, *si;

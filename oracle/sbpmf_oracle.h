@@ -6,7 +6,11 @@
 extern "C" {
 #endif
 
-enum { ORACLE_QUIRKS_FINAL = 0, ORACLE_QUIRKS_SBPMF2 = 1, ORACLE_QUIRKS_NONE = 2 };
+/* BIAS2: the biased sampler /root/reference/gibbs_sbpmf2.cpp (top level: init
+ * 0.1*N(0,1), test clamp [0.5,5]); BIAS22: src/libfm/gibbs_sbpmf22.cpp (same
+ * algorithm, init N(0,1), clamp [1,5]). */
+enum { ORACLE_QUIRKS_FINAL = 0, ORACLE_QUIRKS_SBPMF2 = 1, ORACLE_QUIRKS_NONE = 2, ORACLE_QUIRKS_BIAS2 = 3,
+       ORACLE_QUIRKS_BIAS22 = 4 };
 
 typedef struct {
     uint32_t K, iters, burnin;
@@ -24,6 +28,8 @@ typedef struct {
     double *pred_sum;  /* [n_test] or NULL */
     uint32_t num_users, num_items, sweeps_done;
     double seconds;
+    double *bu, *bv;   /* biased samplers: b_i [I], b_j [J] or NULL */
+    double b0;         /* biased samplers: global bias b_0 */
 } oracle_result;
 
 void oracle_config_default(oracle_config *c);

@@ -9,13 +9,16 @@ import oracle
 from conftest import golden_rmse
 
 
-@pytest.mark.parametrize("variant,data,seed", [("final", "ml100k", 1), ("final", "ml100k", 7),
-                                               ("sbpmf2", "ml100k", 1), ("final", "ragged", 1),
-                                               ("sbpmf2", "ragged", 5)])
-def test_oracle_bitwise_equals_reference(variant, data, seed, ml100k, ragged):
+@pytest.mark.parametrize("variant,data,seed,K", [("final", "ml100k", 1, 20), ("final", "ml100k", 7, 20),
+                                                 ("sbpmf2", "ml100k", 1, 20), ("final", "ragged", 1, 20),
+                                                 ("sbpmf2", "ragged", 5, 20), ("bias2", "ml100k", 1, 20),
+                                                 ("bias2", "ragged", 3, 20), ("bias22", "ml100k", 1, 100)])
+def test_oracle_bitwise_equals_reference(variant, data, seed, K, ml100k, ragged):
+    """bias2 = the biased sampler at the top level of the reference
+    (gibbs_sbpmf2.cpp, D=20), bias22 = src/libfm/gibbs_sbpmf22.cpp (D=100)."""
     tr, te = ml100k if data == "ml100k" else ragged
-    gold = golden_rmse("ref_%s_%s_k20_s%d.txt" % (variant, data, seed))
-    o = oracle.run(tr, te, K=20, iters=100, seed=seed, quirks=variant, want_factors=False)
+    gold = golden_rmse("ref_%s_%s_k%d_s%d.txt" % (variant, data, K, seed))
+    o = oracle.run(tr, te, K=K, iters=100, seed=seed, quirks=variant, want_factors=False)
     assert np.array_equal(o["rmse"], gold), np.abs(o["rmse"] - gold).max()
 
 
