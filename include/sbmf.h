@@ -53,8 +53,15 @@ enum sbmf_rng_mode { SBMF_RNG_REFERENCE = 0, SBMF_RNG_PHILOX = 1 };
  * passed as the stdev of ran_gaussian, :393,413,485,529; init N(0,1); clamp
  * [1,5]).  SBPMF2 = src/libfm/gibbs_sbpmf2.cpp (:240,248,386,406,412,557:
  * init N(0,0.1), nu0 without 1/2, mu_v uses sigma_u*, clamp [0.5,5]).
- * NONE = the statistically correct sampler (stdev = sqrt(variance)). */
-enum sbmf_quirks { SBMF_QUIRKS_FINAL = 0, SBMF_QUIRKS_SBPMF2 = 1, SBMF_QUIRKS_NONE = 2 };
+ * NONE = the statistically correct sampler (stdev = sqrt(variance)).
+ * BIAS2 = the biased sampler at the top level of the reference,
+ * gibbs_sbpmf2.cpp:335-637 (the paper's Algorithm 1, libFM -dim '1,1,K'):
+ * global bias b0 and per-user / per-item biases with Normal-Gamma priors,
+ * alpha ~ G(a0 + N, b0 + sum E^2), factor precisions with shape alpha0 + I,
+ * posterior variance as stdev, init N(0,0.1), clamp [0.5,5].  BIAS22 = the
+ * same sampler as src/libfm/gibbs_sbpmf22.cpp (init N(0,1), clamp [1,5]). */
+enum sbmf_quirks { SBMF_QUIRKS_FINAL = 0, SBMF_QUIRKS_SBPMF2 = 1, SBMF_QUIRKS_NONE = 2, SBMF_QUIRKS_BIAS2 = 3,
+                   SBMF_QUIRKS_BIAS22 = 4 };
 
 /* Arithmetic type of factors, residuals and reductions on the GPU.  F64 is
  * the reference's (all-double) arithmetic. */
@@ -155,6 +162,9 @@ int sbmf_set_factors(sbmf_ctx* ctx, const double* U, const double* V);
 /* Hyperparameters [sigma_u | mu_u | sigma_v | mu_v] (4K doubles) and tau. */
 int sbmf_get_hyper(sbmf_ctx* ctx, double* hyper4k, double* tau);
 int sbmf_get_dims(sbmf_ctx* ctx, uint32_t* num_users, uint32_t* num_items, uint64_t* n_train, uint64_t* n_test);
+/* Biased sampler only: b_i [num_users], b_j [num_items] and the global b_0
+ * (gibbs_sbpmf2.cpp:276-318 state).  Any pointer may be NULL. */
+int sbmf_get_biases(sbmf_ctx* ctx, double* bu, double* bv, double* b0);
 
 /* --- measurement --------------------------------------------------------------------------- */
 /* Device times of the last sweep (HIP events on the context's stream).

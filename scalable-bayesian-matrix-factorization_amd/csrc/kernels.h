@@ -138,7 +138,8 @@ struct ResidTask {
 template <typename T>
 hipError_t launch_resid(const ResidTask* tasks, uint32_t ntask, const uint32_t* tptr, uint32_t r0, uint32_t r1,
                         const uint32_t* part, const uint32_t* perm, const T* r, const T* own, const T* partner,
-                        uint32_t K, uint32_t Kp, T* E_other, double* task_sq, double* row_sq, hipStream_t st);
+                        uint32_t K, uint32_t Kp, T* E_other, double* task_sq, double* row_sq, const double* b_own,
+                        const double* b_part, double b0, hipStream_t st);
 
 // Column partials over table rows [r0,r1): out[c][0..K) = sum (x-mu)^2,
 // out[c][K..2K) = sum x, c = chunk of 256 rows (global chunk index).
@@ -146,12 +147,31 @@ template <typename T>
 hipError_t launch_colstats(const T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, const T* mu,
                            double* out, hipStream_t st);
 
-// Test predictions: pred = clamp(dot(U[u],V[i])); sum[t] += pred if collect;
+// Test predictions: pred = clamp(dot(U[u],V[i])) (+ b0 + bu[u] + bv[i] when bu
+// is non-null: the biased sampler); sum[t] += pred if collect;
 // part[b][0] += (r - sum/div)^2, part[b][1] += (r-pred)^2 per 256-rating block.
 template <typename T>
 hipError_t launch_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t t0, uint64_t t1,
                        const T* U, const T* V, uint32_t K, uint32_t Kp, T lo, T hi, int collect, double div,
-                       double* sum, double* part, hipStream_t st);
+                       double* sum, double* part, const double* bu, const double* bv, double b0, hipStream_t st);
+
+// Biased sampler (top-level gibbs_sbpmf2.cpp, src/libfm/gibbs_sbpmf22.cpp):
+// per-row bias hyperparameters + bias draw + residual shift, one wave per row
+// over rows [r0, r1) of one orientation, E in that orientation's order.
+struct BiasArgs {
+    double alpha;          // noise precision of this sweep
+    double d0;             // global-bias delta added to every residual first (user half), else 0
+    double ag, bg, sg, mg; // prior of every bias group (reference: 1, 1, 1, 0)
+    uint64_t seed;
+    uint32_t sweep, tag;   // Philox row stream (TAG_BIAS_U / TAG_BIAS_V) when var3 is null
+    int sd_is_var;
+};
+template <typename T>
+hipError_t launch_bias_rows(const uint32_t* ptr, uint32_t r0, uint32_t r1, T* E, double* b, double* mu_b,
+                            double* sig_b, const double* var3, const BiasArgs& p, hipStream_t st);
+// out2[0] = sum(E), out2[1] = sum(E^2) over E[0..n), fixed order (part: 2*ceil(n/1024) doubles).
+template <typename T>
+hipError_t launch_esum2(const T* E, uint64_t n, double* part, double* out2, hipStream_t st);
 
 // Deterministic fixed-order sum of in[n] (contiguous) into one double at out.
 // scratch: >= ceil(n/1024) + ceil(n/1024^2) + 2 doubles.

@@ -1294,7 +1294,9 @@ __global__ __launch_bounds__(256) void k_resid(const ResidTask* __restrict__ tas
                                                 const uint32_t* __restrict__ part, const uint32_t* __restrict__ perm,
                                                 const T* __restrict__ r, const T* __restrict__ own,
                                                 const T* __restrict__ partner, uint32_t K, uint32_t Kp,
-                                                T* __restrict__ E_other, double* __restrict__ task_sq) {
+                                                T* __restrict__ E_other, double* __restrict__ task_sq,
+                                                const double* __restrict__ b_own, const double* __restrict__ b_part,
+                                                double b0) {
     const uint32_t ti = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (ti >= ntask) return;
@@ -1316,7 +1318,8 @@ __global__ __launch_bounds__(256) void k_resid(const ResidTask* __restrict__ tas
             if (16 * b < (int)Kp) d += ov[b] * src[16 * b + ci];
         d = row16_sum(d);
         if (ok && ci == 0) {
-            const T e = r[idx] - d;
+            // biased sampler: E = r - (((b0 + b_user) + b_item) + u.v) (gibbs_sbpmf2.cpp:342-359)
+            const T e = b_own ? r[idx] - ((T)((b0 + b_part[part[idx]]) + b_own[tk.row]) + d) : r[idx] - d;
             E_other[perm[idx]] = e;
             sq += (double)(e * e);
         }
@@ -1362,7 +1365,9 @@ __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, c
                                                const double* __restrict__ tr, uint64_t t0, uint64_t t1,
                                                const T* __restrict__ U, const T* __restrict__ V, uint32_t K,
                                                uint32_t Kp, T lo, T hi, int collect, double div,
-                                               double* __restrict__ sum, double* __restrict__ part) {
+                                               double* __restrict__ sum, double* __restrict__ part,
+                                               const double* __restrict__ bu, const double* __restrict__ bv,
+                                               double b0) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ci = lane & 15, rr = lane >> 4;
     const uint64_t base = t0 + (uint64_t)blockIdx.x * 256 + (uint64_t)w * 64;
@@ -1379,6 +1384,7 @@ __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, c
         }
         p = row16_sum(p);
         if (ok && ci == 0) {
+            if (bu) p = (T)((b0 + bu[tu[t]]) + bv[ti[t]]) + p;  // biased sampler (gibbs_sbpmf2.cpp:614-618)
             p = (p < hi) ? p : hi;
             p = (lo < p) ? p : lo;
             double s = sum[t];
@@ -1464,6 +1470,91 @@ __global__ __launch_bounds__(256) void k_init_philox(T* __restrict__ tab, uint32
         const uint32_t i0 = 128 * zs + 2 * lane;
         if (i0 < K) tab[(size_t)row * Kp + i0] = (T)(sd * z0);
         if (i0 + 1 < K) tab[(size_t)row * Kp + i0 + 1] = (T)(sd * z1);
+    }
+}
+
+// ------------------------------------------------------------------ biased sampler
+// Per-row bias step of the biased sampler (top-level gibbs_sbpmf2.cpp
+// users :470-489 + :515-530, items :492-511 + :563-578; same algorithm in
+// src/libfm/gibbs_sbpmf22.cpp).  One wave per row, run before the row's
+// factor draws:
+//   sigma_b ~ G(ag + 1, bg + 0.5 (b - mu_b)^2),  s = 1/(sg + sigma_b),
+//   mu_b ~ N(s (sg mg + b sigma_b), s'),
+//   e += d0 (the global-bias delta, folded into the user half),
+//   sb = 1/(sigma_b + alpha n),  b' ~ N(sb (sigma_b mu_b + alpha sum(e + b)), sb'),
+//   e += b - b'          (s' = s under the reference quirk, sqrt(s) otherwise).
+// Variates: var3[row] = {gamma, normal, normal} from the host reference
+// stream, or a per-row Philox stream (TAG_BIAS_*) when var3 is null.  Every
+// lane evaluates the same draws (wave-uniform control flow); the row sum is
+// a fixed-order lane fold + DPP tree, so results are deterministic.
+template <typename T>
+__global__ __launch_bounds__(256) void k_bias_rows(const uint32_t* __restrict__ ptr, uint32_t r0, uint32_t r1,
+                                                    T* __restrict__ E, double* __restrict__ b,
+                                                    double* __restrict__ mu_b, double* __restrict__ sig_b,
+                                                    const double* __restrict__ var3, BiasArgs p) {
+    // no FMA contraction: rows without ratings replay the host's shadow walk
+    // (sbmf.cpp fill_bias_variates) operation for operation
+#pragma clang fp contract(off)
+    const uint32_t row = r0 + blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= r1) return;
+    double g, zm, zb;
+    if (var3) {
+        g = var3[3 * (size_t)row];
+        zm = var3[3 * (size_t)row + 1];
+        zb = var3[3 * (size_t)row + 2];
+    } else {
+        PhiloxRowStream rs(p.seed, row, p.sweep, p.tag);
+        g = mt_gamma(rs, p.ag + 1.0);
+        zm = leva_normal(rs);
+        zb = leva_normal(rs);
+    }
+    const double bo = b[row], mo = mu_b[row];
+    const double sig = g / (p.bg + (0.5 * (bo - mo) * (bo - mo)));
+    const double s4 = 1.0 / (p.sg + sig);
+    const double mu = s4 * ((p.sg * p.mg) + bo * sig) + (p.sd_is_var ? s4 : sqrt(s4)) * zm;  // zm = 0: draw skipped
+    const uint32_t beg = ptr[row], end = ptr[row + 1];
+    const T d0 = (T)p.d0;
+    double acc = 0.0;
+    for (uint32_t q = beg + lane; q < end; q += 64) acc += (double)(E[q] + d0) + bo;
+    acc = wave_sum(acc);
+    const double sb = 1.0 / (sig + (p.alpha * (double)(end - beg)));
+    const double mb = sb * ((sig * mu) + p.alpha * acc);
+    const double bn = mb + (p.sd_is_var ? sb : sqrt(sb)) * zb;
+    const T db = (T)(bo - bn);
+    for (uint32_t q = beg + lane; q < end; q += 64) E[q] = (E[q] + d0) + db;
+    if (lane == 0) {
+        b[row] = bn;
+        mu_b[row] = mu;
+        sig_b[row] = sig;
+    }
+}
+
+// Per-1024 block partials of sum(e) and sum(e^2) over E[0..n): part[2b], part[2b+1].
+template <typename T>
+__global__ __launch_bounds__(256) void k_esum2(const T* __restrict__ E, uint64_t n, double* __restrict__ part) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * 1024;
+    double s = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t i = b0 + threadIdx.x * 4 + q;
+        if (i < n) {
+            const double e = (double)E[i];
+            s += e;
+            s2 += e * e;
+        }
+    }
+    s = wave_sum(s);
+    s2 = wave_sum(s2);
+    __shared__ double red[4][2];
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6][0] = s;
+        red[threadIdx.x >> 6][1] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
+        part[2 * blockIdx.x + 1] = ((red[0][1] + red[1][1]) + red[2][1]) + red[3][1];
     }
 }
 
@@ -1661,11 +1752,12 @@ hipError_t launch_gram(const GramItem* items, uint32_t nitems, const GramRow* gr
 template <typename T>
 hipError_t launch_resid(const ResidTask* tasks, uint32_t ntask, const uint32_t* tptr, uint32_t r0, uint32_t r1,
                         const uint32_t* part, const uint32_t* perm, const T* r, const T* own, const T* partner,
-                        uint32_t K, uint32_t Kp, T* E_other, double* task_sq, double* row_sq, hipStream_t st) {
+                        uint32_t K, uint32_t Kp, T* E_other, double* task_sq, double* row_sq, const double* b_own,
+                        const double* b_part, double b0, hipStream_t st) {
     if (r1 <= r0) return hipSuccess;
     if (Kp > 256) return hipErrorInvalidValue;
     if (ntask) k_resid<T><<<(ntask + 3) / 4, 256, 0, st>>>(tasks, ntask, part, perm, r, own, partner, K, Kp, E_other,
-                                                          task_sq);
+                                                          task_sq, b_own, b_part, b0);
     k_resid_rows<<<(r1 - r0 + 255) / 256, 256, 0, st>>>(tptr, r0, r1, task_sq, row_sq);
     return hipGetLastError();
 }
@@ -1682,10 +1774,11 @@ hipError_t launch_colstats(const T* tab, uint32_t K, uint32_t Kp, uint32_t r0, u
 template <typename T>
 hipError_t launch_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t t0, uint64_t t1, const T* U,
                        const T* V, uint32_t K, uint32_t Kp, T lo, T hi, int collect, double div, double* sum,
-                       double* part, hipStream_t st) {
+                       double* part, const double* bu, const double* bv, double b0, hipStream_t st) {
     if (t1 <= t0) return hipSuccess;
     const uint64_t nb = (t1 - t0 + 255) / 256;
-    k_test<T><<<(uint32_t)nb, 256, 0, st>>>(tu, ti, tr, t0, t1, U, V, K, Kp, lo, hi, collect, div, sum, part);
+    k_test<T><<<(uint32_t)nb, 256, 0, st>>>(tu, ti, tr, t0, t1, U, V, K, Kp, lo, hi, collect, div, sum, part, bu, bv,
+                                            b0);
     return hipGetLastError();
 }
 
@@ -1730,6 +1823,24 @@ hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint
     return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_bias_rows(const uint32_t* ptr, uint32_t r0, uint32_t r1, T* E, double* b, double* mu_b,
+                            double* sig_b, const double* var3, const BiasArgs& p, hipStream_t st) {
+    if (r1 <= r0) return hipSuccess;
+    k_bias_rows<T><<<(r1 - r0 + 3) / 4, 256, 0, st>>>(ptr, r0, r1, E, b, mu_b, sig_b, var3, p);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_esum2(const T* E, uint64_t n, double* part, double* out2, hipStream_t st) {
+    if (n == 0) return hipMemsetAsync(out2, 0, 2 * sizeof(double), st);
+    const uint64_t nb = (n + 1023) / 1024;
+    k_esum2<T><<<(uint32_t)nb, 256, 0, st>>>(E, n, part);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    return launch_sum_cols(part, (uint32_t)nb, 2, out2, st);
+}
+
 #define SBMF_INST(T)                                                                                                 \
     template hipError_t launch_rows<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);            \
     template hipError_t launch_gblock<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);          \
@@ -1742,16 +1853,20 @@ hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint
                                        double*, const HalfArgs<T>&, hipStream_t);                                    \
     template hipError_t launch_resid<T>(const ResidTask*, uint32_t, const uint32_t*, uint32_t, uint32_t,              \
                                         const uint32_t*, const uint32_t*, const T*, const T*, const T*, uint32_t,     \
-                                        uint32_t, T*, double*, double*, hipStream_t);                                \
+                                        uint32_t, T*, double*, double*, const double*, const double*, double,         \
+                                        hipStream_t);                                                                \
     template hipError_t launch_philox_fill<T>(T*, uint32_t, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t,        \
                                               hipStream_t);                                                          \
     template hipError_t launch_colstats<T>(const T*, uint32_t, uint32_t, uint32_t, uint32_t, const T*, double*,     \
                                            hipStream_t);                                                             \
     template hipError_t launch_test<T>(const uint32_t*, const uint32_t*, const double*, uint64_t, uint64_t,         \
                                        const T*, const T*, uint32_t, uint32_t, T, T, int, double, double*, double*, \
-                                       hipStream_t);                                                                 \
+                                       const double*, const double*, double, hipStream_t);                          \
     template hipError_t launch_init_philox<T>(T*, uint32_t, uint32_t, uint32_t, uint32_t, double, uint64_t,          \
-                                              uint32_t, hipStream_t);
+                                              uint32_t, hipStream_t);                                                \
+    template hipError_t launch_bias_rows<T>(const uint32_t*, uint32_t, uint32_t, T*, double*, double*, double*,      \
+                                            const double*, const BiasArgs&, hipStream_t);                            \
+    template hipError_t launch_esum2<T>(const T*, uint64_t, double*, double*, hipStream_t);
 SBMF_INST(float)
 SBMF_INST(double)
 

@@ -55,8 +55,14 @@ class GlibcRand {
 // Leva normal + Marsaglia-Tsang gamma over any uniform source `U`
 // (U::uniform() in [0,1)).  Expression order follows random.h so that the
 // GlibcRand instantiation reproduces the reference bit for bit.
+#if defined(__HIPCC__)
+#define SBMF_HDT __host__ __device__
+#else
+#define SBMF_HDT
+#endif
+
 template <class U>
-double leva_normal(U& g) {
+SBMF_HDT double leva_normal(U& g) {
     double u, v, x, y, Q;
     do {
         do {
@@ -71,14 +77,19 @@ double leva_normal(U& g) {
     return v / u;
 }
 
+// The shape < 1 boost draws its uniform first and multiplies the boosted
+// draw by u^(1/alpha), as random.h:121-126 does through recursion.
 template <class U>
-double mt_gamma(U& g, double alpha) {
-    if (alpha < 1.0) {
+SBMF_HDT double mt_gamma(U& g, double alpha) {
+    double boost = 1.0;
+    const bool small = alpha < 1.0;
+    if (small) {
         double u;
         do {
             u = g.uniform();
         } while (u == 0.0);
-        return mt_gamma(g, alpha + 1.0) * std::pow(u, 1.0 / alpha);
+        boost = std::pow(u, 1.0 / alpha);
+        alpha = alpha + 1.0;
     }
     const double d = alpha - 1.0 / 3.0;
     const double c = 1.0 / std::sqrt(9.0 * d);
@@ -91,7 +102,7 @@ double mt_gamma(U& g, double alpha) {
         v = v * v * v;
         u = g.uniform();
     } while ((u >= (1.0 - 0.0331 * (x * x) * (x * x))) && (std::log(u) >= (0.5 * x * x + d * (1.0 - v + std::log(v)))));
-    return d * v;
+    return small ? (d * v) * boost : d * v;
 }
 
 // ----------------------------------------------------------- Philox4x32-10
@@ -129,7 +140,8 @@ SBMF_HD P4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uin
 }
 
 // Stream tags (counter word 2, low byte).
-enum : uint32_t { TAG_USERS = 0, TAG_ITEMS = 1, TAG_HOST = 2, TAG_INIT_U = 3, TAG_INIT_V = 4 };
+enum : uint32_t { TAG_USERS = 0, TAG_ITEMS = 1, TAG_HOST = 2, TAG_INIT_U = 3, TAG_INIT_V = 4, TAG_BIAS_U = 5,
+                  TAG_BIAS_V = 6 };
 static const uint32_t PHILOX_SALT = 0x53424d46u;  // "SBMF"
 
 // Two N(0,1) variates (Box-Muller, 53-bit uniforms): normal indices 2*pair
@@ -167,6 +179,32 @@ class PhiloxStream {
   private:
     uint64_t seed_;
     uint32_t sweep_, sub_, idx_ = 0;
+    double buf_[2];
+    int have_ = 0;
+};
+
+// Per-row sequential uniform stream on the device (biased sampler, Philox
+// mode): counter = (row, sweep, tag | index<<8, salt), two 53-bit uniforms
+// per Philox block.  Feeds leva_normal / mt_gamma for the per-row bias
+// hyperparameter and bias draws, whose rejection loops need a stream.
+class PhiloxRowStream {
+  public:
+    SBMF_HD PhiloxRowStream(uint64_t seed, uint32_t row, uint32_t sweep, uint32_t tag)
+        : seed_(seed), row_(row), sweep_(sweep), tag_(tag) {}
+    SBMF_HD double uniform() {
+        if (have_ == 0) {
+            const P4 o = philox4x32_10(row_, sweep_, tag_ | (idx_++ << 8), PHILOX_SALT, (uint32_t)seed_,
+                                       (uint32_t)(seed_ >> 32));
+            buf_[0] = ((((uint64_t)o.x[0] << 32) | o.x[1]) >> 11) * (1.0 / 9007199254740992.0);
+            buf_[1] = ((((uint64_t)o.x[2] << 32) | o.x[3]) >> 11) * (1.0 / 9007199254740992.0);
+            have_ = 2;
+        }
+        return buf_[--have_];
+    }
+
+  private:
+    uint64_t seed_;
+    uint32_t row_, sweep_, tag_, idx_ = 0;
     double buf_[2];
     int have_ = 0;
 };

@@ -220,6 +220,13 @@ struct sbmf_ctx {
     // hyper state (fp64 host copy)
     std::vector<double> sig_u, mu_u, sig_v, mu_v;
     double tau = 1.0;
+    // biased sampler (quirks BIAS2 / BIAS22): global bias + Normal-Gamma state
+    bool bias = false;
+    double b0 = 0.0, mu_b0 = 0.0, sig_b0 = 0.0;
+    // reference mode: host shadow (b, mu_b, sigma_b) of the rows without train
+    // ratings, whose bias walk depends only on its own variates (see fill_bias_variates)
+    std::vector<uint32_t> empty_u, empty_v;
+    std::vector<std::array<double, 3>> shadow_u, shadow_v;
     uint32_t sweep = 0, collected = 0;
     // rng
     GlibcRand grand{1};
@@ -243,6 +250,8 @@ struct sbmf_ctx {
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
     DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
+    DBuf d_bu, d_bv, d_mbu, d_mbv, d_sbu, d_sbv;  // biases b_i / b_j and their per-row (mu, sigma)
+    DBuf d_var3u, d_var3v, d_epart;              // reference-mode per-row bias variates; sum(E) partials
     std::vector<double> h_res;
     double* h_pinned = nullptr;  // pinned staging for z streams
     size_t h_pinned_bytes = 0;
@@ -253,7 +262,7 @@ struct sbmf_ctx {
 namespace sbmf {
 
 // result slots in d_res
-enum { RES_ESQ = 0, RES_TRSQ = 1, RES_TEST_AVG = 2, RES_TEST_THIS = 3, RES_COL = 8 };
+enum { RES_ESQ = 0, RES_TRSQ = 1, RES_TEST_AVG = 2, RES_TEST_THIS = 3, RES_ES = 4, RES_ESQ2 = 5, RES_COL = 8 };
 
 static size_t tsize(const sbmf_ctx* c) { return c->cfg.precision == SBMF_F32 ? 4 : 8; }
 
@@ -473,6 +482,30 @@ static void prepare_T(sbmf_ctx* c) {
         c->d_zU.alloc((size_t)c->I * c->K * sizeof(T));
         c->d_zV.alloc((size_t)c->J * c->K * sizeof(T));
     }
+    {  // biased sampler state: b_i, b_j, their (mu, sigma) start at 0 (gibbs_sbpmf2.cpp:276-318)
+        const size_t nb = c->bias ? 1 : 0;
+        for (DBuf* d : {&c->d_bu, &c->d_mbu, &c->d_sbu}) {
+            d->alloc(nb * c->I * sizeof(double));
+            HIPCHK(hipMemsetAsync(d->p, 0, d->bytes, st));
+        }
+        for (DBuf* d : {&c->d_bv, &c->d_mbv, &c->d_sbv}) {
+            d->alloc(nb * c->J * sizeof(double));
+            HIPCHK(hipMemsetAsync(d->p, 0, d->bytes, st));
+        }
+        const bool refm = cf.rng_mode == SBMF_RNG_REFERENCE;
+        c->d_var3u.alloc((refm ? nb : 0) * 3 * c->I * sizeof(double));
+        c->d_var3v.alloc((refm ? nb : 0) * 3 * c->J * sizeof(double));
+        c->d_epart.alloc(nb * 2 * ((N + 1023) / 1024 + 1) * sizeof(double));
+        c->b0 = c->mu_b0 = c->sig_b0 = 0.0;
+        c->empty_u.clear();
+        c->empty_v.clear();
+        for (uint32_t i = 0; c->bias && i < c->I; ++i)
+            if (c->users.ptr[i + 1] == c->users.ptr[i]) c->empty_u.push_back(i);
+        for (uint32_t j = 0; c->bias && j < c->J; ++j)
+            if (c->items.ptr[j + 1] == c->items.ptr[j]) c->empty_v.push_back(j);
+        c->shadow_u.assign(c->empty_u.size(), {0.0, 0.0, 0.0});
+        c->shadow_v.assign(c->empty_v.size(), {0.0, 0.0, 0.0});
+    }
     c->sig_u.assign(c->K, 0.0);
     c->mu_u.assign(c->K, 0.0);
     c->sig_v.assign(c->K, 0.0);
@@ -556,24 +589,131 @@ static void build_stream_tasks(Side& s, uint32_t cmax, uint32_t gres, uint32_t n
 // ------------------------------------------------------------------ one sweep
 struct HostStream {  // variates of one sweep, in the reference's consumption order
     double g_tau;
+    double g_sb0 = 0, z_mb0 = 0, z_b0 = 0;  // biased sampler: sigma_b0, mu_b0, b0
     std::vector<double> g_su, z_mu, g_sv, z_mv;
 };
 
+// Unbiased samplers: tau (:339-342), then per k {sigma_u, mu_u, sigma_v, mu_v}
+// (:375-414).  Biased sampler (top-level gibbs_sbpmf2.cpp:366-467): alpha with
+// shape a0 + N, sigma_b0 / mu_b0 / b0, then per k with shapes alpha0 + I / + J.
 template <class G>
 static void draw_hyper_variates(G& g, sbmf_ctx* c, HostStream& hs) {
     const sbmf_config& cf = c->cfg;
     const uint64_t N = c->tu.size();
-    hs.g_tau = mt_gamma(g, cf.a0 + 0.5 * (double)N);
+    if (c->bias) {
+        hs.g_tau = mt_gamma(g, cf.a0 + (double)N);
+        hs.g_sb0 = mt_gamma(g, cf.alpha0 + 1);
+        hs.z_mb0 = leva_normal(g);
+        hs.z_b0 = leva_normal(g);
+    } else {
+        hs.g_tau = mt_gamma(g, cf.a0 + 0.5 * (double)N);
+    }
     hs.g_su.resize(c->K);
     hs.z_mu.resize(c->K);
     hs.g_sv.resize(c->K);
     hs.z_mv.resize(c->K);
+    const double shu = c->bias ? cf.alpha0 + c->I : cf.alpha0 + 0.5 * (c->I + 1);
+    const double shv = c->bias ? cf.alpha0 + c->J : cf.alpha0 + 0.5 * (c->J + 1);
     for (uint32_t k = 0; k < c->K; ++k) {
-        hs.g_su[k] = mt_gamma(g, cf.alpha0 + 0.5 * (c->I + 1));
+        hs.g_su[k] = mt_gamma(g, shu);
         hs.z_mu[k] = leva_normal(g);
-        hs.g_sv[k] = mt_gamma(g, cf.alpha0 + 0.5 * (c->J + 1));
+        hs.g_sv[k] = mt_gamma(g, shv);
         hs.z_mv[k] = leva_normal(g);
     }
+}
+
+// Reference mode, biased sampler: the per-row bias hyperparameter variates of
+// every user then every item (:470-489, :492-511), then per user {b_i, K
+// factor normals} (:515-558) and per item {b_j, K normals} (:563-606).
+//
+// ran_gaussian(mean, stdev) consumes no variate when stdev is 0 or NaN
+// (random.h:166-172).  That happens for rows without train ratings: their
+// bias draw has variance 1/sigma_b (no data term), so under the reference's
+// variance-as-stdev quirk the walk b -> N(mu, 1/sigma_b), sigma_b ~ 1/b^2
+// grows like b^2 per sweep, overflows, and turns NaN within a few dozen
+// sweeps.  From then on the reference skips those draws.  The walk of such a
+// row depends only on its own variates, so the host replays it here in the
+// reference's exact expressions to know which draws the stream skips (a
+// skipped slot carries 0: the device then yields the mean, as the reference
+// does); k_bias_rows evaluates the same expressions without contraction and
+// reaches the same values.
+template <typename T>
+static void fill_bias_variates(sbmf_ctx* c) {
+    const uint32_t K = c->K;
+    const sbmf_config& cf = c->cfg;
+    auto sdv = [&](double var) { return c->sd_is_var ? var : std::sqrt(var); };
+    auto consumes = [](double sd) { return !(sd == 0.0 || std::isnan(sd)); };
+    auto hyper_rows = [&](uint32_t R, const std::vector<uint32_t>& empty, std::vector<std::array<double, 3>>& sh,
+                          std::vector<double>& v) {
+        size_t e = 0;
+        for (uint32_t r = 0; r < R; ++r) {
+            const double g = mt_gamma(c->grand, cf.alpha0 + 1);
+            v[3 * (size_t)r] = g;
+            if (e < empty.size() && empty[e] == r) {  // shadow: (b, mu, sigma)
+                std::array<double, 3>& x = sh[e++];
+                x[2] = g / (cf.beta0 + (0.5 * (x[0] - x[1]) * (x[0] - x[1])));
+                const double s4 = 1.0 / (cf.nu0 + x[2]);
+                const double mean = s4 * ((cf.nu0 * cf.mu0) + x[0] * x[2]);
+                const double z = consumes(sdv(s4)) ? leva_normal(c->grand) : 0.0;
+                v[3 * (size_t)r + 1] = z;
+                x[1] = consumes(sdv(s4)) ? mean + sdv(s4) * z : mean;
+            } else {
+                v[3 * (size_t)r + 1] = leva_normal(c->grand);
+            }
+        }
+    };
+    auto bias_draw = [&](const std::vector<uint32_t>& empty, std::vector<std::array<double, 3>>& sh, uint32_t r,
+                         size_t& e) -> double {
+        if (e < empty.size() && empty[e] == r) {
+            std::array<double, 3>& x = sh[e++];
+            const double sb = 1 / (x[2] + (c->tau * 0.0));
+            const double mb = sb * ((x[2] * x[1]) + c->tau * 0.0);
+            if (!consumes(sdv(sb))) {
+                x[0] = mb;
+                return 0.0;
+            }
+            const double z = leva_normal(c->grand);
+            x[0] = mb + sdv(sb) * z;
+            return z;
+        }
+        return leva_normal(c->grand);
+    };
+    std::vector<double> vu((size_t)3 * c->I), vv((size_t)3 * c->J);
+    hyper_rows(c->I, c->empty_u, c->shadow_u, vu);
+    hyper_rows(c->J, c->empty_v, c->shadow_v, vv);
+    const size_t nz = ((size_t)c->I + c->J) * K;
+    ensure_pinned(c, nz * sizeof(T));
+    T* h = reinterpret_cast<T*>(c->h_pinned);
+    size_t e = 0;
+    for (uint32_t i = 0; i < c->I; ++i) {
+        vu[3 * (size_t)i + 2] = bias_draw(c->empty_u, c->shadow_u, i, e);
+        for (uint32_t k = 0; k < K; ++k) h[(size_t)i * K + k] = (T)leva_normal(c->grand);
+    }
+    T* hv = h + (size_t)c->I * K;
+    e = 0;
+    for (uint32_t j = 0; j < c->J; ++j) {
+        vv[3 * (size_t)j + 2] = bias_draw(c->empty_v, c->shadow_v, j, e);
+        for (uint32_t k = 0; k < K; ++k) hv[(size_t)j * K + k] = (T)leva_normal(c->grand);
+    }
+    HIPCHK(hipMemcpy(c->d_zU.p, h, (size_t)c->I * K * sizeof(T), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_zV.p, hv, (size_t)c->J * K * sizeof(T), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_var3u.p, vu.data(), vu.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_var3v.p, vv.data(), vv.size() * sizeof(double), hipMemcpyHostToDevice));
+}
+
+static BiasArgs bias_args(const sbmf_ctx* c, bool users, double d0) {
+    BiasArgs p{};
+    p.alpha = c->tau;
+    p.d0 = d0;
+    p.ag = c->cfg.alpha0;
+    p.bg = c->cfg.beta0;
+    p.sg = c->cfg.nu0;
+    p.mg = c->cfg.mu0;
+    p.seed = c->cfg.seed;
+    p.sweep = c->sweep;
+    p.tag = users ? TAG_BIAS_U : TAG_BIAS_V;
+    p.sd_is_var = c->sd_is_var;
+    return p;
 }
 
 template <typename T>
@@ -738,11 +878,14 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(launch_resid<T>(c->d_rtasks.as<ResidTask>(), (uint32_t)c->items.rtasks.size(),
                                    c->d_rtptr.as<uint32_t>(), c->items.r0, c->items.r1, c->d_vpart.as<uint32_t>(),
                                    c->d_vperm.as<uint32_t>(), c->d_vr.as<T>(), c->d_V.as<T>(), c->d_U.as<T>(), K,
-                                   c->Kp, c->d_Eu.as<T>(), c->d_rtsq.as<double>(), c->d_rowsq_v.as<double>(), st));
+                                   c->Kp, c->d_Eu.as<T>(), c->d_rtsq.as<double>(), c->d_rowsq_v.as<double>(),
+                                   c->bias ? c->d_bv.as<double>() : nullptr, c->d_bu.as<double>(), c->b0, st));
             c->timing.n_launch++;
             if (c->nranks > 1) c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
         }
         HIPCHK(launch_sum(c->d_rowsq_v.as<double>(), c->J, d_res + RES_ESQ, scratch, st));
+        // biased sampler: sum(E) and sum(E^2) of the sweep-start residuals (:342-359)
+        if (c->bias) HIPCHK(launch_esum2<T>(c->d_Eu.as<T>(), N, c->d_epart.as<double>(), d_res + RES_ES, st));
         // ---- column statistics with the current mu (:378-381, :397-401)
         const T* hyp = c->d_hyper.as<T>();
         double* colpart = c->d_colpart.as<double>();
@@ -754,13 +897,35 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         HIPCHK(hipMemcpyAsync(c->h_res.data(), d_res, c->h_res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         // ---- 2. host draws (:339-342, :375-414)
-        const double esq = c->h_res[RES_ESQ];
-        c->tau = hs.g_tau / (cf.b0 + 0.5 * esq);
         const double* Su2 = &c->h_res[RES_COL];
         const double* Su1 = Su2 + K;
         const double* Sv2 = Su2 + 2 * K;
         const double* Sv1 = Su2 + 3 * K;
         auto sd = [&](double var) { return c->sd_is_var ? var : std::sqrt(var); };
+        double d0 = 0.0;  // biased sampler: global-bias delta, folded into the user half's residual pass
+        if (c->bias) {
+            // top-level gibbs_sbpmf2.cpp:366-467 (= src/libfm/gibbs_sbpmf22.cpp:345-446)
+            const double es = c->h_res[RES_ES], esq = c->h_res[RES_ESQ2];
+            c->tau = hs.g_tau / (cf.b0 + esq);
+            c->sig_b0 = hs.g_sb0 / (cf.beta0 + (0.5 * (c->b0 - c->mu_b0) * (c->b0 - c->mu_b0)));
+            const double s0 = 1.0 / (cf.nu0 + c->sig_b0);
+            c->mu_b0 = s0 * ((cf.nu0 * cf.mu0) + c->b0 * c->sig_b0) + sd(s0) * hs.z_mb0;
+            const double sb0 = 1 / (c->sig_b0 + c->tau * (double)N);
+            const double mb0 = sb0 * (c->sig_b0 * c->mu_b0 + c->tau * (es + (double)N * c->b0));
+            const double old = c->b0;
+            c->b0 = mb0 + sd(sb0) * hs.z_b0;
+            d0 = old - c->b0;
+            for (uint32_t k = 0; k < K; ++k) {
+                c->sig_u[k] = hs.g_su[k] / (cf.beta0 + (0.5) * Su2[k]);
+                const double s2 = 1 / (cf.nu0 + c->sig_u[k] * c->I);
+                c->mu_u[k] = s2 * (cf.nu0 * cf.mu0 + c->sig_u[k] * Su1[k]) + sd(s2) * hs.z_mu[k];
+                c->sig_v[k] = hs.g_sv[k] / (cf.beta0 + (0.5) * Sv2[k]);
+                const double s1 = 1 / (cf.nu0 + c->sig_v[k] * c->J);
+                c->mu_v[k] = s1 * (cf.nu0 * cf.mu0 + c->sig_v[k] * Sv1[k]) + sd(s1) * hs.z_mv[k];
+            }
+        } else {
+        const double esq = c->h_res[RES_ESQ];
+        c->tau = hs.g_tau / (cf.b0 + 0.5 * esq);
         for (uint32_t k = 0; k < K; ++k) {
             const double du = c->mu_u[k] - cf.mu0;
             const double bu = q2 ? cf.beta0 + cf.nu0 * du * du + (0.5) * Su2[k]
@@ -777,6 +942,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             const double mv_star = (q2 ? su_star : sv_star) * (cf.nu0 * cf.mu0 * c->sig_v[k] + c->sig_v[k] * Sv1[k]);
             c->mu_v[k] = mv_star + sd(sv_star) * hs.z_mv[k];
         }
+        }
         {
             const size_t Kp = c->Kp;
             std::vector<T> h(4 * Kp, T(0));
@@ -787,7 +953,9 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 h[3 * Kp + k] = (T)c->mu_v[k];
             }
             HIPCHK(hipMemcpyAsync(c->d_hyper.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st));
-            if (ref) {  // user variates then item variates (:485 then :529)
+            if (ref && c->bias) {
+                fill_bias_variates<T>(c);
+            } else if (ref) {  // user variates then item variates (:485 then :529)
                 fill_z<T>(c, c->I, c->d_zU);
                 fill_z<T>(c, c->J, c->d_zV);
             }
@@ -797,6 +965,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // ---- 3. user half-sweep (throughput mode: this half's normals first)
         if (!ref)
             HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep, TAG_USERS, st));
+        if (c->bias)  // per-user bias hyperparameters + b_i draw + residual shift (:470-489, :515-530)
+            HIPCHK(launch_bias_rows<T>(c->d_uptr.as<uint32_t>(), c->users.r0, c->users.r1, c->d_Eu.as<T>(),
+                                       c->d_bu.as<double>(), c->d_mbu.as<double>(), c->d_sbu.as<double>(),
+                                       ref ? c->d_var3u.as<double>() : nullptr, bias_args(c, true, d0), st));
         run_half<T>(c, true);
         HIPCHK(hipEventRecord(c->ev[2], st));
         if (c->nranks > 1) c->comm.bcast_ranges(c->d_U.p, c->Kp * sizeof(T), c->users.bounds, st);
@@ -804,6 +976,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // ---- 4. item half-sweep
         if (!ref)
             HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep, TAG_ITEMS, st));
+        if (c->bias)  // per-item (:492-511, :563-578)
+            HIPCHK(launch_bias_rows<T>(c->d_vptr.as<uint32_t>(), c->items.r0, c->items.r1, c->d_Ev.as<T>(),
+                                       c->d_bv.as<double>(), c->d_mbv.as<double>(), c->d_sbv.as<double>(),
+                                       ref ? c->d_var3v.as<double>() : nullptr, bias_args(c, false, 0.0), st));
         run_half<T>(c, false);
         HIPCHK(hipEventRecord(c->ev[4], st));
         if (c->nranks > 1) {
@@ -820,7 +996,8 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         if (cf.eval_test && T_) {
             HIPCHK(launch_test<T>(c->d_tu.as<uint32_t>(), c->d_ti.as<uint32_t>(), c->d_tr.as<double>(), c->t0, c->t1,
                                   c->d_U.as<T>(), c->d_V.as<T>(), K, c->Kp, (T)c->lo, (T)c->hi, collect ? 1 : 0, div,
-                                  c->d_tsum.as<double>(), c->d_tpart.as<double>(), st));
+                                  c->d_tsum.as<double>(), c->d_tpart.as<double>(),
+                                  c->bias ? c->d_bu.as<double>() : nullptr, c->d_bv.as<double>(), c->b0, st));
             if (c->nranks > 1) c->comm.bcast_ranges(c->d_tpart.p, 2 * sizeof(double), c->tbblocks, st);
             const uint32_t nb = (uint32_t)((T_ + 255) / 256);
             HIPCHK(launch_sum_cols(c->d_tpart.as<double>(), nb, 2, d_res + RES_TEST_AVG, st));
@@ -967,7 +1144,7 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     *out = nullptr;
     if (cfg->num_factor == 0 || cfg->num_factor > 256) sbmf::fail(SBMF_E_ARG, "num_factor must be in [1,256]");
     if (cfg->rng_mode != SBMF_RNG_REFERENCE && cfg->rng_mode != SBMF_RNG_PHILOX) sbmf::fail(SBMF_E_ARG, "bad rng_mode");
-    if (cfg->quirks < 0 || cfg->quirks > 2) sbmf::fail(SBMF_E_ARG, "bad quirks");
+    if (cfg->quirks < 0 || cfg->quirks > 4) sbmf::fail(SBMF_E_ARG, "bad quirks");
     if (cfg->precision != SBMF_F64 && cfg->precision != SBMF_F32) sbmf::fail(SBMF_E_ARG, "bad precision");
     int ndev = 0;
     const hipError_t derr = hipGetDeviceCount(&ndev);
@@ -982,7 +1159,11 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     HIPCHK(hipSetDevice(cfg->device));
     std::unique_ptr<sbmf_ctx> c(new sbmf_ctx());
     c->cfg = *cfg;
-    const bool q2 = cfg->quirks == SBMF_QUIRKS_SBPMF2;
+    // init 0.1 / clamp 0.5: src/libfm/gibbs_sbpmf2.cpp:240,557 and the top-level gibbs_sbpmf2.cpp:242,628
+    const bool q2 = cfg->quirks == SBMF_QUIRKS_SBPMF2 || cfg->quirks == SBMF_QUIRKS_BIAS2;
+    c->bias = cfg->quirks == SBMF_QUIRKS_BIAS2 || cfg->quirks == SBMF_QUIRKS_BIAS22;
+    if (c->bias && (cfg->tune & 2u))
+        sbmf::fail(SBMF_E_ARG, "tune bit 1 (residuals from r - own.partner) does not carry biases");
     c->init_sd = cfg->init_stdev >= 0 ? cfg->init_stdev : (q2 ? 0.1 : 1.0);
     c->lo = cfg->clamp_lo >= 0 ? cfg->clamp_lo : (q2 ? 0.5 : 1.0);
     c->hi = cfg->clamp_hi;
@@ -1131,6 +1312,19 @@ int sbmf_get_hyper(sbmf_ctx* ctx, double* h, double* tau) {
     API_END(ctx)
 }
 
+int sbmf_get_biases(sbmf_ctx* ctx, double* bu, double* bv, double* b0) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
+    if (!ctx->bias) sbmf::fail(SBMF_E_STATE, "not a biased sampler (quirks bias2 / bias22)");
+    HIPCHK(hipSetDevice(ctx->cfg.device));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (bu) HIPCHK(hipMemcpy(bu, ctx->d_bu.p, (size_t)ctx->I * sizeof(double), hipMemcpyDeviceToHost));
+    if (bv) HIPCHK(hipMemcpy(bv, ctx->d_bv.p, (size_t)ctx->J * sizeof(double), hipMemcpyDeviceToHost));
+    if (b0) *b0 = ctx->b0;
+    API_END(ctx)
+}
+
 int sbmf_get_dims(sbmf_ctx* ctx, uint32_t* nu, uint32_t* ni, uint64_t* ntr, uint64_t* nte) {
     API_BEGIN
     if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
@@ -1168,6 +1362,8 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
     HIPCHK(hipSetDevice(ctx->cfg.device));
     ctx->nranks = nranks;
     ctx->rank = rank;
+    if (nranks > 1 && ctx->bias)
+        sbmf::fail(SBMF_E_ARG, "the biased sampler (quirks bias2/bias22) runs on one GPU in this build");
     if (nranks > 1) ctx->comm.init(nranks, rank, id);
     API_END(ctx)
 }

@@ -158,7 +158,8 @@ int main(int argc, char** argv) {
         cl.reg("cache_size", "unused (binary data format)");
         // sampler settings
         cl.reg("rng", "ref (reference glibc/Leva/Marsaglia-Tsang stream; default) | philox (in-kernel, throughput)");
-        cl.reg("quirks", "final (gibbs_sbpmf_final.cpp; default) | sbpmf2 | none (stdev = sqrt(variance))");
+        cl.reg("quirks", "final (gibbs_sbpmf_final.cpp; default) | sbpmf2 | none (stdev = sqrt(variance)) | bias2 | bias22 "
+                         "(biased sampler, top-level gibbs_sbpmf2.cpp / gibbs_sbpmf22.cpp; needs -dim '1,1,K')");
         cl.reg("precision", "f64 (default) | f32");
         cl.reg("burnin", "burn-in sweeps before collection; default=0");
         cl.reg("format", "auto (default) | triple | libfm");
@@ -183,10 +184,15 @@ int main(int argc, char** argv) {
         std::vector<int> dim = split_ints(cl.get("dim", "1,1,8"));
         if (dim.size() != 3) throw std::runtime_error("dim must have 3 numbers");
         if (dim[2] <= 0 || dim[2] > 256) throw std::runtime_error("dim k2 must be in [1,256]");
-        if (dim[0] || dim[1])
+        const std::string q = cl.get("quirks", "final");
+        const bool biased = q == "bias2" || q == "bias22";
+        if (!biased && (dim[0] || dim[1]))
             std::cout << "note: bias terms (k0,k1) are not sampled; the reference SBPMF sampler has them compiled "
-                         "out (gibbs_sbpmf_final.cpp:276-295)"
+                         "out (gibbs_sbpmf_final.cpp:276-295); -quirks bias2|bias22 selects the biased sampler"
                       << std::endl;
+        if (biased && !(dim[0] == 1 && dim[1] == 1))
+            throw std::runtime_error("the biased sampler (gibbs_sbpmf2.cpp) samples b0 and the user/item biases: "
+                                     "use -dim '1,1,K'");
 
         sbmf_config cfg;
         sbmf_config_default(&cfg);
@@ -196,8 +202,18 @@ int main(int argc, char** argv) {
         cfg.seed = (uint64_t)cl.getl("seed", 1);
         const std::string rng = cl.get("rng", "ref");
         cfg.rng_mode = rng == "philox" ? SBMF_RNG_PHILOX : SBMF_RNG_REFERENCE;
-        const std::string q = cl.get("quirks", "final");
-        cfg.quirks = q == "sbpmf2" ? SBMF_QUIRKS_SBPMF2 : (q == "none" ? SBMF_QUIRKS_NONE : SBMF_QUIRKS_FINAL);
+        if (q == "sbpmf2")
+            cfg.quirks = SBMF_QUIRKS_SBPMF2;
+        else if (q == "none")
+            cfg.quirks = SBMF_QUIRKS_NONE;
+        else if (q == "bias2")
+            cfg.quirks = SBMF_QUIRKS_BIAS2;
+        else if (q == "bias22")
+            cfg.quirks = SBMF_QUIRKS_BIAS22;
+        else if (q == "final")
+            cfg.quirks = SBMF_QUIRKS_FINAL;
+        else
+            throw std::runtime_error("unknown -quirks " + q);
         cfg.precision = cl.get("precision", "f64") == "f32" ? SBMF_F32 : SBMF_F64;
         cfg.device = (int32_t)cl.getl("device", 0);
         if (cl.has("init_stdev")) cfg.init_stdev = cl.getd("init_stdev", 1.0);

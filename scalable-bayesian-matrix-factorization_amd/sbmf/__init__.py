@@ -20,11 +20,12 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import (F32, F64, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
+from ._lib import (F32, F64, QUIRKS_BIAS2, QUIRKS_BIAS22, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
                    SBMF_E_COMM, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_NOMEM, SBMF_E_STATE, SBMF_OK)
 
 __all__ = ["FMLearnSBPMF", "Data", "SBMFError", "load_triples", "load_libfm", "config_default",
-           "RNG_REFERENCE", "RNG_PHILOX", "QUIRKS_FINAL", "QUIRKS_SBPMF2", "QUIRKS_NONE", "F64", "F32"]
+           "RNG_REFERENCE", "RNG_PHILOX", "QUIRKS_FINAL", "QUIRKS_SBPMF2", "QUIRKS_NONE",
+           "QUIRKS_BIAS2", "QUIRKS_BIAS22", "F64", "F32"]
 
 lib = _lib.lib
 
@@ -109,12 +110,14 @@ class FMLearnSBPMF:
 
     Attributes mirror the reference: ``num_factor`` (K, -dim), ``num_iter``
     (-iter), ``seed``; plus the sampler's ``rng`` ("ref" | "philox"),
-    ``quirks`` ("final" | "sbpmf2" | "none"), ``precision`` ("f64" | "f32").
+    ``quirks`` ("final" | "sbpmf2" | "none", or the biased sampler "bias2" |
+    "bias22" = libFM ``-dim '1,1,K'``), ``precision`` ("f64" | "f32").
     ``rmse_trajectory`` collects the per-sweep running-mean test RMSE (the
     reference's ``rmse is`` lines / ``test_rmse_*`` file).
     """
 
-    _QUIRKS = {"final": QUIRKS_FINAL, "sbpmf2": QUIRKS_SBPMF2, "none": QUIRKS_NONE}
+    _QUIRKS = {"final": QUIRKS_FINAL, "sbpmf2": QUIRKS_SBPMF2, "none": QUIRKS_NONE, "bias2": QUIRKS_BIAS2,
+               "bias22": QUIRKS_BIAS22}
 
     def __init__(self, num_factor=20, num_iter=100, seed=1, rng="ref", quirks="final", precision="f64", burnin=0,
                  device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, row_kernel=0,
@@ -228,6 +231,13 @@ class FMLearnSBPMF:
         tau = C.c_double()
         self._check(lib.sbmf_get_hyper(self.ctx, _ptr(h, C.c_double), C.byref(tau)))
         return {"sigma_u": h[:K], "mu_u": h[K:2 * K], "sigma_v": h[2 * K:3 * K], "mu_v": h[3 * K:], "tau": tau.value}
+
+    def biases(self):
+        """Biased sampler: (b_i [users], b_j [items], b_0)."""
+        nu, ni, _, _ = self.dims()
+        bu, bv, b0 = np.zeros(nu), np.zeros(ni), C.c_double()
+        self._check(lib.sbmf_get_biases(self.ctx, _ptr(bu, C.c_double), _ptr(bv, C.c_double), C.byref(b0)))
+        return bu, bv, b0.value
 
     def timing(self):
         t = _lib.Timing()

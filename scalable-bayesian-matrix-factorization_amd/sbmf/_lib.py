@@ -13,7 +13,7 @@ CLI_PATH = os.path.join(PKG_DIR, "build", "sbmf")
 
 SBMF_OK, SBMF_E_ARG, SBMF_E_STATE, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_COMM, SBMF_E_NOMEM = 0, -1, -2, -3, -4, -5, -6
 RNG_REFERENCE, RNG_PHILOX = 0, 1
-QUIRKS_FINAL, QUIRKS_SBPMF2, QUIRKS_NONE = 0, 1, 2
+QUIRKS_FINAL, QUIRKS_SBPMF2, QUIRKS_NONE, QUIRKS_BIAS2, QUIRKS_BIAS22 = 0, 1, 2, 3, 4
 F64, F32 = 0, 1
 NKIND = 11  # SBMF_NKIND
 KIND_NAMES = ['gblock_w4', 'gblock_w16', 'gblock_b2', 'gblock_b4', 'gblock_b8', 'gstream', 'rows_w2', 'rows_w8',
@@ -78,6 +78,7 @@ SIGNATURES = {
     "sbmf_get_factors": (C.c_int, [C.c_void_p, _P_F64, _P_F64]),
     "sbmf_set_factors": (C.c_int, [C.c_void_p, _P_F64, _P_F64]),
     "sbmf_get_hyper": (C.c_int, [C.c_void_p, _P_F64, _P_F64]),
+    "sbmf_get_biases": (C.c_int, [C.c_void_p, _P_F64, _P_F64, _P_F64]),
     "sbmf_get_dims": (C.c_int, [C.c_void_p, _P_U32, _P_U32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "sbmf_get_timing": (C.c_int, [C.c_void_p, C.POINTER(Timing)]),
     "sbmf_comm_unique_id": (C.c_int, [_P_U8]),

@@ -33,6 +33,8 @@ def test_no_arguments_prints_help():
     (["-task", "r", "-train", "a"], "mandatory"),
     (["-task", "r", "-train", "a", "-test", "b", "-dim", "1,1"], "dim must have 3"),
     (["-task", "r", "-train", "/nonexistent", "-test", "b"], "unable to open"),
+    (["-task", "r", "-train", "a", "-test", "b", "-quirks", "bias2", "-dim", "0,0,8"], "-dim '1,1,K'"),
+    (["-task", "r", "-train", "a", "-test", "b", "-quirks", "bogus"], "unknown -quirks"),
 ])
 def test_grammar_errors(args, msg):
     r = run(*args)
