@@ -63,6 +63,16 @@ enum sbmf_rng_mode { SBMF_RNG_REFERENCE = 0, SBMF_RNG_PHILOX = 1 };
 enum sbmf_quirks { SBMF_QUIRKS_FINAL = 0, SBMF_QUIRKS_SBPMF2 = 1, SBMF_QUIRKS_NONE = 2, SBMF_QUIRKS_BIAS2 = 3,
                    SBMF_QUIRKS_BIAS22 = 4 };
 
+/* Learner (libFM -method, libfm.cpp:394-445).  MCMC = the SBPMF Gibbs sampler.
+ * VB = online variational Bayes, the reference's fm_learn_vb_online
+ * (src/libfm/src/fm_learn_vb_online.h, -method vb_online; its batch -method vb
+ * is a no-op as shipped): per epoch a shuffle into
+ * mini-batches and natural-gradient steps (t0 + t)^-0.5 on the per-attribute
+ * Gaussian posteriors of w0, w and V.  With VB a "sweep" of sbmf_run is an
+ * epoch, rmse_avg is the test RMSE of the posterior-mean prediction, tau is
+ * alpha, factors / biases are the posterior means, and only F64 is offered. */
+enum sbmf_method { SBMF_METHOD_MCMC = 0, SBMF_METHOD_VB = 1 };
+
 /* Arithmetic type of factors, residuals and reductions on the GPU.  F64 is
  * the reference's (all-double) arithmetic. */
 enum sbmf_precision { SBMF_F64 = 0, SBMF_F32 = 1 };
@@ -101,7 +111,10 @@ typedef struct sbmf_config {
                                          of ceil(ratings / ratings-per-wave),
                                  bit 3 = f64 rows of 33..64 ratings on two 8-vector waves instead
                                          of one 16-vector wave                                   */
-    uint32_t reserved[4];
+    uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
+    uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
+                                 fm_learn_vb_online_simultaneous.h:62)                           */
+    uint32_t reserved[2];
 } sbmf_config;
 
 /* Per-sweep report passed to the run callback. */

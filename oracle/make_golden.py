@@ -18,6 +18,10 @@ Fixtures written (all data, no reference source):
   ref_<variant>_<data>_k<K>_s<seed>.txt       100 lines "%.17g" test RMSE
                                               (variants final, sbpmf2, bias2, bias22)
   ref_rng_s<seed>.txt                         rand / ran_gaussian / ran_gamma
+  ref_vbo_<data>_k<K>_s<seed>_e<E>.txt        E lines "%.17g" per-epoch test RMSE of the
+                                              online VB learner (oracle/ref_vbo_harness.cpp
+                                              over the reference's fm_learn_vb_online*.h)
+`make_golden.py vbo` regenerates only the online VB fixtures.
 Only runnable in the build container (needs /root/reference).
 """
 import gzip
@@ -90,8 +94,58 @@ def write_tsv(path, rows):
             f.write("%d\t%d\t%g\n" % (u, i, r))
 
 
+def write_libfm(triples_path, out_path, num_users):
+    """Triples -> libFM text in the users-first layout the harness reads:
+    "r u:1 (num_users + i):1" (Data.h:192-217)."""
+    opener = gzip.open if triples_path.endswith(".gz") else open
+    with opener(triples_path, "rt") as f, open(out_path, "w") as g:
+        for line in f:
+            a = line.split()
+            if len(a) >= 3:
+                g.write("%s %d:1 %d:1\n" % (a[2], int(a[0]), num_users + int(a[1])))
+
+
+def max_user(*paths):
+    m = 0
+    for pth in paths:
+        opener = gzip.open if pth.endswith(".gz") else open
+        with opener(pth, "rt") as f:
+            for line in f:
+                a = line.split()
+                if len(a) >= 3:
+                    m = max(m, int(a[0]))
+    return m
+
+
+VBO_RUNS = [("ml100k", 8, 1, 10), ("ml100k", 20, 7, 5), ("ragged", 8, 2, 20)]
+
+
+def vbo_goldens():
+    root = "/tmp/sbmf_vborun_%d" % os.getpid()
+    os.makedirs(os.path.join(root, "scratch"), exist_ok=True)
+    sets = {"ml100k": (os.path.join(GOLD, "ml100k_train.tsv.gz"), os.path.join(GOLD, "ml100k_test.tsv.gz")),
+            "ragged": (os.path.join(GOLD, "ragged_train.tsv"), os.path.join(GOLD, "ragged_test.tsv"))}
+    for dname, K, seed, epochs in VBO_RUNS:
+        tr, te = sets[dname]
+        I = max_user(tr, te) + 1
+        write_libfm(tr, os.path.join(root, "train.libfm"), I)
+        write_libfm(te, os.path.join(root, "test.libfm"), I)
+        p = subprocess.run([os.path.join(HERE, "_ref", "ref_vbo_harness"), "train.libfm", "test.libfm", str(K),
+                            str(epochs), str(seed), os.path.join(root, "scratch")], cwd=root, capture_output=True,
+                           text=True, check=True)
+        vals = [l for l in p.stdout.split() if l[0].isdigit()]
+        assert len(vals) == epochs, (dname, p.stdout)
+        with open(os.path.join(GOLD, "ref_vbo_%s_k%d_s%d_e%d.txt" % (dname, K, seed, epochs)), "w") as f:
+            f.write("\n".join(vals) + "\n")
+        print("golden vbo", dname, K, seed, vals[0], vals[-1])
+    shutil.rmtree(root)
+
+
 def main():
     subprocess.run(["make", "-C", HERE, "all", "ref"], check=True, capture_output=True)
+    if sys.argv[1:] == ["vbo"]:
+        vbo_goldens()
+        return 0
     os.makedirs(GOLD, exist_ok=True)
     ml_train = os.path.join(REF, "data", "m100k", "train_sbpmf")
     ml_test = os.path.join(REF, "data", "m100k", "test_sbpmf")
@@ -122,6 +176,7 @@ def main():
                              capture_output=True, text=True, check=True).stdout
         with open(os.path.join(GOLD, "ref_rng_s%d.txt" % seed), "w") as f:
             f.write(out)
+    vbo_goldens()
     return 0
 
 

@@ -28,6 +28,18 @@ class OracleResult(C.Structure):
                 ("bv", C.POINTER(C.c_double)), ("b0", C.c_double)]
 
 
+class VBOConfig(C.Structure):
+    _fields_ = [("K", C.c_uint32), ("epochs", C.c_uint32), ("seed", C.c_uint), ("num_batch", C.c_uint32),
+                ("seconds_limit", C.c_double)]
+
+
+class VBOResult(C.Structure):
+    _fields_ = [("rmse", C.POINTER(C.c_double)), ("rmse_cap", C.c_uint32), ("pred", C.POINTER(C.c_double)),
+                ("mu_w", C.POINTER(C.c_double)), ("mu_v", C.POINTER(C.c_double)), ("alpha", C.c_double),
+                ("mu0", C.c_double), ("seconds", C.c_double), ("num_attribute", C.c_uint32),
+                ("epochs_done", C.c_uint32)]
+
+
 def build():
     import subprocess
     subprocess.run(["make", "-C", HERE, "all"], check=True, capture_output=True)
@@ -44,6 +56,7 @@ def _lib():
     lib.oracle_ran_gamma.argtypes = [C.c_double]
     lib.oracle_ran_uniform.restype = C.c_double
     lib.oracle_srand.argtypes = [C.c_uint]
+    lib.oracle_vbo_run.restype = C.c_int
     return lib
 
 
@@ -100,6 +113,39 @@ def run(train, test, K=20, iters=100, seed=1, quirks="final", burnin=0, num_user
     return {"rmse": rm[:n], "rmse_this": rt[:n], "tau": ta[:n], "U": U, "V": V, "hyper": hyper,
             "pred_sum": ps[:len(sr)], "seconds": res.seconds, "sweeps": n, "num_users": res.num_users,
             "num_items": res.num_items, "bu": bu, "bv": bv, "b0": res.b0}
+
+
+def run_vbo(train, test, K=8, epochs=10, seed=1, num_users=0, num_items=0, seconds_limit=0.0, want_params=True):
+    """The online VB oracle (vbo_oracle.c, the reference's -method vb_online on
+    rating data).  Returns per-epoch test 'rmse', final clamped 'pred', the
+    attribute means 'mu_w' [p] and 'mu_v' [p][K] (users first, then items),
+    'alpha', 'mu0', 'seconds'."""
+    L = lib()
+    cfg = VBOConfig(K, epochs, seed, 0, seconds_limit)
+    tu, ti, tr = (np.ascontiguousarray(train[0], np.uint32), np.ascontiguousarray(train[1], np.uint32),
+                  np.ascontiguousarray(train[2], np.float64))
+    su, si, sr = (np.ascontiguousarray(test[0], np.uint32), np.ascontiguousarray(test[1], np.uint32),
+                  np.ascontiguousarray(test[2], np.float64))
+    I = num_users or int(max(tu.max(initial=0), su.max(initial=0))) + 1
+    J = num_items or int(max(ti.max(initial=0), si.max(initial=0))) + 1
+    p = I + J
+    res = VBOResult()
+    rm = np.full(epochs, np.nan)
+    res.rmse, res.rmse_cap = _p(rm, C.c_double), epochs
+    pred = np.zeros(max(len(sr), 1))
+    res.pred = _p(pred, C.c_double)
+    mu_w = mu_v = None
+    if want_params:
+        mu_w, mu_v = np.zeros(p), np.zeros((p, K))
+        res.mu_w, res.mu_v = _p(mu_w, C.c_double), _p(mu_v, C.c_double)
+    rc = L.oracle_vbo_run(C.byref(cfg), C.c_uint64(len(tr)), _p(tu, C.c_uint32), _p(ti, C.c_uint32),
+                          _p(tr, C.c_double), C.c_uint64(len(sr)), _p(su, C.c_uint32), _p(si, C.c_uint32),
+                          _p(sr, C.c_double), C.c_uint32(I), C.c_uint32(J), C.byref(res))
+    if rc != 0:
+        raise ValueError("oracle_vbo_run failed (an empty batch: fewer ratings than the 30 batches need)")
+    n = res.epochs_done
+    return {"rmse": rm[:n], "pred": pred[:len(sr)], "mu_w": mu_w, "mu_v": mu_v, "alpha": res.alpha, "mu0": res.mu0,
+            "seconds": res.seconds, "epochs": n, "num_attribute": res.num_attribute}
 
 
 def stream(seed, kind, n, shape=1.0):

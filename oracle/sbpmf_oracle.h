@@ -44,6 +44,30 @@ double oracle_ran_uniform(void);
 double oracle_ran_gaussian(void);
 double oracle_ran_gamma(double alpha);
 
+/* Online VB (vbo_oracle.c): the reference's `-method vb_online` learner on
+ * rating data (user attribute u, item attribute num_users + i). */
+typedef struct {
+    uint32_t K, epochs;
+    unsigned seed;
+    uint32_t num_batch;     /* 0: the reference's 30 */
+    double seconds_limit;   /* >0: stop after the epoch that crosses it (bounded CPU baseline) */
+} oracle_vbo_config;
+
+typedef struct {
+    double *rmse;           /* [rmse_cap] per-epoch test RMSE, or NULL */
+    uint32_t rmse_cap;
+    double *pred;           /* [n_test] clamped predictions after the last epoch, or NULL */
+    double *mu_w;           /* [num_attribute] or NULL */
+    double *mu_v;           /* [num_attribute][K] or NULL */
+    double alpha, mu0, seconds;
+    uint32_t num_attribute, epochs_done;
+} oracle_vbo_result;
+
+void oracle_vbo_config_default(oracle_vbo_config *c);
+int oracle_vbo_run(const oracle_vbo_config *cfg, uint64_t n_train, const uint32_t *tu, const uint32_t *ti,
+                   const double *tr, uint64_t n_test, const uint32_t *su, const uint32_t *si, const double *sr,
+                   uint32_t num_users, uint32_t num_items, oracle_vbo_result *res);
+
 #ifdef __cplusplus
 }
 #endif

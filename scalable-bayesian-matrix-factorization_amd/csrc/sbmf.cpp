@@ -28,9 +28,11 @@
 
 #include "../../include/sbmf.h"
 #include "comm.h"
+#include "common.h"
 #include <rccl/rccl.h>
 #include "kernels.h"
 #include "rng.h"
+#include "vbo.h"
 
 namespace {
 thread_local std::string g_err;
@@ -40,57 +42,8 @@ struct sbmf_ctx;
 
 namespace sbmf {
 
-struct Error {
-    int code;
-    std::string msg;
-};
-[[noreturn]] static void fail(int code, const char* fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    throw Error{code, buf};
-}
 [[noreturn]] void comm_fail(const char* what, ncclResult_t r) {
     fail(SBMF_E_COMM, "%s failed: %s", what, ncclGetErrorString(r));
-}
-#define HIPCHK(x)                                                                                     \
-    do {                                                                                              \
-        hipError_t e_ = (x);                                                                          \
-        if (e_ != hipSuccess) sbmf::fail(SBMF_E_DEVICE, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), \
-                                         __FILE__, __LINE__);                                         \
-    } while (0)
-
-// ------------------------------------------------------------------ device buffer
-struct DBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    DBuf() = default;
-    DBuf(const DBuf&) = delete;
-    DBuf& operator=(const DBuf&) = delete;
-    ~DBuf() { release(); }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    void alloc(size_t b) {
-        release();
-        if (b == 0) b = 16;
-        hipError_t e = hipMalloc(&p, b);
-        if (e != hipSuccess) fail(SBMF_E_NOMEM, "hipMalloc(%zu) failed: %s", b, hipGetErrorString(e));
-        bytes = b;
-    }
-    template <typename U>
-    U* as() const {
-        return static_cast<U*>(p);
-    }
-};
-template <typename U>
-static void upload(DBuf& d, const std::vector<U>& h, hipStream_t st) {
-    d.alloc(h.size() * sizeof(U));
-    if (!h.empty()) HIPCHK(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(U), hipMemcpyHostToDevice, st));
 }
 
 // ------------------------------------------------------------------ host layout
@@ -256,6 +209,7 @@ struct sbmf_ctx {
     double* h_pinned = nullptr;  // pinned staging for z streams
     size_t h_pinned_bytes = 0;
     sbmf_timing timing{};
+    VBLearner* vb = nullptr;  // -method vb (vbo.cpp)
     ~sbmf_ctx();
 };
 
@@ -1073,6 +1027,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
 
 // ===================================================================== C ABI
 sbmf_ctx::~sbmf_ctx() {
+    vbo_destroy(vb);
     if (h_pinned) (void)hipHostFree(h_pinned);
     for (auto& e : ev)
         if (e) (void)hipEventDestroy(e);
@@ -1146,6 +1101,9 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     if (cfg->rng_mode != SBMF_RNG_REFERENCE && cfg->rng_mode != SBMF_RNG_PHILOX) sbmf::fail(SBMF_E_ARG, "bad rng_mode");
     if (cfg->quirks < 0 || cfg->quirks > 4) sbmf::fail(SBMF_E_ARG, "bad quirks");
     if (cfg->precision != SBMF_F64 && cfg->precision != SBMF_F32) sbmf::fail(SBMF_E_ARG, "bad precision");
+    if (cfg->method != SBMF_METHOD_MCMC && cfg->method != SBMF_METHOD_VB) sbmf::fail(SBMF_E_ARG, "bad method");
+    if (cfg->method == SBMF_METHOD_VB && cfg->precision != SBMF_F64)
+        sbmf::fail(SBMF_E_ARG, "the online VB learner computes in f64 (the reference's double) only");
     int ndev = 0;
     const hipError_t derr = hipGetDeviceCount(&ndev);
     if (derr != hipSuccess || ndev <= 0)
@@ -1182,6 +1140,25 @@ void sbmf_destroy(sbmf_ctx* ctx) {
     (void)hipSetDevice(ctx->cfg.device);
     (void)hipStreamSynchronize(ctx->st);
     delete ctx;
+}
+
+// -method vb: dims as for the sampler (max id + 1 over train and test)
+static void prepare_vb(sbmf_ctx* c) {
+    uint32_t umax = 0, imax = 0;
+    for (size_t x = 0; x < c->tu.size(); ++x) {
+        umax = std::max(umax, c->tu[x]);
+        imax = std::max(imax, c->ti[x]);
+    }
+    for (size_t x = 0; x < c->su.size(); ++x) {
+        umax = std::max(umax, c->su[x]);
+        imax = std::max(imax, c->si[x]);
+    }
+    c->I = std::max(c->I_req, umax + 1);
+    c->J = std::max(c->J_req, imax + 1);
+    c->K = c->cfg.num_factor;
+    c->vb = vbo_create(c->cfg, c->tu.size(), c->tu.data(), c->ti.data(), c->tr.data(), c->su.size(), c->su.data(),
+                       c->si.data(), c->sr.data(), c->I, c->J, c->st);
+    c->prepared = true;
 }
 
 static void set_triples(uint64_t n, const uint32_t* u, const uint32_t* i, const double* r, std::vector<uint32_t>& U,
@@ -1226,7 +1203,9 @@ int sbmf_prepare(sbmf_ctx* ctx) {
     for (size_t x = 0; x < ctx->tu.size(); ++x)
         if ((ctx->I_req && ctx->tu[x] >= ctx->I_req) || (ctx->J_req && ctx->ti[x] >= ctx->J_req))
             sbmf::fail(SBMF_E_ARG, "rating %zu has an id beyond sbmf_set_dims", x);
-    if (ctx->cfg.precision == SBMF_F32)
+    if (ctx->cfg.method == SBMF_METHOD_VB)
+        prepare_vb(ctx);
+    else if (ctx->cfg.precision == SBMF_F32)
         prepare_T<float>(ctx);
     else
         prepare_T<double>(ctx);
@@ -1237,6 +1216,16 @@ int sbmf_run(sbmf_ctx* ctx, uint32_t sweeps, sbmf_sweep_cb cb, void* user) {
     API_BEGIN
     if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
     HIPCHK(hipSetDevice(ctx->cfg.device));
+    if (!ctx->prepared && ctx->cfg.method == SBMF_METHOD_VB) {
+        if (ctx->tu.empty()) sbmf::fail(SBMF_E_STATE, "no training data (sbmf_set_train)");
+        prepare_vb(ctx);
+    }
+    if (ctx->vb) {
+        vbo_run(ctx->vb, sweeps, cb, user);
+        ctx->timing = sbmf_timing{};
+        ctx->timing.n_launch = vbo_launches(ctx->vb);
+        return SBMF_OK;
+    }
     if (!ctx->prepared) {
         if (ctx->tu.empty()) sbmf::fail(SBMF_E_STATE, "no training data (sbmf_set_train)");
         if (ctx->cfg.precision == SBMF_F32)
@@ -1256,6 +1245,10 @@ int sbmf_predict(sbmf_ctx* ctx, double* out) {
     if (!ctx || !out) sbmf::fail(SBMF_E_ARG, "null argument");
     if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
     HIPCHK(hipSetDevice(ctx->cfg.device));
+    if (ctx->vb) {
+        vbo_predict_out(ctx->vb, out);
+        return SBMF_OK;
+    }
     const uint64_t T_ = ctx->su.size();
     if (ctx->nranks > 1) ctx->comm.bcast_ranges(ctx->d_tsum.p, sizeof(double), ctx->tbounds, ctx->st);
     HIPCHK(hipStreamSynchronize(ctx->st));
@@ -1271,6 +1264,10 @@ int sbmf_get_factors(sbmf_ctx* ctx, double* U, double* V) {
     if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
     HIPCHK(hipSetDevice(ctx->cfg.device));
     HIPCHK(hipStreamSynchronize(ctx->st));
+    if (ctx->vb) {
+        vbo_factors(ctx->vb, U, V);
+        return SBMF_OK;
+    }
     if (ctx->cfg.precision == SBMF_F32) {
         if (U) sbmf::download_table<float>(ctx, ctx->d_U, U, ctx->I);
         if (V) sbmf::download_table<float>(ctx, ctx->d_V, V, ctx->J);
@@ -1285,6 +1282,7 @@ int sbmf_set_factors(sbmf_ctx* ctx, const double* U, const double* V) {
     API_BEGIN
     if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
     if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
+    if (ctx->vb) sbmf::fail(SBMF_E_STATE, "sbmf_set_factors is not supported by the online VB learner");
     HIPCHK(hipSetDevice(ctx->cfg.device));
     HIPCHK(hipStreamSynchronize(ctx->st));
     if (ctx->cfg.precision == SBMF_F32) {
@@ -1301,6 +1299,11 @@ int sbmf_get_hyper(sbmf_ctx* ctx, double* h, double* tau) {
     API_BEGIN
     if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
     if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
+    if (ctx->vb) {
+        HIPCHK(hipSetDevice(ctx->cfg.device));
+        vbo_hyper_out(ctx->vb, h, tau);
+        return SBMF_OK;
+    }
     const uint32_t K = ctx->K;
     if (h) {
         std::copy(ctx->sig_u.begin(), ctx->sig_u.end(), h);
@@ -1316,8 +1319,12 @@ int sbmf_get_biases(sbmf_ctx* ctx, double* bu, double* bv, double* b0) {
     API_BEGIN
     if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
     if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
-    if (!ctx->bias) sbmf::fail(SBMF_E_STATE, "not a biased sampler (quirks bias2 / bias22)");
     HIPCHK(hipSetDevice(ctx->cfg.device));
+    if (ctx->vb) {  // posterior means of w (users, items) and w0
+        vbo_biases(ctx->vb, bu, bv, b0);
+        return SBMF_OK;
+    }
+    if (!ctx->bias) sbmf::fail(SBMF_E_STATE, "not a biased sampler (quirks bias2 / bias22) or the VB learner");
     HIPCHK(hipStreamSynchronize(ctx->st));
     if (bu) HIPCHK(hipMemcpy(bu, ctx->d_bu.p, (size_t)ctx->I * sizeof(double), hipMemcpyDeviceToHost));
     if (bv) HIPCHK(hipMemcpy(bv, ctx->d_bv.p, (size_t)ctx->J * sizeof(double), hipMemcpyDeviceToHost));
@@ -1362,6 +1369,8 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
     HIPCHK(hipSetDevice(ctx->cfg.device));
     ctx->nranks = nranks;
     ctx->rank = rank;
+    if (nranks > 1 && ctx->cfg.method == SBMF_METHOD_VB)
+        sbmf::fail(SBMF_E_ARG, "the online VB learner runs on one GPU in this build");
     if (nranks > 1 && ctx->bias)
         sbmf::fail(SBMF_E_ARG, "the biased sampler (quirks bias2/bias22) runs on one GPU in this build");
     if (nranks > 1) ctx->comm.init(nranks, rank, id);

@@ -110,14 +110,18 @@ void load(const std::string& path, const std::string& fmt, uint32_t item_offset,
 
 struct RunState {
     std::string rmse_file;
+    bool vb = false;  // online VB prints "#Iter=..\tTest=.." (fm_learn_vb_online_simultaneous.h:447)
     std::ofstream* rlog = nullptr;
     int verbosity = 0;
 };
 
 int on_sweep(const sbmf_sweep_info* in, void* user) {
     RunState* rs = static_cast<RunState*>(user);
-    std::cout << "#Iter=" << std::setw(3) << in->sweep << "\tTrain=" << in->rmse_train << "\tTest=" << in->rmse_avg
-              << std::endl;
+    if (rs->vb)
+        std::cout << "#Iter=" << std::setw(3) << in->sweep << "\tTest=" << in->rmse_avg << std::endl;
+    else
+        std::cout << "#Iter=" << std::setw(3) << in->sweep << "\tTrain=" << in->rmse_train << "\tTest=" << in->rmse_avg
+                  << std::endl;
     std::ofstream f(rs->rmse_file, std::ios_base::app);
     f << in->rmse_avg << "\n";
     if (rs->rlog)
@@ -149,7 +153,8 @@ int main(int argc, char** argv) {
         cl.reg("stdev", "unused");
         cl.reg("iter", "number of collection sweeps; default=100");
         cl.reg("learn_rate", "unused (SGD only)");
-        cl.reg("method", "learning method: mcmc (SBPMF Gibbs); default=mcmc");
+        cl.reg("method", "learning method: mcmc (SBPMF Gibbs) | vb (online variational Bayes, libFM's vb_online; "
+                         "alias vb_online); default=mcmc");
         cl.reg("verbosity", "how much infos to print; default=0");
         cl.reg("rlog", "write per-sweep measurements to a TSV file; default=''");
         cl.reg("seed", "integer seed; default=1 (glibc default seed of the reference samplers)");
@@ -178,15 +183,18 @@ int main(int argc, char** argv) {
         const std::string task = cl.get("task", "");
         if (task != "r") throw std::runtime_error("only -task r (regression) is supported by the SBPMF sampler");
         const std::string method = cl.get("method", "mcmc");
-        if (method != "mcmc")
-            throw std::runtime_error("-method " + method + " is not supported (use mcmc)");
+        const bool vb = method == "vb" || method == "vb_online";
+        if (method != "mcmc" && !vb)
+            throw std::runtime_error("-method " + method + " is not supported (use mcmc or vb)");
         if (!cl.has("train") || !cl.has("test")) throw std::runtime_error("-train and -test are mandatory");
         std::vector<int> dim = split_ints(cl.get("dim", "1,1,8"));
         if (dim.size() != 3) throw std::runtime_error("dim must have 3 numbers");
         if (dim[2] <= 0 || dim[2] > 256) throw std::runtime_error("dim k2 must be in [1,256]");
+        if (vb && !(dim[0] == 1 && dim[1] == 1))
+            throw std::runtime_error("the online VB learner updates w0 and the user/item w: use -dim '1,1,K'");
         const std::string q = cl.get("quirks", "final");
         const bool biased = q == "bias2" || q == "bias22";
-        if (!biased && (dim[0] || dim[1]))
+        if (!vb && !biased && (dim[0] || dim[1]))
             std::cout << "note: bias terms (k0,k1) are not sampled; the reference SBPMF sampler has them compiled "
                          "out (gibbs_sbpmf_final.cpp:276-295); -quirks bias2|bias22 selects the biased sampler"
                       << std::endl;
@@ -222,7 +230,8 @@ int main(int argc, char** argv) {
         cfg.stream_threshold = (uint32_t)cl.getl("stream_threshold", 0);
         cfg.row_kernel = (uint32_t)cl.getl("row_kernel", 0);
         cfg.split_chunk = (uint32_t)cl.getl("split_chunk", 0);
-        cfg.eval_train = 1;
+        cfg.eval_train = vb ? 0 : 1;
+        cfg.method = vb ? SBMF_METHOD_VB : SBMF_METHOD_MCMC;
         cfg.eval_test = 1;
 
         const std::string fmt = cl.get("format", "auto");
@@ -250,7 +259,8 @@ int main(int argc, char** argv) {
         RunState rs;
         std::ostringstream nm;
         nm << dim[0] << dim[1] << dim[2];
-        rs.rmse_file = "test_rmse_" + nm.str() + "_" + method;
+        rs.rmse_file = "test_rmse_" + nm.str() + "_" + (vb ? std::string("vb_online") : method);
+        rs.vb = vb;
         { std::ofstream trunc(rs.rmse_file); }
         std::ofstream rlog;
         if (cl.has("rlog") && !cl.get("rlog", "").empty()) {

@@ -1,0 +1,369 @@
+// vbo.cpp -- host side of the online variational-Bayes learner (`-method vb`):
+// the reference's fm_learn_vb_online (src/libfm/src/fm_learn_vb_online.h,
+// fm_learn_vb_online_simultaneous.h) on rating data.
+//
+// Per epoch (fm_learn_vb_online_simultaneous.h:58-447):
+//   1. shuffle the 1-based case ids (libstdc++ random_shuffle over rand() in
+//      reference RNG mode, the array kept across epochs; Fisher-Yates over
+//      Philox otherwise); case l goes to batch ceil(id_l / ceil(N/30));
+//   2. group every batch's cases by user and by item (host, O(N)) and upload;
+//   3. per batch, on the device: e / t terms, update_w0, update_w (users,
+//      items), update_v (per factor: users, items), hyperparameter blends;
+//   4. test predictions of the means, clamped to the train target range.
+// The reference writes each epoch's 30 batches to text files and parses them
+// back (:148-203); here a batch is an index range in device memory.
+#include "vbo.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "common.h"
+#include "rng.h"
+
+namespace sbmf {
+
+struct VBLearner {
+    sbmf_config cfg{};
+    uint32_t K = 0, Kp = 0, I = 0, J = 0, p = 0, N = 0, NB = 30, S = 0;
+    double lo = 1.0, hi = 5.0;
+    uint32_t epoch = 0;
+    GlibcRand grand{1};
+    hipStream_t st = nullptr;
+    hipEvent_t ev[4] = {};
+    // host data
+    std::vector<uint32_t> tu, ti, su, si;
+    std::vector<double> tr, sr;
+    std::vector<uint32_t> shuffle, bid, bloc, keycnt;
+    // this epoch's batch layout
+    std::vector<VRow> urows, irows;
+    std::vector<uint32_t> urow0, irow0, bsize, uloc, upart, iloc, ipart;
+    std::vector<float> ur;
+    // device
+    DBuf d_mu_v, d_sg_v, d_nm_v, d_ns_v, d_mu_w, d_sg_w, d_nm_w, d_ns_w, d_rho_w, d_rho_v, d_t_w, d_t_v, d_cc;
+    DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_E, d_T, d_part;
+    DBuf d_urows, d_irows, d_uloc, d_upart, d_iloc, d_ipart, d_ur;
+    DBuf d_tu, d_ti, d_tr, d_pred, d_tpart;
+    VBTables tb{};
+    double last_rmse = NAN, last_alpha = NAN;
+    double ms_layout = 0.0;
+    uint32_t n_launch = 0;
+
+    ~VBLearner() {
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+
+    void init(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r, uint64_t nt,
+              const uint32_t* tu_, const uint32_t* ti_, const double* tr_, uint32_t I_, uint32_t J_, hipStream_t s);
+    void build_layout();
+    void run(uint32_t epochs, sbmf_sweep_cb cb, void* user);
+};
+
+void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r,
+                     uint64_t nt, const uint32_t* tu_, const uint32_t* ti_, const double* tr_, uint32_t I_, uint32_t J_,
+                     hipStream_t s) {
+    cfg = c;
+    st = s;
+    K = c.num_factor;
+    Kp = (K + 15) / 16 * 16;
+    I = I_;
+    J = J_;
+    p = I + J;  // user u -> u, item i -> I + i; num_attribute = largest id + 1 (libfm.cpp:328)
+    N = (uint32_t)n;
+    NB = c.vb_batches ? c.vb_batches : 30;  // fm_learn_vb_online_simultaneous.h:62
+    S = (uint32_t)std::ceil((double)N / NB);
+    if (N == 0 || (uint64_t)S * (NB - 1) >= N)
+        fail(SBMF_E_ARG, "online VB: %u ratings leave a batch of %u empty (the reference divides by zero)", N, NB);
+    tu.assign(u, u + n);
+    ti.assign(i, i + n);
+    tr.assign(r, r + n);
+    su.assign(tu_, tu_ + nt);
+    si.assign(ti_, ti_ + nt);
+    sr.assign(tr_, tr_ + nt);
+    // train target range as DATA_FLOAT (libfm.cpp:199-214, fm_learn min/max_target)
+    float mn = 3.402823466e+38f, mx = -3.402823466e+38f;
+    for (double x : tr) {
+        mn = std::min(mn, (float)x);
+        mx = std::max(mx, (float)x);
+    }
+    lo = mn;
+    hi = mx;
+
+    // ---- start state (libfm.cpp:387,433; fm_learn_vb_online.h:841-946; matrix.h:358-380)
+    std::vector<double> mu_v((size_t)K * p), mu_w(p);
+    if (c.rng_mode == SBMF_RNG_REFERENCE) {
+        grand.seed_((unsigned)c.seed);
+        for (size_t x = 0; x < (size_t)K * p + p; ++x) (void)leva_normal(grand);  // fm_model v, w
+        for (uint32_t a = 0; a < p; ++a) mu_w[a] = 0.1 * leva_normal(grand);
+        for (size_t x = 0; x < (size_t)K * p; ++x) mu_v[x] = 0.1 * leva_normal(grand);
+    } else {
+        PhiloxStream ps(c.seed, 0xfffffff0u, 5);
+        for (uint32_t a = 0; a < p; ++a) mu_w[a] = 0.1 * leva_normal(ps);
+        for (size_t x = 0; x < (size_t)K * p; ++x) mu_v[x] = 0.1 * leva_normal(ps);
+    }
+    std::vector<double> sg_v((size_t)K * p, .02), nm_v((size_t)K * p), ns_v((size_t)K * p, 1 / .02);
+    std::vector<double> sg_w(p, .02), nm_w(p), ns_w(p, 1 / .02), ones(p, 1.0);
+    for (size_t x = 0; x < (size_t)K * p; ++x) nm_v[x] = mu_v[x] / 0.02;
+    for (uint32_t a = 0; a < p; ++a) nm_w[a] = mu_w[a] / 0.02;
+    std::vector<uint32_t> cc(p, 0), zeros(p, 0);
+    for (uint32_t x = 0; x < N; ++x) {  // column counts of the whole train set (:877-900)
+        cc[tu[x]]++;
+        cc[I + ti[x]]++;
+    }
+    upload(d_mu_v, mu_v, st);
+    upload(d_sg_v, sg_v, st);
+    upload(d_nm_v, nm_v, st);
+    upload(d_ns_v, ns_v, st);
+    upload(d_mu_w, mu_w, st);
+    upload(d_sg_w, sg_w, st);
+    upload(d_nm_w, nm_w, st);
+    upload(d_ns_w, ns_w, st);
+    upload(d_rho_w, ones, st);  // (t0 + 0)^-0.5 = 1
+    upload(d_rho_v, ones, st);
+    upload(d_t_w, zeros, st);
+    upload(d_t_v, zeros, st);
+    upload(d_cc, cc, st);
+    upload(d_sigma_v, std::vector<double>(K, 1.0), st);
+    VBScal sc{};
+    sc.alpha = 1.0;
+    sc.sigma_0 = 1.0;
+    sc.mu0 = 0.0;
+    sc.sg0 = 0.02;
+    sc.nm0 = 0.0;
+    sc.ns0 = 1 / sc.sg0;
+    sc.sigma_w = 1.0;
+    sc.rho0 = 1.0;
+    d_scal.alloc(sizeof(VBScal));
+    HIPCHK(hipMemcpyAsync(d_scal.p, &sc, sizeof sc, hipMemcpyHostToDevice, st));
+    d_muT.alloc((size_t)p * Kp * sizeof(double));
+    d_sgT.alloc((size_t)p * Kp * sizeof(double));
+    HIPCHK(hipMemsetAsync(d_muT.p, 0, d_muT.bytes, st));
+    HIPCHK(hipMemsetAsync(d_sgT.p, 0, d_sgT.bytes, st));
+    d_E.alloc((size_t)S * sizeof(double));
+    d_T.alloc((size_t)S * sizeof(double));
+    d_part.alloc(vbo_scratch_doubles(S, K, p) * sizeof(double));
+    upload(d_tu, su, st);
+    upload(d_ti, si, st);
+    upload(d_tr, sr, st);
+    d_pred.alloc(std::max<size_t>(su.size(), 1) * sizeof(double));
+    d_tpart.alloc(((su.size() + 255) / 256 + 1) * sizeof(double));
+    tb.mu_v = d_mu_v.as<double>();
+    tb.sg_v = d_sg_v.as<double>();
+    tb.nm_v = d_nm_v.as<double>();
+    tb.ns_v = d_ns_v.as<double>();
+    tb.mu_w = d_mu_w.as<double>();
+    tb.sg_w = d_sg_w.as<double>();
+    tb.nm_w = d_nm_w.as<double>();
+    tb.ns_w = d_ns_w.as<double>();
+    tb.rho_w = d_rho_w.as<double>();
+    tb.rho_v = d_rho_v.as<double>();
+    tb.t_w = d_t_w.as<uint32_t>();
+    tb.t_v = d_t_v.as<uint32_t>();
+    tb.cc = d_cc.as<uint32_t>();
+    tb.sigma_v = d_sigma_v.as<double>();
+    tb.scal = d_scal.as<VBScal>();
+    tb.K = K;
+    tb.p = p;
+    tb.N = N;
+    shuffle.resize(N);
+    for (uint32_t x = 0; x < N; ++x) shuffle[x] = x + 1;
+    for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipStreamSynchronize(st));
+}
+
+// One epoch's batches: shuffle, batch membership in file order, and each
+// batch's cases grouped by user and by item (stable counting sorts).
+void VBLearner::build_layout() {
+    if (cfg.rng_mode == SBMF_RNG_REFERENCE) {
+        // libstdc++ random_shuffle: for i = 1..N-1, j = rand() % (i + 1), swap
+        for (uint32_t x = 1; x < N; ++x) {
+            const uint32_t j = (uint32_t)((long)grand.next() % (long)(x + 1));
+            if (x != j) std::swap(shuffle[x], shuffle[j]);
+        }
+    } else {
+        PhiloxStream ps(cfg.seed, epoch, 6);
+        for (uint32_t x = N - 1; x > 0; --x) {
+            const uint32_t j = std::min(x, (uint32_t)(ps.uniform() * (x + 1)));
+            std::swap(shuffle[x], shuffle[j]);
+        }
+    }
+    bid.resize(N);
+    bloc.resize(N);
+    bsize.assign(NB, 0);
+    for (uint32_t l = 0; l < N; ++l) {
+        const uint32_t b = (uint32_t)std::ceil((double)shuffle[l] / S) - 1;  // :175
+        bid[l] = b;
+        bloc[l] = bsize[b]++;
+    }
+    auto group = [&](uint32_t R, bool users, std::vector<VRow>& rows, std::vector<uint32_t>& row0,
+                     std::vector<uint32_t>& loc, std::vector<uint32_t>& part) {
+        keycnt.assign((size_t)NB * R + 1, 0);
+        for (uint32_t l = 0; l < N; ++l) keycnt[(size_t)bid[l] * R + (users ? tu[l] : ti[l]) + 1]++;
+        rows.clear();
+        row0.assign(NB + 1, 0);
+        for (uint32_t b = 0; b < NB; ++b) {
+            row0[b] = (uint32_t)rows.size();
+            for (uint32_t a = 0; a < R; ++a) {
+                const size_t k = (size_t)b * R + a;
+                if (keycnt[k + 1]) rows.push_back(VRow{users ? a : I + a, 0, keycnt[k + 1], 0});
+            }
+        }
+        row0[NB] = (uint32_t)rows.size();
+        for (size_t k = 1; k < keycnt.size(); ++k) keycnt[k] += keycnt[k - 1];
+        // rows appear in key order, so a running offset is each row's start
+        uint32_t off = 0;
+        for (VRow& rw : rows) {
+            rw.start = off;
+            off += rw.len;
+        }
+        loc.resize(N);
+        part.resize(N);
+        if (users) ur.resize(N);
+        for (uint32_t l = 0; l < N; ++l) {
+            const size_t k = (size_t)bid[l] * R + (users ? tu[l] : ti[l]);
+            const uint32_t pos = keycnt[k]++;
+            loc[pos] = bloc[l];
+            part[pos] = users ? I + ti[l] : tu[l];
+            if (users) ur[pos] = (float)tr[l];
+        }
+    };
+    group(I, true, urows, urow0, uloc, upart);
+    group(J, false, irows, irow0, iloc, ipart);
+}
+
+void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
+    for (uint32_t it = 0; it < epochs; ++it) {
+        const auto h0 = std::chrono::steady_clock::now();
+        build_layout();
+        upload(d_urows, urows, st);
+        upload(d_irows, irows, st);
+        upload(d_uloc, uloc, st);
+        upload(d_upart, upart, st);
+        upload(d_ur, ur, st);
+        upload(d_iloc, iloc, st);
+        upload(d_ipart, ipart, st);
+        HIPCHK(hipStreamSynchronize(st));
+        ms_layout = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+        n_launch = 0;
+        HIPCHK(hipEventRecord(ev[0], st));
+        double* E = d_E.as<double>();
+        double* T = d_T.as<double>();
+        double* part = d_part.as<double>();
+        const VRow* ur_ = d_urows.as<VRow>();
+        const VRow* ir_ = d_irows.as<VRow>();
+        for (uint32_t b = 0; b < NB; ++b) {
+            const uint32_t B = bsize[b];
+            const uint32_t nu = urow0[b + 1] - urow0[b], ni = irow0[b + 1] - irow0[b];
+            HIPCHK(vbo_transpose(tb.mu_v, d_muT.as<double>(), K, Kp, p, st));
+            HIPCHK(vbo_transpose(tb.sg_v, d_sgT.as<double>(), K, Kp, p, st));
+            HIPCHK(vbo_predict(ur_ + urow0[b], nu, d_uloc.as<uint32_t>(), d_upart.as<uint32_t>(), d_ur.as<float>(),
+                               d_muT.as<double>(), d_sgT.as<double>(), tb, Kp, E, T, st));
+            HIPCHK(vbo_update_w0(E, B, tb, part, st));
+            HIPCHK(vbo_update_w(ur_ + urow0[b], nu, d_uloc.as<uint32_t>(), 1, tb, E, T, st));
+            HIPCHK(vbo_update_w(ir_ + irow0[b], ni, d_iloc.as<uint32_t>(), 0, tb, E, T, st));
+            for (uint32_t f = 0; f < K; ++f) {
+                HIPCHK(vbo_update_v(ur_ + urow0[b], nu, d_uloc.as<uint32_t>(), d_upart.as<uint32_t>(), f, tb, E, T,
+                                    st));
+                HIPCHK(vbo_update_v(ir_ + irow0[b], ni, d_iloc.as<uint32_t>(), d_ipart.as<uint32_t>(), f, tb, E, T,
+                                    st));
+            }
+            HIPCHK(vbo_hyper(E, T, B, tb, part, st));
+            n_launch += 2 * K + 12;
+        }
+        HIPCHK(hipEventRecord(ev[1], st));
+        // ---- test RMSE of the clamped means (fm_learn_vb_online_simultaneous.h:348-360,441-447)
+        const uint64_t nt = su.size();
+        double rmse = NAN;
+        if (nt) {
+            HIPCHK(vbo_transpose(tb.mu_v, d_muT.as<double>(), K, Kp, p, st));
+            HIPCHK(vbo_test(d_tu.as<uint32_t>(), d_ti.as<uint32_t>(), d_tr.as<double>(), nt, I, d_muT.as<double>(), tb,
+                            Kp, lo, hi, d_pred.as<double>(), d_tpart.as<double>(), st));
+            std::vector<double> h((nt + 255) / 256);
+            HIPCHK(hipMemcpyAsync(h.data(), d_tpart.p, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            double se = 0.0;
+            for (double x : h) se += x;
+            rmse = std::sqrt(se / nt);
+        }
+        HIPCHK(hipEventRecord(ev[2], st));
+        VBScal sc;
+        HIPCHK(hipMemcpyAsync(&sc, d_scal.p, sizeof sc, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        last_rmse = rmse;
+        last_alpha = sc.alpha;
+        float ms_epoch = 0.f, ms_eval = 0.f;
+        (void)hipEventElapsedTime(&ms_epoch, ev[0], ev[1]);
+        (void)hipEventElapsedTime(&ms_eval, ev[1], ev[2]);
+        sbmf_sweep_info info{};
+        info.sweep = epoch;
+        info.collected = 1;
+        info.rmse_avg = rmse;
+        info.rmse_this = rmse;
+        info.rmse_train = NAN;
+        info.tau = sc.alpha;
+        info.ms_sweep = ms_epoch;
+        info.ms_eval = ms_eval;
+        ++epoch;
+        if (cb && cb(&info, user)) break;
+    }
+}
+
+// ---------------------------------------------------------------- entry points used by sbmf.cpp
+VBLearner* vbo_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r,
+                      uint64_t nt, const uint32_t* tu, const uint32_t* ti, const double* tr, uint32_t I, uint32_t J,
+                      hipStream_t st) {
+    std::unique_ptr<VBLearner> L(new VBLearner());
+    L->init(c, n, u, i, r, nt, tu, ti, tr, I, J, st);
+    return L.release();
+}
+void vbo_destroy(VBLearner* L) { delete L; }
+void vbo_run(VBLearner* L, uint32_t epochs, sbmf_sweep_cb cb, void* user) { L->run(epochs, cb, user); }
+void vbo_predict_out(VBLearner* L, double* out) {
+    HIPCHK(hipStreamSynchronize(L->st));
+    if (!L->su.empty()) HIPCHK(hipMemcpy(out, L->d_pred.p, L->su.size() * sizeof(double), hipMemcpyDeviceToHost));
+}
+// means of the factors: users [I][K], items [J][K]
+void vbo_factors(VBLearner* L, double* U, double* V) {
+    HIPCHK(hipStreamSynchronize(L->st));
+    std::vector<double> h((size_t)L->K * L->p);
+    HIPCHK(hipMemcpy(h.data(), L->d_mu_v.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (uint32_t f = 0; f < L->K; ++f) {
+        if (U)
+            for (uint32_t a = 0; a < L->I; ++a) U[(size_t)a * L->K + f] = h[(size_t)f * L->p + a];
+        if (V)
+            for (uint32_t a = 0; a < L->J; ++a) V[(size_t)a * L->K + f] = h[(size_t)f * L->p + L->I + a];
+    }
+}
+void vbo_biases(VBLearner* L, double* bu, double* bv, double* b0) {
+    HIPCHK(hipStreamSynchronize(L->st));
+    std::vector<double> h(L->p);
+    HIPCHK(hipMemcpy(h.data(), L->d_mu_w.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+    if (bu) std::copy(h.begin(), h.begin() + L->I, bu);
+    if (bv) std::copy(h.begin() + L->I, h.end(), bv);
+    if (b0) {
+        VBScal sc;
+        HIPCHK(hipMemcpy(&sc, L->d_scal.p, sizeof sc, hipMemcpyDeviceToHost));
+        *b0 = sc.mu0;
+    }
+}
+// [sigma_v (K) | 0 ...] and alpha
+void vbo_hyper_out(VBLearner* L, double* h4k, double* alpha) {
+    HIPCHK(hipStreamSynchronize(L->st));
+    if (h4k) {
+        std::fill(h4k, h4k + 4 * (size_t)L->K, 0.0);
+        HIPCHK(hipMemcpy(h4k, L->d_sigma_v.p, L->K * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    if (alpha) {
+        VBScal sc;
+        HIPCHK(hipMemcpy(&sc, L->d_scal.p, sizeof sc, hipMemcpyDeviceToHost));
+        *alpha = sc.alpha;
+    }
+}
+double vbo_layout_ms(const VBLearner* L) { return L->ms_layout; }
+uint32_t vbo_launches(const VBLearner* L) { return L->n_launch; }
+
+}  // namespace sbmf

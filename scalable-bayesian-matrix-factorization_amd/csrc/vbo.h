@@ -1,0 +1,88 @@
+// vbo.h -- online variational Bayes (`-method vb`): the reference's
+// fm_learn_vb_online learner (src/libfm/src/fm_learn_vb_online.h,
+// fm_learn_vb_online_simultaneous.h) on rating data, on the GPU.
+//
+// Model: attributes 0..I-1 are users, I..I+J-1 items (libFM's users-first
+// one-hot layout); per attribute a bias mean / variance (mu_w, sigma_w') and
+// K factor means / variances (mu_v, sigma_v'), each with its natural
+// parameters; the global bias (mu_0', sigma_0'); the noise precision alpha
+// and the prior precisions sigma_0, sigma_w, sigma_v[f].  One epoch = a
+// shuffle into 30 batches, and per batch: predictions and their variances,
+// update_w0, update_w (users, then items), update_v (factor-outer: users,
+// then items, per factor), hyperparameter blends.  Step sizes (t0 + t)^-0.5.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/sbmf.h"
+
+namespace sbmf {
+
+// One attribute's cases inside one batch: entries [start, start + len) of
+// the orientation's case arrays (batch-local case index, partner attribute).
+struct VRow {
+    uint32_t attr, start, len, pad;
+};
+
+// Scalar state kept on the device so a batch needs no host round trip.
+struct VBScal {
+    double alpha, sigma_0, mu0, sg0, nm0, ns0, sigma_w, rho0;
+    double d_mu0, d_sg0;  // this batch's update_w0 deltas, applied by the user bias pass
+    uint32_t t_w0, n_skip;  // n_skip: batches whose alpha was NaN/inf (the reference then skips the blends)
+};
+
+// Parameter tables, f-major [K][p] like the reference's DMatrix (the column
+// of factor f is contiguous and small enough to stay in L2 during a pass).
+struct VBTables {
+    double *mu_v, *sg_v, *nm_v, *ns_v;  // [K][p]
+    double *mu_w, *sg_w, *nm_w, *ns_w;  // [p]
+    double *rho_w, *rho_v;              // [p] step sizes (t0 + t)^-0.5
+    uint32_t *t_w, *t_v, *cc;           // [p] step counts, train column counts
+    double* sigma_v;                    // [K] prior precisions of the factors
+    VBScal* scal;
+    uint32_t K, p, N;                   // N: train ratings (the reference's _size)
+};
+
+// [K][p] -> [p][Kp] (attribute-major rows for the prediction gathers)
+hipError_t vbo_transpose(const double* src, double* dst, uint32_t K, uint32_t Kp, uint32_t p, hipStream_t st);
+// e = r - prediction and t = its variance for every case of a batch, driven
+// by the batch's user rows (fm_learn_vb_online.h:80-310)
+hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* loc, const uint32_t* part, const float* r,
+                       const double* muT, const double* sgT, const VBTables& tb, uint32_t Kp, double* E, double* T,
+                       hipStream_t st);
+// update_w0 (:586-633): the global bias blend; its deltas are applied to e / t
+// by the user pass of vbo_update_w (apply_w0 = 1)
+hipError_t vbo_update_w0(const double* E, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
+// update_w (:635-710) over the rows of one orientation
+hipError_t vbo_update_w(const VRow* rows, uint32_t nrows, const uint32_t* loc, int apply_w0, const VBTables& tb,
+                        double* E, double* T, hipStream_t st);
+// update_v (:712-800) of factor f over the rows of one orientation
+hipError_t vbo_update_v(const VRow* rows, uint32_t nrows, const uint32_t* loc, const uint32_t* part, uint32_t f,
+                        const VBTables& tb, double* E, double* T, hipStream_t st);
+// step sizes of update_v (:447-453) and the hyperparameter blends (:523-580)
+hipError_t vbo_hyper(const double* E, const double* T, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
+// test predictions clamped to [lo, hi] and their squared errors per 256-case block
+hipError_t vbo_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t n, uint32_t I,
+                    const double* muT, const VBTables& tb, uint32_t Kp, double lo, double hi, double* pred,
+                    double* part, hipStream_t st);
+// ---- host learner (vbo.cpp), driven by the C ABI in sbmf.cpp
+struct VBLearner;
+VBLearner* vbo_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r,
+                      uint64_t nt, const uint32_t* tu, const uint32_t* ti, const double* tr, uint32_t I, uint32_t J,
+                      hipStream_t st);
+void vbo_destroy(VBLearner* L);
+void vbo_run(VBLearner* L, uint32_t epochs, sbmf_sweep_cb cb, void* user);
+void vbo_predict_out(VBLearner* L, double* out);  // clamped test predictions of the means
+void vbo_factors(VBLearner* L, double* U, double* V);  // factor means, users [I][K], items [J][K]
+void vbo_biases(VBLearner* L, double* bu, double* bv, double* b0);
+void vbo_hyper_out(VBLearner* L, double* h4k, double* alpha);  // [sigma_v | 0 | 0 | 0], alpha
+double vbo_layout_ms(const VBLearner* L);  // host time of the last epoch's shuffle + batch layout
+uint32_t vbo_launches(const VBLearner* L);
+
+// scratch doubles vbo_update_w0 / vbo_hyper need for B cases
+inline size_t vbo_scratch_doubles(uint32_t B, uint32_t K, uint32_t p) {
+    return (size_t)(B + 1023) / 1024 + 16 + (size_t)(K + 1) * ((p + 2047) / 2048 + 1);
+}
+
+}  // namespace sbmf

@@ -1,0 +1,417 @@
+// vbo.hip -- gfx950 kernels of the online variational-Bayes learner
+// (`sbmf -method vb`; the reference's fm_learn_vb_online on rating data).
+//
+// The work unit is an attribute row of one batch: a user (or an item) and the
+// batch's cases that carry it.  16 lanes own a row (16 rows per 256-thread
+// block): the row's natural-parameter sums are 16-lane reductions and its
+// cases are visited 16 at a time.  A case's residual e and variance term t
+// live in the batch-local arrays E, T; every case belongs to exactly one
+// user row and one item row, so the rows of one pass never share a case.
+// In an update_v pass the partner values (item factors for user rows, the
+// fresh user factors for item rows) are read from the factor column f of the
+// f-major tables, which stays in L2.  Every reduction has a fixed order, so
+// results are bitwise repeatable run to run.
+//
+// With x = 1 for every feature the reference's cached sums collapse:
+// q - x mu = partner mean, t.q - x^2 sigma = partner variance, t.z - ... =
+// partner mean^2 (fm_learn_vb_online.h:729-733,781-784), and the prediction
+// 1/2 sum_f (v_u + v_i)^2 - 1/2 sum_f (v_u^2 + v_i^2) = sum_f v_u v_i.  The
+// GPU uses the collapsed forms (same values up to rounding).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "vbo.h"
+
+namespace sbmf {
+namespace {
+
+constexpr int KBMAX = 16;  // Kp / 16 <= 16 (K <= 256)
+
+// sum over the 16 lanes of a row group, lane 0's value broadcast to the group
+__device__ __forceinline__ double sum16(double x) {
+    x += __shfl_xor(x, 8, 16);
+    x += __shfl_xor(x, 4, 16);
+    x += __shfl_xor(x, 2, 16);
+    x += __shfl_xor(x, 1, 16);
+    return __shfl(x, 0, 16);
+}
+
+// fixed-order block sum of 256 threads (every thread gets the total)
+__device__ __forceinline__ double block_sum256(double x, double* red) {
+    red[threadIdx.x] = x;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    const double t = red[0];
+    __syncthreads();
+    return t;
+}
+
+__global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ src, double* __restrict__ dst, uint32_t K,
+                                                    uint32_t Kp, uint32_t p) {
+    __shared__ double tile[32][33];
+    const uint32_t a0 = blockIdx.x * 32, f0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int j = ty; j < 32; j += 8) {
+        const uint32_t f = f0 + j, a = a0 + tx;
+        tile[j][tx] = (f < K && a < p) ? src[(size_t)f * p + a] : 0.0;
+    }
+    __syncthreads();
+    for (int j = ty; j < 32; j += 8) {
+        const uint32_t a = a0 + j, f = f0 + tx;
+        if (a < p && f < K) dst[(size_t)a * Kp + f] = tile[tx][j];
+    }
+}
+
+// predict_data_and_write_to_eterms + predict_t_and_write_to_qterms
+// (fm_learn_vb_online.h:80-310) for the cases of the batch's user rows:
+//   e = r - (sum_f v_u v_i + w_u + w_i + mu_0'),
+//   t = sum_f (s_u s_i + s_u v_i^2 + s_i v_u^2) + s^w_u + s^w_i + sigma_0'.
+__global__ __launch_bounds__(256) void k_predict(const VRow* __restrict__ rows, uint32_t nrows,
+                                                  const uint32_t* __restrict__ loc, const uint32_t* __restrict__ part,
+                                                  const float* __restrict__ r, const double* __restrict__ muT,
+                                                  const double* __restrict__ sgT, VBTables tb, uint32_t Kp,
+                                                  double* __restrict__ E, double* __restrict__ T) {
+    const uint32_t ri = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int ci = threadIdx.x & 15;
+    if (ri >= nrows) return;  // whole 16-lane groups
+    const VRow rw = rows[ri];
+    const uint32_t nb = Kp / 16;
+    double vu[KBMAX], su[KBMAX];
+#pragma unroll
+    for (int b = 0; b < KBMAX; ++b) {
+        vu[b] = b < (int)nb ? muT[(size_t)rw.attr * Kp + 16 * b + ci] : 0.0;
+        su[b] = b < (int)nb ? sgT[(size_t)rw.attr * Kp + 16 * b + ci] : 0.0;
+    }
+    const double wu = tb.mu_w[rw.attr], swu = tb.sg_w[rw.attr];
+    const double mu0 = tb.scal->mu0, sg0 = tb.scal->sg0;
+    for (uint32_t x = 0; x < rw.len; ++x) {
+        const uint32_t q = rw.start + x;
+        const uint32_t pa = part[q];
+        double d = 0.0, tv = 0.0;
+#pragma unroll
+        for (int b = 0; b < KBMAX; ++b) {
+            if (b < (int)nb) {
+                const double vi = muT[(size_t)pa * Kp + 16 * b + ci], si = sgT[(size_t)pa * Kp + 16 * b + ci];
+                d += vu[b] * vi;
+                tv += su[b] * si + su[b] * (vi * vi) + si * (vu[b] * vu[b]);
+            }
+        }
+        d = sum16(d);
+        tv = sum16(tv);
+        if (ci == 0) {
+            const uint32_t c = loc[q];
+            E[c] = (double)r[q] - (((d + wu) + tb.mu_w[pa]) + mu0);
+            T[c] = ((tv + swu) + tb.sg_w[pa]) + sg0;
+        }
+    }
+}
+
+// update_w0 (:586-633): partial sums of the per-case natural mean
+// (1 - rho0) nm0 + rho0 N alpha (e + mu0'), 1024 cases per block
+__global__ __launch_bounds__(256) void k_w0_partial(const double* __restrict__ E, uint32_t B, VBTables tb,
+                                                     double* __restrict__ part) {
+    __shared__ double red[256];
+    const VBScal s = *tb.scal;
+    const double cmu = (1 - s.rho0) * s.nm0, kmu = s.rho0 * tb.N * s.alpha;
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t c = blockIdx.x * 1024 + threadIdx.x * 4 + u;
+        if (c < B) acc += cmu + kmu * (E[c] + s.mu0);
+    }
+    acc = block_sum256(acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_w0_final(const double* __restrict__ part, uint32_t nblk, uint32_t B,
+                                                   VBTables tb) {
+    __shared__ double red[256];
+    double acc = 0.0;
+    for (uint32_t i = threadIdx.x; i < nblk; i += 256) acc += part[i];
+    acc = block_sum256(acc, red);
+    if (threadIdx.x == 0) {
+        VBScal& s = *tb.scal;
+        // every case contributes the same natural precision; their mean is that value
+        const double ns = ((1 - s.rho0) * s.ns0) + s.rho0 * (s.sigma_0 + tb.N * s.alpha);
+        const double nm = acc / B;
+        const double mu = nm / ns, sg = 1.0 / ns;
+        s.d_mu0 = s.mu0 - mu;
+        s.d_sg0 = sg - s.sg0;
+        s.nm0 = nm;
+        s.ns0 = ns;
+        s.mu0 = mu;
+        s.sg0 = sg;
+    }
+}
+
+// update_w (:635-710) for the rows of one orientation.  apply_w0: first add
+// update_w0's deltas to the row's cases (the user pass touches every case once).
+__global__ __launch_bounds__(256) void k_update_w(const VRow* __restrict__ rows, uint32_t nrows,
+                                                   const uint32_t* __restrict__ loc, int apply_w0, VBTables tb,
+                                                   double* __restrict__ E, double* __restrict__ T) {
+    const uint32_t ri = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int ci = threadIdx.x & 15;
+    if (ri >= nrows) return;
+    const VRow rw = rows[ri];
+    const uint32_t a = rw.attr, n = rw.len;
+    const double alpha = tb.scal->alpha, sigma_w = tb.scal->sigma_w;
+    if (apply_w0) {
+        const double dm = tb.scal->d_mu0, ds = tb.scal->d_sg0;
+        for (uint32_t x = ci; x < n; x += 16) {
+            const uint32_t c = loc[rw.start + x];
+            E[c] = E[c] + dm;
+            T[c] = T[c] + ds;
+        }
+    }
+    const double md = tb.mu_w[a], sd = tb.sg_w[a], mo = tb.nm_w[a], so = tb.ns_w[a], rho = tb.rho_w[a];
+    const double cc = (double)tb.cc[a];
+    const double cs = ((1 - rho) * so) + rho * (sigma_w + alpha * cc * 1.0);
+    double e1 = 0.0, e2 = 0.0;
+    for (uint32_t x = ci; x < n; x += 16) {  // the same lanes read what they just wrote
+        const double w_mean = E[loc[rw.start + x]] + md;
+        e1 += ((1 - rho) * mo) + rho * cc * alpha * w_mean;
+        e2 += cs;
+    }
+    e1 = sum16(e1);
+    e2 = sum16(e2);
+    const uint32_t tw = tb.t_w[a] + n;
+    const double nm = e1 / n, ns = e2 / n;
+    const double mu = nm / ns;
+    double sigma = 1 / ns;
+    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+    const bool ok = !(std::isnan(mu) || std::isinf(mu));
+    if (ci == 0) {
+        tb.t_w[a] = tw;
+        tb.rho_w[a] = pow((double)(1 + tw), -0.5);
+        tb.nm_w[a] = nm;
+        tb.ns_w[a] = ns;
+        tb.sg_w[a] = sigma;
+        tb.mu_w[a] = ok ? mu : md;
+    }
+    if (!ok) return;  // the reference reverts the mean and leaves e, t alone
+    for (uint32_t x = ci; x < n; x += 16) {
+        const uint32_t c = loc[rw.start + x];
+        E[c] += md - mu;
+        T[c] += sigma - sd;
+    }
+}
+
+// update_v (:712-800) of factor f for the rows of one orientation
+__global__ __launch_bounds__(256) void k_update_v(const VRow* __restrict__ rows, uint32_t nrows,
+                                                   const uint32_t* __restrict__ loc, const uint32_t* __restrict__ part,
+                                                   uint32_t f, VBTables tb, double* __restrict__ E,
+                                                   double* __restrict__ T) {
+    const uint32_t ri = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int ci = threadIdx.x & 15;
+    if (ri >= nrows) return;
+    const VRow rw = rows[ri];
+    const uint32_t a = rw.attr, n = rw.len;
+    const size_t off = (size_t)f * tb.p;
+    double* __restrict__ v = tb.mu_v + off;
+    double* __restrict__ s = tb.sg_v + off;
+    const double alpha = tb.scal->alpha, svg = tb.sigma_v[f];
+    const double md = v[a], sd = s[a], mo = tb.nm_v[off + a], so = tb.ns_v[off + a], rho = tb.rho_v[a];
+    const double cc = (double)tb.cc[a];
+    double e1 = 0.0, e2 = 0.0;
+    for (uint32_t x = ci; x < n; x += 16) {
+        const uint32_t q = rw.start + x, pa = part[q];
+        const double h = v[pa], h1 = s[pa], e = E[loc[q]];
+        const double v_mean = h * (e + md * h);
+        const double vss = h * h + h1;
+        e2 += (1 - rho) * so + rho * (svg + alpha * cc * vss);
+        e1 += ((1 - rho) * mo) + rho * cc * alpha * v_mean;
+    }
+    e1 = sum16(e1);
+    e2 = sum16(e2);
+    const double nm = e1 / n, ns = e2 / n;
+    const double mu = nm / ns;
+    double sigma = 1 / ns;
+    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+    const bool ok = !(std::isnan(mu) || std::isinf(mu));
+    if (ci == 0) {
+        tb.nm_v[off + a] = nm;
+        tb.ns_v[off + a] = ns;
+        s[a] = sigma;
+        v[a] = ok ? mu : md;
+        if (f == 0) tb.t_v[a] += n;  // the caller's count (:447-450)
+    }
+    if (!ok) return;
+    const double dmu = md - mu, ds = sigma - sd, dm2 = mu * mu - md * md;
+    for (uint32_t x = ci; x < n; x += 16) {
+        const uint32_t q = rw.start + x, pa = part[q];
+        const double h = v[pa], h1 = s[pa], h2 = h * h;
+        const uint32_t c = loc[q];
+        E[c] += h * dmu;
+        double t = T[c];
+        t += (h1 + h2) * ds;
+        t += h1 * dm2;
+        T[c] = t;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rho_v(VBTables tb) {
+    const uint32_t a = blockIdx.x * 256 + threadIdx.x;
+    if (a < tb.p) tb.rho_v[a] = pow((double)(1 + tb.t_v[a]), -0.5);
+}
+
+// alpha's sum of e^2 + t over the batch, 1024 cases per block
+__global__ __launch_bounds__(256) void k_alpha_partial(const double* __restrict__ E, const double* __restrict__ T,
+                                                        uint32_t B, double* __restrict__ part) {
+    __shared__ double red[256];
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t c = blockIdx.x * 1024 + threadIdx.x * 4 + u;
+        if (c < B) acc += E[c] * E[c] + T[c];
+    }
+    acc = block_sum256(acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+// sum over every attribute of mean^2 + variance: row r < K = factor r, r == K = bias
+__global__ __launch_bounds__(256) void k_sig_partial(VBTables tb, double* __restrict__ part, uint32_t nchunk) {
+    __shared__ double red[256];
+    const uint32_t r = blockIdx.y, c = blockIdx.x;
+    const double* m = r < tb.K ? tb.mu_v + (size_t)r * tb.p : tb.mu_w;
+    const double* v = r < tb.K ? tb.sg_v + (size_t)r * tb.p : tb.sg_w;
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const uint32_t a = c * 2048 + u * 256 + threadIdx.x;
+        if (a < tb.p) acc += m[a] * m[a] + v[a];
+    }
+    acc = block_sum256(acc, red);
+    if (threadIdx.x == 0) part[(size_t)r * nchunk + c] = acc;
+}
+
+// the blends of :523-580; a NaN / inf alpha reverts and skips the rest, as the reference returns
+__global__ __launch_bounds__(256) void k_hyper_final(const double* __restrict__ apart, uint32_t nab,
+                                                      const double* __restrict__ spart, uint32_t nchunk, uint32_t B,
+                                                      VBTables tb) {
+    __shared__ double red[256];
+    __shared__ int skip;
+    double acc = 0.0;
+    for (uint32_t i = threadIdx.x; i < nab; i += 256) acc += apart[i];
+    acc = block_sum256(acc, red);
+    VBScal& s = *tb.scal;
+    const double rho0 = s.rho0;
+    if (threadIdx.x == 0) {
+        const double alpha = (1 - rho0) * s.alpha + rho0 * ((double)B / acc);
+        skip = std::isnan(alpha) || std::isinf(alpha);
+        if (skip)
+            s.n_skip += 1;
+        else
+            s.alpha = alpha;
+    }
+    __syncthreads();
+    if (skip) return;
+    const double pd = (double)tb.p;
+    for (uint32_t r = threadIdx.x; r <= tb.K; r += 256) {
+        double t = 0.0;
+        for (uint32_t c = 0; c < nchunk; ++c) t += spart[(size_t)r * nchunk + c];
+        if (r < tb.K)
+            tb.sigma_v[r] = (1 - rho0) * tb.sigma_v[r] + rho0 * (pd / t);
+        else
+            red[0] = t;  // bias sum, read by thread 0 below
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s.sigma_0 = (1 - rho0) * s.sigma_0 + rho0 * (1.0 / (s.mu0 * s.mu0 + s.sg0));
+        s.sigma_w = (1 - rho0) * s.sigma_w + rho0 * (pd / red[0]);
+        s.t_w0 += 1;
+        s.rho0 = pow((double)(1 + s.t_w0), -0.5);
+    }
+}
+
+// test predictions: 16 lanes per case, 256 cases per block
+__global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ti,
+                                               const double* __restrict__ tr, uint64_t n, uint32_t I,
+                                               const double* __restrict__ muT, VBTables tb, uint32_t Kp, double lo,
+                                               double hi, double* __restrict__ pred, double* __restrict__ part) {
+    __shared__ double red[256];
+    const int g = threadIdx.x >> 4, ci = threadIdx.x & 15;
+    const uint32_t nb = Kp / 16;
+    const double mu0 = tb.scal->mu0;
+    double se = 0.0;
+    for (int m = 0; m < 16; ++m) {
+        const uint64_t c = (uint64_t)blockIdx.x * 256 + g + 16 * m;
+        if (c >= n) break;  // uniform per group
+        const uint32_t u = tu[c], it = I + ti[c];
+        double d = 0.0;
+        for (uint32_t b = 0; b < nb; ++b) d += muT[(size_t)u * Kp + 16 * b + ci] * muT[(size_t)it * Kp + 16 * b + ci];
+        d = sum16(d);
+        double p = ((d + tb.mu_w[u]) + tb.mu_w[it]) + mu0;
+        p = (p < hi) ? p : hi;  // std::min(max_target, p), std::max(min_target, p)
+        p = (lo < p) ? p : lo;
+        if (ci == 0) {
+            pred[c] = p;
+            const double err = p - (double)(float)tr[c];
+            se += err * err;
+        }
+    }
+    se = block_sum256(se, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = se;
+}
+
+}  // namespace
+
+hipError_t vbo_transpose(const double* src, double* dst, uint32_t K, uint32_t Kp, uint32_t p, hipStream_t st) {
+    if (p == 0 || K == 0) return hipSuccess;
+    k_transpose<<<dim3((p + 31) / 32, (K + 31) / 32), 256, 0, st>>>(src, dst, K, Kp, p);
+    return hipGetLastError();
+}
+
+hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* loc, const uint32_t* part, const float* r,
+                       const double* muT, const double* sgT, const VBTables& tb, uint32_t Kp, double* E, double* T,
+                       hipStream_t st) {
+    if (nrows == 0) return hipSuccess;
+    if (Kp > 16 * KBMAX) return hipErrorInvalidValue;
+    k_predict<<<(nrows + 15) / 16, 256, 0, st>>>(rows, nrows, loc, part, r, muT, sgT, tb, Kp, E, T);
+    return hipGetLastError();
+}
+
+hipError_t vbo_update_w0(const double* E, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
+    if (B == 0) return hipErrorInvalidValue;
+    const uint32_t nblk = (B + 1023) / 1024;
+    k_w0_partial<<<nblk, 256, 0, st>>>(E, B, tb, part);
+    k_w0_final<<<1, 256, 0, st>>>(part, nblk, B, tb);
+    return hipGetLastError();
+}
+
+hipError_t vbo_update_w(const VRow* rows, uint32_t nrows, const uint32_t* loc, int apply_w0, const VBTables& tb,
+                        double* E, double* T, hipStream_t st) {
+    if (nrows == 0) return hipSuccess;
+    k_update_w<<<(nrows + 15) / 16, 256, 0, st>>>(rows, nrows, loc, apply_w0, tb, E, T);
+    return hipGetLastError();
+}
+
+hipError_t vbo_update_v(const VRow* rows, uint32_t nrows, const uint32_t* loc, const uint32_t* part, uint32_t f,
+                        const VBTables& tb, double* E, double* T, hipStream_t st) {
+    if (nrows == 0) return hipSuccess;
+    k_update_v<<<(nrows + 15) / 16, 256, 0, st>>>(rows, nrows, loc, part, f, tb, E, T);
+    return hipGetLastError();
+}
+
+hipError_t vbo_hyper(const double* E, const double* T, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
+    k_rho_v<<<(tb.p + 255) / 256, 256, 0, st>>>(tb);
+    const uint32_t nab = (B + 1023) / 1024, nchunk = (tb.p + 2047) / 2048;
+    double* spart = part + nab + 8;
+    k_alpha_partial<<<nab, 256, 0, st>>>(E, T, B, part);
+    k_sig_partial<<<dim3(nchunk, tb.K + 1), 256, 0, st>>>(tb, spart, nchunk);
+    k_hyper_final<<<1, 256, 0, st>>>(part, nab, spart, nchunk, B, tb);
+    return hipGetLastError();
+}
+
+hipError_t vbo_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t n, uint32_t I,
+                    const double* muT, const VBTables& tb, uint32_t Kp, double lo, double hi, double* pred,
+                    double* part, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    k_test<<<(uint32_t)((n + 255) / 256), 256, 0, st>>>(tu, ti, tr, n, I, muT, tb, Kp, lo, hi, pred, part);
+    return hipGetLastError();
+}
+
+}  // namespace sbmf

@@ -20,10 +20,10 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import (F32, F64, QUIRKS_BIAS2, QUIRKS_BIAS22, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
+from ._lib import (F32, F64, METHOD_MCMC, METHOD_VB, QUIRKS_BIAS2, QUIRKS_BIAS22, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
                    SBMF_E_COMM, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_NOMEM, SBMF_E_STATE, SBMF_OK)
 
-__all__ = ["FMLearnSBPMF", "Data", "SBMFError", "load_triples", "load_libfm", "config_default",
+__all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "config_default",
            "RNG_REFERENCE", "RNG_PHILOX", "QUIRKS_FINAL", "QUIRKS_SBPMF2", "QUIRKS_NONE",
            "QUIRKS_BIAS2", "QUIRKS_BIAS22", "F64", "F32"]
 
@@ -121,8 +121,12 @@ class FMLearnSBPMF:
 
     def __init__(self, num_factor=20, num_iter=100, seed=1, rng="ref", quirks="final", precision="f64", burnin=0,
                  device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, row_kernel=0,
-                 stream_threshold=0, split_chunk=0, tune=0, **hyper):
+                 stream_threshold=0, split_chunk=0, tune=0, method="mcmc", vb_batches=0, **hyper):
         self.cfg = config_default()
+        if method not in ("mcmc", "vb", "vb_online"):
+            raise ValueError("method must be mcmc or vb")
+        self.cfg.method = METHOD_VB if method in ("vb", "vb_online") else METHOD_MCMC
+        self.cfg.vb_batches = vb_batches
         self.cfg.num_factor = num_factor
         self.cfg.num_iter = num_iter
         self.cfg.burnin = burnin
@@ -254,6 +258,18 @@ class FMLearnSBPMF:
             self.close()
         except Exception:
             pass
+
+
+class FMLearnVBOnline(FMLearnSBPMF):
+    """Online variational Bayes learner (the reference's fm_learn_vb_online,
+    `bin/libFM -method vb_online`; src/libfm/src/fm_learn_vb_online.h).
+    ``learn(sweeps=n)`` runs n epochs of 30 mini-batches; ``rmse_trajectory``
+    holds the per-epoch test RMSE of the posterior-mean prediction,
+    ``factors()`` / ``biases()`` the posterior means, ``hyper()["tau"]`` alpha."""
+
+    def __init__(self, num_factor=8, num_iter=100, seed=1, rng="ref", device=0, vb_batches=0, **kw):
+        super().__init__(num_factor=num_factor, num_iter=num_iter, seed=seed, rng=rng, device=device, method="vb",
+                         vb_batches=vb_batches, **kw)
 
 
 def comm_unique_id():

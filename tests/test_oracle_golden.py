@@ -28,3 +28,14 @@ def test_oracle_dims_follow_reference_rule(ragged):
     o = oracle.run(tr, te, K=4, iters=1, seed=1, want_factors=False)
     assert o["num_users"] == max(tr[0].max(), te[0].max()) + 1
     assert o["num_items"] == max(tr[1].max(), te[1].max()) + 1
+
+
+@pytest.mark.parametrize("data,K,seed,epochs", [("ml100k", 8, 1, 10), ("ml100k", 20, 7, 5), ("ragged", 8, 2, 20)])
+def test_vbo_oracle_bitwise_equals_reference(data, K, seed, epochs, ml100k, ragged):
+    """Online VB (-method vb_online): the oracle (vbo_oracle.c) against the
+    reference learner itself (fm_learn_vb_online*.h compiled unmodified, driven
+    by oracle/ref_vbo_harness.cpp): every per-epoch test RMSE identical."""
+    tr, te = ml100k if data == "ml100k" else ragged
+    gold = golden_rmse("ref_vbo_%s_k%d_s%d_e%d.txt" % (data, K, seed, epochs))
+    o = oracle.run_vbo(tr, te, K=K, epochs=epochs, seed=seed, want_params=False)
+    assert np.array_equal(o["rmse"], gold), np.abs(o["rmse"] - gold).max()
