@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -62,6 +63,13 @@ struct DBuf {
 template <typename U>
 inline void upload(DBuf& d, const std::vector<U>& h, hipStream_t st) {
     d.alloc(h.size() * sizeof(U));
+    if (!h.empty()) HIPCHK(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(U), hipMemcpyHostToDevice, st));
+}
+
+// per-epoch staging: keeps the allocation when it is large enough
+template <typename U>
+inline void upload_grow(DBuf& d, const std::vector<U>& h, hipStream_t st) {
+    d.ensure(std::max<size_t>(h.size(), 1) * sizeof(U));
     if (!h.empty()) HIPCHK(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(U), hipMemcpyHostToDevice, st));
 }
 

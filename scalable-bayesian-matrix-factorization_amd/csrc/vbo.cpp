@@ -37,15 +37,16 @@ struct VBLearner {
     // host data
     std::vector<uint32_t> tu, ti, su, si;
     std::vector<double> tr, sr;
-    std::vector<uint32_t> shuffle, bid, bloc, keycnt;
+    std::vector<uint32_t> shuffle, bid, upos, ipos, keycnt;
     // this epoch's batch layout
     std::vector<VRow> urows, irows;
-    std::vector<uint32_t> urow0, irow0, bsize, uloc, upart, iloc, ipart;
+    std::vector<uint32_t> urow0, irow0, utask0, itask0, bsize, bbase, u2i, upart, i2u, ipart;
+    std::vector<VTask> utasks, itasks;
     std::vector<float> ur;
     // device
     DBuf d_mu_v, d_sg_v, d_nm_v, d_ns_v, d_mu_w, d_sg_w, d_nm_w, d_ns_w, d_rho_w, d_rho_v, d_t_w, d_t_v, d_cc;
-    DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_E, d_T, d_part;
-    DBuf d_urows, d_irows, d_uloc, d_upart, d_iloc, d_ipart, d_ur;
+    DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_ETu, d_ETv, d_part;
+    DBuf d_urows, d_irows, d_u2i, d_upart, d_i2u, d_ipart, d_ur, d_utasks, d_itasks;
     DBuf d_tu, d_ti, d_tr, d_pred, d_tpart;
     VBTables tb{};
     double last_rmse = NAN, last_alpha = NAN;
@@ -143,8 +144,8 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     d_sgT.alloc((size_t)p * Kp * sizeof(double));
     HIPCHK(hipMemsetAsync(d_muT.p, 0, d_muT.bytes, st));
     HIPCHK(hipMemsetAsync(d_sgT.p, 0, d_sgT.bytes, st));
-    d_E.alloc((size_t)S * sizeof(double));
-    d_T.alloc((size_t)S * sizeof(double));
+    d_ETu.alloc((size_t)N * sizeof(double2));  // {e, t} per case, user-grouped epoch order
+    d_ETv.alloc((size_t)N * sizeof(double2));  // item-grouped epoch order
     d_part.alloc(vbo_scratch_doubles(S, K, p) * sizeof(double));
     upload(d_tu, su, st);
     upload(d_ti, si, st);
@@ -192,15 +193,17 @@ void VBLearner::build_layout() {
         }
     }
     bid.resize(N);
-    bloc.resize(N);
     bsize.assign(NB, 0);
     for (uint32_t l = 0; l < N; ++l) {
         const uint32_t b = (uint32_t)std::ceil((double)shuffle[l] / S) - 1;  // :175
         bid[l] = b;
-        bloc[l] = bsize[b]++;
+        bsize[b]++;
     }
+    bbase.assign(NB + 1, 0);  // a batch's cases are entries [bbase[b], bbase[b+1]) of either order
+    for (uint32_t b = 0; b < NB; ++b) bbase[b + 1] = bbase[b] + bsize[b];
     auto group = [&](uint32_t R, bool users, std::vector<VRow>& rows, std::vector<uint32_t>& row0,
-                     std::vector<uint32_t>& loc, std::vector<uint32_t>& part) {
+                     std::vector<VTask>& tasks, std::vector<uint32_t>& task0, std::vector<uint32_t>& pos,
+                     std::vector<uint32_t>& part) {
         keycnt.assign((size_t)NB * R + 1, 0);
         for (uint32_t l = 0; l < N; ++l) keycnt[(size_t)bid[l] * R + (users ? tu[l] : ti[l]) + 1]++;
         rows.clear();
@@ -220,58 +223,92 @@ void VBLearner::build_layout() {
             rw.start = off;
             off += rw.len;
         }
-        loc.resize(N);
+        // per batch: rows ordered by lane-group size (stable), packed into
+        // 256-thread tasks of 256 / G rows each
+        auto lg_of = [](uint32_t n) {
+            uint32_t lg = 2;
+            while (lg < 8 && (1u << lg) < n) ++lg;
+            return lg;
+        };
+        tasks.clear();
+        task0.assign(NB + 1, 0);
+        for (uint32_t b = 0; b < NB; ++b) {
+            task0[b] = (uint32_t)tasks.size();
+            auto first = rows.begin() + row0[b], last = rows.begin() + row0[b + 1];
+            std::stable_sort(first, last, [&](const VRow& x, const VRow& y) { return lg_of(x.len) > lg_of(y.len); });
+            for (uint32_t r = row0[b]; r < row0[b + 1];) {
+                const uint32_t lg = lg_of(rows[r].len);
+                uint32_t m = 0;
+                while (r + m < row0[b + 1] && m < (256u >> lg) && lg_of(rows[r + m].len) == lg) ++m;
+                tasks.push_back(VTask{r, m, lg, 0});
+                r += m;
+            }
+        }
+        task0[NB] = (uint32_t)tasks.size();
+        pos.resize(N);
         part.resize(N);
         if (users) ur.resize(N);
         for (uint32_t l = 0; l < N; ++l) {
             const size_t k = (size_t)bid[l] * R + (users ? tu[l] : ti[l]);
-            const uint32_t pos = keycnt[k]++;
-            loc[pos] = bloc[l];
-            part[pos] = users ? I + ti[l] : tu[l];
-            if (users) ur[pos] = (float)tr[l];
+            const uint32_t q = keycnt[k]++;
+            pos[l] = q;
+            part[q] = users ? I + ti[l] : tu[l];
+            if (users) ur[q] = (float)tr[l];
         }
     };
-    group(I, true, urows, urow0, uloc, upart);
-    group(J, false, irows, irow0, iloc, ipart);
+    group(I, true, urows, urow0, utasks, utask0, upos, upart);
+    group(J, false, irows, irow0, itasks, itask0, ipos, ipart);
+    u2i.resize(N);
+    i2u.resize(N);
+    for (uint32_t l = 0; l < N; ++l) {
+        u2i[upos[l]] = ipos[l];
+        i2u[ipos[l]] = upos[l];
+    }
 }
 
 void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
     for (uint32_t it = 0; it < epochs; ++it) {
         const auto h0 = std::chrono::steady_clock::now();
         build_layout();
-        upload(d_urows, urows, st);
-        upload(d_irows, irows, st);
-        upload(d_uloc, uloc, st);
-        upload(d_upart, upart, st);
-        upload(d_ur, ur, st);
-        upload(d_iloc, iloc, st);
-        upload(d_ipart, ipart, st);
+        upload_grow(d_urows, urows, st);
+        upload_grow(d_irows, irows, st);
+        upload_grow(d_u2i, u2i, st);
+        upload_grow(d_upart, upart, st);
+        upload_grow(d_ur, ur, st);
+        upload_grow(d_i2u, i2u, st);
+        upload_grow(d_ipart, ipart, st);
+        upload_grow(d_utasks, utasks, st);
+        upload_grow(d_itasks, itasks, st);
         HIPCHK(hipStreamSynchronize(st));
         ms_layout = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
         n_launch = 0;
         HIPCHK(hipEventRecord(ev[0], st));
-        double* E = d_E.as<double>();
-        double* T = d_T.as<double>();
+        double2* ETu = d_ETu.as<double2>();
+        double2* ETv = d_ETv.as<double2>();
         double* part = d_part.as<double>();
         const VRow* ur_ = d_urows.as<VRow>();
         const VRow* ir_ = d_irows.as<VRow>();
         for (uint32_t b = 0; b < NB; ++b) {
             const uint32_t B = bsize[b];
-            const uint32_t nu = urow0[b + 1] - urow0[b], ni = irow0[b + 1] - irow0[b];
+            const uint32_t nu = urow0[b + 1] - urow0[b];
             HIPCHK(vbo_transpose(tb.mu_v, d_muT.as<double>(), K, Kp, p, st));
             HIPCHK(vbo_transpose(tb.sg_v, d_sgT.as<double>(), K, Kp, p, st));
-            HIPCHK(vbo_predict(ur_ + urow0[b], nu, d_uloc.as<uint32_t>(), d_upart.as<uint32_t>(), d_ur.as<float>(),
-                               d_muT.as<double>(), d_sgT.as<double>(), tb, Kp, E, T, st));
-            HIPCHK(vbo_update_w0(E, B, tb, part, st));
-            HIPCHK(vbo_update_w(ur_ + urow0[b], nu, d_uloc.as<uint32_t>(), 1, tb, E, T, st));
-            HIPCHK(vbo_update_w(ir_ + irow0[b], ni, d_iloc.as<uint32_t>(), 0, tb, E, T, st));
+            HIPCHK(vbo_predict(ur_ + urow0[b], nu, d_upart.as<uint32_t>(), d_ur.as<float>(), d_muT.as<double>(),
+                               d_sgT.as<double>(), tb, Kp, ETu, st));
+            HIPCHK(vbo_update_w0(ETu + bbase[b], B, tb, part, st));
+            const VTask* ut = d_utasks.as<VTask>() + utask0[b];
+            const VTask* it_ = d_itasks.as<VTask>() + itask0[b];
+            const uint32_t nut = utask0[b + 1] - utask0[b], nit = itask0[b + 1] - itask0[b];
+            // every pass reads its own order and writes the other one: users ETu -> ETv, items ETv -> ETu
+            const uint32_t* u2i_ = d_u2i.as<uint32_t>();
+            const uint32_t* i2u_ = d_i2u.as<uint32_t>();
+            HIPCHK(vbo_update_w(ut, nut, ur_, u2i_, 1, tb, ETu, ETv, st));
+            HIPCHK(vbo_update_w(it_, nit, ir_, i2u_, 0, tb, ETv, ETu, st));
             for (uint32_t f = 0; f < K; ++f) {
-                HIPCHK(vbo_update_v(ur_ + urow0[b], nu, d_uloc.as<uint32_t>(), d_upart.as<uint32_t>(), f, tb, E, T,
-                                    st));
-                HIPCHK(vbo_update_v(ir_ + irow0[b], ni, d_iloc.as<uint32_t>(), d_ipart.as<uint32_t>(), f, tb, E, T,
-                                    st));
+                HIPCHK(vbo_update_v(ut, nut, ur_, u2i_, d_upart.as<uint32_t>(), f, tb, ETu, ETv, st));
+                HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st));
             }
-            HIPCHK(vbo_hyper(E, T, B, tb, part, st));
+            HIPCHK(vbo_hyper(ETu + bbase[b], B, tb, part, st));
             n_launch += 2 * K + 12;
         }
         HIPCHK(hipEventRecord(ev[1], st));

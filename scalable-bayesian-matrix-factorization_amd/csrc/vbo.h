@@ -20,7 +20,8 @@
 namespace sbmf {
 
 // One attribute's cases inside one batch: entries [start, start + len) of
-// the orientation's case arrays (batch-local case index, partner attribute).
+// the orientation's case arrays (partner attribute, position of the case in
+// the other orientation's order), which hold the epoch's cases batch-major.
 struct VRow {
     uint32_t attr, start, len, pad;
 };
@@ -48,20 +49,26 @@ struct VBTables {
 hipError_t vbo_transpose(const double* src, double* dst, uint32_t K, uint32_t Kp, uint32_t p, hipStream_t st);
 // e = r - prediction and t = its variance for every case of a batch, driven
 // by the batch's user rows (fm_learn_vb_online.h:80-310)
-hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* loc, const uint32_t* part, const float* r,
-                       const double* muT, const double* sgT, const VBTables& tb, uint32_t Kp, double* E, double* T,
-                       hipStream_t st);
+hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* part, const float* r, const double* muT,
+                       const double* sgT, const VBTables& tb, uint32_t Kp, double2* ET, hipStream_t st);
 // update_w0 (:586-633): the global bias blend; its deltas are applied to e / t
 // by the user pass of vbo_update_w (apply_w0 = 1)
-hipError_t vbo_update_w0(const double* E, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
+hipError_t vbo_update_w0(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
+// One 256-thread block of an update pass: rows [row0, row0 + nrows) of the
+// orientation's row list, each owned by 2^lg lanes (256 >> lg rows at most).
+struct VTask {
+    uint32_t row0, nrows, lg, pad;
+};
 // update_w (:635-710) over the rows of one orientation
-hipError_t vbo_update_w(const VRow* rows, uint32_t nrows, const uint32_t* loc, int apply_w0, const VBTables& tb,
-                        double* E, double* T, hipStream_t st);
+// (ETin in the rows' own order, ETout in the other order: ETout[xperm[q]])
+hipError_t vbo_update_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm, int apply_w0,
+                        const VBTables& tb, const double2* ETin, double2* ETout, hipStream_t st);
 // update_v (:712-800) of factor f over the rows of one orientation
-hipError_t vbo_update_v(const VRow* rows, uint32_t nrows, const uint32_t* loc, const uint32_t* part, uint32_t f,
-                        const VBTables& tb, double* E, double* T, hipStream_t st);
+hipError_t vbo_update_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm,
+                        const uint32_t* part, uint32_t f, const VBTables& tb, const double2* ETin, double2* ETout,
+                        hipStream_t st);
 // step sizes of update_v (:447-453) and the hyperparameter blends (:523-580)
-hipError_t vbo_hyper(const double* E, const double* T, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
+hipError_t vbo_hyper(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
 // test predictions clamped to [lo, hi] and their squared errors per 256-case block
 hipError_t vbo_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t n, uint32_t I,
                     const double* muT, const VBTables& tb, uint32_t Kp, double lo, double hi, double* pred,

@@ -2,11 +2,20 @@
 // (`sbmf -method vb`; the reference's fm_learn_vb_online on rating data).
 //
 // The work unit is an attribute row of one batch: a user (or an item) and the
-// batch's cases that carry it.  16 lanes own a row (16 rows per 256-thread
-// block): the row's natural-parameter sums are 16-lane reductions and its
-// cases are visited 16 at a time.  A case's residual e and variance term t
-// live in the batch-local arrays E, T; every case belongs to exactly one
-// user row and one item row, so the rows of one pass never share a case.
+// batch's cases that carry it.  A group of G lanes owns a row, G the power of
+// two (4..256) that covers the row's cases one per lane, so a 256-thread
+// block holds 64 four-case user rows or one popular item; rows longer than
+// 4 x 256 loop.  Each block reads a task {first row, rows, log2 G} built on
+// the host.  A lane keeps its cases' values in registers between the
+// row's two passes (sums, then residual updates).  The row's
+// natural-parameter sums are fixed-order group reductions.  A case's
+// residual e and variance term t travel as one 16-byte {e, t} record in two
+// copies: ETu in the epoch's user-grouped order and ETv in its item-grouped
+// order.  A pass reads its own order (consecutive lanes, consecutive
+// records) and writes the other order through the case's position there
+// (xperm), which is the order the next pass reads -- the same scatter
+// scheme as the Gibbs half-sweeps.  Every case belongs to exactly one user
+// row and one item row, so the rows of one pass never share a case.
 // In an update_v pass the partner values (item factors for user rows, the
 // fresh user factors for item rows) are read from the factor column f of the
 // f-major tables, which stays in L2.  Every reduction has a fixed order, so
@@ -38,6 +47,8 @@ __device__ __forceinline__ double sum16(double x) {
 }
 
 // fixed-order block sum of 256 threads (every thread gets the total)
+__device__ __forceinline__ double block_sum256(double x, double* red);
+
 __device__ __forceinline__ double block_sum256(double x, double* red) {
     red[threadIdx.x] = x;
     __syncthreads();
@@ -71,10 +82,10 @@ __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ sr
 //   e = r - (sum_f v_u v_i + w_u + w_i + mu_0'),
 //   t = sum_f (s_u s_i + s_u v_i^2 + s_i v_u^2) + s^w_u + s^w_i + sigma_0'.
 __global__ __launch_bounds__(256) void k_predict(const VRow* __restrict__ rows, uint32_t nrows,
-                                                  const uint32_t* __restrict__ loc, const uint32_t* __restrict__ part,
+                                                  const uint32_t* __restrict__ part,
                                                   const float* __restrict__ r, const double* __restrict__ muT,
                                                   const double* __restrict__ sgT, VBTables tb, uint32_t Kp,
-                                                  double* __restrict__ E, double* __restrict__ T) {
+                                                  double2* __restrict__ ET) {
     const uint32_t ri = blockIdx.x * 16 + (threadIdx.x >> 4);
     const int ci = threadIdx.x & 15;
     if (ri >= nrows) return;  // whole 16-lane groups
@@ -103,16 +114,17 @@ __global__ __launch_bounds__(256) void k_predict(const VRow* __restrict__ rows, 
         d = sum16(d);
         tv = sum16(tv);
         if (ci == 0) {
-            const uint32_t c = loc[q];
-            E[c] = (double)r[q] - (((d + wu) + tb.mu_w[pa]) + mu0);
-            T[c] = ((tv + swu) + tb.sg_w[pa]) + sg0;
+            double2 o;
+            o.x = (double)r[q] - (((d + wu) + tb.mu_w[pa]) + mu0);
+            o.y = ((tv + swu) + tb.sg_w[pa]) + sg0;
+            ET[q] = o;
         }
     }
 }
 
 // update_w0 (:586-633): partial sums of the per-case natural mean
 // (1 - rho0) nm0 + rho0 N alpha (e + mu0'), 1024 cases per block
-__global__ __launch_bounds__(256) void k_w0_partial(const double* __restrict__ E, uint32_t B, VBTables tb,
+__global__ __launch_bounds__(256) void k_w0_partial(const double2* __restrict__ ET, uint32_t B, VBTables tb,
                                                      double* __restrict__ part) {
     __shared__ double red[256];
     const VBScal s = *tb.scal;
@@ -121,7 +133,7 @@ __global__ __launch_bounds__(256) void k_w0_partial(const double* __restrict__ E
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const uint32_t c = blockIdx.x * 1024 + threadIdx.x * 4 + u;
-        if (c < B) acc += cmu + kmu * (E[c] + s.mu0);
+        if (c < B) acc += cmu + kmu * (ET[c].x + s.mu0);
     }
     acc = block_sum256(acc, red);
     if (threadIdx.x == 0) part[blockIdx.x] = acc;
@@ -148,36 +160,70 @@ __global__ __launch_bounds__(256) void k_w0_final(const double* __restrict__ par
     }
 }
 
+// Reduction over a group of G lanes (G = 4..256, block-uniform): butterfly
+// shuffles inside a wave, an LDS tree for 128 / 256; lane 0's value is
+// returned to every lane, so the result is one fixed-order sum.
+__device__ __forceinline__ double gsum(double x, int G, double* red) {
+    if (G <= 64) {
+        for (int m = G >> 1; m > 0; m >>= 1) x += __shfl_xor(x, m, G);
+        return __shfl(x, 0, G);
+    }
+    const int base = threadIdx.x & ~(G - 1), li = threadIdx.x & (G - 1);
+    red[threadIdx.x] = x;
+    __syncthreads();
+    for (int m = G >> 1; m > 0; m >>= 1) {
+        if (li < m) red[threadIdx.x] += red[threadIdx.x + m];
+        __syncthreads();
+    }
+    const double t = red[base];
+    __syncthreads();
+    return t;
+}
+
+constexpr int MC = 4;  // cases a lane keeps in registers between the two passes of a row
+
 // update_w (:635-710) for the rows of one orientation.  apply_w0: first add
 // update_w0's deltas to the row's cases (the user pass touches every case once).
-__global__ __launch_bounds__(256) void k_update_w(const VRow* __restrict__ rows, uint32_t nrows,
-                                                   const uint32_t* __restrict__ loc, int apply_w0, VBTables tb,
-                                                   double* __restrict__ E, double* __restrict__ T) {
-    const uint32_t ri = blockIdx.x * 16 + (threadIdx.x >> 4);
-    const int ci = threadIdx.x & 15;
-    if (ri >= nrows) return;
-    const VRow rw = rows[ri];
-    const uint32_t a = rw.attr, n = rw.len;
+__global__ __launch_bounds__(256) void k_update_w(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
+                                                   const uint32_t* __restrict__ xperm, int apply_w0, VBTables tb,
+                                                   const double2* __restrict__ ETin, double2* __restrict__ ETout) {
+    __shared__ double red[256];
+    const VTask tk = tasks[blockIdx.x];
+    const int G = 1 << tk.lg;
+    const uint32_t g = threadIdx.x >> tk.lg;
+    const int ci = threadIdx.x & (G - 1);
+    const bool live = g < tk.nrows;  // G >= 128 blocks hold one row: always live
+    const VRow rw = rows[tk.row0 + (live ? g : 0)];
+    const uint32_t a = rw.attr, n = live ? rw.len : 0;
     const double alpha = tb.scal->alpha, sigma_w = tb.scal->sigma_w;
-    if (apply_w0) {
-        const double dm = tb.scal->d_mu0, ds = tb.scal->d_sg0;
-        for (uint32_t x = ci; x < n; x += 16) {
-            const uint32_t c = loc[rw.start + x];
-            E[c] = E[c] + dm;
-            T[c] = T[c] + ds;
-        }
-    }
+    const double dm = apply_w0 ? tb.scal->d_mu0 : 0.0, ds = apply_w0 ? tb.scal->d_sg0 : 0.0;
     const double md = tb.mu_w[a], sd = tb.sg_w[a], mo = tb.nm_w[a], so = tb.ns_w[a], rho = tb.rho_w[a];
     const double cc = (double)tb.cc[a];
     const double cs = ((1 - rho) * so) + rho * (sigma_w + alpha * cc * 1.0);
+    double2 et[MC];
     double e1 = 0.0, e2 = 0.0;
-    for (uint32_t x = ci; x < n; x += 16) {  // the same lanes read what they just wrote
-        const double w_mean = E[loc[rw.start + x]] + md;
-        e1 += ((1 - rho) * mo) + rho * cc * alpha * w_mean;
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const uint32_t x = ci + j * G;
+        if (x < n) {
+            et[j] = ETin[rw.start + x];
+            if (apply_w0) {
+                et[j].x = et[j].x + dm;
+                et[j].y = et[j].y + ds;
+            }
+            e1 += ((1 - rho) * mo) + rho * cc * alpha * (et[j].x + md);
+            e2 += cs;
+        }
+    }
+    for (uint32_t x = ci + MC * G; x < n; x += G) {  // rows longer than MC * G
+        double e = ETin[rw.start + x].x;
+        if (apply_w0) e = e + dm;
+        e1 += ((1 - rho) * mo) + rho * cc * alpha * (e + md);
         e2 += cs;
     }
-    e1 = sum16(e1);
-    e2 = sum16(e2);
+    e1 = gsum(e1, G, red);
+    e2 = gsum(e2, G, red);
+    if (!live) return;  // after the last block-wide reduction
     const uint32_t tw = tb.t_w[a] + n;
     const double nm = e1 / n, ns = e2 / n;
     const double mu = nm / ns;
@@ -192,41 +238,78 @@ __global__ __launch_bounds__(256) void k_update_w(const VRow* __restrict__ rows,
         tb.sg_w[a] = sigma;
         tb.mu_w[a] = ok ? mu : md;
     }
-    if (!ok) return;  // the reference reverts the mean and leaves e, t alone
-    for (uint32_t x = ci; x < n; x += 16) {
-        const uint32_t c = loc[rw.start + x];
-        E[c] += md - mu;
-        T[c] += sigma - sd;
+    // the reference reverts a non-finite mean and leaves e, t alone (the w0 deltas stay)
+    const double dmu = ok ? md - mu : 0.0, dsg = ok ? sigma - sd : 0.0;
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const uint32_t x = ci + j * G;
+        if (x < n) {
+            double2 o = et[j];
+            if (ok) {
+                o.x += dmu;
+                o.y += dsg;
+            }
+            ETout[xperm[rw.start + x]] = o;
+        }
+    }
+    for (uint32_t x = ci + MC * G; x < n; x += G) {
+        double2 o = ETin[rw.start + x];
+        if (apply_w0) {
+            o.x = o.x + dm;
+            o.y = o.y + ds;
+        }
+        if (ok) {
+            o.x += dmu;
+            o.y += dsg;
+        }
+        ETout[xperm[rw.start + x]] = o;
     }
 }
 
 // update_v (:712-800) of factor f for the rows of one orientation
-__global__ __launch_bounds__(256) void k_update_v(const VRow* __restrict__ rows, uint32_t nrows,
-                                                   const uint32_t* __restrict__ loc, const uint32_t* __restrict__ part,
-                                                   uint32_t f, VBTables tb, double* __restrict__ E,
-                                                   double* __restrict__ T) {
-    const uint32_t ri = blockIdx.x * 16 + (threadIdx.x >> 4);
-    const int ci = threadIdx.x & 15;
-    if (ri >= nrows) return;
-    const VRow rw = rows[ri];
-    const uint32_t a = rw.attr, n = rw.len;
+__global__ __launch_bounds__(256) void k_update_v(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
+                                                   const uint32_t* __restrict__ xperm, const uint32_t* __restrict__ part,
+                                                   uint32_t f, VBTables tb, const double2* __restrict__ ETin,
+                                                   double2* __restrict__ ETout) {
+    __shared__ double red[256];
+    const VTask tk = tasks[blockIdx.x];
+    const int G = 1 << tk.lg;
+    const uint32_t g = threadIdx.x >> tk.lg;
+    const int ci = threadIdx.x & (G - 1);
+    const bool live = g < tk.nrows;
+    const VRow rw = rows[tk.row0 + (live ? g : 0)];
+    const uint32_t a = rw.attr, n = live ? rw.len : 0;
     const size_t off = (size_t)f * tb.p;
     double* __restrict__ v = tb.mu_v + off;
     double* __restrict__ s = tb.sg_v + off;
     const double alpha = tb.scal->alpha, svg = tb.sigma_v[f];
     const double md = v[a], sd = s[a], mo = tb.nm_v[off + a], so = tb.ns_v[off + a], rho = tb.rho_v[a];
     const double cc = (double)tb.cc[a];
+    double hh[MC], hs[MC];
+    double2 et[MC];
     double e1 = 0.0, e2 = 0.0;
-    for (uint32_t x = ci; x < n; x += 16) {
-        const uint32_t q = rw.start + x, pa = part[q];
-        const double h = v[pa], h1 = s[pa], e = E[loc[q]];
-        const double v_mean = h * (e + md * h);
-        const double vss = h * h + h1;
-        e2 += (1 - rho) * so + rho * (svg + alpha * cc * vss);
-        e1 += ((1 - rho) * mo) + rho * cc * alpha * v_mean;
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const uint32_t x = ci + j * G;
+        if (x < n) {
+            const uint32_t pa = part[rw.start + x];
+            hh[j] = v[pa];
+            hs[j] = s[pa];
+            et[j] = ETin[rw.start + x];
+            const double h = hh[j];
+            e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + hs[j]));
+            e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (et[j].x + md * h));
+        }
     }
-    e1 = sum16(e1);
-    e2 = sum16(e2);
+    for (uint32_t x = ci + MC * G; x < n; x += G) {
+        const uint32_t q = rw.start + x, pa = part[q];
+        const double h = v[pa], h1 = s[pa], e = ETin[q].x;
+        e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + h1));
+        e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (e + md * h));
+    }
+    e1 = gsum(e1, G, red);
+    e2 = gsum(e2, G, red);
+    if (!live) return;
     const double nm = e1 / n, ns = e2 / n;
     const double mu = nm / ns;
     double sigma = 1 / ns;
@@ -239,17 +322,33 @@ __global__ __launch_bounds__(256) void k_update_v(const VRow* __restrict__ rows,
         v[a] = ok ? mu : md;
         if (f == 0) tb.t_v[a] += n;  // the caller's count (:447-450)
     }
-    if (!ok) return;
-    const double dmu = md - mu, ds = sigma - sd, dm2 = mu * mu - md * md;
-    for (uint32_t x = ci; x < n; x += 16) {
-        const uint32_t q = rw.start + x, pa = part[q];
-        const double h = v[pa], h1 = s[pa], h2 = h * h;
-        const uint32_t c = loc[q];
-        E[c] += h * dmu;
-        double t = T[c];
-        t += (h1 + h2) * ds;
-        t += h1 * dm2;
-        T[c] = t;
+    // a non-finite mean: the reference returns before touching e, t -- forwarded unchanged
+    const double dmu = ok ? md - mu : 0.0, dsg = ok ? sigma - sd : 0.0, dm2 = ok ? mu * mu - md * md : 0.0;
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const uint32_t x = ci + j * G;
+        if (x < n) {
+            double2 o = et[j];
+            if (ok) {
+                const double h = hh[j], h1 = hs[j];
+                o.x += h * dmu;
+                o.y += (h1 + h * h) * dsg;
+                o.y += h1 * dm2;
+            }
+            ETout[xperm[rw.start + x]] = o;
+        }
+    }
+    for (uint32_t x = ci + MC * G; x < n; x += G) {
+        const uint32_t q = rw.start + x;
+        double2 o = ETin[q];
+        if (ok) {
+            const uint32_t pa = part[q];
+            const double h = v[pa], h1 = s[pa];
+            o.x += h * dmu;
+            o.y += (h1 + h * h) * dsg;
+            o.y += h1 * dm2;
+        }
+        ETout[xperm[q]] = o;
     }
 }
 
@@ -259,14 +358,14 @@ __global__ __launch_bounds__(256) void k_rho_v(VBTables tb) {
 }
 
 // alpha's sum of e^2 + t over the batch, 1024 cases per block
-__global__ __launch_bounds__(256) void k_alpha_partial(const double* __restrict__ E, const double* __restrict__ T,
-                                                        uint32_t B, double* __restrict__ part) {
+__global__ __launch_bounds__(256) void k_alpha_partial(const double2* __restrict__ ET, uint32_t B,
+                                                        double* __restrict__ part) {
     __shared__ double red[256];
     double acc = 0.0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const uint32_t c = blockIdx.x * 1024 + threadIdx.x * 4 + u;
-        if (c < B) acc += E[c] * E[c] + T[c];
+        if (c < B) acc += ET[c].x * ET[c].x + ET[c].y;
     }
     acc = block_sum256(acc, red);
     if (threadIdx.x == 0) part[blockIdx.x] = acc;
@@ -365,42 +464,42 @@ hipError_t vbo_transpose(const double* src, double* dst, uint32_t K, uint32_t Kp
     return hipGetLastError();
 }
 
-hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* loc, const uint32_t* part, const float* r,
-                       const double* muT, const double* sgT, const VBTables& tb, uint32_t Kp, double* E, double* T,
-                       hipStream_t st) {
+hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* part, const float* r, const double* muT,
+                       const double* sgT, const VBTables& tb, uint32_t Kp, double2* ET, hipStream_t st) {
     if (nrows == 0) return hipSuccess;
     if (Kp > 16 * KBMAX) return hipErrorInvalidValue;
-    k_predict<<<(nrows + 15) / 16, 256, 0, st>>>(rows, nrows, loc, part, r, muT, sgT, tb, Kp, E, T);
+    k_predict<<<(nrows + 15) / 16, 256, 0, st>>>(rows, nrows, part, r, muT, sgT, tb, Kp, ET);
     return hipGetLastError();
 }
 
-hipError_t vbo_update_w0(const double* E, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
+hipError_t vbo_update_w0(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
     if (B == 0) return hipErrorInvalidValue;
     const uint32_t nblk = (B + 1023) / 1024;
-    k_w0_partial<<<nblk, 256, 0, st>>>(E, B, tb, part);
+    k_w0_partial<<<nblk, 256, 0, st>>>(ET, B, tb, part);
     k_w0_final<<<1, 256, 0, st>>>(part, nblk, B, tb);
     return hipGetLastError();
 }
 
-hipError_t vbo_update_w(const VRow* rows, uint32_t nrows, const uint32_t* loc, int apply_w0, const VBTables& tb,
-                        double* E, double* T, hipStream_t st) {
-    if (nrows == 0) return hipSuccess;
-    k_update_w<<<(nrows + 15) / 16, 256, 0, st>>>(rows, nrows, loc, apply_w0, tb, E, T);
+hipError_t vbo_update_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm, int apply_w0,
+                        const VBTables& tb, const double2* ETin, double2* ETout, hipStream_t st) {
+    if (ntask == 0) return hipSuccess;
+    k_update_w<<<ntask, 256, 0, st>>>(tasks, rows, xperm, apply_w0, tb, ETin, ETout);
     return hipGetLastError();
 }
 
-hipError_t vbo_update_v(const VRow* rows, uint32_t nrows, const uint32_t* loc, const uint32_t* part, uint32_t f,
-                        const VBTables& tb, double* E, double* T, hipStream_t st) {
-    if (nrows == 0) return hipSuccess;
-    k_update_v<<<(nrows + 15) / 16, 256, 0, st>>>(rows, nrows, loc, part, f, tb, E, T);
+hipError_t vbo_update_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm,
+                        const uint32_t* part, uint32_t f, const VBTables& tb, const double2* ETin, double2* ETout,
+                        hipStream_t st) {
+    if (ntask == 0) return hipSuccess;
+    k_update_v<<<ntask, 256, 0, st>>>(tasks, rows, xperm, part, f, tb, ETin, ETout);
     return hipGetLastError();
 }
 
-hipError_t vbo_hyper(const double* E, const double* T, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
+hipError_t vbo_hyper(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
     k_rho_v<<<(tb.p + 255) / 256, 256, 0, st>>>(tb);
     const uint32_t nab = (B + 1023) / 1024, nchunk = (tb.p + 2047) / 2048;
     double* spart = part + nab + 8;
-    k_alpha_partial<<<nab, 256, 0, st>>>(E, T, B, part);
+    k_alpha_partial<<<nab, 256, 0, st>>>(ET, B, part);
     k_sig_partial<<<dim3(nchunk, tb.K + 1), 256, 0, st>>>(tb, spart, nchunk);
     k_hyper_final<<<1, 256, 0, st>>>(part, nab, spart, nchunk, B, tb);
     return hipGetLastError();
