@@ -19,12 +19,24 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "common.h"
 #include "rng.h"
 
 namespace sbmf {
+
+// One epoch's batch layout (host side), built by a worker thread while the
+// GPU runs the previous epoch, and its device copy.
+struct VBLayout {
+    std::vector<VRow> urows, irows;    // every batch's rows, batch-major
+    std::vector<VTask> utasks, itasks; // 256-thread tasks over those rows
+    std::vector<uint32_t> urow0, irow0, utask0, itask0, bsize, bbase;
+    std::vector<uint32_t> u2i, upart, i2u, ipart;  // [N] per entry of each order
+    std::vector<float> ur;                          // [N] target per user-order entry
+    DBuf d_urows, d_irows, d_utasks, d_itasks, d_u2i, d_upart, d_i2u, d_ipart, d_ur;
+};
 
 struct VBLearner {
     sbmf_config cfg{};
@@ -37,16 +49,13 @@ struct VBLearner {
     // host data
     std::vector<uint32_t> tu, ti, su, si;
     std::vector<double> tr, sr;
-    std::vector<uint32_t> shuffle, bid, upos, ipos, keycnt;
-    // this epoch's batch layout
-    std::vector<VRow> urows, irows;
-    std::vector<uint32_t> urow0, irow0, utask0, itask0, bsize, bbase, u2i, upart, i2u, ipart;
-    std::vector<VTask> utasks, itasks;
-    std::vector<float> ur;
+    std::vector<uint32_t> shuffle, bid, bcase, upos, ipos;
+    VBLayout lay[2];                 // epoch e uses lay[e & 1]
+    std::thread worker;              // builds lay[(e + 1) & 1] during epoch e
+    uint32_t built = 0;              // epochs whose layout exists (ready or being built)
     // device
     DBuf d_mu_v, d_sg_v, d_nm_v, d_ns_v, d_mu_w, d_sg_w, d_nm_w, d_ns_w, d_rho_w, d_rho_v, d_t_w, d_t_v, d_cc;
     DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_ETu, d_ETv, d_part;
-    DBuf d_urows, d_irows, d_u2i, d_upart, d_i2u, d_ipart, d_ur, d_utasks, d_itasks;
     DBuf d_tu, d_ti, d_tr, d_pred, d_tpart;
     VBTables tb{};
     double last_rmse = NAN, last_alpha = NAN;
@@ -54,13 +63,14 @@ struct VBLearner {
     uint32_t n_launch = 0;
 
     ~VBLearner() {
+        if (worker.joinable()) worker.join();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
     }
 
     void init(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r, uint64_t nt,
               const uint32_t* tu_, const uint32_t* ti_, const double* tr_, uint32_t I_, uint32_t J_, hipStream_t s);
-    void build_layout();
+    void build_layout(VBLayout& L, uint32_t ep);
     void run(uint32_t epochs, sbmf_sweep_cb cb, void* user);
 };
 
@@ -176,140 +186,236 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     HIPCHK(hipStreamSynchronize(st));
 }
 
+namespace {
+unsigned host_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
+// f(t, lo, hi) over [0, n) split into host_threads() contiguous chunks
+template <class F>
+void parallel_chunks(uint32_t n, F&& f) {
+    const unsigned nth = host_threads();
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nth; ++t) {
+        const uint32_t lo = (uint32_t)((uint64_t)n * t / nth), hi = (uint32_t)((uint64_t)n * (t + 1) / nth);
+        th.emplace_back([&f, t, lo, hi] { f(t, lo, hi); });
+    }
+    for (auto& x : th) x.join();
+}
+// Keyed pseudorandom permutation of [0, n) (throughput mode's shuffle):
+// a 4-round balanced Feistel network on 2h >= log2(n) bits with Philox round
+// keys, cycle-walking back into [0, n).  O(1) per case, no shared state, so
+// every case's batch is computed in parallel.
+struct FeistelPerm {
+    uint64_t seed;
+    uint32_t ep, n, h, mask;
+    FeistelPerm(uint64_t s, uint32_t e, uint32_t n_) : seed(s), ep(e), n(n_) {
+        h = 1;
+        while ((1ull << (2 * h)) < n) ++h;
+        mask = (1u << h) - 1;
+    }
+    uint32_t operator()(uint32_t x) const {
+        do {
+            uint32_t L = x >> h, R = x & mask;
+            for (uint32_t r = 0; r < 4; ++r) {
+                const P4 o = philox4x32_10(R, ep, 0x56424f00u | r, PHILOX_SALT, (uint32_t)seed, (uint32_t)(seed >> 32));
+                const uint32_t nl = R;
+                R = (L ^ o.x[0]) & mask;
+                L = nl;
+            }
+            x = (L << h) | R;
+        } while (x >= n);
+        return x;
+    }
+};
+}  // namespace
+
 // One epoch's batches: shuffle, batch membership in file order, and each
-// batch's cases grouped by user and by item (stable counting sorts).
-void VBLearner::build_layout() {
+// batch's cases grouped by user and by item.  The reference-mode shuffle is
+// sequential (the reference's rand() stream); everything else runs on
+// host_threads() threads (one batch per thread for the grouping).
+void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
+    bid.resize(N);
     if (cfg.rng_mode == SBMF_RNG_REFERENCE) {
         // libstdc++ random_shuffle: for i = 1..N-1, j = rand() % (i + 1), swap
         for (uint32_t x = 1; x < N; ++x) {
             const uint32_t j = (uint32_t)((long)grand.next() % (long)(x + 1));
             if (x != j) std::swap(shuffle[x], shuffle[j]);
         }
+        parallel_chunks(N, [&](unsigned, uint32_t lo, uint32_t hi) {
+            for (uint32_t l = lo; l < hi; ++l) bid[l] = (uint32_t)std::ceil((double)shuffle[l] / S) - 1;  // :175
+        });
     } else {
-        PhiloxStream ps(cfg.seed, epoch, 6);
-        for (uint32_t x = N - 1; x > 0; --x) {
-            const uint32_t j = std::min(x, (uint32_t)(ps.uniform() * (x + 1)));
-            std::swap(shuffle[x], shuffle[j]);
-        }
+        const FeistelPerm perm(cfg.seed, ep, N);
+        parallel_chunks(N, [&](unsigned, uint32_t lo, uint32_t hi) {
+            for (uint32_t l = lo; l < hi; ++l) bid[l] = perm(l) / S;  // = ceil((perm + 1) / S) - 1
+        });
     }
-    bid.resize(N);
-    bsize.assign(NB, 0);
-    for (uint32_t l = 0; l < N; ++l) {
-        const uint32_t b = (uint32_t)std::ceil((double)shuffle[l] / S) - 1;  // :175
-        bid[l] = b;
-        bsize[b]++;
+    L.bsize.assign(NB, 0);
+    for (uint32_t l = 0; l < N; ++l) L.bsize[bid[l]]++;
+    L.bbase.assign(NB + 1, 0);  // a batch's cases are entries [bbase[b], bbase[b+1]) of either order
+    for (uint32_t b = 0; b < NB; ++b) L.bbase[b + 1] = L.bbase[b] + L.bsize[b];
+    bcase.resize(N);  // the cases of each batch, in file order
+    {
+        std::vector<uint32_t> fill(L.bbase.begin(), L.bbase.end() - 1);
+        for (uint32_t l = 0; l < N; ++l) bcase[fill[bid[l]]++] = l;
     }
-    bbase.assign(NB + 1, 0);  // a batch's cases are entries [bbase[b], bbase[b+1]) of either order
-    for (uint32_t b = 0; b < NB; ++b) bbase[b + 1] = bbase[b] + bsize[b];
-    auto group = [&](uint32_t R, bool users, std::vector<VRow>& rows, std::vector<uint32_t>& row0,
-                     std::vector<VTask>& tasks, std::vector<uint32_t>& task0, std::vector<uint32_t>& pos,
-                     std::vector<uint32_t>& part) {
-        keycnt.assign((size_t)NB * R + 1, 0);
-        for (uint32_t l = 0; l < N; ++l) keycnt[(size_t)bid[l] * R + (users ? tu[l] : ti[l]) + 1]++;
-        rows.clear();
-        row0.assign(NB + 1, 0);
-        for (uint32_t b = 0; b < NB; ++b) {
-            row0[b] = (uint32_t)rows.size();
-            for (uint32_t a = 0; a < R; ++a) {
-                const size_t k = (size_t)b * R + a;
-                if (keycnt[k + 1]) rows.push_back(VRow{users ? a : I + a, 0, keycnt[k + 1], 0});
-            }
+    upos.resize(N);
+    ipos.resize(N);
+    L.upart.resize(N);
+    L.ipart.resize(N);
+    L.ur.resize(N);
+    // per batch and orientation: rows in attribute order, then stably by lane-group size
+    struct Part {
+        std::vector<VRow> rows;
+        std::vector<VTask> tasks;  // row0 relative to the batch's first row
+    };
+    std::vector<Part> pu(NB), pi(NB);
+    auto lg_of = [](uint32_t n) {
+        uint32_t lg = 2;
+        while (lg < 8 && (1u << lg) < n) ++lg;
+        return lg;
+    };
+    auto group = [&](uint32_t b, bool users, std::vector<uint32_t>& off, Part& P) {
+        const uint32_t R = users ? I : J;
+        const uint32_t c0 = L.bbase[b], c1 = L.bbase[b + 1];
+        std::fill(off.begin(), off.end(), 0u);
+        for (uint32_t x = c0; x < c1; ++x) off[users ? tu[bcase[x]] : ti[bcase[x]]]++;
+        std::vector<VRow> rows;
+        uint32_t run = c0;
+        for (uint32_t a = 0; a < R; ++a) {
+            const uint32_t n = off[a];
+            if (!n) continue;
+            rows.push_back(VRow{users ? a : I + a, run, n, 0});
+            off[a] = run;  // becomes the fill position
+            run += n;
         }
-        row0[NB] = (uint32_t)rows.size();
-        for (size_t k = 1; k < keycnt.size(); ++k) keycnt[k] += keycnt[k - 1];
-        // rows appear in key order, so a running offset is each row's start
-        uint32_t off = 0;
-        for (VRow& rw : rows) {
-            rw.start = off;
-            off += rw.len;
-        }
-        // per batch: rows ordered by lane-group size (stable), packed into
-        // 256-thread tasks of 256 / G rows each
-        auto lg_of = [](uint32_t n) {
-            uint32_t lg = 2;
-            while (lg < 8 && (1u << lg) < n) ++lg;
-            return lg;
-        };
-        tasks.clear();
-        task0.assign(NB + 1, 0);
-        for (uint32_t b = 0; b < NB; ++b) {
-            task0[b] = (uint32_t)tasks.size();
-            auto first = rows.begin() + row0[b], last = rows.begin() + row0[b + 1];
-            std::stable_sort(first, last, [&](const VRow& x, const VRow& y) { return lg_of(x.len) > lg_of(y.len); });
-            for (uint32_t r = row0[b]; r < row0[b + 1];) {
-                const uint32_t lg = lg_of(rows[r].len);
-                uint32_t m = 0;
-                while (r + m < row0[b + 1] && m < (256u >> lg) && lg_of(rows[r + m].len) == lg) ++m;
-                tasks.push_back(VTask{r, m, lg, 0});
-                r += m;
-            }
-        }
-        task0[NB] = (uint32_t)tasks.size();
-        pos.resize(N);
-        part.resize(N);
-        if (users) ur.resize(N);
-        for (uint32_t l = 0; l < N; ++l) {
-            const size_t k = (size_t)bid[l] * R + (users ? tu[l] : ti[l]);
-            const uint32_t q = keycnt[k]++;
+        std::vector<uint32_t>& pos = users ? upos : ipos;
+        std::vector<uint32_t>& part = users ? L.upart : L.ipart;
+        for (uint32_t x = c0; x < c1; ++x) {
+            const uint32_t l = bcase[x];
+            const uint32_t q = off[users ? tu[l] : ti[l]]++;
             pos[l] = q;
             part[q] = users ? I + ti[l] : tu[l];
-            if (users) ur[q] = (float)tr[l];
+            if (users) L.ur[q] = (float)tr[l];
+        }
+        // counting sort by lane-group size, largest first
+        std::vector<uint32_t> cls(10, 0);
+        for (const VRow& r : rows) cls[lg_of(r.len)]++;
+        uint32_t at = 0;
+        std::vector<uint32_t> first(10, 0);
+        for (int lg = 8; lg >= 2; --lg) {
+            first[lg] = at;
+            at += cls[lg];
+        }
+        P.rows.resize(rows.size());
+        for (const VRow& r : rows) P.rows[first[lg_of(r.len)]++] = r;
+        P.tasks.clear();
+        for (uint32_t r = 0; r < P.rows.size();) {
+            const uint32_t lg = lg_of(P.rows[r].len);
+            uint32_t m = 0;
+            while (r + m < P.rows.size() && m < (256u >> lg) && lg_of(P.rows[r + m].len) == lg) ++m;
+            P.tasks.push_back(VTask{r, m, lg, 0});
+            r += m;
         }
     };
-    group(I, true, urows, urow0, utasks, utask0, upos, upart);
-    group(J, false, irows, irow0, itasks, itask0, ipos, ipart);
-    u2i.resize(N);
-    i2u.resize(N);
-    for (uint32_t l = 0; l < N; ++l) {
-        u2i[upos[l]] = ipos[l];
-        i2u[ipos[l]] = upos[l];
+    const unsigned nth = host_threads();
+    {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nth; ++t)
+            th.emplace_back([&, t] {
+                std::vector<uint32_t> offu(I), offi(J);
+                for (uint32_t b = t; b < NB; b += nth) {
+                    group(b, true, offu, pu[b]);
+                    group(b, false, offi, pi[b]);
+                }
+            });
+        for (auto& x : th) x.join();
     }
+    auto concat = [&](std::vector<Part>& P, std::vector<VRow>& rows, std::vector<uint32_t>& row0,
+                      std::vector<VTask>& tasks, std::vector<uint32_t>& task0) {
+        rows.clear();
+        tasks.clear();
+        row0.assign(NB + 1, 0);
+        task0.assign(NB + 1, 0);
+        for (uint32_t b = 0; b < NB; ++b) {
+            row0[b] = (uint32_t)rows.size();
+            task0[b] = (uint32_t)tasks.size();
+            for (VTask tk : P[b].tasks) {
+                tk.row0 += row0[b];
+                tasks.push_back(tk);
+            }
+            rows.insert(rows.end(), P[b].rows.begin(), P[b].rows.end());
+        }
+        row0[NB] = (uint32_t)rows.size();
+        task0[NB] = (uint32_t)tasks.size();
+    };
+    concat(pu, L.urows, L.urow0, L.utasks, L.utask0);
+    concat(pi, L.irows, L.irow0, L.itasks, L.itask0);
+    L.u2i.resize(N);
+    L.i2u.resize(N);
+    parallel_chunks(N, [&](unsigned, uint32_t lo, uint32_t hi) {
+        for (uint32_t l = lo; l < hi; ++l) {
+            L.u2i[upos[l]] = ipos[l];
+            L.i2u[ipos[l]] = upos[l];
+        }
+    });
 }
 
 void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
     for (uint32_t it = 0; it < epochs; ++it) {
         const auto h0 = std::chrono::steady_clock::now();
-        build_layout();
-        upload_grow(d_urows, urows, st);
-        upload_grow(d_irows, irows, st);
-        upload_grow(d_u2i, u2i, st);
-        upload_grow(d_upart, upart, st);
-        upload_grow(d_ur, ur, st);
-        upload_grow(d_i2u, i2u, st);
-        upload_grow(d_ipart, ipart, st);
-        upload_grow(d_utasks, utasks, st);
-        upload_grow(d_itasks, itasks, st);
-        HIPCHK(hipStreamSynchronize(st));
+        // this epoch's layout: built by the worker during the previous epoch (or now)
+        if (built == epoch) {
+            build_layout(lay[epoch & 1], epoch);
+            built = epoch + 1;
+        } else if (worker.joinable()) {
+            worker.join();
+        }
+        VBLayout& L = lay[epoch & 1];
+        upload_grow(L.d_urows, L.urows, st);
+        upload_grow(L.d_irows, L.irows, st);
+        upload_grow(L.d_u2i, L.u2i, st);
+        upload_grow(L.d_upart, L.upart, st);
+        upload_grow(L.d_ur, L.ur, st);
+        upload_grow(L.d_i2u, L.i2u, st);
+        upload_grow(L.d_ipart, L.ipart, st);
+        upload_grow(L.d_utasks, L.utasks, st);
+        upload_grow(L.d_itasks, L.itasks, st);
         ms_layout = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
         n_launch = 0;
         HIPCHK(hipEventRecord(ev[0], st));
         double2* ETu = d_ETu.as<double2>();
         double2* ETv = d_ETv.as<double2>();
         double* part = d_part.as<double>();
-        const VRow* ur_ = d_urows.as<VRow>();
-        const VRow* ir_ = d_irows.as<VRow>();
+        const VRow* ur_ = L.d_urows.as<VRow>();
+        const VRow* ir_ = L.d_irows.as<VRow>();
         for (uint32_t b = 0; b < NB; ++b) {
-            const uint32_t B = bsize[b];
-            const uint32_t nu = urow0[b + 1] - urow0[b];
+            const uint32_t B = L.bsize[b];
+            const uint32_t nu = L.urow0[b + 1] - L.urow0[b];
             HIPCHK(vbo_transpose(tb.mu_v, d_muT.as<double>(), K, Kp, p, st));
             HIPCHK(vbo_transpose(tb.sg_v, d_sgT.as<double>(), K, Kp, p, st));
-            HIPCHK(vbo_predict(ur_ + urow0[b], nu, d_upart.as<uint32_t>(), d_ur.as<float>(), d_muT.as<double>(),
+            HIPCHK(vbo_predict(ur_ + L.urow0[b], nu, L.d_upart.as<uint32_t>(), L.d_ur.as<float>(), d_muT.as<double>(),
                                d_sgT.as<double>(), tb, Kp, ETu, st));
-            HIPCHK(vbo_update_w0(ETu + bbase[b], B, tb, part, st));
-            const VTask* ut = d_utasks.as<VTask>() + utask0[b];
-            const VTask* it_ = d_itasks.as<VTask>() + itask0[b];
-            const uint32_t nut = utask0[b + 1] - utask0[b], nit = itask0[b + 1] - itask0[b];
+            HIPCHK(vbo_update_w0(ETu + L.bbase[b], B, tb, part, st));
+            const VTask* ut = L.d_utasks.as<VTask>() + L.utask0[b];
+            const VTask* it_ = L.d_itasks.as<VTask>() + L.itask0[b];
+            const uint32_t nut = L.utask0[b + 1] - L.utask0[b], nit = L.itask0[b + 1] - L.itask0[b];
             // every pass reads its own order and writes the other one: users ETu -> ETv, items ETv -> ETu
-            const uint32_t* u2i_ = d_u2i.as<uint32_t>();
-            const uint32_t* i2u_ = d_i2u.as<uint32_t>();
+            const uint32_t* u2i_ = L.d_u2i.as<uint32_t>();
+            const uint32_t* i2u_ = L.d_i2u.as<uint32_t>();
             HIPCHK(vbo_update_w(ut, nut, ur_, u2i_, 1, tb, ETu, ETv, st));
             HIPCHK(vbo_update_w(it_, nit, ir_, i2u_, 0, tb, ETv, ETu, st));
             for (uint32_t f = 0; f < K; ++f) {
-                HIPCHK(vbo_update_v(ut, nut, ur_, u2i_, d_upart.as<uint32_t>(), f, tb, ETu, ETv, st));
-                HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st));
+                HIPCHK(vbo_update_v(ut, nut, ur_, u2i_, L.d_upart.as<uint32_t>(), f, tb, ETu, ETv, st));
+                HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st));
             }
-            HIPCHK(vbo_hyper(ETu + bbase[b], B, tb, part, st));
+            HIPCHK(vbo_hyper(ETu + L.bbase[b], B, tb, part, st));
             n_launch += 2 * K + 12;
+        }
+        // the next epoch's shuffle and layout, on the host while this epoch runs
+        // (the reference stream after this epoch's shuffle is exactly the next one's)
+        if (built == epoch + 1) {
+            built = epoch + 2;
+            const uint32_t nx = epoch + 1;
+            worker = std::thread([this, nx] { build_layout(lay[nx & 1], nx); });
         }
         HIPCHK(hipEventRecord(ev[1], st));
         // ---- test RMSE of the clamped means (fm_learn_vb_online_simultaneous.h:348-360,441-447)
