@@ -9,6 +9,11 @@ hyperparameter draws (tau, sigma, mu), user half-sweep, item half-sweep and
 test evaluation (running-mean RMSE), all with inputs resident in HBM.
 RNG: Philox in-kernel (throughput mode); arithmetic: f64 (the reference's).
 
+Online VB (BASELINE config 5, `-method vb`): python bench.py --method vb
+  [--shape netflix --K 200]; a step is one epoch (30 mini-batches) of the
+  online variational-Bayes learner over a Netflix-shaped synthetic set of
+  100 M ratings; single GPU (the VB learner is not partitioned in this build).
+
 Single GPU:  python bench.py [--steps K --warmup W]
 Multi GPU:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
   one process per GPU; users/items are row-block partitioned (nnz balanced)
@@ -37,8 +42,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--shape", default="ml-20m")
-    ap.add_argument("--K", type=int, default=100)
+    ap.add_argument("--method", default="mcmc", choices=["mcmc", "vb"])
+    ap.add_argument("--shape", default=None, help="ml-20m (mcmc default) | netflix (vb default) | ml-1m | ...")
+    ap.add_argument("--K", type=int, default=None, help="factors (default 100 mcmc / 200 vb)")
     ap.add_argument("--precision", default="f64")
     ap.add_argument("--no-f32", action="store_true", help="skip the extra f32 measurement")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
@@ -201,8 +207,78 @@ def mk_uid(world, rank):
     return obj[0]
 
 
+def vb_main(args):
+    """BASELINE config 5: online VB epochs (ratings/s per epoch)."""
+    from sbmf import Data, FMLearnVBOnline, synth
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        raise SystemExit("bench.py --method vb: the online VB learner runs on one GPU in this build")
+    train, test, dims = synth.generate(args.shape)
+    n_train = len(train[0])
+    L = FMLearnVBOnline(num_factor=args.K, seed=2015, rng="philox", device=max(args.device, 0))
+    t0 = time.time()
+    L.set_data(Data(*train), Data(*test))
+    prep_s = time.time() - t0
+    for _ in range(args.warmup):
+        L.learn(sweeps=1)
+    device_sync()
+    t0 = time.perf_counter()
+    L.learn(sweeps=args.steps)
+    device_sync()
+    dt = time.perf_counter() - t0
+    hist = L.history[-args.steps:]
+    gpu_ms = float(np.mean([h["ms_sweep"] for h in hist]))
+    K = args.K
+    # algorithmic bytes per epoch (f64): per case the two partner rows of
+    # means and variances for the prediction (4 * 8K), and per factor pass
+    # (2K of them) the {e,t} record read + written (32), the partner mean and
+    # variance (16) and its ids (8)
+    bytes_epoch = n_train * (32.0 * K + 2 * K * 56.0)
+    out = {
+        "metric": "ratings/sec per online-VB epoch, %s K=%d" % ({"netflix": "synthetic 100M (Netflix-shaped)"}.get(
+            args.shape, args.shape), K),
+        "value": n_train * args.steps / dt, "unit": "ratings/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic %s-shaped (sbmf/synth.py)" % args.shape,
+        "config": {"workload": "online VB epoch (30 mini-batches: e/t terms, update_w0, update_w, factor-outer "
+                               "update_v, hyperparameter blends) + test RMSE", "method": "vb",
+                   "num_users": dims[0], "num_items": dims[1], "n_train": n_train, "n_test": len(test[0]), "K": K,
+                   "rng": "philox", "prep_s": prep_s, "gpu_ms_per_epoch": gpu_ms,
+                   "test_rmse_after": hist[-1]["rmse_avg"], "epochs_run": len(L.history)},
+        "roofline": {"kernel": "epoch (all VB kernels)", "bound": "hbm", "achieved": bytes_epoch / (gpu_ms * 1e-3) / 1e9,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": bytes_epoch / (gpu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "traffic": None, "bytes_per_epoch": bytes_epoch},
+    }
+    L.close()
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+        n = len(train[0])
+        take = int(min(n, 2_000_000))
+        idx = np.random.default_rng(7).permutation(n)[:take]
+        sub = tuple(a[idx] for a in train)
+        tsub = tuple(a[:1000] for a in test)
+        r = oracle.run_vbo(sub, tsub, K=K, epochs=1, seed=1, num_users=dims[0], num_items=dims[1],
+                           seconds_limit=args.cpu_seconds, want_params=False)
+        out["cpu_baseline"] = {"value": take * r["epochs"] / r["seconds"], "unit": "ratings/s", "cores": 1,
+                               "kind": "port",
+                               "sample": "oracle (vbo_oracle.c, serial C restatement of fm_learn_vb_online, f64) for "
+                                         "1 epoch on a random %d-rating subsample (all %d users x %d items kept), "
+                                         "K=%d, %.1f s" % (take, dims[0], dims[1], K, r["seconds"])}
+    print(json.dumps(out), flush=True)
+    from sbmf import _lib
+    _lib.unload()
+
+
 def main():
     args = parse()
+    if args.shape is None:
+        args.shape = "netflix" if args.method == "vb" else "ml-20m"
+    if args.K is None:
+        args.K = 200 if args.method == "vb" else 100
+    if args.method == "vb":
+        return vb_main(args)
     # load libsbmf (ROCm's HIP runtime) before torch.distributed pulls in torch's bundled copy
     from sbmf import synth
     world, rank, local = dist_setup(args)

@@ -42,13 +42,15 @@ int main(void) {
   printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(sbmf_config), sizeof(sbmf_sweep_info), sizeof(sbmf_timing),
          sizeof(sbmf_ratings), offsetof(sbmf_config, init_stdev), offsetof(sbmf_config, recompute_every),
          offsetof(sbmf_timing, bytes_algorithmic));
+  printf("%zu %zu\n", offsetof(sbmf_config, method), offsetof(sbmf_config, vb_batches));
   return 0; }''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     import ctypes as C
     want = [C.sizeof(_lib.Config), C.sizeof(_lib.SweepInfo), C.sizeof(_lib.Timing), C.sizeof(_lib.Ratings),
-            _lib.Config.init_stdev.offset, _lib.Config.recompute_every.offset, _lib.Timing.bytes_algorithmic.offset]
+            _lib.Config.init_stdev.offset, _lib.Config.recompute_every.offset, _lib.Timing.bytes_algorithmic.offset,
+            _lib.Config.method.offset, _lib.Config.vb_batches.offset]
     assert got == want
 
 
@@ -59,6 +61,7 @@ def test_defaults_are_the_reference_constants():
     assert (c.a0, c.b0, c.alpha0, c.beta0, c.nu0, c.mu0) == (1, 1, 1, 1, 1, 0)
     assert c.clamp_hi == 5.0 and c.rng_mode == sbmf.RNG_REFERENCE and c.quirks == sbmf.QUIRKS_FINAL
     assert c.precision == sbmf.F64
+    assert c.method == sbmf._lib.METHOD_MCMC and c.vb_batches == 0
     assert _lib.lib.sbmf_abi_version() == 1
 
 
@@ -78,4 +81,10 @@ def test_bad_config_rejected_before_device():
     ctx = C.c_void_p()
     assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG
     cfg.num_factor = 300
+    assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG
+    cfg = sbmf.config_default()
+    cfg.method = 7
+    assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG
+    cfg.method = sbmf._lib.METHOD_VB
+    cfg.precision = sbmf.F32  # the VB learner is f64 only
     assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG

@@ -30,6 +30,7 @@ def test_no_arguments_prints_help():
     (["task", "r"], "cannot parse"),
     (["-task", "c", "-train", "a", "-test", "b"], "only -task r"),
     (["-task", "r", "-train", "a", "-test", "b", "-method", "sgd"], "not supported"),
+    (["-task", "r", "-train", "a", "-test", "b", "-method", "vb", "-dim", "0,0,8"], "-dim '1,1,K'"),
     (["-task", "r", "-train", "a"], "mandatory"),
     (["-task", "r", "-train", "a", "-test", "b", "-dim", "1,1"], "dim must have 3"),
     (["-task", "r", "-train", "/nonexistent", "-test", "b"], "unable to open"),
