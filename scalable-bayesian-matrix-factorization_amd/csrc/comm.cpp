@@ -8,6 +8,7 @@
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -137,6 +138,57 @@ void Comm::bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_
         char* p = static_cast<char*>(base) + (size_t)bounds[k] * unit_bytes;
         r = ncclBroadcast(p, p, bytes, ncclUint8, k, (ncclComm_t)comm_, st);
         if (r != ncclSuccess) comm_fail("ncclBroadcast", r);
+    }
+    r = ncclGroupEnd();
+    if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
+}
+
+void Comm::alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const std::vector<size_t>& scnt,
+                     void* recvbuf, const std::vector<size_t>& roff, const std::vector<size_t>& rcnt, hipStream_t st) {
+    if (nranks_ <= 1) return;
+    if (shm_) {  // host backend: rank s publishes [offsets | its send buffer], every other rank takes its part
+        if (hipStreamSynchronize(st) != hipSuccess) throw std::runtime_error("hipStreamSynchronize failed");
+        unsigned char* win = shm_ + kHostHeader;
+        const size_t hdr = 16 * (size_t)nranks_;
+        for (int s = 0; s < nranks_; ++s) {
+            if (rank_ == s) {
+                size_t* h = reinterpret_cast<size_t*>(win);
+                for (int k = 0; k < nranks_; ++k) {
+                    h[2 * k] = soff[k];
+                    h[2 * k + 1] = scnt[k];
+                }
+                size_t end = 0;
+                for (int k = 0; k < nranks_; ++k)
+                    if (k != rank_ && scnt[k]) end = std::max(end, soff[k] + scnt[k]);
+                if (hdr + end > kHostWindow) throw std::runtime_error("host comm: exchange larger than the window");
+                if (end && hipMemcpy(win + hdr, sendbuf, end, hipMemcpyDeviceToHost) != hipSuccess)
+                    throw std::runtime_error("host comm: D2H failed");
+            }
+            host_barrier();
+            if (rank_ != s && rcnt[s]) {
+                const size_t* h = reinterpret_cast<const size_t*>(win);
+                if (h[2 * rank_ + 1] != rcnt[s]) throw std::runtime_error("host comm: exchange size mismatch");
+                if (hipMemcpy(static_cast<char*>(recvbuf) + roff[s], win + hdr + h[2 * rank_], rcnt[s],
+                              hipMemcpyHostToDevice) != hipSuccess)
+                    throw std::runtime_error("host comm: H2D failed");
+            }
+            host_barrier();
+        }
+        return;
+    }
+    if (!comm_) return;
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) comm_fail("ncclGroupStart", r);
+    for (int k = 0; k < nranks_; ++k) {
+        if (k == rank_) continue;
+        if (scnt[k]) {
+            r = ncclSend(static_cast<const char*>(sendbuf) + soff[k], scnt[k], ncclUint8, k, (ncclComm_t)comm_, st);
+            if (r != ncclSuccess) comm_fail("ncclSend", r);
+        }
+        if (rcnt[k]) {
+            r = ncclRecv(static_cast<char*>(recvbuf) + roff[k], rcnt[k], ncclUint8, k, (ncclComm_t)comm_, st);
+            if (r != ncclSuccess) comm_fail("ncclRecv", r);
+        }
     }
     r = ncclGroupEnd();
     if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);

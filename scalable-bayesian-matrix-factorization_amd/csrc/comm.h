@@ -27,6 +27,11 @@ class Comm {
     // Rank k owns units [bounds[k], bounds[k+1]) of unit_bytes each, starting
     // at base; after the call every rank holds every rank's units.
     void bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_t>& bounds, hipStream_t st);
+    // Point-to-point exchange (grouped ncclSend / ncclRecv): to every other
+    // rank k, send [soff[k], soff[k] + scnt[k]) of sendbuf, and receive
+    // rcnt[k] bytes from it at recvbuf + roff[k] (byte offsets and counts).
+    void alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const std::vector<size_t>& scnt,
+                   void* recvbuf, const std::vector<size_t>& roff, const std::vector<size_t>& rcnt, hipStream_t st);
 
   private:
     void host_barrier();

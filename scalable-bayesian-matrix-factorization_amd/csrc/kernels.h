@@ -173,6 +173,10 @@ hipError_t launch_bias_rows(const uint32_t* ptr, uint32_t r0, uint32_t r1, T* E,
 template <typename T>
 hipError_t launch_esum2(const T* E, uint64_t n, double* part, double* out2, hipStream_t st);
 
+// E[idx[j]] = recv[j] for j < n (multi-GPU residual exchange, receiving side)
+template <typename T>
+hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, hipStream_t st);
+
 // Deterministic fixed-order sum of in[n] (contiguous) into one double at out.
 // scratch: >= ceil(n/1024) + ceil(n/1024^2) + 2 doubles.
 hipError_t launch_sum(const double* in, uint64_t n, double* out, double* scratch, hipStream_t st);

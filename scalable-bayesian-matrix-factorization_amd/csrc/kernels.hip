@@ -1558,6 +1558,15 @@ __global__ __launch_bounds__(256) void k_esum2(const T* __restrict__ E, uint64_t
     }
 }
 
+// Multi-GPU residual exchange: residuals other ranks computed for this
+// rank's rows arrive packed; put each at its position in this orientation.
+template <typename T>
+__global__ __launch_bounds__(256) void k_unpack(const T* __restrict__ recv, const uint32_t* __restrict__ idx,
+                                                 uint64_t n, T* __restrict__ E) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j < n) E[idx[j]] = recv[j];
+}
+
 }  // namespace
 
 // ===================================================================== launchers
@@ -1841,6 +1850,13 @@ hipError_t launch_esum2(const T* E, uint64_t n, double* part, double* out2, hipS
     return launch_sum_cols(part, (uint32_t)nb, 2, out2, st);
 }
 
+template <typename T>
+hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    k_unpack<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(recv, idx, n, E);
+    return hipGetLastError();
+}
+
 #define SBMF_INST(T)                                                                                                 \
     template hipError_t launch_rows<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);            \
     template hipError_t launch_gblock<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);          \
@@ -1866,7 +1882,8 @@ hipError_t launch_esum2(const T* E, uint64_t n, double* part, double* out2, hipS
                                               uint32_t, hipStream_t);                                                \
     template hipError_t launch_bias_rows<T>(const uint32_t*, uint32_t, uint32_t, T*, double*, double*, double*,      \
                                             const double*, const BiasArgs&, hipStream_t);                            \
-    template hipError_t launch_esum2<T>(const T*, uint64_t, double*, double*, hipStream_t);
+    template hipError_t launch_esum2<T>(const T*, uint64_t, double*, double*, hipStream_t);                        \
+    template hipError_t launch_unpack<T>(const T*, const uint32_t*, uint64_t, T*, hipStream_t);
 SBMF_INST(float)
 SBMF_INST(double)
 

@@ -68,7 +68,64 @@ struct Side {
     std::vector<uint32_t> rtptr;     // [r1-r0+1] first task of each own row
     uint32_t nxchunk = 0;            // tasks belonging to split rows (slab / staging slots)
     uint32_t sgrid = 0;              // persistent grid of the streaming launch
+    // multi-GPU residual exchange (see build_exchange): where this rank's rows
+    // scatter their residuals (the other orientation's position, or a send slot
+    // past its end), and where the residuals other ranks send land
+    std::vector<uint32_t> perm2, unpack;
+    std::vector<size_t> soff, scnt, roff, rcnt;  // elements, per peer
+    size_t nsend = 0, nrecv = 0;
 };
+
+// Multi-GPU residuals.  A half-sweep on rank p updates the residuals of its
+// own rows' ratings and scatters them into the other orientation's order
+// (E_other[perm[idx]]); the next half on rank q reads the residuals of q's
+// rows, which every rank contributed to.  So each half ends with a
+// point-to-point exchange: rank p's kernels write the residuals bound for
+// rank q into a send area past the end of E_other (perm2 = N + slot), in
+// rating order, and rank q unpacks what arrives from p into its positions
+// (unpack, the same order).  Both lists follow from the rating structure,
+// which every rank holds, so no index travels.  About N / P residuals per
+// rank per half cross xGMI -- instead of recomputing every residual from
+// r - own.partner, which re-reads every partner row.
+static void build_exchange(Side& s, const Side& other, int nranks, int rank) {
+    const uint64_t N = s.perm.size();
+    std::vector<uint64_t> obase(nranks + 1);
+    for (int k = 0; k <= nranks; ++k) obase[k] = other.ptr[other.bounds[k]];
+    auto owner = [&](uint32_t pos) {
+        return (int)(std::upper_bound(obase.begin(), obase.end(), (uint64_t)pos) - obase.begin()) - 1;
+    };
+    s.scnt.assign(nranks, 0);
+    s.rcnt.assign(nranks, 0);
+    const uint64_t m0 = s.ptr[s.bounds[rank]], m1 = s.ptr[s.bounds[rank + 1]];
+    for (uint64_t idx = m0; idx < m1; ++idx) {
+        const int q = owner(s.perm[idx]);
+        if (q != rank) s.scnt[q]++;
+    }
+    s.soff.assign(nranks, 0);
+    size_t off = 0;
+    for (int k = 0; k < nranks; ++k) {
+        s.soff[k] = off;
+        off += s.scnt[k];
+    }
+    s.nsend = off;
+    s.perm2.assign(s.perm.begin(), s.perm.end());
+    std::vector<size_t> fill(s.soff);
+    for (uint64_t idx = m0; idx < m1; ++idx) {
+        const int q = owner(s.perm[idx]);
+        if (q != rank) s.perm2[idx] = (uint32_t)(N + fill[q]++);
+    }
+    s.unpack.clear();
+    s.roff.assign(nranks, 0);
+    for (int k = 0; k < nranks; ++k) {  // what rank k sends here, in k's rating order
+        s.roff[k] = s.unpack.size();
+        if (k == rank) continue;
+        for (uint64_t idx = s.ptr[s.bounds[k]]; idx < s.ptr[s.bounds[k + 1]]; ++idx)
+            if (owner(s.perm[idx]) == rank) s.unpack.push_back(s.perm[idx]);
+        s.rcnt[k] = s.unpack.size() - s.roff[k];
+    }
+    s.nrecv = s.unpack.size();
+    if (N + s.nsend >= 0xffffffffull) fail(SBMF_E_ARG, "too many ratings for the 32-bit residual exchange");
+}
 
 static void build_side(uint64_t N, const uint32_t* key, const uint32_t* other, const double* rat, uint32_t R,
                        Side& s, std::vector<uint32_t>& pos_of_case) {
@@ -203,6 +260,7 @@ struct sbmf_ctx {
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
     DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
+    DBuf d_uperm2, d_vperm2, d_uunpack, d_vunpack, d_xrecv;  // multi-GPU residual exchange
     DBuf d_bu, d_bv, d_mbu, d_mbv, d_sbu, d_sbv;  // biases b_i / b_j and their per-row (mu, sigma)
     DBuf d_var3u, d_var3v, d_epart;              // reference-mode per-row bias variates; sum(E) partials
     std::vector<double> h_res;
@@ -285,6 +343,10 @@ static void prepare_T(sbmf_ctx* c) {
     }
     partition(c->users, c->nranks, c->rank);
     partition(c->items, c->nranks, c->rank);
+    if (c->nranks > 1) {
+        build_exchange(c->users, c->items, c->nranks, c->rank);  // user half -> item order
+        build_exchange(c->items, c->users, c->nranks, c->rank);  // item half -> user order
+    }
     // row_kernel 0: Gram-block kernels for rows <= stream threshold, the
     // streaming kernel above it, the Gram route only if a threshold is set.
     // row_kernel 1: per-coordinate kernels up to 4096 ratings, Gram route above.
@@ -404,8 +466,16 @@ static void prepare_T(sbmf_ctx* c) {
     c->d_V.alloc((size_t)(c->J + 2) * c->Kp * sizeof(T));
     HIPCHK(hipMemsetAsync(c->d_U.p, 0, c->d_U.bytes, st));
     HIPCHK(hipMemsetAsync(c->d_V.p, 0, c->d_V.bytes, st));
-    c->d_Eu.alloc(std::max<uint64_t>(N, 1) * sizeof(T));
-    c->d_Ev.alloc(std::max<uint64_t>(N, 1) * sizeof(T));
+    // E_v: the user half's scatter target (+ its send area), E_u: the item half's
+    c->d_Eu.alloc(std::max<uint64_t>(N + c->items.nsend, 1) * sizeof(T));
+    c->d_Ev.alloc(std::max<uint64_t>(N + c->users.nsend, 1) * sizeof(T));
+    if (c->nranks > 1) {
+        upload(c->d_uperm2, c->users.perm2, st);
+        upload(c->d_vperm2, c->items.perm2, st);
+        upload(c->d_uunpack, c->users.unpack, st);
+        upload(c->d_vunpack, c->items.unpack, st);
+        c->d_xrecv.alloc(std::max<size_t>(std::max(c->users.nrecv, c->items.nrecv), 1) * sizeof(T));
+    }
     HIPCHK(hipMemsetAsync(c->d_Eu.p, 0, c->d_Eu.bytes, st));
     HIPCHK(hipMemsetAsync(c->d_Ev.p, 0, c->d_Ev.bytes, st));
     c->d_rowsq_u.alloc((size_t)c->I * sizeof(double));
@@ -686,7 +756,7 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     if (users) {
         a.ptr = c->d_uptr.as<uint32_t>();
         a.part = c->d_upart.as<uint32_t>();
-        a.perm = c->d_uperm.as<uint32_t>();
+        a.perm = (md ? c->d_uperm2 : c->d_uperm).as<uint32_t>();
         a.E_this = c->d_Eu.as<T>();   // user order
         a.E_other = c->d_Ev.as<T>();  // item order
         a.r_this = c->d_ur.as<T>();
@@ -702,7 +772,7 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     } else {
         a.ptr = c->d_vptr.as<uint32_t>();
         a.part = c->d_vpart.as<uint32_t>();
-        a.perm = c->d_vperm.as<uint32_t>();
+        a.perm = (md ? c->d_vperm2 : c->d_vperm).as<uint32_t>();
         a.E_this = c->d_Ev.as<T>();   // item order
         a.E_other = c->d_Eu.as<T>();  // user order
         a.r_this = c->d_vr.as<T>();
@@ -726,8 +796,9 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     a.sweep = c->sweep;
     a.lo = (T)c->lo;
     a.hi = (T)c->hi;
-    // multi-GPU: residuals from r - own.partner (tune bit 1 forces it on one GPU, for validation)
-    a.e_from_dot = (md || (c->cfg.tune & 2u)) ? 1 : 0;
+    // tune bit 1: residuals from r - own.partner (the former multi-GPU form, kept for validation);
+    // otherwise every rank reads the residuals the exchange delivered
+    a.e_from_dot = (c->cfg.tune & 2u) ? 1 : 0;
     return a;
 }
 
@@ -805,6 +876,24 @@ static double ev_ms(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
+// After a half (users: scatter into item order, E_v; items: into E_u): send
+// the residuals bound for other ranks' rows, unpack what arrives.
+template <typename T>
+static void exchange_residuals(sbmf_ctx* c, bool users, hipStream_t st) {
+    if (c->nranks <= 1) return;
+    const Side& s = users ? c->users : c->items;
+    DBuf& E = users ? c->d_Ev : c->d_Eu;
+    auto bytes = [](const std::vector<size_t>& v) {
+        std::vector<size_t> b(v);
+        for (size_t& x : b) x *= sizeof(T);
+        return b;
+    };
+    c->comm.alltoallv(E.as<T>() + c->tu.size(), bytes(s.soff), bytes(s.scnt), c->d_xrecv.p, bytes(s.roff),
+                      bytes(s.rcnt), st);
+    HIPCHK(launch_unpack<T>(c->d_xrecv.as<T>(), (users ? c->d_uunpack : c->d_vunpack).as<uint32_t>(), s.nrecv,
+                            E.as<T>(), st));
+}
+
 template <typename T>
 static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* user) {
     const sbmf_config& cf = c->cfg;
@@ -831,11 +920,13 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             // residuals of every rating, scattered into user order for the user half
             HIPCHK(launch_resid<T>(c->d_rtasks.as<ResidTask>(), (uint32_t)c->items.rtasks.size(),
                                    c->d_rtptr.as<uint32_t>(), c->items.r0, c->items.r1, c->d_vpart.as<uint32_t>(),
-                                   c->d_vperm.as<uint32_t>(), c->d_vr.as<T>(), c->d_V.as<T>(), c->d_U.as<T>(), K,
+                                   (c->nranks > 1 ? c->d_vperm2 : c->d_vperm).as<uint32_t>(), c->d_vr.as<T>(),
+                                   c->d_V.as<T>(), c->d_U.as<T>(), K,
                                    c->Kp, c->d_Eu.as<T>(), c->d_rtsq.as<double>(), c->d_rowsq_v.as<double>(),
                                    c->bias ? c->d_bv.as<double>() : nullptr, c->d_bu.as<double>(), c->b0, st));
             c->timing.n_launch++;
             if (c->nranks > 1) c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
+            exchange_residuals<T>(c, false, st);
         }
         HIPCHK(launch_sum(c->d_rowsq_v.as<double>(), c->J, d_res + RES_ESQ, scratch, st));
         // biased sampler: sum(E) and sum(E^2) of the sweep-start residuals (:342-359)
@@ -925,7 +1016,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                                        ref ? c->d_var3u.as<double>() : nullptr, bias_args(c, true, d0), st));
         run_half<T>(c, true);
         HIPCHK(hipEventRecord(c->ev[2], st));
-        if (c->nranks > 1) c->comm.bcast_ranges(c->d_U.p, c->Kp * sizeof(T), c->users.bounds, st);
+        if (c->nranks > 1) {
+            c->comm.bcast_ranges(c->d_U.p, c->Kp * sizeof(T), c->users.bounds, st);
+            exchange_residuals<T>(c, true, st);
+        }
         HIPCHK(hipEventRecord(c->ev[3], st));
         // ---- 4. item half-sweep
         if (!ref)
@@ -938,6 +1032,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         HIPCHK(hipEventRecord(c->ev[4], st));
         if (c->nranks > 1) {
             c->comm.bcast_ranges(c->d_V.p, c->Kp * sizeof(T), c->items.bounds, st);
+            exchange_residuals<T>(c, false, st);
             c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
             if (cf.eval_train) c->comm.bcast_ranges(c->d_rowtr_v.p, sizeof(double), c->items.bounds, st);
         }

@@ -1,7 +1,9 @@
 """Several ranks on one GPU (host comm backend instead of RCCL, which refuses
 two ranks on one device): the row-block partition, the per-half block
-exchange, the rank-local residual form and the fixed-order partial sums must
-reproduce a single-rank run bit for bit."""
+exchange, the point-to-point residual exchange and the fixed-order partial
+sums must reproduce a single-rank run bit for bit.  tune=2 runs every rank
+(and the single-rank reference) with residuals recomputed from r - own.partner
+instead of exchanged."""
 import os
 import subprocess
 import sys
@@ -16,12 +18,12 @@ pytestmark = pytest.mark.gpu
 WORKER = os.path.join(REPO, "tests", "workers", "multirank_worker.py")
 
 
-@pytest.mark.parametrize("nranks,rng", [(2, "ref"), (3, "philox")])
-def test_ranks_on_one_gpu_match_single_rank(ml100k, tmp_path, nranks, rng):
+@pytest.mark.parametrize("nranks,rng,tune", [(2, "ref", 0), (3, "philox", 0), (2, "philox", 2)])
+def test_ranks_on_one_gpu_match_single_rank(ml100k, tmp_path, nranks, rng, tune):
     K, sweeps, seed = 30, 3, 6
     tr, te = ml100k
-    # single rank, same residual form as every rank of a multi-rank run (tune bit 1)
-    L = FMLearnSBPMF(num_factor=K, seed=seed, rng=rng, tune=2)
+    # single rank, same residual form as every rank of the multi-rank run
+    L = FMLearnSBPMF(num_factor=K, seed=seed, rng=rng, tune=tune)
     L.set_data(Data(*tr), Data(*te))
     L.learn(sweeps=sweeps)
     U1, V1 = L.factors()
@@ -39,7 +41,7 @@ def test_ranks_on_one_gpu_match_single_rank(ml100k, tmp_path, nranks, rng):
             os.environ["SBMF_COMM"] = old
     outs = [str(tmp_path / ("r%d.npz" % r)) for r in range(nranks)]
     procs = [subprocess.Popen([sys.executable, WORKER, str(r), str(nranks), uid.hex(), outs[r], str(K), str(sweeps),
-                               str(seed), rng], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                               str(seed), rng, str(tune)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
              for r in range(nranks)]
     logs = []
     for p in procs:

@@ -1,6 +1,6 @@
 """One rank of the multi-rank sampler (spawned by tests/test_gpu_multirank.py).
 
-usage: python multirank_worker.py <rank> <nranks> <id-hex> <out.npz> <K> <sweeps> <seed> <rng>
+usage: python multirank_worker.py <rank> <nranks> <id-hex> <out.npz> <K> <sweeps> <seed> <rng> [tune]
 The ranks share one GPU and exchange their row blocks through the host comm
 backend (the id was made with SBMF_COMM=host); the result must equal a
 single-rank run in the same residual form.
@@ -29,10 +29,11 @@ def read(path):
 
 def main():
     rank, nranks, idhex, out, K, sweeps, seed, rng = sys.argv[1:9]
+    tune = int(sys.argv[9]) if len(sys.argv) > 9 else 0
     from sbmf import Data, FMLearnSBPMF
     g = os.path.join(REPO, "tests", "golden")
     tr, te = read(os.path.join(g, "ml100k_train.tsv.gz")), read(os.path.join(g, "ml100k_test.tsv.gz"))
-    L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0)
+    L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, tune=tune)
     L.init(comm=(int(nranks), int(rank), bytes.fromhex(idhex)))
     L.set_data(Data(*tr), Data(*te))
     L.learn(sweeps=int(sweeps))
