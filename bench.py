@@ -213,7 +213,10 @@ def vb_main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         raise SystemExit("bench.py --method vb: the online VB learner runs on one GPU in this build")
+    print("[bench vb] generating the %s-shaped set" % args.shape, file=sys.stderr, flush=True)
+    t0 = time.time()
     train, test, dims = synth.generate(args.shape)
+    print("[bench vb] %d train ratings in %.0f s" % (len(train[0]), time.time() - t0), file=sys.stderr, flush=True)
     n_train = len(train[0])
     L = FMLearnVBOnline(num_factor=args.K, seed=2015, rng="philox", device=max(args.device, 0))
     t0 = time.time()
@@ -221,9 +224,11 @@ def vb_main(args):
     prep_s = time.time() - t0
     for _ in range(args.warmup):
         L.learn(sweeps=1)
+        print("[bench vb] warm-up epoch %.0f ms (GPU)" % L.history[-1]["ms_sweep"], file=sys.stderr, flush=True)
     device_sync()
     t0 = time.perf_counter()
-    L.learn(sweeps=args.steps)
+    L.learn(sweeps=args.steps, callback=lambda h: print("[bench vb] epoch %.0f ms (GPU)" % h["ms_sweep"],
+                                                          file=sys.stderr, flush=True) and False)
     device_sync()
     dt = time.perf_counter() - t0
     hist = L.history[-args.steps:]

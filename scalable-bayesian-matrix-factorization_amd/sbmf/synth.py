@@ -21,6 +21,9 @@ SHAPES = {
 }
 
 
+FAST_ABOVE = 50_000_000  # shapes with more ratings use the sort-based generator
+
+
 def _degrees(rng, n, total, dmin, dmax, kind):
     if kind == "pareto":
         d = dmin * (1.0 - rng.random(n)) ** (-1.0 / 1.2)
@@ -67,17 +70,29 @@ def _generate(shape, seed, rank, noise, test_frac):
     # the target degrees, oversample, drop duplicate pairs, keep `total`.
     pu = du / du.sum()
     pi = di / di.sum()
-    keys = np.zeros(0, np.int64)
-    m = int(total * 1.3)
-    while True:
-        us = rng.choice(I, m, p=pu).astype(np.int64)
-        its = rng.choice(J, m, p=pi).astype(np.int64)
-        keys = np.concatenate([keys, us * J + its])
-        _, first = np.unique(keys, return_index=True)
-        if len(first) >= total:
-            break
-        m = int((total - len(first)) * 1.5) + 1000
-    key = keys[np.sort(first)][:total]  # first occurrences, draw order = random file order
+    if total <= FAST_ABOVE:
+        keys = np.zeros(0, np.int64)
+        m = int(total * 1.3)
+        while True:
+            us = rng.choice(I, m, p=pu).astype(np.int64)
+            its = rng.choice(J, m, p=pi).astype(np.int64)
+            keys = np.concatenate([keys, us * J + its])
+            _, first = np.unique(keys, return_index=True)
+            if len(first) >= total:
+                break
+            m = int((total - len(first)) * 1.5) + 1000
+        key = keys[np.sort(first)][:total]  # first occurrences, draw order = random file order
+    else:
+        # large shapes: sorted unique pairs (one plain sort per round), then a
+        # random permutation as the file order -- minutes faster at 100 M
+        uk = np.zeros(0, np.int64)
+        m = int(total * 1.4)
+        while len(uk) < total:
+            us = rng.choice(I, m, p=pu).astype(np.int64)
+            its = rng.choice(J, m, p=pi).astype(np.int64)
+            uk = np.union1d(uk, us * J + its) if len(uk) else np.unique(us * J + its)
+            m = int((total - len(uk)) * 2.0) + 100000
+        key = rng.permutation(uk)[:total]
     u = (key // J).astype(np.uint32)
     i = (key % J).astype(np.uint32)
     P = rng.normal(0.0, (1.0 / rank) ** 0.25, (I, rank))
