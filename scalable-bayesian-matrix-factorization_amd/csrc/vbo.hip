@@ -184,7 +184,7 @@ constexpr int MC = 4;  // cases a lane keeps in registers between the two passes
 
 // update_w (:635-710) for the rows of one orientation.  apply_w0: first add
 // update_w0's deltas to the row's cases (the user pass touches every case once).
-__global__ __launch_bounds__(256) void k_update_w(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
+__global__ __launch_bounds__(256, 6) void k_update_w(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
                                                    const uint32_t* __restrict__ xperm, int apply_w0, VBTables tb,
                                                    const double2* __restrict__ ETin, double2* __restrict__ ETout) {
     __shared__ double red[256];
@@ -201,12 +201,14 @@ __global__ __launch_bounds__(256) void k_update_w(const VTask* __restrict__ task
     const double cc = (double)tb.cc[a];
     const double cs = ((1 - rho) * so) + rho * (sigma_w + alpha * cc * 1.0);
     double2 et[MC];
+    uint32_t xp[MC];
     double e1 = 0.0, e2 = 0.0;
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
             et[j] = ETin[rw.start + x];
+            xp[j] = xperm[rw.start + x];
             if (apply_w0) {
                 et[j].x = et[j].x + dm;
                 et[j].y = et[j].y + ds;
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(256) void k_update_w(const VTask* __restrict__ task
                 o.x += dmu;
                 o.y += dsg;
             }
-            ETout[xperm[rw.start + x]] = o;
+            ETout[xp[j]] = o;
         }
     }
     for (uint32_t x = ci + MC * G; x < n; x += G) {
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(256) void k_update_w(const VTask* __restrict__ task
 }
 
 // update_v (:712-800) of factor f for the rows of one orientation
-__global__ __launch_bounds__(256) void k_update_v(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
+__global__ __launch_bounds__(256, 6) void k_update_v(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
                                                    const uint32_t* __restrict__ xperm, const uint32_t* __restrict__ part,
                                                    uint32_t f, VBTables tb, const double2* __restrict__ ETin,
                                                    double2* __restrict__ ETout) {
@@ -287,12 +289,14 @@ __global__ __launch_bounds__(256) void k_update_v(const VTask* __restrict__ task
     const double cc = (double)tb.cc[a];
     double hh[MC], hs[MC];
     double2 et[MC];
+    uint32_t xp[MC];  // the other order's positions, fetched with the partners (off the store's critical path)
     double e1 = 0.0, e2 = 0.0;
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
             const uint32_t pa = part[rw.start + x];
+            xp[j] = xperm[rw.start + x];
             hh[j] = v[pa];
             hs[j] = s[pa];
             et[j] = ETin[rw.start + x];
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(256) void k_update_v(const VTask* __restrict__ task
                 o.y += (h1 + h * h) * dsg;
                 o.y += h1 * dm2;
             }
-            ETout[xperm[rw.start + x]] = o;
+            ETout[xp[j]] = o;
         }
     }
     for (uint32_t x = ci + MC * G; x < n; x += G) {
