@@ -18,7 +18,8 @@ Single GPU:  python bench.py [--steps K --warmup W]
 Multi GPU:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
   one process per GPU; users/items are row-block partitioned (nnz balanced)
   and the fresh U / V blocks are exchanged with RCCL (grouped in-place
-  broadcasts over xGMI) between half-sweeps.  The dataset is fixed, so the
+  broadcasts over xGMI) between half-sweeps, the cross-rank residuals with a
+  grouped ncclSend/ncclRecv exchange.  The dataset is fixed, so the
   scaling is strong.  Rank 0 prints one JSON line.
 """
 import argparse
@@ -323,7 +324,7 @@ def main():
                                % (args.shape, args.K),
                    "num_users": dims[0], "num_items": dims[1], "n_train": n_train, "n_test": len(test[0]),
                    "K": args.K, "rng": "philox", "quirks": "final",
-                   "parallelism": "rows x%d (RCCL block broadcast)" % world,
+                   "parallelism": "rows x%d (%s)" % (world, "host-shm exchange, testing only" if os.environ.get("SBMF_COMM") == "host" else "RCCL block broadcast + p2p residual exchange"),
                    "test_rmse_after": main_res["rmse"], "sweeps_run": main_res["sweeps_run"],
                    "time_to_test_rmse_0.85": ttr,
                    "ms_user_half": main_res["ms_user"], "ms_item_half": main_res["ms_item"],
