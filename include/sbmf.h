@@ -226,6 +226,16 @@ int sbmf_load_triples(const char* path, sbmf_ratings* out);
  * item feature per line: the first feature is the user id, the second the
  * item id minus item_offset (users-first layout, e.g. data/m1m/m100k). */
 int sbmf_load_libfm(const char* path, uint32_t item_offset, sbmf_ratings* out);
+/* libFM binary input <stem>.x + <stem>.y (or .data + .target, preferred as in
+ * Data::load, Data.h:113-160): the files tools/convert.cpp:55-205 writes,
+ * layouts fmatrix.h:36-52 (sparse rows) and matrix.h:280-328 (targets).  Same
+ * one-user-one-item rule and item_offset meaning as sbmf_load_libfm.  Replaces
+ * the binary branch of Data::load (Data.h:115-160). */
+int sbmf_load_libfm_binary(const char* stem, uint32_t item_offset, sbmf_ratings* out);
+/* Writes <stem>.x / <stem>.y in that format (the convert tool's output for
+ * rating data): row q = {user[q]:1, item_offset + item[q]:1}, f32 targets;
+ * num_cols = max(num_cols, largest feature id + 1). */
+int sbmf_save_libfm_binary(const char* stem, const sbmf_ratings* in, uint32_t item_offset, uint32_t num_cols);
 void sbmf_free_ratings(sbmf_ratings* r);
 
 /* --- multi-GPU layout (host only) ---------------------------------------------------------- */

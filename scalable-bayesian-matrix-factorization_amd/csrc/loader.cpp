@@ -8,6 +8,7 @@
 //   blanks skipped, empty and '#' lines skipped, target read as DATA_FLOAT
 //   (float, fm_data.h:25), anything unparsable is an error.  The SBPMF path
 //   needs exactly two features per line: user id, then item id.
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -191,6 +192,165 @@ int sbmf_load_libfm(const char* path, uint32_t item_offset, sbmf_ratings* out) {
         p = le + 1;
     }
     return fill(out, u, i, r);
+}
+
+// ---- libFM binary input: <stem>.x (or .data) + <stem>.y (or .target), the
+// files tools/convert.cpp writes.  Layouts (fmatrix.h:36-52, matrix.h:280-328):
+//   .x  file_header {u32 id = 2; u32 float_size = 4; u64 num_values; u32 num_rows;
+//       u32 num_cols} (24 bytes, natural alignment), then per row u32 size and
+//       size x sparse_entry {u32 id; f32 value}
+//   .y  u32 version = 1; u32 float_size = 4; u32 num_rows; num_rows x f32
+// Data::load (Data.h:113-160) prefers .data/.target over .x/.y and asserts
+// target.dim == rows; the same order and checks apply here, as errors.
+namespace {
+struct FmHeader {
+    uint32_t id, float_size;
+    uint64_t num_values;
+    uint32_t num_rows, num_cols;
+};
+static_assert(sizeof(FmHeader) == 24, "fmatrix.h file_header layout");
+
+bool file_exists(const std::string& f) {
+    FILE* h = std::fopen(f.c_str(), "rb");
+    if (h) std::fclose(h);
+    return h != nullptr;
+}
+}  // namespace
+
+int sbmf_load_libfm_binary(const char* stem, uint32_t item_offset, sbmf_ratings* out) {
+    if (!stem || !out) return SBMF_E_ARG;
+    std::memset(out, 0, sizeof *out);
+    const std::string s(stem);
+    std::string xf, yf;
+    if (file_exists(s + ".data") && file_exists(s + ".target")) {
+        xf = s + ".data";
+        yf = s + ".target";
+    } else if (file_exists(s + ".x") && file_exists(s + ".y")) {
+        xf = s + ".x";
+        yf = s + ".y";
+    } else {
+        g_lerr = "unable to open " + s + ".x/.y (or .data/.target)";
+        return SBMF_E_IO;
+    }
+    std::vector<char> xb, yb;
+    if (!read_file(xf.c_str(), xb) || !read_file(yf.c_str(), yb)) {
+        g_lerr = "unable to open " + xf + " / " + yf;
+        return SBMF_E_IO;
+    }
+    // read_file appends one terminating byte
+    const size_t xn = xb.size() - 1, yn = yb.size() - 1;
+    if (yn < 12) {
+        g_lerr = yf + ": truncated header";
+        return SBMF_E_IO;
+    }
+    uint32_t yh[3];
+    std::memcpy(yh, yb.data(), 12);
+    if (yh[0] != 1 || yh[1] != sizeof(float) || yn < 12 + (size_t)yh[2] * sizeof(float)) {
+        g_lerr = yf + ": not a libFM DVector<float> file (version 1, 4-byte values)";
+        return SBMF_E_IO;
+    }
+    FmHeader h;
+    if (xn < sizeof h) {
+        g_lerr = xf + ": truncated header";
+        return SBMF_E_IO;
+    }
+    std::memcpy(&h, xb.data(), sizeof h);
+    if (h.id != 2 || h.float_size != sizeof(float)) {
+        g_lerr = xf + ": not a libFM sparse matrix file (id 2, 4-byte values)";
+        return SBMF_E_IO;
+    }
+    if (h.num_rows != yh[2]) {
+        g_lerr = xf + ": " + std::to_string(h.num_rows) + " rows but " + std::to_string(yh[2]) + " targets";
+        return SBMF_E_IO;
+    }
+    std::vector<uint32_t> u, i;
+    std::vector<double> r;
+    u.reserve(h.num_rows);
+    i.reserve(h.num_rows);
+    r.reserve(h.num_rows);
+    size_t at = sizeof h;
+    uint64_t nv = 0;
+    for (uint32_t row = 0; row < h.num_rows; ++row) {
+        uint32_t sz;
+        if (at + 4 > xn) {
+            g_lerr = xf + ": truncated at row " + std::to_string(row);
+            return SBMF_E_IO;
+        }
+        std::memcpy(&sz, xb.data() + at, 4);
+        at += 4;
+        if (at + (size_t)sz * 8 > xn) {
+            g_lerr = xf + ": truncated at row " + std::to_string(row);
+            return SBMF_E_IO;
+        }
+        uint32_t f0 = 0, f1 = 0;
+        if (sz == 2) {
+            std::memcpy(&f0, xb.data() + at, 4);
+            std::memcpy(&f1, xb.data() + at + 8, 4);
+        }
+        if (sz != 2 || f1 < item_offset) {
+            g_lerr = xf + " row " + std::to_string(row) +
+                     ": the SBPMF sampler needs exactly one user and one item feature per row";
+            return SBMF_E_IO;
+        }
+        at += (size_t)sz * 8;
+        nv += sz;
+        float t;
+        std::memcpy(&t, yb.data() + 12 + (size_t)row * 4, 4);
+        u.push_back(f0);
+        i.push_back(f1 - item_offset);
+        r.push_back((double)t);
+    }
+    if (nv != h.num_values) {
+        g_lerr = xf + ": header says " + std::to_string(h.num_values) + " values, rows hold " + std::to_string(nv);
+        return SBMF_E_IO;
+    }
+    return fill(out, u, i, r);
+}
+
+// the convert tool's output for rating data (tools/convert.cpp:55-205): row q
+// holds {user[q]:1, item_offset + item[q]:1}, target rating[q] as f32
+int sbmf_save_libfm_binary(const char* stem, const sbmf_ratings* in, uint32_t item_offset, uint32_t num_cols) {
+    if (!stem || !in || (in->n && (!in->user || !in->item || !in->rating))) return SBMF_E_ARG;
+    if (in->n > 0xffffffffull) return SBMF_E_ARG;
+    const std::string s(stem);
+    FILE* fx = std::fopen((s + ".x").c_str(), "wb");
+    FILE* fy = fx ? std::fopen((s + ".y").c_str(), "wb") : nullptr;
+    if (!fx || !fy) {
+        if (fx) std::fclose(fx);
+        g_lerr = "unable to write " + s + ".x/.y";
+        return SBMF_E_IO;
+    }
+    uint32_t cols = num_cols;
+    for (uint64_t q = 0; q < in->n; ++q) {
+        cols = std::max(cols, in->user[q] + 1);
+        cols = std::max(cols, item_offset + in->item[q] + 1);
+    }
+    const FmHeader h{2, (uint32_t)sizeof(float), 2 * in->n, (uint32_t)in->n, cols};
+    bool ok = std::fwrite(&h, sizeof h, 1, fx) == 1;
+    std::vector<char> row(4 + 16);
+    for (uint64_t q = 0; ok && q < in->n; ++q) {
+        const uint32_t sz = 2, a = in->user[q], b = item_offset + in->item[q];
+        const float one = 1.0f;
+        std::memcpy(row.data(), &sz, 4);
+        std::memcpy(row.data() + 4, &a, 4);
+        std::memcpy(row.data() + 8, &one, 4);
+        std::memcpy(row.data() + 12, &b, 4);
+        std::memcpy(row.data() + 16, &one, 4);
+        ok = std::fwrite(row.data(), row.size(), 1, fx) == 1;
+    }
+    const uint32_t yh[3] = {1, (uint32_t)sizeof(float), (uint32_t)in->n};
+    ok = ok && std::fwrite(yh, sizeof yh, 1, fy) == 1;
+    for (uint64_t q = 0; ok && q < in->n; ++q) {
+        const float t = (float)in->rating[q];
+        ok = std::fwrite(&t, 4, 1, fy) == 1;
+    }
+    ok = (std::fclose(fx) == 0) & ok;
+    ok = (std::fclose(fy) == 0) & ok;
+    if (!ok) {
+        g_lerr = "write error on " + s + ".x/.y";
+        return SBMF_E_IO;
+    }
+    return SBMF_OK;
 }
 
 void sbmf_free_ratings(sbmf_ratings* r) {

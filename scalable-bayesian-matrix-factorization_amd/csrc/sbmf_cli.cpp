@@ -102,9 +102,22 @@ bool looks_libfm(const std::string& path) {
     return false;
 }
 
+bool exists(const std::string& f) { return std::ifstream(f).good(); }
+
+// Data::load (Data.h:113-117) takes the binary pair <stem>.data/.target or
+// <stem>.x/.y when it exists, before the text file itself
+bool has_binary(const std::string& stem) {
+    return (exists(stem + ".data") && exists(stem + ".target")) || (exists(stem + ".x") && exists(stem + ".y"));
+}
+
 void load(const std::string& path, const std::string& fmt, uint32_t item_offset, sbmf_ratings& r) {
-    const bool libfm = fmt == "libfm" || (fmt == "auto" && looks_libfm(path));
-    const int rc = libfm ? sbmf_load_libfm(path.c_str(), item_offset, &r) : sbmf_load_triples(path.c_str(), &r);
+    int rc;
+    if (fmt == "binary" || (fmt == "auto" && has_binary(path))) {
+        rc = sbmf_load_libfm_binary(path.c_str(), item_offset, &r);
+    } else {
+        const bool libfm = fmt == "libfm" || (fmt == "auto" && looks_libfm(path));
+        rc = libfm ? sbmf_load_libfm(path.c_str(), item_offset, &r) : sbmf_load_triples(path.c_str(), &r);
+    }
     if (rc != SBMF_OK) throw std::runtime_error(sbmf_loader_error());
 }
 
@@ -167,7 +180,7 @@ int main(int argc, char** argv) {
                          "(biased sampler, top-level gibbs_sbpmf2.cpp / gibbs_sbpmf22.cpp; needs -dim '1,1,K')");
         cl.reg("precision", "f64 (default) | f32");
         cl.reg("burnin", "burn-in sweeps before collection; default=0");
-        cl.reg("format", "auto (default) | triple | libfm");
+        cl.reg("format", "auto (default: <name>.x/.y binary if present, else triple or libfm text) | triple | libfm | binary");
         cl.reg("item_offset", "libFM input: item feature id offset; default=0");
         cl.reg("device", "HIP device ordinal; default=0");
         cl.reg("recompute_every", "recompute residuals from scratch every n sweeps; default=1");

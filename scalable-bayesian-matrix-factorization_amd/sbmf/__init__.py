@@ -23,7 +23,7 @@ from . import _lib
 from ._lib import (F32, F64, METHOD_MCMC, METHOD_VB, QUIRKS_BIAS2, QUIRKS_BIAS22, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
                    SBMF_E_COMM, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_NOMEM, SBMF_E_STATE, SBMF_OK)
 
-__all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "config_default",
+__all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "load_libfm_binary", "save_libfm_binary", "config_default",
            "RNG_REFERENCE", "RNG_PHILOX", "QUIRKS_FINAL", "QUIRKS_SBPMF2", "QUIRKS_NONE",
            "QUIRKS_BIAS2", "QUIRKS_BIAS22", "F64", "F32"]
 
@@ -85,6 +85,34 @@ def load_triples(path):
         return _from_ratings(r)
     finally:
         lib.sbmf_free_ratings(C.byref(r))
+
+
+def load_libfm_binary(stem, item_offset=0):
+    """libFM binary <stem>.x/.y (or .data/.target), Data.h:113-160; one user and
+    one item feature per row."""
+    r = _lib.Ratings()
+    rc = lib.sbmf_load_libfm_binary(str(stem).encode(), item_offset, C.byref(r))
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_loader_error().decode())
+    try:
+        return _from_ratings(r)
+    finally:
+        lib.sbmf_free_ratings(C.byref(r))
+
+
+def save_libfm_binary(stem, data, item_offset=0, num_cols=0):
+    """Write <stem>.x / <stem>.y as tools/convert.cpp does for rating data."""
+    u = np.ascontiguousarray(data.user, dtype=np.uint32)
+    i = np.ascontiguousarray(data.item, dtype=np.uint32)
+    v = np.ascontiguousarray(data.rating, dtype=np.float64)
+    r = _lib.Ratings()
+    r.n = len(u)
+    r.user = u.ctypes.data_as(C.POINTER(C.c_uint32))
+    r.item = i.ctypes.data_as(C.POINTER(C.c_uint32))
+    r.rating = v.ctypes.data_as(C.POINTER(C.c_double))
+    rc = lib.sbmf_save_libfm_binary(str(stem).encode(), C.byref(r), item_offset, num_cols)
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_loader_error().decode())
 
 
 def load_libfm(path, item_offset=0):

@@ -54,3 +54,17 @@ def test_valid_command_fails_loudly_without_gpu(tmp_path):
     tr.write_text("0\t0\t5\n1\t1\t3\n")
     r = run("-task", "r", "-train", str(tr), "-test", str(tr), "-dim", "1,1,8", "-iter", "2")
     assert r.returncode == 1 and "no HIP device" in r.stderr
+
+
+@pytest.mark.skipif(gpu_available(), reason="no-GPU path")
+def test_binary_stem_loaded_before_device(tmp_path):
+    """-train <stem> with <stem>.x/.y present takes the binary branch (Data.h:113-117);
+    a loader error would surface before the device check."""
+    import sbmf
+    stem = str(tmp_path / "bin")
+    sbmf.save_libfm_binary(stem, sbmf.Data([0, 1], [0, 1], [5.0, 3.0]), item_offset=2)
+    r = run("-task", "r", "-train", stem, "-test", stem, "-dim", "1,1,8", "-iter", "2", "--item_offset", "2")
+    assert r.returncode == 1 and "no HIP device" in r.stderr
+    r = run("-task", "r", "-train", stem, "-test", stem, "-dim", "1,1,8", "-iter", "2", "--format", "binary",
+            "--item_offset", "3")
+    assert r.returncode == 1 and "one user and one item" in r.stderr
