@@ -370,6 +370,7 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             worker.join();
         }
         VBLayout& L = lay[epoch & 1];
+        const auto h1 = std::chrono::steady_clock::now();
         upload_grow(L.d_urows, L.urows, st);
         upload_grow(L.d_irows, L.irows, st);
         upload_grow(L.d_u2i, L.u2i, st);
@@ -380,6 +381,10 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         upload_grow(L.d_utasks, L.utasks, st);
         upload_grow(L.d_itasks, L.itasks, st);
         ms_layout = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+        if (std::getenv("SBMF_VB_TRACE"))  // host side of an epoch: layout wait / build, then uploads
+            std::fprintf(stderr, "[vbo] epoch %u host: layout %.1f ms, upload %.1f ms\n", epoch,
+                         std::chrono::duration<double, std::milli>(h1 - h0).count(),
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h1).count());
         n_launch = 0;
         HIPCHK(hipEventRecord(ev[0], st));
         double2* ETu = d_ETu.as<double2>();
