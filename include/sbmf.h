@@ -110,11 +110,17 @@ typedef struct sbmf_config {
                                  bit 2 = power-of-two waves per Gram-block row (2/4/8) instead
                                          of ceil(ratings / ratings-per-wave),
                                  bit 3 = f64 rows of 33..64 ratings on two 8-vector waves instead
-                                         of one 16-vector wave                                   */
+                                         of one 16-vector wave,
+                                 bit 5 = streaming kernel on one 16-wave workgroup per CU
+                                         (default: two 8-wave workgroups)                        */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */
-    uint32_t reserved[2];
+    uint32_t average;         /* running mean of the test prediction: 0 = quirk-set default
+                                 (sum / (sweep + 1), gibbs_sbpmf_final.cpp:559, which counts
+                                 burn-in sweeps; quirks none: collected sweeps), 1 = sum over
+                                 the collected sweeps / their number, 2 = sum / (sweep + 1)       */
+    uint32_t reserved[1];
 } sbmf_config;
 
 /* Per-sweep report passed to the run callback. */

@@ -18,6 +18,8 @@ typedef struct {
     int quirks;
     double init_stdev, clamp_lo, clamp_hi;
     double sweep_seconds_limit; /* >0: stop after this many seconds (bounded CPU baseline) */
+    int rng;                    /* 0: glibc rand() stream (the reference's); 1: the GPU build's Philox
+                                   stream mode (unbiased samplers only) */
 } oracle_config;
 
 typedef struct {

@@ -702,21 +702,28 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
 // stores -> agent release -> counter; poll -> agent acquire -> loads, the
 // CDNA guide's G16 hand-off); every chunk sums them in chunk order, so all
 // chunks draw identical coordinates.  Wave w owns vectors w, w+NW, ...
-// Padding of a task's LDS arrays: two traversal strides (4*NW*UNR <= 256
-// ratings) -- the task rounded up to a stride, plus the group a prefetching
-// traversal reads past its end.  The residual array is followed by 8 x 64
-// per-lane sink slots for masked-off stores.
-constexpr uint32_t GSTREAM_PAD = 2 * 4 * 8 * 8;
-constexpr uint32_t GSTREAM_SINK = 8 * 64;
-// dynamic LDS: [cmax+pad] partner ids, then (16-byte aligned) [cmax+pad+sink] residuals
-__host__ __device__ constexpr size_t gstream_ids_bytes(uint32_t cmax) {
-    return ((size_t)(cmax + GSTREAM_PAD) * sizeof(uint32_t) + 15) / 16 * 16;
-}
-template <typename T>
-__host__ __device__ constexpr size_t gstream_dyn_bytes(uint32_t cmax) {
-    return gstream_ids_bytes(cmax) + (size_t)(cmax + GSTREAM_PAD + GSTREAM_SINK) * sizeof(T);
-}
-
+// LDS geometry of a task, derived from the workgroup shape (NW waves, UNR
+// vectors of 4 ratings per wave per group):
+//   STRIDE  ratings one traversal group covers across the workgroup;
+//   PAD     slots past the task's end: the task rounded up to a stride, plus
+//           the group a prefetching traversal reads past its end (the padded
+//           slots hold the zero partner row and zero residuals);
+//   SINK    one private slot per lane of every wave, the target of the
+//           masked-off residual stores (eDummy below).
+template <int NW, int UNR>
+struct GsGeom {
+    static constexpr uint32_t STRIDE = 4 * NW * UNR;
+    static constexpr uint32_t PAD = 2 * STRIDE;
+    static constexpr uint32_t SINK = 64 * NW;
+    // dynamic LDS: [cmax+PAD] partner ids, then (16-byte aligned) [cmax+PAD+SINK] residuals
+    static __host__ __device__ constexpr size_t ids_bytes(uint32_t cmax) {
+        return ((size_t)(cmax + PAD) * sizeof(uint32_t) + 15) / 16 * 16;
+    }
+    template <typename T>
+    static __host__ __device__ constexpr size_t dyn_bytes(uint32_t cmax) {
+        return ids_bytes(cmax) + (size_t)(cmax + PAD + SINK) * sizeof(T);
+    }
+};
 // SIDE (0 users, 1 items) only names the instantiation, so profiles tell the
 // two half-sweeps apart.
 template <typename T, int NW, int UNR, bool SW, int SIDE>
@@ -737,7 +744,8 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
     __shared__ T Dsh[GB];             // SW: the block's D from the solving wave
     extern __shared__ unsigned char dyn_lds[];
     uint32_t* pjL = reinterpret_cast<uint32_t*>(dyn_lds);  // [cmax+pad] partner ids
-    T* eL = reinterpret_cast<T*>(dyn_lds + gstream_ids_bytes(sy.cmax));  // [cmax+pad] residuals
+    typedef GsGeom<NW, UNR> Geo;
+    T* eL = reinterpret_cast<T*>(dyn_lds + Geo::ids_bytes(sy.cmax));  // [cmax+PAD] residuals
     const T tau = a.tau;
     const uint32_t nblk = (K + GB - 1) / GB;
 
@@ -777,7 +785,8 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
         // ---- stage the task's partner ids and initial residuals in LDS; the
         // slots up to the traversal stride (4*NW*UNR ratings) hold the zero
         // row and zero residuals, so the traversal needs no per-rating masks
-        const uint32_t npad = (n + 4 * NW * UNR - 1) / (4 * NW * UNR) * (4 * NW * UNR) + 4 * NW * UNR;
+        // npad <= cmax + PAD: n rounded up to a stride, plus one stride
+        const uint32_t npad = (n + Geo::STRIDE - 1) / Geo::STRIDE * Geo::STRIDE + Geo::STRIDE;
         for (uint32_t x = threadIdx.x; x < npad; x += 64 * NW) pjL[x] = x < n ? a.part[beg + x] : a.zrow;
         for (uint32_t x = n + threadIdx.x; x < npad; x += 64 * NW) eL[x] = T(0);
         if (a.e_from_dot) {
@@ -808,7 +817,8 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
         //   PH 2: t = nblk  apply the last block, emit residuals
         // All loads are unconditional: the unused slice of phases 0 / 2 reads
         // a valid column (padding / slack row) and is ignored.
-        T* const eDummy = eL + (size_t)(sy.cmax + GSTREAM_PAD) + 64 * wr;  // per-lane sink of masked stores
+        static_assert(Geo::SINK >= 64 * NW, "every lane of every wave needs its own sink slot");
+        T* const eDummy = eL + (size_t)(sy.cmax + Geo::PAD) + 64 * wr;  // per-lane sink of masked stores
         for (uint32_t t = 0; t <= nblk; ++t) {
             const bool app = t > 0, acc = t < nblk;
             const uint32_t kc = t * GB + ci;
@@ -1642,8 +1652,13 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
 
 // Default: the block solve by one wave, D handed to the others in LDS;
 // tune bit 0: every wave solves redundantly (no extra barrier).
-static int gstream_nw(uint32_t) { return 8; }
-int gstream_wg_target(uint32_t) { return 2; }
+// tune bit 5: 16-wave workgroups (UNR 4), one per CU, instead of two 8-wave ones.
+static int gstream_nw(uint32_t tune) { return (tune & 32u) ? 16 : 8; }
+int gstream_wg_target(uint32_t tune) { return (tune & 32u) ? 1 : 2; }
+template <typename T>
+static size_t gstream_dyn(uint32_t tune, uint32_t cmax) {
+    return (tune & 32u) ? GsGeom<16, 4>::dyn_bytes<T>(cmax) : GsGeom<8, 8>::dyn_bytes<T>(cmax);
+}
 
 template <typename T>
 hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st) {
@@ -1674,9 +1689,13 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
 
 template <typename T>
 static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
-    if (side)
-        return (tune & 1u) ? (const void*)k_gstream<T, 8, 8, false, 1> : (const void*)k_gstream<T, 8, 8, true, 1>;
-    return (tune & 1u) ? (const void*)k_gstream<T, 8, 8, false, 0> : (const void*)k_gstream<T, 8, 8, true, 0>;
+    const bool sw = !(tune & 1u);
+    if (tune & 32u) {
+        if (side) return sw ? (const void*)k_gstream<T, 16, 4, true, 1> : (const void*)k_gstream<T, 16, 4, false, 1>;
+        return sw ? (const void*)k_gstream<T, 16, 4, true, 0> : (const void*)k_gstream<T, 16, 4, false, 0>;
+    }
+    if (side) return sw ? (const void*)k_gstream<T, 8, 8, true, 1> : (const void*)k_gstream<T, 8, 8, false, 1>;
+    return sw ? (const void*)k_gstream<T, 8, 8, true, 0> : (const void*)k_gstream<T, 8, 8, false, 0>;
 }
 
 template <typename T>
@@ -1688,7 +1707,8 @@ uint32_t gstream_cmax(uint32_t tune) {
     (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
     // gstream_wg_target workgroups per CU: static + [ids | residuals] each
     const long per_wg = lds_cu / gstream_wg_target(tune) - (long)fa.sharedSizeBytes - 16;
-    const long c = (per_wg - (long)(GSTREAM_SINK * sizeof(T))) / (long)(sizeof(uint32_t) + sizeof(T)) - (long)GSTREAM_PAD;
+    const long fixed = (long)gstream_dyn<T>(tune, 0);  // PAD ids + PAD and SINK residuals (+ alignment)
+    const long c = (per_wg - fixed) / (long)(sizeof(uint32_t) + sizeof(T));
     const long cap = sizeof(T) == 8 ? 4096 : 8192;
     return (uint32_t)std::max(256L, std::min(cap, c) / 64 * 64);
 }
@@ -1696,7 +1716,7 @@ uint32_t gstream_cmax(uint32_t tune) {
 template <typename T>
 int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune) {
     int n = 0;
-    const size_t dyn = gstream_dyn_bytes<T>(cmax);
+    const size_t dyn = gstream_dyn<T>(tune, cmax);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gstream_fn<T>(tune), 64 * gstream_nw(tune), dyn) != hipSuccess)
         return 1;
     return n;
@@ -1718,7 +1738,7 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     HalfArgs<T> ap = a;
     SplitSync syp = sy;
     void* args[] = {(void*)&tp, (void*)&ntask, (void*)&ap, (void*)&syp};
-    const size_t dyn = gstream_dyn_bytes<T>(sy.cmax);
+    const size_t dyn = gstream_dyn<T>(a.tune, sy.cmax);
     err = hipLaunchCooperativeKernel(gstream_fn<T>(a.tune, a.tag == TAG_ITEMS ? 1u : 0u), dim3(std::min(grid, ntask)),
                                      dim3(64 * gstream_nw(a.tune)),
                                      args, (unsigned)dyn, st);

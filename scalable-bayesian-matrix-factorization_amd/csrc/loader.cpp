@@ -181,9 +181,10 @@ int sbmf_load_libfm(const char* path, uint32_t item_offset, sbmf_ratings* out) {
             if (nf < 3) feats[nf] = id;
             ++nf;
         }
-        if (nf != 2 || feats[0] < 0 || feats[1] < (long)item_offset) {
+        if (nf != 2 || feats[0] < 0 || feats[1] < (long)item_offset || (item_offset > 0 && feats[0] >= (long)item_offset)) {
             g_lerr = "libFM line " + std::to_string(lineno) + " of " + path +
-                     ": the SBPMF sampler needs exactly one user and one item feature per line";
+                     ": the SBPMF sampler needs exactly one user and one item feature per line" +
+                     (item_offset > 0 ? " (user id < item_offset <= item id)" : "");
             return SBMF_E_IO;
         }
         u.push_back((uint32_t)feats[0]);
@@ -287,9 +288,10 @@ int sbmf_load_libfm_binary(const char* stem, uint32_t item_offset, sbmf_ratings*
             std::memcpy(&f0, xb.data() + at, 4);
             std::memcpy(&f1, xb.data() + at + 8, 4);
         }
-        if (sz != 2 || f1 < item_offset) {
+        if (sz != 2 || f1 < item_offset || (item_offset > 0 && f0 >= item_offset)) {
             g_lerr = xf + " row " + std::to_string(row) +
-                     ": the SBPMF sampler needs exactly one user and one item feature per row";
+                     ": the SBPMF sampler needs exactly one user and one item feature per row" +
+                     (item_offset > 0 ? " (user id < item_offset <= item id)" : "");
             return SBMF_E_IO;
         }
         at += (size_t)sz * 8;
@@ -312,6 +314,17 @@ int sbmf_load_libfm_binary(const char* stem, uint32_t item_offset, sbmf_ratings*
 int sbmf_save_libfm_binary(const char* stem, const sbmf_ratings* in, uint32_t item_offset, uint32_t num_cols) {
     if (!stem || !in || (in->n && (!in->user || !in->item || !in->rating))) return SBMF_E_ARG;
     if (in->n > 0xffffffffull) return SBMF_E_ARG;
+    // feature ids are written as uint32 and num_cols = max id + 1 must fit too:
+    // computed in 64 bits, anything past UINT32_MAX - 1 is refused (no wrap)
+    uint64_t cols = num_cols;
+    for (uint64_t q = 0; q < in->n; ++q) {
+        cols = std::max<uint64_t>(cols, (uint64_t)in->user[q] + 1);
+        cols = std::max<uint64_t>(cols, (uint64_t)item_offset + in->item[q] + 1);
+    }
+    if (cols > 0xffffffffull) {
+        g_lerr = "feature id past UINT32_MAX - 1 (item_offset + item id): not representable in the .x format";
+        return SBMF_E_ARG;
+    }
     const std::string s(stem);
     FILE* fx = std::fopen((s + ".x").c_str(), "wb");
     FILE* fy = fx ? std::fopen((s + ".y").c_str(), "wb") : nullptr;
@@ -320,12 +333,7 @@ int sbmf_save_libfm_binary(const char* stem, const sbmf_ratings* in, uint32_t it
         g_lerr = "unable to write " + s + ".x/.y";
         return SBMF_E_IO;
     }
-    uint32_t cols = num_cols;
-    for (uint64_t q = 0; q < in->n; ++q) {
-        cols = std::max(cols, in->user[q] + 1);
-        cols = std::max(cols, item_offset + in->item[q] + 1);
-    }
-    const FmHeader h{2, (uint32_t)sizeof(float), 2 * in->n, (uint32_t)in->n, cols};
+    const FmHeader h{2, (uint32_t)sizeof(float), 2 * in->n, (uint32_t)in->n, (uint32_t)cols};
     bool ok = std::fwrite(&h, sizeof h, 1, fx) == 1;
     std::vector<char> row(4 + 16);
     for (uint64_t q = 0; ok && q < in->n; ++q) {

@@ -278,6 +278,11 @@ enum { RES_ESQ = 0, RES_TRSQ = 1, RES_TEST_AVG = 2, RES_TEST_THIS = 3, RES_ES = 
 
 static size_t tsize(const sbmf_ctx* c) { return c->cfg.precision == SBMF_F32 ? 4 : 8; }
 
+// running-mean divisor: collected sweeps (average 1, or quirks none by default) or sweep + 1
+static bool avg_collected(const sbmf_config& cf) {
+    return cf.average == 1 || (cf.average == 0 && cf.quirks == SBMF_QUIRKS_NONE);
+}
+
 template <typename T>
 static std::vector<T> to_T(const std::vector<double>& v) {
     return std::vector<T>(v.begin(), v.end());
@@ -1040,7 +1045,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // ---- 5. evaluation
         const bool collect = q2 ? true : (c->sweep >= cf.burnin);
         if (collect) c->collected++;
-        const double div = (cf.quirks == SBMF_QUIRKS_NONE) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
+        const double div = avg_collected(cf) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
         const uint64_t T_ = c->su.size();
         if (cf.eval_test && T_) {
             HIPCHK(launch_test<T>(c->d_tu.as<uint32_t>(), c->d_ti.as<uint32_t>(), c->d_tr.as<double>(), c->t0, c->t1,
@@ -1195,6 +1200,7 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     if (cfg->num_factor == 0 || cfg->num_factor > 256) sbmf::fail(SBMF_E_ARG, "num_factor must be in [1,256]");
     if (cfg->rng_mode != SBMF_RNG_REFERENCE && cfg->rng_mode != SBMF_RNG_PHILOX) sbmf::fail(SBMF_E_ARG, "bad rng_mode");
     if (cfg->quirks < 0 || cfg->quirks > 4) sbmf::fail(SBMF_E_ARG, "bad quirks");
+    if (cfg->average > 2) sbmf::fail(SBMF_E_ARG, "bad average (0 default, 1 collected sweeps, 2 sweep + 1)");
     if (cfg->precision != SBMF_F64 && cfg->precision != SBMF_F32) sbmf::fail(SBMF_E_ARG, "bad precision");
     if (cfg->method != SBMF_METHOD_MCMC && cfg->method != SBMF_METHOD_VB) sbmf::fail(SBMF_E_ARG, "bad method");
     if (cfg->method == SBMF_METHOD_VB && cfg->precision != SBMF_F64)
@@ -1348,7 +1354,7 @@ int sbmf_predict(sbmf_ctx* ctx, double* out) {
     if (ctx->nranks > 1) ctx->comm.bcast_ranges(ctx->d_tsum.p, sizeof(double), ctx->tbounds, ctx->st);
     HIPCHK(hipStreamSynchronize(ctx->st));
     HIPCHK(hipMemcpy(out, ctx->d_tsum.p, T_ * sizeof(double), hipMemcpyDeviceToHost));
-    const double div = ctx->cfg.quirks == SBMF_QUIRKS_NONE ? (double)std::max(1u, ctx->collected) : (double)std::max(1u, ctx->sweep);
+    const double div = sbmf::avg_collected(ctx->cfg) ? (double)std::max(1u, ctx->collected) : (double)std::max(1u, ctx->sweep);
     for (uint64_t t = 0; t < T_; ++t) out[t] /= div;
     API_END(ctx)
 }

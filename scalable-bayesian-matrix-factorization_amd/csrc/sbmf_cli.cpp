@@ -180,6 +180,8 @@ int main(int argc, char** argv) {
                          "(biased sampler, top-level gibbs_sbpmf2.cpp / gibbs_sbpmf22.cpp; needs -dim '1,1,K')");
         cl.reg("precision", "f64 (default) | f32");
         cl.reg("burnin", "burn-in sweeps before collection; default=0");
+        cl.reg("average", "running-mean divisor: default (quirk set) | collected (collected sweeps only) | "
+                          "reference (sweep + 1, counts burn-in as gibbs_sbpmf_final.cpp:559 does)");
         cl.reg("format", "auto (default: <name>.x/.y binary if present, else triple or libfm text) | triple | libfm | binary");
         cl.reg("item_offset", "libFM input: item feature id offset; default=0");
         cl.reg("device", "HIP device ordinal; default=0");
@@ -220,6 +222,13 @@ int main(int argc, char** argv) {
         cfg.num_factor = (uint32_t)dim[2];
         cfg.num_iter = (uint32_t)cl.getl("iter", 100);
         cfg.burnin = (uint32_t)cl.getl("burnin", 0);
+        {
+            const std::string av = cl.get("average", "default");
+            if (av == "default") cfg.average = 0;
+            else if (av == "collected") cfg.average = 1;
+            else if (av == "reference") cfg.average = 2;
+            else throw std::runtime_error("unknown -average " + av);
+        }
         cfg.seed = (uint64_t)cl.getl("seed", 1);
         const std::string rng = cl.get("rng", "ref");
         cfg.rng_mode = rng == "philox" ? SBMF_RNG_PHILOX : SBMF_RNG_REFERENCE;
@@ -278,6 +287,7 @@ int main(int argc, char** argv) {
         std::ofstream rlog;
         if (cl.has("rlog") && !cl.get("rlog", "").empty()) {
             rlog.open(cl.get("rlog", ""));
+            rlog.precision(17);  // our own diagnostic file: full precision (the libFM outputs keep the default 6)
             rlog << "iter\trmse\trmse_this\trmse_train\ttau\tms_sweep\tms_eval\n";
             rs.rlog = &rlog;
         }

@@ -370,7 +370,23 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             worker.join();
         }
         VBLayout& L = lay[epoch & 1];
+        // SBMF_VB_TRACE=1: the host side of an epoch -- layout wait / build, device
+        // (re)allocation of the layout buffers (first epochs), and the uploads timed to
+        // their completion (the stream is drained before and after, trace runs only)
+        const bool trace = std::getenv("SBMF_VB_TRACE") != nullptr;
+        if (trace) HIPCHK(hipStreamSynchronize(st));
         const auto h1 = std::chrono::steady_clock::now();
+        auto grow = [](DBuf& d, size_t bytes) { d.ensure(std::max<size_t>(bytes, 1)); };
+        grow(L.d_urows, L.urows.size() * sizeof(L.urows[0]));
+        grow(L.d_irows, L.irows.size() * sizeof(L.irows[0]));
+        grow(L.d_u2i, L.u2i.size() * sizeof(L.u2i[0]));
+        grow(L.d_upart, L.upart.size() * sizeof(L.upart[0]));
+        grow(L.d_ur, L.ur.size() * sizeof(L.ur[0]));
+        grow(L.d_i2u, L.i2u.size() * sizeof(L.i2u[0]));
+        grow(L.d_ipart, L.ipart.size() * sizeof(L.ipart[0]));
+        grow(L.d_utasks, L.utasks.size() * sizeof(L.utasks[0]));
+        grow(L.d_itasks, L.itasks.size() * sizeof(L.itasks[0]));
+        const auto h2 = std::chrono::steady_clock::now();
         upload_grow(L.d_urows, L.urows, st);
         upload_grow(L.d_irows, L.irows, st);
         upload_grow(L.d_u2i, L.u2i, st);
@@ -380,11 +396,16 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         upload_grow(L.d_ipart, L.ipart, st);
         upload_grow(L.d_utasks, L.utasks, st);
         upload_grow(L.d_itasks, L.itasks, st);
+        if (trace) {
+            HIPCHK(hipStreamSynchronize(st));
+            const auto h3 = std::chrono::steady_clock::now();
+            auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+                return std::chrono::duration<double, std::milli>(b - a).count();
+            };
+            std::fprintf(stderr, "[vbo] epoch %u host: layout %.1f ms, device alloc %.1f ms, upload %.1f ms (to completion)\n",
+                         epoch, ms(h0, h1), ms(h1, h2), ms(h2, h3));
+        }
         ms_layout = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
-        if (std::getenv("SBMF_VB_TRACE"))  // host side of an epoch: layout wait / build, then uploads
-            std::fprintf(stderr, "[vbo] epoch %u host: layout %.1f ms, upload %.1f ms\n", epoch,
-                         std::chrono::duration<double, std::milli>(h1 - h0).count(),
-                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h1).count());
         n_launch = 0;
         HIPCHK(hipEventRecord(ev[0], st));
         double2* ETu = d_ETu.as<double2>();

@@ -37,6 +37,13 @@ class SBMFError(RuntimeError):
 
 
 def _u32(a):
+    """ids as uint32, refusing values the cast would wrap (negative or >= 2^32)."""
+    a = np.asarray(a)
+    if a.dtype != np.uint32 and a.size:
+        if a.dtype.kind == "f" and not np.all(np.isfinite(a) & (a == np.floor(a))):
+            raise ValueError("ids must be integers")
+        if a.min() < 0 or a.max() > 0xffffffff:
+            raise ValueError("ids must be in [0, 2^32 - 1]")
     return np.ascontiguousarray(a, dtype=np.uint32)
 
 
@@ -102,8 +109,10 @@ def load_libfm_binary(stem, item_offset=0):
 
 def save_libfm_binary(stem, data, item_offset=0, num_cols=0):
     """Write <stem>.x / <stem>.y as tools/convert.cpp does for rating data."""
-    u = np.ascontiguousarray(data.user, dtype=np.uint32)
-    i = np.ascontiguousarray(data.item, dtype=np.uint32)
+    u, i = _u32(data.user), _u32(data.item)  # refuses negative / >= 2^32 ids before the cast
+    # the .x format holds feature ids (user, item_offset + item) as uint32 with num_cols = max + 1
+    if len(u) and (int(u.max()) > 0xfffffffe or int(i.max()) + int(item_offset) > 0xfffffffe):
+        raise ValueError("feature ids must stay below 2^32 - 1 in the libFM binary format")
     v = np.ascontiguousarray(data.rating, dtype=np.float64)
     r = _lib.Ratings()
     r.n = len(u)
@@ -149,7 +158,8 @@ class FMLearnSBPMF:
 
     def __init__(self, num_factor=20, num_iter=100, seed=1, rng="ref", quirks="final", precision="f64", burnin=0,
                  device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, row_kernel=0,
-                 stream_threshold=0, split_chunk=0, tune=0, method="mcmc", vb_batches=0, **hyper):
+                 stream_threshold=0, split_chunk=0, tune=0, method="mcmc", vb_batches=0, average="default",
+                 **hyper):
         self.cfg = config_default()
         if method not in ("mcmc", "vb", "vb_online"):
             raise ValueError("method must be mcmc or vb")
@@ -172,6 +182,8 @@ class FMLearnSBPMF:
         self.cfg.stream_threshold = stream_threshold
         self.cfg.split_chunk = split_chunk
         self.cfg.tune = tune
+        # running-mean divisor: "default" (quirk set), "collected" (collected sweeps), "reference" (sweep + 1)
+        self.cfg.average = {"default": 0, "collected": 1, "reference": 2}[average]
         for k, v in hyper.items():
             setattr(self.cfg, k, v)
         self.ctx = None

@@ -31,7 +31,7 @@ class Config(C.Structure):
         ("recompute_every", C.c_uint32), ("eval_train", C.c_uint32), ("eval_test", C.c_uint32),
         ("gram_threshold", C.c_uint32), ("row_kernel", C.c_uint32), ("stream_threshold", C.c_uint32),
         ("split_chunk", C.c_uint32), ("tune", C.c_uint32), ("method", C.c_uint32), ("vb_batches", C.c_uint32),
-        ("reserved", C.c_uint32 * 2),
+        ("average", C.c_uint32), ("reserved", C.c_uint32 * 1),
     ]
 
 

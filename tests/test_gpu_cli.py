@@ -1,0 +1,89 @@
+"""The `sbmf` command line end to end on the GPU: the libFM outputs a user of
+`bin/libFM -task r -method mcmc` reads (fm_learn_mcmc_simultaneous.h:57-62,
+146, 244; libfm.cpp:629-634), checked against the compiled reference's
+golden trajectory and the oracle.
+
+Tolerances: the libFM-format files carry the reference's default 6
+significant digits, so they are compared within 2e-6 (rounding + the 1e-6
+parity bar); the full-precision -rlog is compared within 1e-6."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden_rmse
+from sbmf._lib import CLI_PATH
+
+pytestmark = pytest.mark.gpu
+
+ITER_RE = re.compile(r"^#Iter=([ \d]{3,})\tTrain=([-+0-9.eEnai]+)\tTest=([-+0-9.eEnai]+)$")
+
+
+def _write(path, data):
+    u, i, r = data
+    with open(path, "w") as f:
+        for a, b, c in zip(u, i, r):
+            f.write("%d\t%d\t%g\n" % (a, b, c))
+
+
+def _cli(tmp_path, ml100k, *args):
+    tr, te = tmp_path / "train.tsv", tmp_path / "test.tsv"
+    _write(tr, ml100k[0])
+    _write(te, ml100k[1])
+    cmd = [CLI_PATH, "-task", "r", "-train", str(tr), "-test", str(te), *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    return r
+
+
+def _rlog(path):
+    rows = [l.split("\t") for l in open(path).read().splitlines()[1:]]
+    return np.array([float(x[1]) for x in rows])
+
+
+def test_cli_mcmc_k20_matches_reference_golden(tmp_path, ml100k):
+    """bin/libFM-style run: stdout #Iter lines, test_rmse_0020_mcmc (truncated,
+    one running-mean RMSE per line), -out predictions, -rlog."""
+    r = _cli(tmp_path, ml100k, "-dim", "0,0,20", "-iter", "100", "-seed", "1", "-method", "mcmc",
+             "-out", str(tmp_path / "pred.txt"), "-rlog", str(tmp_path / "rlog.tsv"))
+    gold = golden_rmse("ref_final_ml100k_k20_s1.txt")
+    lines = [l for l in r.stdout.splitlines() if l.startswith("#Iter")]
+    assert len(lines) == 100
+    for k, l in enumerate(lines):
+        m = ITER_RE.match(l)
+        assert m, repr(l)
+        assert int(m.group(1)) == k and len(m.group(1)) == 3  # std::setw(3)
+        assert abs(float(m.group(3)) - gold[k]) < 2e-6
+    f = tmp_path / "test_rmse_0020_mcmc"
+    vals = np.array([float(x) for x in f.read_text().split()])
+    assert vals.shape == gold.shape
+    assert np.abs(vals - gold).max() < 2e-6
+    assert np.abs(_rlog(tmp_path / "rlog.tsv") - gold).max() < 1e-6
+    o = oracle.run(*ml100k, K=20, iters=100, seed=1, want_factors=False)
+    pred = np.array([float(x) for x in (tmp_path / "pred.txt").read_text().split()])
+    assert pred.shape == (len(ml100k[1][0]),)
+    assert np.abs(pred - o["pred_sum"] / 100).max() < 1e-5
+
+
+def test_cli_truncates_rmse_file_and_runs_config1_k8(tmp_path, ml100k):
+    """BASELINE config 1 (ML-100k, K=8) through the CLI; a stale
+    test_rmse_0008_mcmc is truncated at start (fm_learn_mcmc_simultaneous.h:61)."""
+    (tmp_path / "test_rmse_0008_mcmc").write_text("stale\n" * 500)
+    _cli(tmp_path, ml100k, "-dim", "0,0,8", "-iter", "30", "-seed", "7", "-rlog", str(tmp_path / "rlog.tsv"))
+    o = oracle.run(*ml100k, K=8, iters=30, seed=7, want_factors=False)
+    vals = (tmp_path / "test_rmse_0008_mcmc").read_text().split()
+    assert len(vals) == 30
+    assert np.abs(np.array([float(x) for x in vals]) - o["rmse"]).max() < 2e-6
+    assert np.abs(_rlog(tmp_path / "rlog.tsv") - o["rmse"]).max() < 1e-6
+
+
+def test_cli_philox_bench_mode_matches_oracle(tmp_path, ml100k):
+    """The benchmark's throughput configuration through the CLI: Philox stream,
+    residuals carried across sweeps (-recompute_every 0)."""
+    _cli(tmp_path, ml100k, "-dim", "0,0,32", "-iter", "20", "-seed", "2015", "--rng", "philox",
+         "--recompute_every", "0", "-rlog", str(tmp_path / "rlog.tsv"))
+    o = oracle.run(*ml100k, K=32, iters=20, seed=2015, rng="philox", want_factors=False)
+    assert np.abs(_rlog(tmp_path / "rlog.tsv") - o["rmse"]).max() < 1e-6

@@ -121,10 +121,11 @@ def test_split_rows_match_oracle(ml100k, chunk, K):
     np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("tune", [0, 1, 4, 8, 13])
+@pytest.mark.parametrize("tune", [0, 1, 4, 8, 13, 32, 33])
 def test_kernel_variants_match_oracle(ml100k, tune):
     """Kernel variants (sbmf_config.tune): block solve by one wave that hands D
-    over in LDS (default, bit 0 clear) or by every wave of a row (bit 0 set)."""
+    over in LDS (default, bit 0 clear) or by every wave of a row (bit 0 set);
+    bit 5: the streaming kernel on 16-wave workgroups (LDS geometry GsGeom<16, 4>)."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=50, iters=3, seed=4)
     for kw in ({}, {"stream_threshold": 40, "split_chunk": 64}):

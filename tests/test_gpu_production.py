@@ -1,0 +1,144 @@
+"""The benchmarked configuration, pinned (VERDICT r1 "next round" item 1).
+
+bench.py runs the sampler with residuals carried across sweeps
+(recompute_every=0: every half reads the residuals the previous half
+scattered; tau's sum of squares comes from the item half's per-row sums), the
+Philox stream (rng="philox"), the default kernel selection (Gram-block bins,
+the persistent streaming kernel with split rows over co-resident workgroups,
+LDS-capacity task size) and f64.  These tests run exactly that configuration:
+
+  * ML-100k, reference stream, 100 sweeps: the running-mean test RMSE tracks
+    the compiled reference's golden within 1e-6 (as the recompute_every=1
+    tests in test_gpu_parity.py do);
+  * ML-100k, Philox: against the oracle's Philox mode (oracle/sbpmf_oracle.c,
+    rng=1 restates the GPU build's stream), RMSE within 1e-6 over 50 sweeps,
+    factors within 1e-7 after 3;
+  * the BASELINE configs' shapes at full size (sbmf/synth.py): ML-1M K=50,
+    ML-10M K=100, ML-20M K=100 (the bench workload) and ML-20M K=200 (the
+    single-GPU half of the 8-GPU config), one or two sweeps each against the
+    oracle: U and V within 1e-7, RMSE and tau within 1e-9 (relative for tau).
+    The item side at these sizes takes the production schedule: thousands of
+    streaming tasks in rounds of the full cooperative grid, rows longer than
+    the 4096-rating task split over co-resident workgroups.  A split-row
+    hand-off that timed out raises inside learn() (sbmf_run fails).
+
+Reference: gibbs_sbpmf_final.cpp:317-334 (E recompute), :453-535 (halves).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden_rmse
+from sbmf import Data, FMLearnSBPMF, synth
+
+pytestmark = pytest.mark.gpu
+
+BENCH = dict(recompute_every=0)  # + rng / precision per test; kernel selection left at its defaults
+
+
+def _run(train, test, sweeps, **kw):
+    L = FMLearnSBPMF(**kw)
+    L.set_data(Data(*train), Data(*test))
+    L.learn(sweeps=sweeps)
+    return L
+
+
+@pytest.mark.parametrize("seed", [1, 7])
+def test_bench_mode_ref_stream_tracks_reference_100_sweeps(ml100k, seed):
+    tr, te = ml100k
+    gold = golden_rmse("ref_final_ml100k_k20_s%d.txt" % seed)
+    L = _run(tr, te, 100, num_factor=20, seed=seed, **BENCH)
+    err = np.abs(L.rmse_trajectory - gold)
+    print("recompute_every=0: max |dRMSE| over 100 sweeps = %.3e" % err.max())
+    assert err.max() < 1e-6
+
+
+@pytest.mark.parametrize("K", [20, 100])
+def test_bench_mode_philox_matches_oracle(ml100k, K):
+    tr, te = ml100k
+    o = oracle.run(tr, te, K=K, iters=50, seed=2015, rng="philox", want_factors=False)
+    L = _run(tr, te, 50, num_factor=K, seed=2015, rng="philox", **BENCH)
+    err = np.abs(L.rmse_trajectory - o["rmse"])
+    print("philox K=%d: max |dRMSE| over 50 sweeps = %.3e" % (K, err.max()))
+    assert err.max() < 1e-6
+    o3 = oracle.run(tr, te, K=K, iters=3, seed=2015, rng="philox")
+    L3 = _run(tr, te, 3, num_factor=K, seed=2015, rng="philox", **BENCH)
+    U, V = L3.factors()
+    assert np.abs(U - o3["U"]).max() < 1e-7
+    assert np.abs(V - o3["V"]).max() < 1e-7
+    assert abs(L3.hyper()["tau"] - o3["tau"][-1]) < 1e-9 * o3["tau"][-1]
+
+
+_SETS = {}
+_ORACLE = {}
+
+
+def _shape(name):
+    if name not in _SETS:
+        _SETS.clear()  # keep one full-size set (and its oracle runs) in memory at a time
+        _ORACLE.clear()
+        _SETS[name] = synth.generate(name)
+    return _SETS[name]
+
+
+def _oracle(name, K, sweeps, rng, seed):
+    key = (name, K, sweeps, rng, seed)
+    if key not in _ORACLE:
+        tr, te, dims = _shape(name)
+        _ORACLE[key] = oracle.run(tr, te, K=K, iters=sweeps, seed=seed, rng=rng, num_users=dims[0],
+                                  num_items=dims[1])
+    return _ORACLE[key]
+
+
+def _check_shape(name, K, sweeps, rng, seed):
+    tr, te, dims = _shape(name)
+    deg_items = np.bincount(tr[1], minlength=dims[1])
+    o = _oracle(name, K, sweeps, rng, seed)
+    L = _run(tr, te, sweeps, num_factor=K, seed=seed, rng=rng, **BENCH)
+    U, V = L.factors()
+    t = L.timing()
+    du, dv = np.abs(U - o["U"]).max(), np.abs(V - o["V"]).max()
+    dr = np.abs(L.rmse_trajectory - o["rmse"]).max()
+    print("%s K=%d %s: %d train, max item degree %d, item streaming rows %d: max|dU| %.2e max|dV| %.2e "
+          "max|dRMSE| %.2e (oracle %.1f s)" % (name, K, rng, len(tr[0]), deg_items.max(), t.kern_rows[1][5], du, dv,
+                                               dr, o["seconds"]))
+    assert du < 1e-7 and dv < 1e-7
+    assert dr < 1e-9
+    assert abs(L.hyper()["tau"] - o["tau"][-1]) < 1e-9 * o["tau"][-1]
+    L.close()
+    return deg_items, t
+
+
+@pytest.mark.timeout(900)
+def test_ml1m_k50_philox_two_sweeps():
+    _check_shape("ml-1m", 50, 2, "philox", 2015)
+
+
+@pytest.mark.timeout(900)
+def test_ml10m_k100_philox_two_sweeps():
+    deg, _ = _check_shape("ml-10m", 100, 2, "philox", 2015)
+    assert deg.max() > 4096  # split rows on the item side
+
+
+@pytest.mark.timeout(900)
+def test_ml20m_k100_bench_workload_two_sweeps():
+    """The bench.py workload itself (shape, K, seed, Philox, carried residuals)."""
+    deg, t = _check_shape("ml-20m", 100, 2, "philox", 2015)
+    assert deg.max() > 8 * 4096  # item rows split over many co-resident chunks
+    assert t.kern_rows[1][5] > 1024  # several rounds of the cooperative streaming grid
+
+
+@pytest.mark.timeout(900)
+def test_ml20m_k100_f32_within_north_star():
+    """f32 (bench's f32_value) at the bench workload: RMSE within 1e-3 of the f64 oracle."""
+    tr, te, dims = _shape("ml-20m")
+    o = _oracle("ml-20m", 100, 2, "philox", 2015)
+    L = _run(tr, te, 2, num_factor=100, seed=2015, rng="philox", precision="f32", **BENCH)
+    assert np.abs(L.rmse_trajectory - o["rmse"]).max() < 1e-3
+
+
+@pytest.mark.timeout(900)
+def test_ml20m_k200_reference_stream_one_sweep():
+    """The single-GPU share of BASELINE config 4 (ML-20M, K=200): 13 k-blocks,
+    the widest factor tables (221 MB U), reference RNG stream."""
+    _check_shape("ml-20m", 200, 1, "ref", 1)

@@ -53,6 +53,11 @@ def test_libfm_loader(tmp_path):
     assert d.rating.tolist() == [5, 3, 4.5]
     d2 = sbmf.load_libfm(p, item_offset=944)
     assert d2.item.tolist() == [0, 1, 6]
+    # with an item offset, a line whose first feature is in the item range is not a user
+    q = tmp_path / "b.libfm"
+    q.write_text("5 0:1 944:1\n4 1005:1 1007:1\n")
+    with pytest.raises(sbmf.SBMFError):
+        sbmf.load_libfm(q, item_offset=944)
 
 
 @pytest.mark.parametrize("bad", ["5 0:1\n", "5 0:1 3:1 4:1\n", "x 0:1 1:1\n", "5 0-1 1:1\n"])

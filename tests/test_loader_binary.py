@@ -84,7 +84,7 @@ def test_empty_file_pair(tmp_path):
 
 
 @pytest.mark.parametrize("case", ["bad_id", "bad_float", "row_mismatch", "three_features", "one_feature",
-                                  "item_below_offset", "truncated", "num_values", "bad_y"])
+                                  "item_below_offset", "two_items", "truncated", "num_values", "bad_y"])
 def test_errors(tmp_path, case):
     stem = str(tmp_path / "b")
     rows = [[(0, 1.0), (9, 1.0)], [(1, 1.0), (10, 1.0)]]
@@ -100,6 +100,8 @@ def test_errors(tmp_path, case):
         rows[0] = rows[0][:1]
     elif case == "item_below_offset":
         rows[0] = [(0, 1.0), (3, 1.0)]
+    elif case == "two_items":  # both features in the item range: not a user id (item_offset 9)
+        rows[0] = [(10, 1.0), (11, 1.0)]
     elif case == "num_values":
         kw = {"num_values": 5}
     write_x(stem + ".x", rows, 12, **kw)
@@ -115,3 +117,27 @@ def test_missing_pair(tmp_path):
     with pytest.raises(sbmf.SBMFError) as e:
         sbmf.load_libfm_binary(str(tmp_path / "nothing"))
     assert "unable to open" in str(e.value)
+
+
+def test_writer_refuses_ids_that_would_wrap(tmp_path):
+    """Feature ids are uint32 in the .x format and num_cols = max id + 1: ids
+    that would wrap are refused (no silently wrong files)."""
+    stem = str(tmp_path / "w")
+    with pytest.raises(ValueError):  # item_offset + item past 2^32 - 2
+        sbmf.save_libfm_binary(stem, sbmf.Data([0], [5], [3.0]), item_offset=0xfffffffc)
+    assert not os.path.exists(stem + ".x")
+    with pytest.raises(ValueError):  # negative ids never reach the uint32 cast
+        sbmf.Data([-1], [0], [3.0])
+    with pytest.raises(ValueError):
+        sbmf.Data([2 ** 32], [0], [3.0])
+    # the C entry point checks on its own (64-bit arithmetic)
+    import ctypes as C
+    from sbmf import _lib
+    u = np.array([0], np.uint32)
+    i = np.array([0xfffffffe], np.uint32)
+    v = np.array([3.0])
+    r = _lib.Ratings()
+    r.n, r.user, r.item = 1, u.ctypes.data_as(C.POINTER(C.c_uint32)), i.ctypes.data_as(C.POINTER(C.c_uint32))
+    r.rating = v.ctypes.data_as(C.POINTER(C.c_double))
+    assert sbmf.lib.sbmf_save_libfm_binary(stem.encode(), C.byref(r), 1, 0) == sbmf.SBMF_E_ARG
+    assert not os.path.exists(stem + ".x")

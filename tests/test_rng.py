@@ -52,3 +52,19 @@ def test_philox_normals_deterministic_and_standard():
     assert not np.array_equal(a[:128], a[128:])
     z = np.concatenate([philox_normals(9, s, 0, r, 200) for s in range(4) for r in range(100)])
     assert abs(z.mean()) < 0.02 and abs(z.std() - 1) < 0.02
+
+
+def test_oracle_philox_mode_restates_the_device_stream(ml100k):
+    """oracle rng='philox' (test infrastructure) draws the GPU build's Philox
+    normals: its initial factors equal sbmf_philox_normals (host C ABI) for
+    (seed, sweep 0xffffffff, TAG_INIT_U / TAG_INIT_V, row)."""
+    import oracle
+    from sbmf import philox_normals
+    tr, te = ml100k
+    o = oracle.run(tr, te, K=20, iters=0, seed=2015, rng="philox")
+    for row in (0, 17, 942):
+        assert np.array_equal(o["U"][row], philox_normals(2015, 0xffffffff, 3, row, 20))
+    for row in (0, 1681):
+        assert np.array_equal(o["V"][row], philox_normals(2015, 0xffffffff, 4, row, 20))
+    with pytest.raises(ValueError):
+        oracle.run(tr, te, K=8, iters=1, rng="philox", quirks="bias2")
