@@ -40,6 +40,20 @@ class VBOResult(C.Structure):
                 ("epochs_done", C.c_uint32)]
 
 
+class FMMConfig(C.Structure):
+    _fields_ = [("K", C.c_uint32), ("iters", C.c_uint32), ("seed", C.c_uint), ("k0", C.c_int), ("k1", C.c_int),
+                ("do_sample", C.c_int), ("do_multilevel", C.c_int), ("init_stdev", C.c_double),
+                ("reg0", C.c_double), ("regw", C.c_double), ("regv", C.c_double)]
+
+
+class FMMResult(C.Structure):
+    _fields_ = [("rmse_test", C.POINTER(C.c_double)), ("rmse_this", C.POINTER(C.c_double)),
+                ("rmse_train", C.POINTER(C.c_double)), ("alpha", C.POINTER(C.c_double)), ("cap", C.c_uint32),
+                ("pred", C.POINTER(C.c_double)), ("w", C.POINTER(C.c_double)), ("v", C.POINTER(C.c_double)),
+                ("w0", C.c_double), ("min_target", C.c_double), ("max_target", C.c_double),
+                ("num_attribute", C.c_uint32), ("iters_done", C.c_uint32)]
+
+
 def build():
     import subprocess
     subprocess.run(["make", "-C", HERE, "all"], check=True, capture_output=True)
@@ -57,6 +71,7 @@ def _lib():
     lib.oracle_ran_uniform.restype = C.c_double
     lib.oracle_srand.argtypes = [C.c_uint]
     lib.oracle_vbo_run.restype = C.c_int
+    lib.oracle_fmm_run.restype = C.c_int
     return lib
 
 
@@ -149,6 +164,56 @@ def run_vbo(train, test, K=8, epochs=10, seed=1, num_users=0, num_items=0, secon
     n = res.epochs_done
     return {"rmse": rm[:n], "pred": pred[:len(sr)], "mu_w": mu_w, "mu_v": mu_v, "alpha": res.alpha, "mu0": res.mu0,
             "seconds": res.seconds, "epochs": n, "num_attribute": res.num_attribute}
+
+
+def libfm_attrs(train, test, num_users=0):
+    """Rating triples -> libFM users-first attribute pairs (a0 = u, a1 = I + i,
+    the layout of "r u:1 (I+i):1" lines) and the data sets' num_feature
+    (largest attribute id + 1, Data.h:221)."""
+    tu, ti = np.asarray(train[0], np.int64), np.asarray(train[1], np.int64)
+    su, si = np.asarray(test[0], np.int64), np.asarray(test[1], np.int64)
+    I = num_users or int(max(tu.max(initial=0), su.max(initial=0))) + 1
+    ta = (tu.astype(np.uint32), (I + ti).astype(np.uint32))
+    sa = (su.astype(np.uint32), (I + si).astype(np.uint32))
+    p_train = int(ta[1].max(initial=0)) + 1
+    p_test = int(sa[1].max(initial=0)) + 1 if len(su) else 0
+    return ta, sa, p_train, p_test, I
+
+
+def run_fmm(train, test, K=8, iters=10, seed=1, method="mcmc", k0=1, k1=1, init_stdev=0.1, regular=(0.0, 0.0, 0.0),
+            num_users=0, want_params=True):
+    """The libFM MCMC / ALS oracle (fmm_oracle.c: bin/libFM -method mcmc|als on
+    users-first rating data).  Returns per-iteration 'rmse_test' (the "Test="
+    value), 'rmse_this', 'rmse_train', 'alpha', the -out predictions 'pred',
+    the final 'w' [p], 'v' [K][p], 'w0'."""
+    L = lib()
+    als = method == "als"
+    cfg = FMMConfig(K, iters, seed, k0, k1, 0 if als else 1, 0 if als else 1, init_stdev, *regular)
+    ta, sa, p_train, p_test, I = libfm_attrs(train, test, num_users)
+    ty = np.ascontiguousarray(train[2], np.float64)
+    sy = np.ascontiguousarray(test[2], np.float64)
+    p = max(p_train, p_test) + 1
+    res = FMMResult()
+    rt, rh, rr, al = (np.full(iters, np.nan) for _ in range(4))
+    res.rmse_test, res.rmse_this, res.rmse_train, res.alpha = (_p(a, C.c_double) for a in (rt, rh, rr, al))
+    res.cap = iters
+    pred = np.zeros(max(len(sy), 1))
+    res.pred = _p(pred, C.c_double)
+    w = v = None
+    if want_params:
+        w, v = np.zeros(p), np.zeros((K, p))
+        res.w, res.v = _p(w, C.c_double), _p(v, C.c_double)
+    a0, a1 = (np.ascontiguousarray(x, np.uint32) for x in ta)
+    b0, b1 = (np.ascontiguousarray(x, np.uint32) for x in sa)
+    rc = L.oracle_fmm_run(C.byref(cfg), C.c_uint64(len(ty)), _p(a0, C.c_uint32), _p(a1, C.c_uint32),
+                          _p(ty, C.c_double), C.c_uint64(len(sy)), _p(b0, C.c_uint32), _p(b1, C.c_uint32),
+                          _p(sy, C.c_double), C.c_uint32(p_train), C.c_uint32(p_test), C.byref(res))
+    if rc != 0:
+        raise ValueError("oracle_fmm_run failed (%d)" % rc)
+    n = res.iters_done
+    return {"rmse_test": rt[:n], "rmse_this": rh[:n], "rmse_train": rr[:n], "alpha": al[:n],
+            "pred": pred[:len(sy)], "w": w, "v": v, "w0": res.w0, "num_attribute": res.num_attribute,
+            "num_users": I}
 
 
 def stream(seed, kind, n, shape=1.0):

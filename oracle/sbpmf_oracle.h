@@ -70,6 +70,35 @@ int oracle_vbo_run(const oracle_vbo_config *cfg, uint64_t n_train, const uint32_
                    const double *tr, uint64_t n_test, const uint32_t *su, const uint32_t *si, const double *sr,
                    uint32_t num_users, uint32_t num_items, oracle_vbo_result *res);
 
+/* libFM MCMC / ALS (fmm_oracle.c): the reference's `bin/libFM -method mcmc|als`
+ * learner (fm_learn_mcmc.h, fm_learn_mcmc_simultaneous.h) on cases with two
+ * one-hot attributes a0 < a1, one attribute group, no relations. */
+typedef struct {
+    uint32_t K, iters;
+    unsigned seed;        /* srand() value (libfm.cpp:124 seeds with time(NULL)) */
+    int k0, k1;           /* -dim 'k0,k1,K' */
+    int do_sample;        /* 0: ALS (libfm.cpp:132-136) */
+    int do_multilevel;    /* 0: ALS */
+    double init_stdev;    /* -init_stdev (default 0.1) */
+    double reg0, regw, regv; /* -regular (initial / fixed lambdas; libfm.cpp:484-513) */
+} oracle_fmm_config;
+
+typedef struct {
+    double *rmse_test, *rmse_this, *rmse_train, *alpha; /* [cap] per iteration, or NULL */
+    uint32_t cap;
+    double *pred;         /* [n_test] the -out predictions, or NULL */
+    double *w;            /* [num_attribute] or NULL */
+    double *v;            /* [K][num_attribute] (f-major, as fm_model::v) or NULL */
+    double w0, min_target, max_target;
+    uint32_t num_attribute, iters_done;
+} oracle_fmm_result;
+
+void oracle_fmm_config_default(oracle_fmm_config *c);
+/* p_train / p_test: the data sets' num_feature (largest attribute id + 1). */
+int oracle_fmm_run(const oracle_fmm_config *cfg, uint64_t n_train, const uint32_t *ta0, const uint32_t *ta1,
+                   const double *ty, uint64_t n_test, const uint32_t *sa0, const uint32_t *sa1, const double *sy,
+                   uint32_t p_train, uint32_t p_test, oracle_fmm_result *res);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,7 @@ struct SplitRow {
 };
 struct SplitSync {
     double* slabs;       // [nchunk_total][nblk][16*16+16]
+    double* totals;      // k_gres: [nsplit_rows * nblk][16*16+16] the chunk-ordered sum (rows > GRES_ALLREAD chunks)
     uint32_t* counters;  // [nsplit_rows * nblk], zeroed per launch
     uint32_t ncounters;
     uint32_t nblk;       // ceil(K/16)

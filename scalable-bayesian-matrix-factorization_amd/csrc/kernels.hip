@@ -353,6 +353,18 @@ __device__ __forceinline__ T row16_sum(T x) {
     x += dpp<0x128, 0xf>(x);  // row_ror:8
     return x;
 }
+// Same sum, bit-identical in all 16 lanes of the row: xor-1 and xor-2 pairs
+// (quad_perm), then rotations by 8 and 4 -- every lane adds the same two
+// operands at every step (in one order or the other), so no lane rounds
+// differently.
+template <typename T>
+__device__ __forceinline__ T row16_sum_sym(T x) {
+    x += dpp<0xb1, 0xf>(x);   // quad_perm [1,0,3,2]
+    x += dpp<0x4e, 0xf>(x);   // quad_perm [2,3,0,1]
+    x += dpp<0x128, 0xf>(x);  // row_ror:8
+    x += dpp<0x124, 0xf>(x);  // row_ror:4
+    return x;
+}
 __device__ __forceinline__ float shfl_xor_t(float v, int m) { return __shfl_xor(v, m); }
 __device__ __forceinline__ double shfl_xor_t(double v, int m) { return __shfl_xor(v, m); }
 __device__ __forceinline__ float shfl_t(float v, int src) { return __shfl(v, src); }
@@ -1044,6 +1056,333 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
     }
 }
 
+// ------------------------------------------------- register-resident streaming rows
+// The default kernel for rows above the Gram-block bins: one 8-wave workgroup
+// per task of at most CAP = 4*NW*VW ratings (a whole row, or one equal chunk
+// of a longer row), in one persistent cooperative launch per half-sweep, with
+// k_gstream's rounds (a split row's chunks share a round, so they are
+// co-resident).  Wave w owns vectors w, w+NW, ... (4 ratings x 16 k each).
+// The partner slice of the current k-block stays in VGPRs from the accumulate
+// (G_B = S^T S by MFMA, c_B = S^T e) until the apply (e -= S_B D_B) after the
+// block's draws, so each slice is gathered once per half-sweep (k_gstream
+// gathers it twice: to accumulate, and again one traversal later to apply).
+// Per block t, per vector: apply D_{t-1} with the held slice, then issue the
+// gather of slice t into the same registers; then accumulate block t.  The
+// task's partner ids, residuals, scatter targets and ratings sit in LDS.
+// Split rows hand their (G_B, c_B) partials over without fences: write-through
+// (sc1) stores, drained, then one agent-scope counter add per workgroup.  Rows
+// of up to GRES_ALLREAD chunks: every chunk polls the counter (sc1 loads) for
+// nch and sums all partials in chunk order (sc1 loads).  Longer rows: the
+// workgroup whose add returns nch-1 sums them, publishes the total the same
+// way and adds once more; the others poll for nch+1 and read the total --
+// MI355X_MICROARCH.md hand-off table, first row.  The sums never depend on
+// which chunk arrives last.
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+struct GresSums {
+    double sq, tr;
+};
+constexpr uint32_t GRES_ALLREAD = 16;  // split rows of up to this many chunks exchange in one hop
+template <typename T>
+struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of slices
+    static constexpr int VW = sizeof(T) == 8 ? 32 : 64;
+};
+template <typename T, int NW, int SIDE>
+__global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict__ tasks, uint32_t ntask,
+                                                  HalfArgs<T> a, SplitSync sy) {
+    typedef typename MfmaT<T>::acc_t acc_t;
+    constexpr int VW = GresW<T>::VW;
+    constexpr uint32_t CAP = 4 * NW * VW;
+    constexpr int SL = GB * GB + GB;  // slab doubles per (chunk, block): 16x16 image (lower + diagonal) | c
+    const int lane = threadIdx.x & 63;
+    const int wr = threadIdx.x >> 6;
+    const int ci = lane & 15;
+    const int rr = lane >> 4;
+    const uint32_t K = a.K, Kp = a.Kp;
+    const uint32_t nblk = (K + GB - 1) / GB;
+    const T tau = a.tau;
+    __shared__ uint32_t pjL[CAP];      // partner row offset (row * Kp) per rating slot (zero row past the end)
+    __shared__ uint32_t pmL[CAP];      // residual scatter target per rating
+    __shared__ T eL[CAP];              // residuals (bit-identical in the 16 lanes of a rating)
+    __shared__ T rL[CAP];              // ratings (train error), when requested
+    __shared__ T Ls[NW][GB][GLD];      // per-wave strictly lower part of G_B
+    __shared__ T Ps[NW][GB];           // per-wave diagonal
+    __shared__ T Cs[NW][GB];           // per-wave c_B
+    __shared__ T Lr[GB][GLD];          // reduced: strictly lower part (diagonal and upper stay 0)
+    __shared__ T Pr[GB];
+    __shared__ T Cr[GB];
+    __shared__ T Dsh[GB];
+    __shared__ T newS[256];
+    __shared__ double red2[NW][2];
+    __shared__ uint32_t lastf;
+    for (int x = threadIdx.x; x < GB * GLD; x += 64 * NW) (&Lr[0][0])[x] = T(0);
+    // this lane's slots: vector j of wave wr is rating 4*(wr + j*NW) + rr, i.e.
+    // a fixed per-lane base plus j*4*NW (an immediate LDS offset)
+    const uint32_t* const pjW = pjL + 4 * wr + rr;
+    T* const eW = eL + 4 * wr + rr;
+    constexpr int JS = 4 * NW;
+
+    for (uint32_t ti = blockIdx.x; ti < ntask; ti += gridDim.x) {
+        const SplitTask tk = tasks[ti];
+        const uint32_t n = tk.len;
+        if (n == 0) continue;  // empty round slot (uniform)
+        const uint32_t row = tk.row, beg = tk.beg, nch = tk.nch;
+        const uint32_t vpw = ((n + 3) / 4 + NW - 1) / NW;  // vectors per wave
+        // optional phase profile (build with KPROF=1, run with SBMF_KPROF=1): wave 0's cycles per phase
+#ifdef SBMF_KPROF_BUILD
+        unsigned long long tp = (sy.prof && threadIdx.x == 0) ? clock64() : 0ull;
+        auto stamp = [&](int ph) {
+            if (sy.prof && threadIdx.x == 0) {
+                const unsigned long long now = clock64();
+                atomicAdd(&sy.prof[ph], now - tp);
+                tp = now;
+            }
+        };
+#else
+        auto stamp = [](int) {};
+#endif
+        // size class: the task's vectors per wave, rounded up to VW/4, VW/2 or VW
+        auto body = [&](auto vc) {
+            constexpr int VC = decltype(vc)::value;
+            const uint32_t npad = 4 * NW * VC;
+            for (uint32_t x = threadIdx.x; x < npad; x += 64 * NW) {
+                const bool in = x < n;
+                pjL[x] = (in ? a.part[beg + x] : a.zrow) * Kp;  // host checks (P+2)*Kp < 2^32
+                pmL[x] = in ? a.perm[beg + x] : 0u;
+                if (!a.e_from_dot) eL[x] = in ? a.E_this[beg + x] : T(0);
+                if (a.row_tr) rL[x] = in ? a.r_this[beg + x] : T(0);
+            }
+            T zA0, zA1, zB0 = T(0), zB1 = T(0);
+            {  // per-half normals of the row (used by the solving wave)
+                const uint32_t i0 = 2 * lane;
+                zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
+                zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
+                if (K > 128) {
+                    zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
+                    zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
+                }
+            }
+            __syncthreads();
+            if (a.e_from_dot) {  // validation mode (tune bit 1): e0 = r - own.partner
+                for (uint32_t v = wr; v < (npad >> 2); v += NW) {
+                    const uint32_t q = 4 * v + rr;
+                    const uint32_t pj = pjL[q];
+                    T d = T(0);
+                    for (uint32_t k0 = 0; k0 < K; k0 += GB)
+                        d += a.partner[(size_t)pj + k0 + ci] * a.own[(size_t)row * Kp + k0 + ci];
+                    d = row16_sum(d);
+                    if (ci == 0) eL[q] = q < n ? a.r_this[beg + q] - d : T(0);
+                }
+                __syncthreads();
+            }
+            stamp(0);  // staging
+            const T* __restrict__ pbase = a.partner + ci;
+            T s[VC];
+#pragma unroll
+            for (int j = 0; j < VC; ++j) s[j] = pbase[pjW[j * JS]];
+            T Dl = T(0);
+            for (uint32_t t = 0; t < nblk; ++t) {
+                // keep the per-vector partner offsets in LDS: hoisting them out of
+                // the block loop would hold VC 64-bit addresses in VGPRs
+                asm volatile("" ::: "memory");
+                const uint32_t kk = t * GB + ci;
+                const bool kin = kk < K;
+                // the block's old values and hyperparameters (zero padded; used by wave 0)
+                const T old = a.own[(size_t)row * Kp + kk];
+                const T sg = a.sig[kk];
+                const T mu = a.mu[kk];
+                if (t > 0) {
+                    // apply block t-1 with the held slice, then gather slice t into it
+#pragma unroll
+                    for (int j = 0; j < VC; ++j) {
+                        eW[j * JS] = eW[j * JS] - row16_sum_sym(s[j] * Dl);  // same value from all 16 lanes
+                        s[j] = pbase[(size_t)pjW[j * JS] + t * GB];
+                    }
+                }
+                stamp(1);  // apply + gather issue
+                acc_t g = {T(0), T(0), T(0), T(0)};
+                T cc = T(0);
+#pragma unroll
+                for (int j = 0; j < VC; ++j) {
+                    g = MfmaT<T>::mfma(s[j], g);
+                    cc += s[j] * eW[j * JS];
+                }
+                cc += shfl_xor_t(cc, 16);
+                cc += shfl_xor_t(cc, 32);
+                stamp(2);  // gather wait + accumulate
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = MfmaT<T>::row(lane, j);
+                    Ls[wr][r][ci] = ci < r ? g[j] : T(0);
+                    if (r == ci) Ps[wr][ci] = g[j];
+                }
+                if (lane < GB) Cs[wr][lane] = cc;
+                __syncthreads();
+                stamp(3);  // wait for the other waves
+                // cross-wave sum in wave order: entry x of the slab image
+                const int x = threadIdx.x;
+                T val = T(0);
+                if (x < SL) {
+                    const int r0 = (x >> 4) & 15, c0 = x & 15;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w)
+                        val += x >= GB * GB ? Cs[w][x - GB * GB] : (r0 == c0 ? Ps[w][r0] : Ls[w][r0][c0]);
+                }
+                if (nch > 1) {
+                    // cross-chunk sum over the row's chunks (see the header comment)
+                    const size_t cstride = (size_t)nblk * SL;  // between one chunk's slabs and the next's
+                    const double* p0 = sy.slabs + ((size_t)tk.slab0 * nblk + t) * SL + x;
+                    auto sum_chunks = [&]() {  // chunk order, 8 sc1 loads in flight
+                        double sum = 0.0;
+                        uint32_t c = 0;
+                        for (; c + 8 <= nch; c += 8) {
+                            double v[8];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) v[u] = ld_sc1(p0 + (c + u) * cstride);
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) sum += v[u];
+                        }
+                        for (; c < nch; ++c) sum += ld_sc1(p0 + c * cstride);
+                        return sum;
+                    };
+                    if (x < SL) st_sc1(const_cast<double*>(p0) + tk.chunk * cstride, (double)val);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    uint32_t* cnt = sy.counters + (size_t)tk.cnt0 + t;
+                    // up to GRES_ALLREAD chunks: every chunk reads every partial (one hop);
+                    // more: the last arriver sums and publishes the total (two hops, O(nch) traffic)
+                    const bool allread = nch <= GRES_ALLREAD;
+                    if (threadIdx.x == 0) {
+                        const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        lastf = !allread && old == nch - 1;
+                        if (allread || old != nch - 1) {
+                            const uint32_t want = allread ? nch : nch + 1;
+                            uint32_t spins = 0;
+                            while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                                __builtin_amdgcn_s_sleep(1);
+                                if (++spins > (1u << 26)) {  // give up: flag, never hang the device
+                                    __hip_atomic_store(sy.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    break;
+                                }
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    double* tot = sy.totals + ((size_t)tk.cnt0 + t) * SL;
+                    if (allread) {
+                        if (x < SL) val = (T)sum_chunks();
+                    } else if (lastf) {
+                        if (x < SL) {
+                            const double sum = sum_chunks();
+                            st_sc1(tot + x, sum);
+                            val = (T)sum;
+                        }
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __syncthreads();
+                        if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } else {
+                        if (x < SL) val = (T)ld_sc1(tot + x);
+                    }
+                }
+                if (x < SL) {
+                    if (x >= GB * GB)
+                        Cr[x - GB * GB] = val;
+                    else if ((x >> 4) == (x & 15))
+                        Pr[x & 15] = val;
+                    else if ((x & 15) < (x >> 4))
+                        Lr[x >> 4][x & 15] = val;
+                }
+                __syncthreads();
+                stamp(4);  // cross-wave sum + split-row exchange
+                if (wr == 0) {  // the 16 draws (wave 0), D handed over in LDS
+                    const T P = Pr[ci];
+                    const int zl = (int)((kk >> 1) & 63);
+                    const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
+                    T z = (kk & 1) ? za1 : za0;
+                    if (K > 128) {
+                        const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
+                        z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
+                    }
+                    const T var = kin ? T(1) / (sg + tau * P) : T(0);
+                    const T sd = a.sd_is_var ? var : tsqrt(var);
+                    const T A = var * sg * mu + sd * z;
+                    const T Bq = var * tau;
+                    const T dlt = gblock_solve_lds(&Lr[ci][0], Bq, A - old + Bq * (Cr[ci] + P * old));
+                    if (lane < GB) {
+                        if (kin) newS[kk] = old + dlt;
+                        Dsh[lane] = dlt;
+                    }
+                }
+                __syncthreads();
+                Dl = Dsh[ci];
+                stamp(5);  // solve
+            }
+            // apply the last block; then residuals out and the per-row sums, one
+            // rating per thread in rating order (no per-vector branches)
+#pragma unroll
+            for (int j = 0; j < VC; ++j) eW[j * JS] = eW[j * JS] - row16_sum_sym(s[j] * Dl);
+            __syncthreads();
+            double sq = 0.0, trs = 0.0;
+            for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) {
+                const T e = eL[x];
+                a.E_other[pmL[x]] = e;
+                sq += (double)(e * e);
+                if (a.row_tr) {
+                    const T r = rL[x];
+                    T pr = r - e;
+                    pr = (pr < a.hi) ? pr : a.hi;
+                    pr = (a.lo < pr) ? pr : a.lo;
+                    trs += (double)((pr - r) * (pr - r));
+                }
+            }
+            return GresSums{sq, trs};
+        };
+        GresSums sums;
+        if (vpw <= (uint32_t)VW / 4)
+            sums = body(std::integral_constant<int, VW / 4>{});
+        else if (vpw <= (uint32_t)VW / 2)
+            sums = body(std::integral_constant<int, VW / 2>{});
+        else
+            sums = body(std::integral_constant<int, VW>{});
+        // ---- new own row: whole rows write it, split rows stage it (k_split_finish publishes)
+        if (tk.chunk == 0)
+            for (uint32_t k = threadIdx.x; k < K; k += 64 * NW) {
+                if (nch > 1)
+                    static_cast<T*>(sy.newown)[(size_t)tk.slab0 * Kp + k] = newS[k];
+                else
+                    a.own[(size_t)row * Kp + k] = newS[k];
+            }
+        double dsq = wave_sum(sums.sq);
+        double dtr = wave_sum(sums.tr);
+        if (lane == 0) {
+            red2[wr][0] = dsq;
+            red2[wr][1] = dtr;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            dsq = 0.0;
+            dtr = 0.0;
+            for (int w = 0; w < NW; ++w) {
+                dsq += red2[w][0];
+                dtr += red2[w][1];
+            }
+            if (nch > 1) {
+                sy.chunk_sq[tk.slab0 + tk.chunk] = dsq;
+                sy.chunk_tr[tk.slab0 + tk.chunk] = dtr;
+            } else {
+                if (a.row_sq) a.row_sq[row] = dsq;
+                if (a.row_tr) a.row_tr[row] = dtr;
+            }
+        }
+        __syncthreads();  // LDS (ids, residuals, newS, red2) is reused by the next task
+        stamp(6);  // epilogue
+    }
+}
+
 // Split rows: publish the new own rows and fold the chunk partial sums.
 template <typename T>
 __global__ __launch_bounds__(64) void k_split_finish(const SplitRow* __restrict__ srows, uint32_t nrows, HalfArgs<T> a,
@@ -1650,13 +1989,16 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
     return hipGetLastError();
 }
 
-// Default: the block solve by one wave, D handed to the others in LDS;
-// tune bit 0: every wave solves redundantly (no extra barrier).
-// tune bit 5: 16-wave workgroups (UNR 4), one per CU, instead of two 8-wave ones.
-static int gstream_nw(uint32_t tune) { return (tune & 32u) ? 16 : 8; }
-int gstream_wg_target(uint32_t tune) { return (tune & 32u) ? 1 : 2; }
+// Streaming rows: k_gres (register-resident slices, default) or, with tune
+// bit 6, the LDS-staged k_gstream.  k_gstream variants: tune bit 0 = every
+// wave solves redundantly (no extra barrier); tune bit 5 = 16-wave
+// workgroups (UNR 4), one per CU, instead of two 8-wave ones.
+static bool use_gres(uint32_t tune) { return !(tune & 64u); }
+static int gstream_nw(uint32_t tune) { return use_gres(tune) ? 8 : (tune & 32u) ? 16 : 8; }
+int gstream_wg_target(uint32_t tune) { return use_gres(tune) ? 2 : (tune & 32u) ? 1 : 2; }
 template <typename T>
 static size_t gstream_dyn(uint32_t tune, uint32_t cmax) {
+    if (use_gres(tune)) return 0;
     return (tune & 32u) ? GsGeom<16, 4>::dyn_bytes<T>(cmax) : GsGeom<8, 8>::dyn_bytes<T>(cmax);
 }
 
@@ -1689,6 +2031,7 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
 
 template <typename T>
 static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
+    if (use_gres(tune)) return side ? (const void*)k_gres<T, 8, 1> : (const void*)k_gres<T, 8, 0>;
     const bool sw = !(tune & 1u);
     if (tune & 32u) {
         if (side) return sw ? (const void*)k_gstream<T, 16, 4, true, 1> : (const void*)k_gstream<T, 16, 4, false, 1>;
@@ -1702,6 +2045,7 @@ template <typename T>
 uint32_t gstream_cmax(uint32_t tune) {
     hipFuncAttributes fa{};
     int dev = 0, lds_cu = 65536;
+    if (use_gres(tune)) return 4 * 8 * GresW<T>::VW;  // the VGPR-resident task
     if (hipFuncGetAttributes(&fa, gstream_fn<T>(tune)) != hipSuccess) return 1024;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);

@@ -258,7 +258,7 @@ struct sbmf_ctx {
     DBuf d_kprof;
     DBuf d_stasks_u, d_stasks_v, d_xrows_u, d_xrows_v;
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
-    DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
+    DBuf d_xslabs, d_xtotals, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
     DBuf d_uperm2, d_vperm2, d_uunpack, d_vunpack, d_xrecv;  // multi-GPU residual exchange
     DBuf d_bu, d_bv, d_mbu, d_mbv, d_sbu, d_sbv;  // biases b_i / b_j and their per-row (mu, sigma)
@@ -336,6 +336,9 @@ static void prepare_T(sbmf_ctx* c) {
     if (N >= 0xffffffffull) fail(SBMF_E_ARG, "more than 2^32-1 ratings are not supported");
     c->K = cf.num_factor;
     c->Kp = (c->K + 15) / 16 * 16;  // k-blocks of 16 start on 128-byte (f64) / 64-byte (f32) boundaries
+    // the streaming kernel keeps partner-row element offsets (row * Kp) in 32 bits
+    if ((uint64_t)(std::max(c->I, c->J) + 2) * c->Kp >= 0xffffffffull)
+        fail(SBMF_E_ARG, "factor tables of %u x %u rows at K=%u exceed 2^32 elements", c->I, c->J, c->K);
 
     std::vector<uint32_t> pos_u, pos_v;
     build_side(N, c->tu.data(), c->ti.data(), c->tr.data(), c->I, c->users, pos_u);
@@ -444,6 +447,7 @@ static void prepare_T(sbmf_ctx* c) {
         const size_t nr = std::max(c->users.xrows.size(), c->items.xrows.size());
         c->d_xslabs.alloc(std::max<size_t>(nx, 1) * nblk * (16 * 16 + 16) * sizeof(double));
         c->d_xcnt.alloc(std::max<size_t>(nr, 1) * nblk * sizeof(uint32_t));
+        c->d_xtotals.alloc(std::max<size_t>(nr, 1) * nblk * (16 * 16 + 16) * sizeof(double));
         c->d_xchunk_sq.alloc(std::max<size_t>(nx, 1) * sizeof(double));
         c->d_xchunk_tr.alloc(std::max<size_t>(nx, 1) * sizeof(double));
         HIPCHK(hipMemsetAsync(c->d_xchunk_tr.p, 0, c->d_xchunk_tr.bytes, st));
@@ -834,6 +838,7 @@ static void run_half(sbmf_ctx* c, bool users) {
         else if (k == KIND_STREAM) {
             SplitSync sy{};
             sy.slabs = c->d_xslabs.as<double>();
+            sy.totals = c->d_xtotals.as<double>();
             sy.counters = c->d_xcnt.as<uint32_t>();
             sy.nblk = (c->K + 15) / 16;
             sy.ncounters = (uint32_t)s.xrows.size() * sy.nblk;
@@ -1080,13 +1085,15 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                                  100.0 * (double)h[16 + 8 * sd + k] / tot);
                 std::fprintf(stderr, "\n");
             }
-            static const char* nm[7] = {"stage", "traverse", "wg-wait", "reduce", "split-xchg", "solve", "epilogue"};
+            static const char* nm_gs[7] = {"stage", "traverse", "wg-wait", "reduce", "split-xchg", "solve", "epilogue"};
+            static const char* nm_gr[7] = {"stage", "apply+issue", "gather+acc", "wg-wait", "xwave+xchg", "solve", "epilogue"};
+            const char* const* nm = (cf.tune & 64u) ? nm_gs : nm_gr;
             for (int sd = 0; sd < 2; ++sd) {
                 const Side& S = sd ? c->items : c->users;
                 double tot = 0;
                 for (int k = 0; k < 7; ++k) tot += (double)h[8 * sd + k];
                 if (tot == 0) continue;
-                std::fprintf(stderr, "[kprof] sweep %u %s gstream (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep,
+                std::fprintf(stderr, "[kprof] sweep %u %s %s (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep, (cf.tune & 64u) ? "gstream" : "gres",
                              sd ? "items" : "users", S.sgrid, S.stasks.size());
                 for (int k = 0; k < 7; ++k)
                     std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.sgrid / 1e6,
