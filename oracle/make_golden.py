@@ -21,7 +21,13 @@ Fixtures written (all data, no reference source):
   ref_vbo_<data>_k<K>_s<seed>_e<E>.txt        E lines "%.17g" per-epoch test RMSE of the
                                               online VB learner (oracle/ref_vbo_harness.cpp
                                               over the reference's fm_learn_vb_online*.h)
-`make_golden.py vbo` regenerates only the online VB fixtures.
+  ref_libfm_<method>_<data>_d<k0><k1><K>_s<seed>_i<N>.txt
+                                              libFM's stdout "#Iter=..." lines of bin/libFM -method
+                                              mcmc|als (libfm.cpp compiled unmodified, time() pinned
+                                              to <seed> by oracle/ref_pin_time.c) on the users-first
+                                              libFM text of the data set
+  ref_libfm_<...>_pred.txt.gz                 its -out file (averaged clamped test predictions)
+`make_golden.py vbo` / `make_golden.py libfm` regenerate only those fixtures.
 Only runnable in the build container (needs /root/reference).
 """
 import gzip
@@ -141,10 +147,51 @@ def vbo_goldens():
     shutil.rmtree(root)
 
 
+# (method, data, dim, seed = pinned time(), iterations, -regular)
+LIBFM_RUNS = [("mcmc", "ml100k", "1,1,8", 1, 10, None), ("als", "ml100k", "1,1,8", 1, 10, "0,0,10"),
+              ("mcmc", "ml100k", "0,0,20", 7, 20, None), ("mcmc", "ragged", "1,1,8", 3, 20, None),
+              ("als", "ragged", "1,1,4", 2, 10, "1,2,5")]
+
+
+def libfm_name(method, dname, dim, seed, iters):
+    return "ref_libfm_%s_%s_d%s_s%d_i%d" % (method, dname, dim.replace(",", ""), seed, iters)
+
+
+def libfm_goldens():
+    root = "/tmp/sbmf_libfmrun_%d" % os.getpid()
+    os.makedirs(root, exist_ok=True)
+    sets = {"ml100k": (os.path.join(GOLD, "ml100k_train.tsv.gz"), os.path.join(GOLD, "ml100k_test.tsv.gz")),
+            "ragged": (os.path.join(GOLD, "ragged_train.tsv"), os.path.join(GOLD, "ragged_test.tsv"))}
+    for method, dname, dim, seed, iters, reg in LIBFM_RUNS:
+        tr, te = sets[dname]
+        I = max_user(tr, te) + 1
+        write_libfm(tr, os.path.join(root, "train.libfm"), I)
+        write_libfm(te, os.path.join(root, "test.libfm"), I)
+        cmd = [os.path.join(HERE, "_ref", "libFM"), "-task", "r", "-train", "train.libfm", "-test", "test.libfm",
+               "-dim", dim, "-iter", str(iters), "-method", method, "-out", "pred.txt"]
+        if reg:
+            cmd += ["-regular", reg]
+        p = subprocess.run(cmd, cwd=root, env=dict(os.environ, LIBFM_PIN_TIME=str(seed)), capture_output=True,
+                           text=True, check=True)
+        lines = [l for l in p.stdout.splitlines() if l.startswith("#Iter=")]
+        assert len(lines) == iters, (method, dname, p.stdout[-500:])
+        name = libfm_name(method, dname, dim, seed, iters)
+        with open(os.path.join(GOLD, name + ".txt"), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        with open(os.path.join(root, "pred.txt"), "rb") as f, \
+                gzip.GzipFile(os.path.join(GOLD, name + "_pred.txt.gz"), "wb", mtime=0) as g:
+            g.write(f.read())
+        print("golden libfm", name, lines[-1])
+    shutil.rmtree(root)
+
+
 def main():
     subprocess.run(["make", "-C", HERE, "all", "ref"], check=True, capture_output=True)
     if sys.argv[1:] == ["vbo"]:
         vbo_goldens()
+        return 0
+    if sys.argv[1:] == ["libfm"]:
+        libfm_goldens()
         return 0
     os.makedirs(GOLD, exist_ok=True)
     ml_train = os.path.join(REF, "data", "m100k", "train_sbpmf")
@@ -177,6 +224,7 @@ def main():
         with open(os.path.join(GOLD, "ref_rng_s%d.txt" % seed), "w") as f:
             f.write(out)
     vbo_goldens()
+    libfm_goldens()
     return 0
 
 

@@ -1223,20 +1223,26 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 if (lane < GB) Cs[wr][lane] = cc;
                 __syncthreads();
                 stamp(3);  // wait for the other waves
-                // cross-wave sum in wave order: entry x of the slab image
-                const int x = threadIdx.x;
-                T val = T(0);
-                if (x < SL) {
-                    const int r0 = (x >> 4) & 15, c0 = x & 15;
+                // cross-wave sum in wave order: entries x = threadIdx.x + j*64*NW of the slab image
+                constexpr int NE = (SL + 64 * NW - 1) / (64 * NW);  // entries per thread (1, or 2 for NW = 4)
+                T val[NE];
 #pragma unroll
-                    for (int w = 0; w < NW; ++w)
-                        val += x >= GB * GB ? Cs[w][x - GB * GB] : (r0 == c0 ? Ps[w][r0] : Ls[w][r0][c0]);
+                for (int j = 0; j < NE; ++j) {
+                    const int x = threadIdx.x + j * 64 * NW;
+                    val[j] = T(0);
+                    if (x < SL) {
+                        const int r0 = (x >> 4) & 15, c0 = x & 15;
+#pragma unroll
+                        for (int w = 0; w < NW; ++w)
+                            val[j] += x >= GB * GB ? Cs[w][x - GB * GB] : (r0 == c0 ? Ps[w][r0] : Ls[w][r0][c0]);
+                    }
                 }
                 if (nch > 1) {
                     // cross-chunk sum over the row's chunks (see the header comment)
                     const size_t cstride = (size_t)nblk * SL;  // between one chunk's slabs and the next's
-                    const double* p0 = sy.slabs + ((size_t)tk.slab0 * nblk + t) * SL + x;
-                    auto sum_chunks = [&]() {  // chunk order, 8 sc1 loads in flight
+                    const double* pb = sy.slabs + ((size_t)tk.slab0 * nblk + t) * SL;
+                    auto sum_chunks = [&](int x) {  // chunk order, 8 sc1 loads in flight
+                        const double* p0 = pb + x;
                         double sum = 0.0;
                         uint32_t c = 0;
                         for (; c + 8 <= nch; c += 8) {
@@ -1249,7 +1255,11 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                         for (; c < nch; ++c) sum += ld_sc1(p0 + c * cstride);
                         return sum;
                     };
-                    if (x < SL) st_sc1(const_cast<double*>(p0) + tk.chunk * cstride, (double)val);
+#pragma unroll
+                    for (int j = 0; j < NE; ++j) {
+                        const int x = threadIdx.x + j * 64 * NW;
+                        if (x < SL) st_sc1(const_cast<double*>(pb) + tk.chunk * cstride + x, (double)val[j]);
+                    }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __syncthreads();
                     uint32_t* cnt = sy.counters + (size_t)tk.cnt0 + t;
@@ -1274,27 +1284,43 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     __syncthreads();
                     double* tot = sy.totals + ((size_t)tk.cnt0 + t) * SL;
                     if (allread) {
-                        if (x < SL) val = (T)sum_chunks();
+#pragma unroll
+                        for (int j = 0; j < NE; ++j) {
+                            const int x = threadIdx.x + j * 64 * NW;
+                            if (x < SL) val[j] = (T)sum_chunks(x);
+                        }
                     } else if (lastf) {
-                        if (x < SL) {
-                            const double sum = sum_chunks();
-                            st_sc1(tot + x, sum);
-                            val = (T)sum;
+#pragma unroll
+                        for (int j = 0; j < NE; ++j) {
+                            const int x = threadIdx.x + j * 64 * NW;
+                            if (x < SL) {
+                                const double sum = sum_chunks(x);
+                                st_sc1(tot + x, sum);
+                                val[j] = (T)sum;
+                            }
                         }
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         __syncthreads();
                         if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     } else {
-                        if (x < SL) val = (T)ld_sc1(tot + x);
+#pragma unroll
+                        for (int j = 0; j < NE; ++j) {
+                            const int x = threadIdx.x + j * 64 * NW;
+                            if (x < SL) val[j] = (T)ld_sc1(tot + x);
+                        }
                     }
                 }
-                if (x < SL) {
-                    if (x >= GB * GB)
-                        Cr[x - GB * GB] = val;
-                    else if ((x >> 4) == (x & 15))
-                        Pr[x & 15] = val;
-                    else if ((x & 15) < (x >> 4))
-                        Lr[x >> 4][x & 15] = val;
+#pragma unroll
+                for (int j = 0; j < NE; ++j) {
+                    const int x = threadIdx.x + j * 64 * NW;
+                    if (x < SL) {
+                        if (x >= GB * GB)
+                            Cr[x - GB * GB] = val[j];
+                        else if ((x >> 4) == (x & 15))
+                            Pr[x & 15] = val[j];
+                        else if ((x & 15) < (x >> 4))
+                            Lr[x >> 4][x & 15] = val[j];
+                    }
                 }
                 __syncthreads();
                 stamp(4);  // cross-wave sum + split-row exchange
@@ -1993,9 +2019,11 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
 // bit 6, the LDS-staged k_gstream.  k_gstream variants: tune bit 0 = every
 // wave solves redundantly (no extra barrier); tune bit 5 = 16-wave
 // workgroups (UNR 4), one per CU, instead of two 8-wave ones.
+// k_gres variant: tune bit 7 = 4-wave workgroups (4 per CU, 512-rating f64 tasks)
 static bool use_gres(uint32_t tune) { return !(tune & 64u); }
-static int gstream_nw(uint32_t tune) { return use_gres(tune) ? 8 : (tune & 32u) ? 16 : 8; }
-int gstream_wg_target(uint32_t tune) { return use_gres(tune) ? 2 : (tune & 32u) ? 1 : 2; }
+static int gres_nw(uint32_t tune) { return (tune & 128u) ? 4 : 8; }
+static int gstream_nw(uint32_t tune) { return use_gres(tune) ? gres_nw(tune) : (tune & 32u) ? 16 : 8; }
+int gstream_wg_target(uint32_t tune) { return use_gres(tune) ? 16 / gres_nw(tune) : (tune & 32u) ? 1 : 2; }
 template <typename T>
 static size_t gstream_dyn(uint32_t tune, uint32_t cmax) {
     if (use_gres(tune)) return 0;
@@ -2031,7 +2059,10 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
 
 template <typename T>
 static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
-    if (use_gres(tune)) return side ? (const void*)k_gres<T, 8, 1> : (const void*)k_gres<T, 8, 0>;
+    if (use_gres(tune)) {
+        if (gres_nw(tune) == 4) return side ? (const void*)k_gres<T, 4, 1> : (const void*)k_gres<T, 4, 0>;
+        return side ? (const void*)k_gres<T, 8, 1> : (const void*)k_gres<T, 8, 0>;
+    }
     const bool sw = !(tune & 1u);
     if (tune & 32u) {
         if (side) return sw ? (const void*)k_gstream<T, 16, 4, true, 1> : (const void*)k_gstream<T, 16, 4, false, 1>;
@@ -2045,7 +2076,7 @@ template <typename T>
 uint32_t gstream_cmax(uint32_t tune) {
     hipFuncAttributes fa{};
     int dev = 0, lds_cu = 65536;
-    if (use_gres(tune)) return 4 * 8 * GresW<T>::VW;  // the VGPR-resident task
+    if (use_gres(tune)) return 4 * gres_nw(tune) * GresW<T>::VW;  // the VGPR-resident task
     if (hipFuncGetAttributes(&fa, gstream_fn<T>(tune)) != hipSuccess) return 1024;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);

@@ -61,13 +61,19 @@ struct Side {
     std::vector<uint32_t> bin_rows[NBIN];  // kinds: GK_* (0..4), KIND_STREAM (5), KIND_RK0 + RK_* (6..9)
     std::vector<GramItem> gitems;
     std::vector<GramRow> grows;
-    std::vector<SplitTask> stasks;   // streaming kernel tasks, in rounds of `sgrid` slots
-    std::vector<SplitRow> xrows;     // rows split over several tasks
+    // streaming rows: set 0 (k_gres, or k_gstream with tune bit 6) and, in the
+    // hybrid schedule, set 1 = the rows above the hybrid threshold (k_gstream)
+    struct StreamSet {
+        std::vector<SplitTask> stasks;  // tasks, in rounds of `sgrid` slots
+        std::vector<SplitRow> xrows;    // rows split over several tasks
+        uint32_t nxchunk = 0;           // tasks belonging to split rows (slab / staging slots)
+        uint32_t sgrid = 0;             // persistent grid of the launch
+        uint32_t cmax = 0;              // task capacity (ratings)
+        uint32_t tune = 0;              // kernel variant bits of the launch
+    } ss[2];
     std::vector<std::array<uint32_t, 3>> gsub[GK_NUM];  // multi-wave bins: (waves, offset, count) sub-ranges
     std::vector<ResidTask> rtasks;   // residual recompute: own rows in chunks of <= RESID_CHUNK
     std::vector<uint32_t> rtptr;     // [r1-r0+1] first task of each own row
-    uint32_t nxchunk = 0;            // tasks belonging to split rows (slab / staging slots)
-    uint32_t sgrid = 0;              // persistent grid of the streaming launch
     // multi-GPU residual exchange (see build_exchange): where this rank's rows
     // scatter their residuals (the other orientation's position, or a send slot
     // past its end), and where the residuals other ranks send land
@@ -253,10 +259,10 @@ struct sbmf_ctx {
     DBuf d_bins_u[NBIN], d_bins_v[NBIN];
     DBuf d_gitems_u, d_grows_u, d_gitems_v, d_grows_v, d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
     DBuf d_colpart, d_res, d_scratch;
-    uint32_t cmax = 0;  // streaming-kernel task capacity (ratings)
+
     bool kprof = false; // SBMF_KPROF=1: streaming-kernel phase cycles printed per sweep
     DBuf d_kprof;
-    DBuf d_stasks_u, d_stasks_v, d_xrows_u, d_xrows_v;
+    DBuf d_stasks[2][2], d_xrows[2][2];  // [side][stream set]
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
     DBuf d_xslabs, d_xtotals, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
@@ -313,7 +319,8 @@ static void ensure_pinned(sbmf_ctx* c, size_t bytes) {
 }
 
 static void fill_kernel_bytes(sbmf_ctx* c);
-static void build_stream_tasks(Side& s, uint32_t chunk, uint32_t gres, uint32_t nblk);
+static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vector<uint32_t>& rows, uint32_t gres,
+                               uint32_t nblk);
 
 // ------------------------------------------------------------------ prepare
 template <typename T>
@@ -391,14 +398,25 @@ static void prepare_T(sbmf_ctx* c) {
     {
         int dev_cus = 0;
         HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, cf.device));
-        // task capacity: the LDS-resident maximum, or smaller if split_chunk asks
-        c->cmax = gstream_cmax<T>(cf.tune);
-        if (cf.split_chunk) c->cmax = std::min(c->cmax, std::max(cf.split_chunk, 1u));
-        const int per_cu =
-            std::max(1, std::min(gstream_wg_target(cf.tune), gstream_blocks_per_cu<T>(c->cmax, cf.tune)));
-        const uint32_t gres = (uint32_t)(dev_cus * per_cu);
-        build_stream_tasks(c->users, c->cmax, gres, nblk);
-        build_stream_tasks(c->items, c->cmax, gres, nblk);
+        // hybrid schedule (tune bits 8/9/10): rows up to 1024 / 4096 / 128 (tests)
+        // ratings in k_gres, longer ones in k_gstream's LDS-staged tasks
+        const uint32_t hyb = (cf.tune & 256u) ? 1024u : (cf.tune & 512u) ? 4096u : (cf.tune & 1024u) ? 128u : 0u;
+        const uint32_t tunes[2] = {cf.tune, cf.tune | 64u};
+        for (Side* sd : {&c->users, &c->items}) {
+            std::vector<uint32_t> rows[2];
+            for (uint32_t r : sd->bin_rows[KIND_STREAM])  // degree-descending
+                rows[hyb && sd->ptr[r + 1] - sd->ptr[r] > hyb ? 1 : 0].push_back(r);
+            for (int k = 0; k < 2; ++k) {
+                Side::StreamSet& S = sd->ss[k];
+                S.tune = tunes[k];
+                // task capacity: the kernel's on-chip maximum, or smaller if split_chunk asks
+                S.cmax = gstream_cmax<T>(S.tune);
+                if (cf.split_chunk) S.cmax = std::min(S.cmax, std::max(cf.split_chunk, 1u));
+                const int per_cu =
+                    std::max(1, std::min(gstream_wg_target(S.tune), gstream_blocks_per_cu<T>(S.cmax, S.tune)));
+                build_stream_tasks(*sd, S, rows[k], (uint32_t)(dev_cus * per_cu), nblk);
+            }
+        }
     }
     {  // test split in 256-aligned blocks
         const uint64_t T_ = c->su.size(), nb = (T_ + 255) / 256;
@@ -438,13 +456,16 @@ static void prepare_T(sbmf_ctx* c) {
         upload(c->d_rtptr, s.rtptr, st);
         c->d_rtsq.alloc(std::max<size_t>(s.rtasks.size(), 1) * sizeof(double));
     }
-    upload(c->d_stasks_u, c->users.stasks, st);
-    upload(c->d_stasks_v, c->items.stasks, st);
-    upload(c->d_xrows_u, c->users.xrows, st);
-    upload(c->d_xrows_v, c->items.xrows, st);
+    size_t nx = 0, nr = 0;  // split-row slots of the largest stream set (the sets run one after another)
+    for (int sd = 0; sd < 2; ++sd)
+        for (int k = 0; k < 2; ++k) {
+            const Side::StreamSet& S = (sd ? c->items : c->users).ss[k];
+            upload(c->d_stasks[sd][k], S.stasks, st);
+            upload(c->d_xrows[sd][k], S.xrows, st);
+            nx = std::max<size_t>(nx, S.nxchunk);
+            nr = std::max<size_t>(nr, S.xrows.size());
+        }
     {
-        const size_t nx = std::max(c->users.nxchunk, c->items.nxchunk);
-        const size_t nr = std::max(c->users.xrows.size(), c->items.xrows.size());
         c->d_xslabs.alloc(std::max<size_t>(nx, 1) * nblk * (16 * 16 + 16) * sizeof(double));
         c->d_xcnt.alloc(std::max<size_t>(nr, 1) * nblk * sizeof(uint32_t));
         c->d_xtotals.alloc(std::max<size_t>(nr, 1) * nblk * (16 * 16 + 16) * sizeof(double));
@@ -577,13 +598,14 @@ static void prepare_T(sbmf_ctx* c) {
 // rows first; a split row's chunks always share a round, so its workgroups
 // are co-resident (workgroup w runs slot w of every round).  Rounds alternate
 // direction so no slot always gets the largest task.
-static void build_stream_tasks(Side& s, uint32_t cmax, uint32_t gres, uint32_t nblk) {
-    s.stasks.clear();
-    s.xrows.clear();
-    s.nxchunk = 0;
-    s.sgrid = 0;
-    const std::vector<uint32_t>& rows = s.bin_rows[KIND_STREAM];  // degree-descending
-    if (rows.empty()) return;
+static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vector<uint32_t>& rows, uint32_t gres,
+                               uint32_t nblk) {
+    const uint32_t cmax = S.cmax;
+    S.stasks.clear();
+    S.xrows.clear();
+    S.nxchunk = 0;
+    S.sgrid = 0;
+    if (rows.empty()) return;  // rows: degree-descending
     std::vector<std::vector<SplitTask>> rounds;
     uint32_t fill = gres;
     for (uint32_t r : rows) {
@@ -598,24 +620,24 @@ static void build_stream_tasks(Side& s, uint32_t cmax, uint32_t gres, uint32_t n
         if (nch == 1) {
             rounds.back().push_back(SplitTask{r, s.ptr[r], n, 1, 0, 0, 0, 0});
         } else {
-            const uint32_t slab0 = s.nxchunk;
-            const uint32_t cnt0 = (uint32_t)s.xrows.size() * nblk;
+            const uint32_t slab0 = S.nxchunk;
+            const uint32_t cnt0 = (uint32_t)S.xrows.size() * nblk;
             const uint32_t per = (n + nch - 1) / nch;
             for (uint32_t c = 0; c < nch; ++c) {
                 const uint32_t b = c * per, e = std::min(n, b + per);
                 rounds.back().push_back(SplitTask{r, s.ptr[r] + b, e - b, nch, c, slab0, cnt0, 0});
             }
-            s.xrows.push_back(SplitRow{r, slab0, nch, 0});
-            s.nxchunk += nch;
+            S.xrows.push_back(SplitRow{r, slab0, nch, 0});
+            S.nxchunk += nch;
         }
         fill += nch;
     }
-    s.sgrid = rounds.size() > 1 ? gres : (uint32_t)rounds[0].size();
+    S.sgrid = rounds.size() > 1 ? gres : (uint32_t)rounds[0].size();
     for (size_t k = 0; k < rounds.size(); ++k) {
         std::vector<SplitTask>& rd = rounds[k];
         if (k + 1 < rounds.size()) rd.resize(gres, SplitTask{0, 0, 0, 1, 0, 0, 0, 0});  // empty slots
         if (k & 1) std::reverse(rd.begin(), rd.end());
-        s.stasks.insert(s.stasks.end(), rd.begin(), rd.end());
+        S.stasks.insert(S.stasks.end(), rd.begin(), rd.end());
     }
 }
 
@@ -836,21 +858,26 @@ static void run_half(sbmf_ctx* c, bool users) {
         } else if (k < GK_NUM)
             HIPCHK(launch_gblock<T>(k, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
         else if (k == KIND_STREAM) {
-            SplitSync sy{};
-            sy.slabs = c->d_xslabs.as<double>();
-            sy.totals = c->d_xtotals.as<double>();
-            sy.counters = c->d_xcnt.as<uint32_t>();
-            sy.nblk = (c->K + 15) / 16;
-            sy.ncounters = (uint32_t)s.xrows.size() * sy.nblk;
-            sy.chunk_sq = c->d_xchunk_sq.as<double>();
-            sy.chunk_tr = c->d_xchunk_tr.as<double>();
-            sy.newown = c->d_xnewown.p;
-            sy.timeout = c->d_xtimeout.as<uint32_t>();
-            sy.cmax = c->cmax;
-            sy.prof = c->kprof ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
-            HIPCHK(launch_gstream<T>((users ? c->d_stasks_u : c->d_stasks_v).as<SplitTask>(), (uint32_t)s.stasks.size(),
-                                     s.sgrid, (users ? c->d_xrows_u : c->d_xrows_v).as<SplitRow>(),
-                                     (uint32_t)s.xrows.size(), a, sy, st));
+            for (int set = 0; set < 2; ++set) {
+                const Side::StreamSet& S = s.ss[set];
+                if (S.stasks.empty()) continue;
+                SplitSync sy{};
+                sy.slabs = c->d_xslabs.as<double>();
+                sy.totals = c->d_xtotals.as<double>();
+                sy.counters = c->d_xcnt.as<uint32_t>();
+                sy.nblk = (c->K + 15) / 16;
+                sy.ncounters = (uint32_t)S.xrows.size() * sy.nblk;
+                sy.chunk_sq = c->d_xchunk_sq.as<double>();
+                sy.chunk_tr = c->d_xchunk_tr.as<double>();
+                sy.newown = c->d_xnewown.p;
+                sy.timeout = c->d_xtimeout.as<uint32_t>();
+                sy.cmax = S.cmax;
+                sy.prof = c->kprof && set == 0 ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
+                HalfArgs<T> as = a;
+                as.tune = S.tune;
+                HIPCHK(launch_gstream<T>(c->d_stasks[sd][set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
+                                         c->d_xrows[sd][set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, st));
+            }
         }
         else
             HIPCHK(launch_rows<T>(k - KIND_RK0, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
@@ -1093,10 +1120,11 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 double tot = 0;
                 for (int k = 0; k < 7; ++k) tot += (double)h[8 * sd + k];
                 if (tot == 0) continue;
-                std::fprintf(stderr, "[kprof] sweep %u %s %s (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep, (cf.tune & 64u) ? "gstream" : "gres",
-                             sd ? "items" : "users", S.sgrid, S.stasks.size());
+                std::fprintf(stderr, "[kprof] sweep %u %s %s (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep,
+                             (cf.tune & 64u) ? "gstream" : "gres", sd ? "items" : "users", S.ss[0].sgrid,
+                             S.ss[0].stasks.size());
                 for (int k = 0; k < 7; ++k)
-                    std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.sgrid / 1e6,
+                    std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.ss[0].sgrid / 1e6,
                                  100.0 * (double)h[8 * sd + k] / tot);
                 std::fprintf(stderr, "\n");
             }

@@ -121,14 +121,18 @@ def test_split_rows_match_oracle(ml100k, chunk, K):
     np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("tune", [0, 1, 4, 8, 13, 32, 33])
+@pytest.mark.parametrize("tune", [0, 1, 4, 8, 13, 64, 65, 96, 97, 128, 1024, 1024 + 128])
 def test_kernel_variants_match_oracle(ml100k, tune):
     """Kernel variants (sbmf_config.tune): block solve by one wave that hands D
     over in LDS (default, bit 0 clear) or by every wave of a row (bit 0 set);
-    bit 5: the streaming kernel on 16-wave workgroups (LDS geometry GsGeom<16, 4>)."""
+    bit 6: the LDS-staged streaming kernel k_gstream instead of k_gres, with
+    bit 5 on 16-wave workgroups (LDS geometry GsGeom<16, 4>); bit 7: k_gres on
+    4-wave workgroups; bit 10: the hybrid schedule (k_gres up to 128 ratings,
+    k_gstream above).  split_chunk 16 splits the longest rows into more than
+    16 chunks (k_gres' two-hop hand-off), 64 into fewer (one hop)."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=50, iters=3, seed=4)
-    for kw in ({}, {"stream_threshold": 40, "split_chunk": 64}):
+    for kw in ({}, {"stream_threshold": 40, "split_chunk": 64}, {"stream_threshold": 40, "split_chunk": 16}):
         L = _run(tr, te, 3, num_factor=50, seed=4, tune=tune, **kw)
         U, V = L.factors()
         assert np.abs(U - o["U"]).max() < 1e-7
