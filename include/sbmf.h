@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SBMF_ABI_VERSION 1
+#define SBMF_ABI_VERSION 2
 #define SBMF_NKIND 11 /* kernel kinds reported by sbmf_get_timing */
 
 enum sbmf_status {
@@ -71,7 +71,18 @@ enum sbmf_quirks { SBMF_QUIRKS_FINAL = 0, SBMF_QUIRKS_SBPMF2 = 1, SBMF_QUIRKS_NO
  * Gaussian posteriors of w0, w and V.  With VB a "sweep" of sbmf_run is an
  * epoch, rmse_avg is the test RMSE of the posterior-mean prediction, tau is
  * alpha, factors / biases are the posterior means, and only F64 is offered. */
-enum sbmf_method { SBMF_METHOD_MCMC = 0, SBMF_METHOD_VB = 1 };
+/* LIBFM_MCMC = libFM's own MCMC chain (bin/libFM -method mcmc,
+ * src/libfm/src/fm_learn_mcmc.h:411-623 draw_all, fm_learn_mcmc_simultaneous.h):
+ * a factorization machine over the users-first one-hot attributes (user u,
+ * item I + i) with global bias w0, attribute biases w and factors v, one
+ * attribute group with Normal-Gamma hyperpriors, noise precision alpha, the
+ * factors drawn f-outer (per factor: every user, then every item) with the
+ * posterior standard deviation; a sweep re-predicts train and test.  ALS =
+ * the same learner without sampling or hyperparameter inference (bin/libFM
+ * -method als, libfm.cpp:132-136): deterministic.  Both use libfm_dim and
+ * reg0 / regw / regv, f64 only, one GPU; rmse_train / rmse_avg are libFM's
+ * "Train=" / "Test=", tau is alpha. */
+enum sbmf_method { SBMF_METHOD_MCMC = 0, SBMF_METHOD_VB = 1, SBMF_METHOD_LIBFM_MCMC = 2, SBMF_METHOD_ALS = 3 };
 
 /* Arithmetic type of factors, residuals and reductions on the GPU.  F64 is
  * the reference's (all-double) arithmetic. */
@@ -120,7 +131,10 @@ typedef struct sbmf_config {
                                  (sum / (sweep + 1), gibbs_sbpmf_final.cpp:559, which counts
                                  burn-in sweeps; quirks none: collected sweeps), 1 = sum over
                                  the collected sweeps / their number, 2 = sum / (sweep + 1)       */
-    uint32_t reserved[1];
+    uint32_t libfm_dim;       /* LIBFM_MCMC / ALS: the k0,k1 of -dim 'k0,k1,K' as bits: bit 0 =
+                                 global bias w0, bit 1 = attribute biases w (default 3)          */
+    double reg0, regw, regv;  /* LIBFM_MCMC / ALS: -regular 'r0,r1,r2' (libfm.cpp:484-513): ALS's
+                                 fixed precisions, MCMC's starting w / v precisions (default 0) */
 } sbmf_config;
 
 /* Per-sweep report passed to the run callback. */

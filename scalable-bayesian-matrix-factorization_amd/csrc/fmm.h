@@ -1,0 +1,89 @@
+// fmm.h -- libFM-order MCMC and ALS (`-method mcmc --order libfm`, `-method
+// als`): the reference's fm_learn_mcmc / fm_learn_mcmc_simultaneous learner
+// (src/libfm/src/fm_learn_mcmc.h:411-623 draw_all, :627-835 draw_w0/w/v,
+// :901-1089 hyperparameters; fm_learn_mcmc_simultaneous.h:50-303) on rating
+// data, on the GPU.
+//
+// Model: a factorization machine over libFM's users-first one-hot layout
+// (attribute u for user u, I + i for item i, p = the libFM attribute count):
+// global bias w0, per-attribute bias w[p] and factors v[K][p] (f-major, as
+// fm_model::v), one attribute group with Normal-Gamma hyperpriors, noise
+// precision alpha.  A sweep draws alpha, w0, the w group hyperparameters and
+// every w (users, then items), the v hyperparameters, then per factor f
+// every v[f][.] (users, then items: the "f-outer" order), re-predicts train
+// and test, and evaluates the running-mean test RMSE.  Per-row conditionals
+// are independent within one (factor, side) pass, so a pass is one launch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/sbmf.h"
+
+namespace sbmf {
+
+// One attribute row of an orientation: its cases are [ptr[row], ptr[row+1]).
+// Rows are binned by length; a bin is launched with 64, 256 or 1024 threads
+// per row.
+struct FMPassArgs {
+    const uint32_t* rows;   // [nrows] rows of this bin
+    uint32_t nrows;
+    const uint32_t* ptr;    // [R+1] case offsets of the orientation (rows past the data: empty)
+    const uint32_t* part;   // [N] partner row of each case (users: item id, items: user id)
+    const uint32_t* perm;   // [N] position of the case in the other orientation's order
+    const double* e_in;     // [N] residuals e = prediction - target, this orientation's order
+    double* e_out;          // [N] residuals, the other orientation's order (e_out[perm[q]])
+    double* own;            // w (bias pass) or column f of v (factor pass), indexed by attribute
+    const double* partner_col;  // factor pass: column f of v (partner values, by attribute)
+    const double* vold_u;   // factor pass, item side: the users' column f before the user pass
+    const double* z;        // normals, z[a * zs + zoff] (do_sample)
+    uint32_t zs, zoff;
+    uint32_t a0;            // attribute of row 0 (0: users, I: items)
+    uint32_t pa0;           // attribute of partner row 0 (I for users, 0 for items)
+    double alpha, mu, lambda;
+    int do_sample;
+    int item_side;          // factor pass: 1 = items (q carries the user pass's updates)
+};
+// draw_w (:670-719) over the rows of a bin
+hipError_t fmm_wpass(const FMPassArgs& a, int threads_per_row, hipStream_t st);
+// draw_v (:780-835) of one factor over the rows of a bin
+hipError_t fmm_vpass(const FMPassArgs& a, int threads_per_row, hipStream_t st);
+// part[b] = {sum e^2, sum (e - w0)} over 1024-case blocks
+hipError_t fmm_esums(const double* e, uint64_t n, double w0, double* part, hipStream_t st);
+// e[q] -= d (the w0 update, :663-666)
+hipError_t fmm_shift(double* e, uint64_t n, double d, hipStream_t st);
+// [K][p] -> [p][Kp] (attribute-major rows for the predictions)
+hipError_t fmm_transpose(const double* v, double* vT, uint32_t K, uint32_t Kp, uint32_t p, hipStream_t st);
+// predict_data_and_write_to_eterms (:117-348) per case, in the reference's
+// accumulation order.  Train (cases in user order, a0 = own_u[q], a1 = I +
+// part_u[q]): e[q] = pred - y[q]; part[b] = sum over the block of
+// (clamp(pred) - y)^2.  Test: pthis[t] = pred, sum_all[t] += clamp(pred);
+// part[2b] = (clamp(sum_all / it1) - y)^2, part[2b+1] = (clamp(pthis) - y)^2.
+struct FMPredictArgs {
+    const double* vT;       // [p][Kp]
+    const double* w;        // [p]
+    double w0;
+    uint32_t K, Kp, I;
+    int k0, k1;
+    double lo, hi;          // train target range (the reference's min/max_target)
+};
+hipError_t fmm_predict_train(const FMPredictArgs& a, const uint32_t* own_u, const uint32_t* part_u, const float* y,
+                             uint64_t n, double* e, double* part, hipStream_t st);
+hipError_t fmm_predict_test(const FMPredictArgs& a, const uint32_t* su, const uint32_t* si, const float* y,
+                            uint64_t n, double it1, double* pthis, double* sum_all, double* part, hipStream_t st);
+
+// ---- host learner (fmm.cpp), driven by the C ABI in sbmf.cpp
+struct FMLearner;
+FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r,
+                      uint64_t nt, const uint32_t* tu, const uint32_t* ti, const double* tr, uint32_t I, uint32_t J,
+                      hipStream_t st);
+void fmm_destroy(FMLearner* L);
+void fmm_run(FMLearner* L, uint32_t iters, sbmf_sweep_cb cb, void* user);
+void fmm_predict_out(FMLearner* L, double* out);       // the -out predictions (fm_learn_mcmc::predict)
+void fmm_factors(FMLearner* L, double* U, double* V);  // v of the users [I][K] and items [J][K]
+void fmm_biases(FMLearner* L, double* bu, double* bv, double* b0);  // w of users, items; w0
+void fmm_hyper_out(FMLearner* L, double* h4k, double* alpha);       // [v_lambda | v_mu | w_lambda,w_mu,0.. | 0]
+uint32_t fmm_launches(const FMLearner* L);
+uint32_t fmm_num_attribute(const FMLearner* L);
+
+}  // namespace sbmf

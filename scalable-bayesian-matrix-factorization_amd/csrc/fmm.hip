@@ -1,0 +1,296 @@
+// fmm.hip -- gfx950 kernels of the libFM-order MCMC / ALS learner (fmm.h).
+//
+// A factor pass is one launch over the attribute rows of one side: a row
+// gathers its cases' residuals (its own order, sequential) and the partner
+// attribute's value of factor f (column f of the f-major table, L2-resident),
+// reduces sum h e and sum h^2 in a fixed order, draws its value, and writes
+// every case's updated residual into the other side's order (e_out[perm[q]]),
+// which is exactly the order the next pass reads.  The libFM cache q (sum of
+// the case's two factor values) is not stored: the user pass rebuilds it as
+// v_u + v_i, the item pass as (v_u_old + v_i) - (v_u_old - v_u_new), the
+// same operations fm_learn_mcmc.h:385-409 and :826-834 apply to it.
+#include <hip/hip_runtime.h>
+
+#include "fmm.h"
+
+namespace sbmf {
+namespace {
+
+__device__ __forceinline__ double wsum(double x) {  // xor butterfly: bit-identical in every lane
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+    return x;
+}
+
+// MODE 0: draw_w (fm_learn_mcmc.h:670-719); MODE 1: draw_v (:780-835).
+// NT threads per row; a 256-thread block holds 256 / NT rows (NT <= 256) or
+// one row (NT = 1024).
+template <int MODE, int NT>
+__global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) {
+    constexpr int RPB = NT >= 256 ? 1 : 256 / NT;
+    constexpr int NWR = NT >= 64 ? NT / 64 : 1;  // waves per row
+    const int sub = threadIdx.x / NT, lt = threadIdx.x % NT;
+    const uint32_t ri = blockIdx.x * RPB + sub;
+    if (NT == 64 && ri >= a.nrows) return;  // a whole wave: no block barriers on this path
+    const uint32_t row = a.rows[ri];
+    const uint32_t beg = a.ptr[row], n = a.ptr[row + 1] - beg;
+    const uint32_t at = a.a0 + row;
+    const double old = a.own[at];
+    const float x = 1.0f;  // one-hot value (DATA_FLOAT)
+    // h of the case at position q (factor pass): x * (q_c - x * v) with the
+    // case's q rebuilt from the factor column (see the file header)
+    auto hval = [&](uint32_t q) {
+        const uint32_t pr = a.part[q];
+        double qc;
+        if (a.item_side) {
+            const double vo = a.vold_u[pr], vn = a.partner_col[pr];
+            qc = ((0.0 + vo * x) + old * x) - x * (vo - vn);
+        } else {
+            qc = (0.0 + old * x) + a.partner_col[a.pa0 + pr] * x;
+        }
+        return x * (qc - x * old);
+    };
+    double m = 0.0, s2 = 0.0;
+    for (uint32_t k = lt; k < n; k += NT) {
+        const double e = a.e_in[beg + k];
+        if constexpr (MODE == 0) {
+            m += x * (e - old * x);
+            s2 += x * x;
+        } else {
+            const double h = hval(beg + k);
+            m += h * e;
+            s2 += h * h;
+        }
+    }
+    m = wsum(m);
+    s2 = wsum(s2);
+    if constexpr (NWR > 1) {  // waves of the row meet in LDS, summed in wave order
+        __shared__ double red[2][NWR];
+        const int w = lt >> 6;
+        if ((lt & 63) == 0) {
+            red[0][w] = m;
+            red[1][w] = s2;
+        }
+        __syncthreads();
+        m = 0.0;
+        s2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < NWR; ++k) {
+            m += red[0][k];
+            s2 += red[1][k];
+        }
+    }
+    if constexpr (MODE == 1) m -= old * s2;
+    s2 = 1.0 / (a.lambda + a.alpha * s2);
+    m = -s2 * (a.alpha * m - a.mu * a.lambda);
+    double nv;
+    if (isnan(s2) || isinf(s2)) {
+        nv = 0.0;
+    } else if (a.do_sample) {  // ran_gaussian(mean, stdev), random.h:166-172
+        const double sd = sqrt(s2);
+        nv = (sd == 0.0 || isnan(sd)) ? m : m + sd * a.z[(size_t)at * a.zs + a.zoff];
+    } else {
+        nv = m;
+    }
+    const bool keep = isnan(nv) || isinf(nv);  // the reference restores the old value and returns
+    if (keep) nv = old;
+    if (lt == 0) a.own[at] = nv;
+    for (uint32_t k = lt; k < n; k += NT) {
+        const uint32_t q = beg + k;
+        const double e = a.e_in[q];
+        double eo = e;
+        if (!keep) {
+            if constexpr (MODE == 0) {
+                const double h = x;
+                eo = e - h * (old - nv);
+            } else {
+                eo = e - hval(q) * (old - nv);
+            }
+        }
+        a.e_out[a.perm[q]] = eo;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fmm_esums(const double* __restrict__ e, uint64_t n, double w0,
+                                                   double* __restrict__ part) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * 1024;
+    double s = 0.0, d = 0.0;
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t q = b0 + k * 256 + threadIdx.x;
+        if (q < n) {
+            const double v = e[q];
+            s += v * v;
+            d += v - w0;
+        }
+    }
+    s = wsum(s);
+    d = wsum(d);
+    __shared__ double red[2][4];
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = s;
+        red[1][threadIdx.x >> 6] = d;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        part[2 * blockIdx.x + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fmm_shift(double* __restrict__ e, uint64_t n, double d) {
+    const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q < n) e[q] -= d;
+}
+
+__global__ __launch_bounds__(256) void k_fmm_transpose(const double* __restrict__ v, double* __restrict__ vT,
+                                                       uint32_t K, uint32_t Kp, uint32_t p) {
+    __shared__ double tile[32][33];
+    const uint32_t a0 = blockIdx.x * 32, f0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int r = ty; r < 32; r += 8) {
+        const uint32_t f = f0 + r, a = a0 + tx;
+        tile[r][tx] = (f < K && a < p) ? v[(size_t)f * p + a] : 0.0;
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const uint32_t a = a0 + r, f = f0 + tx;
+        if (a < p && f < Kp) vT[(size_t)a * Kp + f] = tile[tx][r];
+    }
+}
+
+// prediction of the case with attributes (p0 < p1), in the order of
+// predict_data_and_write_to_eterms: e = sum_f 1/2 q_f^2, q2 = sum_f (-1/2 v0^2 x^2 - 1/2 v1^2 x^2)
+// (+ w0 x + w1 x), e + q2 (+ w0)
+__device__ __forceinline__ double fm_pred(const FMPredictArgs& a, uint32_t p0, uint32_t p1) {
+    const float x = 1.0f;
+    const double* v0 = a.vT + (size_t)p0 * a.Kp;
+    const double* v1 = a.vT + (size_t)p1 * a.Kp;
+    double e = 0.0, q2 = 0.0;
+    for (uint32_t f = 0; f < a.K; ++f) {
+        const double x0 = v0[f], x1 = v1[f];
+        const double q = (0.0 + x0 * x) + x1 * x;
+        e += 0.5 * q * q;
+        q2 -= 0.5 * x0 * x0 * x * x;
+        q2 -= 0.5 * x1 * x1 * x * x;
+    }
+    if (a.k1) {
+        q2 += a.w[p0] * x;
+        q2 += a.w[p1] * x;
+    }
+    e = e + q2;
+    if (a.k0) e += a.w0;
+    return e;
+}
+
+__device__ __forceinline__ double clampd(double p, double lo, double hi) {
+    p = p < hi ? p : hi;  // std::min(max_target, p)
+    return p > lo ? p : lo;  // std::max(min_target, p)
+}
+
+__device__ __forceinline__ double block_sum(double s, double* red) {  // 256 threads, fixed order
+    s = wsum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ __launch_bounds__(256) void k_fmm_predict_train(FMPredictArgs a, const uint32_t* __restrict__ own_u,
+                                                           const uint32_t* __restrict__ part_u,
+                                                           const float* __restrict__ y, uint64_t n,
+                                                           double* __restrict__ e, double* __restrict__ part) {
+    const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    double se = 0.0;
+    if (q < n) {
+        const double pr = fm_pred(a, own_u[q], a.I + part_u[q]);
+        const double err = clampd(pr, a.lo, a.hi) - y[q];
+        se = err * err;
+        e[q] = pr - y[q];
+    }
+    __shared__ double red[4];
+    se = block_sum(se, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = se;
+}
+
+__global__ __launch_bounds__(256) void k_fmm_predict_test(FMPredictArgs a, const uint32_t* __restrict__ su,
+                                                          const uint32_t* __restrict__ si,
+                                                          const float* __restrict__ y, uint64_t n, double it1,
+                                                          double* __restrict__ pthis, double* __restrict__ sum_all,
+                                                          double* __restrict__ part) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    double sa = 0.0, st = 0.0;
+    if (t < n) {
+        const double pr = fm_pred(a, su[t], a.I + si[t]);
+        pthis[t] = pr;
+        const double s = sum_all[t] + clampd(pr, a.lo, a.hi);
+        sum_all[t] = s;
+        const double ea = clampd(s * (1.0 / it1), a.lo, a.hi) - y[t];  // _evaluate: pred * normalizer
+        const double et = clampd(pr * 1.0, a.lo, a.hi) - y[t];
+        sa = ea * ea;
+        st = et * et;
+    }
+    __shared__ double red[2][4];
+    sa = block_sum(sa, red[0]);
+    st = block_sum(st, red[1]);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = sa;
+        part[2 * blockIdx.x + 1] = st;
+    }
+}
+
+template <int MODE>
+hipError_t launch_pass(const FMPassArgs& a, int tpr, hipStream_t st) {
+    if (a.nrows == 0) return hipSuccess;
+    switch (tpr) {
+        case 64:
+            k_fmm_pass<MODE, 64><<<(a.nrows + 3) / 4, 256, 0, st>>>(a);
+            break;
+        case 256:
+            k_fmm_pass<MODE, 256><<<a.nrows, 256, 0, st>>>(a);
+            break;
+        case 1024:
+            k_fmm_pass<MODE, 1024><<<a.nrows, 1024, 0, st>>>(a);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t fmm_wpass(const FMPassArgs& a, int tpr, hipStream_t st) { return launch_pass<0>(a, tpr, st); }
+hipError_t fmm_vpass(const FMPassArgs& a, int tpr, hipStream_t st) { return launch_pass<1>(a, tpr, st); }
+
+hipError_t fmm_esums(const double* e, uint64_t n, double w0, double* part, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    k_fmm_esums<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(e, n, w0, part);
+    return hipGetLastError();
+}
+
+hipError_t fmm_shift(double* e, uint64_t n, double d, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    k_fmm_shift<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(e, n, d);
+    return hipGetLastError();
+}
+
+hipError_t fmm_transpose(const double* v, double* vT, uint32_t K, uint32_t Kp, uint32_t p, hipStream_t st) {
+    dim3 grid((p + 31) / 32, (Kp + 31) / 32);
+    k_fmm_transpose<<<grid, 256, 0, st>>>(v, vT, K, Kp, p);
+    return hipGetLastError();
+}
+
+hipError_t fmm_predict_train(const FMPredictArgs& a, const uint32_t* own_u, const uint32_t* part_u, const float* y,
+                             uint64_t n, double* e, double* part, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    k_fmm_predict_train<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(a, own_u, part_u, y, n, e, part);
+    return hipGetLastError();
+}
+
+hipError_t fmm_predict_test(const FMPredictArgs& a, const uint32_t* su, const uint32_t* si, const float* y,
+                            uint64_t n, double it1, double* pthis, double* sum_all, double* part, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    k_fmm_predict_test<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(a, su, si, y, n, it1, pthis, sum_all, part);
+    return hipGetLastError();
+}
+
+}  // namespace sbmf

@@ -32,6 +32,7 @@
 #include <rccl/rccl.h>
 #include "kernels.h"
 #include "rng.h"
+#include "fmm.h"
 #include "vbo.h"
 
 namespace {
@@ -274,6 +275,7 @@ struct sbmf_ctx {
     size_t h_pinned_bytes = 0;
     sbmf_timing timing{};
     VBLearner* vb = nullptr;  // -method vb (vbo.cpp)
+    FMLearner* fm = nullptr;  // -method mcmc --order libfm / als (fmm.cpp)
     ~sbmf_ctx();
 };
 
@@ -1163,6 +1165,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
 // ===================================================================== C ABI
 sbmf_ctx::~sbmf_ctx() {
     vbo_destroy(vb);
+    fmm_destroy(fm);
     if (h_pinned) (void)hipHostFree(h_pinned);
     for (auto& e : ev)
         if (e) (void)hipEventDestroy(e);
@@ -1221,6 +1224,7 @@ int sbmf_config_default(sbmf_config* c) {
     c->eval_train = 0;
     c->eval_test = 1;
     c->gram_threshold = 0;
+    c->libfm_dim = 3;  // libfm.cpp:130 default -dim 1,1,8
     return SBMF_OK;
 }
 
@@ -1237,9 +1241,12 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     if (cfg->quirks < 0 || cfg->quirks > 4) sbmf::fail(SBMF_E_ARG, "bad quirks");
     if (cfg->average > 2) sbmf::fail(SBMF_E_ARG, "bad average (0 default, 1 collected sweeps, 2 sweep + 1)");
     if (cfg->precision != SBMF_F64 && cfg->precision != SBMF_F32) sbmf::fail(SBMF_E_ARG, "bad precision");
-    if (cfg->method != SBMF_METHOD_MCMC && cfg->method != SBMF_METHOD_VB) sbmf::fail(SBMF_E_ARG, "bad method");
+    if (cfg->method > SBMF_METHOD_ALS) sbmf::fail(SBMF_E_ARG, "bad method");
     if (cfg->method == SBMF_METHOD_VB && cfg->precision != SBMF_F64)
         sbmf::fail(SBMF_E_ARG, "the online VB learner computes in f64 (the reference's double) only");
+    if ((cfg->method == SBMF_METHOD_LIBFM_MCMC || cfg->method == SBMF_METHOD_ALS) && cfg->precision != SBMF_F64)
+        sbmf::fail(SBMF_E_ARG, "the libFM MCMC / ALS learner computes in f64 (the reference's double) only");
+    if (cfg->libfm_dim > 3) sbmf::fail(SBMF_E_ARG, "bad libfm_dim (bit 0 = w0, bit 1 = w)");
     int ndev = 0;
     const hipError_t derr = hipGetDeviceCount(&ndev);
     if (derr != hipSuccess || ndev <= 0)
@@ -1297,6 +1304,31 @@ static void prepare_vb(sbmf_ctx* c) {
     c->prepared = true;
 }
 
+static bool is_fmm(const sbmf_ctx* c) {
+    return c->cfg.method == SBMF_METHOD_LIBFM_MCMC || c->cfg.method == SBMF_METHOD_ALS;
+}
+
+// -method mcmc --order libfm / als: I (the item attribute offset of the
+// users-first layout) and J as for the sampler (max id + 1 over train and
+// test, or sbmf_set_dims)
+static void prepare_fmm(sbmf_ctx* c) {
+    uint32_t umax = 0, imax = 0;
+    for (size_t x = 0; x < c->tu.size(); ++x) {
+        umax = std::max(umax, c->tu[x]);
+        imax = std::max(imax, c->ti[x]);
+    }
+    for (size_t x = 0; x < c->su.size(); ++x) {
+        umax = std::max(umax, c->su[x]);
+        imax = std::max(imax, c->si[x]);
+    }
+    c->I = std::max(c->I_req, umax + 1);
+    c->J = std::max(c->J_req, imax + 1);
+    c->K = c->cfg.num_factor;
+    c->fm = fmm_create(c->cfg, c->tu.size(), c->tu.data(), c->ti.data(), c->tr.data(), c->su.size(), c->su.data(),
+                       c->si.data(), c->sr.data(), c->I, c->J, c->st);
+    c->prepared = true;
+}
+
 static void set_triples(uint64_t n, const uint32_t* u, const uint32_t* i, const double* r, std::vector<uint32_t>& U,
                         std::vector<uint32_t>& I, std::vector<double>& R) {
     if (n && (!u || !i || !r)) sbmf::fail(SBMF_E_ARG, "null array with n > 0");
@@ -1341,6 +1373,8 @@ int sbmf_prepare(sbmf_ctx* ctx) {
             sbmf::fail(SBMF_E_ARG, "rating %zu has an id beyond sbmf_set_dims", x);
     if (ctx->cfg.method == SBMF_METHOD_VB)
         prepare_vb(ctx);
+    else if (is_fmm(ctx))
+        prepare_fmm(ctx);
     else if (ctx->cfg.precision == SBMF_F32)
         prepare_T<float>(ctx);
     else
@@ -1356,10 +1390,20 @@ int sbmf_run(sbmf_ctx* ctx, uint32_t sweeps, sbmf_sweep_cb cb, void* user) {
         if (ctx->tu.empty()) sbmf::fail(SBMF_E_STATE, "no training data (sbmf_set_train)");
         prepare_vb(ctx);
     }
+    if (!ctx->prepared && is_fmm(ctx)) {
+        if (ctx->tu.empty()) sbmf::fail(SBMF_E_STATE, "no training data (sbmf_set_train)");
+        prepare_fmm(ctx);
+    }
     if (ctx->vb) {
         vbo_run(ctx->vb, sweeps, cb, user);
         ctx->timing = sbmf_timing{};
         ctx->timing.n_launch = vbo_launches(ctx->vb);
+        return SBMF_OK;
+    }
+    if (ctx->fm) {
+        fmm_run(ctx->fm, sweeps, cb, user);
+        ctx->timing = sbmf_timing{};
+        ctx->timing.n_launch = fmm_launches(ctx->fm);
         return SBMF_OK;
     }
     if (!ctx->prepared) {
@@ -1385,6 +1429,10 @@ int sbmf_predict(sbmf_ctx* ctx, double* out) {
         vbo_predict_out(ctx->vb, out);
         return SBMF_OK;
     }
+    if (ctx->fm) {
+        fmm_predict_out(ctx->fm, out);
+        return SBMF_OK;
+    }
     const uint64_t T_ = ctx->su.size();
     if (ctx->nranks > 1) ctx->comm.bcast_ranges(ctx->d_tsum.p, sizeof(double), ctx->tbounds, ctx->st);
     HIPCHK(hipStreamSynchronize(ctx->st));
@@ -1404,6 +1452,10 @@ int sbmf_get_factors(sbmf_ctx* ctx, double* U, double* V) {
         vbo_factors(ctx->vb, U, V);
         return SBMF_OK;
     }
+    if (ctx->fm) {
+        fmm_factors(ctx->fm, U, V);
+        return SBMF_OK;
+    }
     if (ctx->cfg.precision == SBMF_F32) {
         if (U) sbmf::download_table<float>(ctx, ctx->d_U, U, ctx->I);
         if (V) sbmf::download_table<float>(ctx, ctx->d_V, V, ctx->J);
@@ -1418,7 +1470,7 @@ int sbmf_set_factors(sbmf_ctx* ctx, const double* U, const double* V) {
     API_BEGIN
     if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
     if (!ctx->prepared) sbmf::fail(SBMF_E_STATE, "not prepared");
-    if (ctx->vb) sbmf::fail(SBMF_E_STATE, "sbmf_set_factors is not supported by the online VB learner");
+    if (ctx->vb || ctx->fm) sbmf::fail(SBMF_E_STATE, "sbmf_set_factors is not supported by the VB / libFM learners");
     HIPCHK(hipSetDevice(ctx->cfg.device));
     HIPCHK(hipStreamSynchronize(ctx->st));
     if (ctx->cfg.precision == SBMF_F32) {
@@ -1440,6 +1492,10 @@ int sbmf_get_hyper(sbmf_ctx* ctx, double* h, double* tau) {
         vbo_hyper_out(ctx->vb, h, tau);
         return SBMF_OK;
     }
+    if (ctx->fm) {
+        fmm_hyper_out(ctx->fm, h, tau);
+        return SBMF_OK;
+    }
     const uint32_t K = ctx->K;
     if (h) {
         std::copy(ctx->sig_u.begin(), ctx->sig_u.end(), h);
@@ -1458,6 +1514,10 @@ int sbmf_get_biases(sbmf_ctx* ctx, double* bu, double* bv, double* b0) {
     HIPCHK(hipSetDevice(ctx->cfg.device));
     if (ctx->vb) {  // posterior means of w (users, items) and w0
         vbo_biases(ctx->vb, bu, bv, b0);
+        return SBMF_OK;
+    }
+    if (ctx->fm) {  // libFM's w (users, items) and w0
+        fmm_biases(ctx->fm, bu, bv, b0);
         return SBMF_OK;
     }
     if (!ctx->bias) sbmf::fail(SBMF_E_STATE, "not a biased sampler (quirks bias2 / bias22) or the VB learner");
@@ -1507,6 +1567,8 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
     ctx->rank = rank;
     if (nranks > 1 && ctx->cfg.method == SBMF_METHOD_VB)
         sbmf::fail(SBMF_E_ARG, "the online VB learner runs on one GPU in this build");
+    if (nranks > 1 && is_fmm(ctx))
+        sbmf::fail(SBMF_E_ARG, "the libFM MCMC / ALS learner runs on one GPU in this build");
     if (nranks > 1 && ctx->bias)
         sbmf::fail(SBMF_E_ARG, "the biased sampler (quirks bias2/bias22) runs on one GPU in this build");
     if (nranks > 1) ctx->comm.init(nranks, rank, id);

@@ -76,6 +76,22 @@ struct CmdLine {
     }
 };
 
+// cmdline.h getStrValues: comma / semicolon separated tokens
+std::vector<std::string> split_strs(const std::string& s) {
+    std::vector<std::string> out;
+    std::string cur;
+    for (char ch : s) {
+        if (ch == ',' || ch == ';') {
+            out.push_back(cur);
+            cur.clear();
+        } else {
+            cur += ch;
+        }
+    }
+    if (!cur.empty()) out.push_back(cur);
+    return out;
+}
+
 std::vector<int> split_ints(const std::string& s) {
     std::vector<int> out;
     std::string cur;
@@ -161,13 +177,17 @@ int main(int argc, char** argv) {
         cl.reg("validation", "unused (SGDA only in libFM)");
         cl.reg("out", "filename for output: averaged test predictions");
         cl.reg("dim", "'k0,k1,k2': k0=use bias, k1=use 1-way interactions, k2=dim of 2-way interactions; default=1,1,8");
-        cl.reg("regular", "unused by the Bayesian sampler (SGD/ALS only in libFM)");
+        cl.reg("regular", "'r0,r1,r2' (or one value for all) for -method als and -method mcmc -order libfm: "
+                          "fixed / starting precisions of w0, w, v (libfm.cpp:484-513); default=0");
         cl.reg("init_stdev", "stdev for initialization of the factors; default: 1.0 (quirks final) / 0.1 (sbpmf2)");
         cl.reg("stdev", "unused");
         cl.reg("iter", "number of collection sweeps; default=100");
         cl.reg("learn_rate", "unused (SGD only)");
-        cl.reg("method", "learning method: mcmc (SBPMF Gibbs) | vb (online variational Bayes, libFM's vb_online; "
-                         "alias vb_online); default=mcmc");
+        cl.reg("method", "learning method: mcmc (SBPMF Gibbs; with -order libfm libFM's own MCMC chain) | "
+                         "als (libFM's ALS) | vb (online variational Bayes, libFM's vb_online; alias vb_online); "
+                         "default=mcmc");
+        cl.reg("order", "-method mcmc: sbpmf (the SBPMF sampler, default) | libfm (libFM's fm_learn_mcmc chain: "
+                        "f-outer, one hyperprior group, w0 / w per -dim k0,k1, sqrt(variance) stdev)");
         cl.reg("verbosity", "how much infos to print; default=0");
         cl.reg("rlog", "write per-sweep measurements to a TSV file; default=''");
         cl.reg("seed", "integer seed; default=1 (glibc default seed of the reference samplers)");
@@ -199,8 +219,12 @@ int main(int argc, char** argv) {
         if (task != "r") throw std::runtime_error("only -task r (regression) is supported by the SBPMF sampler");
         const std::string method = cl.get("method", "mcmc");
         const bool vb = method == "vb" || method == "vb_online";
-        if (method != "mcmc" && !vb)
-            throw std::runtime_error("-method " + method + " is not supported (use mcmc or vb)");
+        const std::string order = cl.get("order", "sbpmf");
+        if (order != "sbpmf" && order != "libfm") throw std::runtime_error("unknown -order " + order);
+        const bool als = method == "als";
+        const bool lfm = als || (method == "mcmc" && order == "libfm");  // libFM's fm_learn_mcmc learner
+        if (method != "mcmc" && !vb && !als)
+            throw std::runtime_error("-method " + method + " is not supported (use mcmc, als or vb)");
         if (!cl.has("train") || !cl.has("test")) throw std::runtime_error("-train and -test are mandatory");
         std::vector<int> dim = split_ints(cl.get("dim", "1,1,8"));
         if (dim.size() != 3) throw std::runtime_error("dim must have 3 numbers");
@@ -209,7 +233,8 @@ int main(int argc, char** argv) {
             throw std::runtime_error("the online VB learner updates w0 and the user/item w: use -dim '1,1,K'");
         const std::string q = cl.get("quirks", "final");
         const bool biased = q == "bias2" || q == "bias22";
-        if (!vb && !biased && (dim[0] || dim[1]))
+        if (lfm && biased) throw std::runtime_error("-quirks bias2|bias22 selects the SBPMF biased sampler, not libFM's");
+        if (!vb && !lfm && !biased && (dim[0] || dim[1]))
             std::cout << "note: bias terms (k0,k1) are not sampled; the reference SBPMF sampler has them compiled "
                          "out (gibbs_sbpmf_final.cpp:276-295); -quirks bias2|bias22 selects the biased sampler"
                       << std::endl;
@@ -253,7 +278,21 @@ int main(int argc, char** argv) {
         cfg.row_kernel = (uint32_t)cl.getl("row_kernel", 0);
         cfg.split_chunk = (uint32_t)cl.getl("split_chunk", 0);
         cfg.eval_train = vb ? 0 : 1;
-        cfg.method = vb ? SBMF_METHOD_VB : SBMF_METHOD_MCMC;
+        cfg.method = vb ? SBMF_METHOD_VB : als ? SBMF_METHOD_ALS : lfm ? SBMF_METHOD_LIBFM_MCMC : SBMF_METHOD_MCMC;
+        if (lfm) {
+            cfg.libfm_dim = (dim[0] ? 1u : 0u) | (dim[1] ? 2u : 0u);
+            if (!cl.has("init_stdev")) cfg.init_stdev = 0.1;  // libfm.cpp:127
+            std::vector<double> reg;
+            for (const std::string& x : split_strs(cl.get("regular", ""))) reg.push_back(std::stod(x));
+            if (reg.size() == 1) reg = {reg[0], reg[0], reg[0]};
+            if (!reg.empty() && reg.size() != 3)
+                throw std::runtime_error("-regular takes 'r' or 'r0,r1,r2' (no -meta groups in this build)");
+            if (reg.size() == 3) {
+                cfg.reg0 = reg[0];
+                cfg.regw = reg[1];
+                cfg.regv = reg[2];
+            }
+        }
         cfg.eval_test = 1;
 
         const std::string fmt = cl.get("format", "auto");
@@ -271,6 +310,9 @@ int main(int argc, char** argv) {
         };
         chk(sbmf_set_train(ctx, tr.n, tr.user, tr.item, tr.rating));
         chk(sbmf_set_test(ctx, te.n, te.user, te.item, te.rating));
+        // libFM's attributes are the file's feature ids: with a libFM input the
+        // users-first item offset is -item_offset
+        if (lfm && off) chk(sbmf_set_dims(ctx, off, 0));
         chk(sbmf_prepare(ctx));
         uint32_t nu, ni;
         uint64_t ntr, nte;
@@ -281,7 +323,8 @@ int main(int argc, char** argv) {
         RunState rs;
         std::ostringstream nm;
         nm << dim[0] << dim[1] << dim[2];
-        rs.rmse_file = "test_rmse_" + nm.str() + "_" + (vb ? std::string("vb_online") : method);
+        // libFM names the file after "mcmc" for als too (the als switch rewrites -method, libfm.cpp:133)
+        rs.rmse_file = "test_rmse_" + nm.str() + "_" + (vb ? std::string("vb_online") : std::string("mcmc"));
         rs.vb = vb;
         { std::ofstream trunc(rs.rmse_file); }
         std::ofstream rlog;

@@ -20,7 +20,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import (F32, F64, METHOD_MCMC, METHOD_VB, QUIRKS_BIAS2, QUIRKS_BIAS22, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
+from ._lib import (F32, F64, METHOD_ALS, METHOD_LIBFM_MCMC, METHOD_MCMC, METHOD_VB, QUIRKS_BIAS2, QUIRKS_BIAS22, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
                    SBMF_E_COMM, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_NOMEM, SBMF_E_STATE, SBMF_OK)
 
 __all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "load_libfm_binary", "save_libfm_binary", "config_default",
@@ -159,11 +159,22 @@ class FMLearnSBPMF:
     def __init__(self, num_factor=20, num_iter=100, seed=1, rng="ref", quirks="final", precision="f64", burnin=0,
                  device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, row_kernel=0,
                  stream_threshold=0, split_chunk=0, tune=0, method="mcmc", vb_batches=0, average="default",
-                 **hyper):
+                 order="sbpmf", k0=1, k1=1, regular=(0.0, 0.0, 0.0), **hyper):
+        """method "mcmc" with order "sbpmf" (default): the SBPMF Gibbs sampler;
+        method "mcmc" with order "libfm": libFM's own MCMC chain (f-outer, one
+        hyperprior group, w0 / w with k0 / k1, -regular = ``regular``);
+        "als": libFM's ALS (the same learner without sampling); "vb": online VB."""
         self.cfg = config_default()
-        if method not in ("mcmc", "vb", "vb_online"):
-            raise ValueError("method must be mcmc or vb")
-        self.cfg.method = METHOD_VB if method in ("vb", "vb_online") else METHOD_MCMC
+        if method not in ("mcmc", "vb", "vb_online", "als") or order not in ("sbpmf", "libfm"):
+            raise ValueError("method must be mcmc, als or vb (order sbpmf or libfm)")
+        if method in ("vb", "vb_online"):
+            self.cfg.method = METHOD_VB
+        elif method == "als":
+            self.cfg.method = METHOD_ALS
+        else:
+            self.cfg.method = METHOD_LIBFM_MCMC if order == "libfm" else METHOD_MCMC
+        self.cfg.libfm_dim = (1 if k0 else 0) | (2 if k1 else 0)
+        self.cfg.reg0, self.cfg.regw, self.cfg.regv = (float(x) for x in regular)
         self.cfg.vb_batches = vb_batches
         self.cfg.num_factor = num_factor
         self.cfg.num_iter = num_iter

@@ -15,7 +15,7 @@ SBMF_OK, SBMF_E_ARG, SBMF_E_STATE, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_COMM, SBMF_E
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 QUIRKS_FINAL, QUIRKS_SBPMF2, QUIRKS_NONE, QUIRKS_BIAS2, QUIRKS_BIAS22 = 0, 1, 2, 3, 4
 F64, F32 = 0, 1
-METHOD_MCMC, METHOD_VB = 0, 1
+METHOD_MCMC, METHOD_VB, METHOD_LIBFM_MCMC, METHOD_ALS = 0, 1, 2, 3
 NKIND = 11  # SBMF_NKIND
 KIND_NAMES = ['gblock_w4', 'gblock_w16', 'gblock_b2', 'gblock_b4', 'gblock_b8', 'gstream', 'rows_w2', 'rows_w8',
               'rows_b4', 'rows_b8', 'gram']
@@ -31,7 +31,8 @@ class Config(C.Structure):
         ("recompute_every", C.c_uint32), ("eval_train", C.c_uint32), ("eval_test", C.c_uint32),
         ("gram_threshold", C.c_uint32), ("row_kernel", C.c_uint32), ("stream_threshold", C.c_uint32),
         ("split_chunk", C.c_uint32), ("tune", C.c_uint32), ("method", C.c_uint32), ("vb_batches", C.c_uint32),
-        ("average", C.c_uint32), ("reserved", C.c_uint32 * 1),
+        ("average", C.c_uint32), ("libfm_dim", C.c_uint32), ("reg0", C.c_double), ("regw", C.c_double),
+        ("regv", C.c_double),
     ]
 
 

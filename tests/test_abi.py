@@ -42,7 +42,8 @@ int main(void) {
   printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(sbmf_config), sizeof(sbmf_sweep_info), sizeof(sbmf_timing),
          sizeof(sbmf_ratings), offsetof(sbmf_config, init_stdev), offsetof(sbmf_config, recompute_every),
          offsetof(sbmf_timing, bytes_algorithmic));
-  printf("%zu %zu\n", offsetof(sbmf_config, method), offsetof(sbmf_config, vb_batches));
+  printf("%zu %zu %zu %zu\n", offsetof(sbmf_config, method), offsetof(sbmf_config, vb_batches),
+         offsetof(sbmf_config, libfm_dim), offsetof(sbmf_config, regv));
   return 0; }''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
@@ -50,7 +51,8 @@ int main(void) {
     import ctypes as C
     want = [C.sizeof(_lib.Config), C.sizeof(_lib.SweepInfo), C.sizeof(_lib.Timing), C.sizeof(_lib.Ratings),
             _lib.Config.init_stdev.offset, _lib.Config.recompute_every.offset, _lib.Timing.bytes_algorithmic.offset,
-            _lib.Config.method.offset, _lib.Config.vb_batches.offset]
+            _lib.Config.method.offset, _lib.Config.vb_batches.offset, _lib.Config.libfm_dim.offset,
+            _lib.Config.regv.offset]
     assert got == want
 
 
@@ -62,7 +64,9 @@ def test_defaults_are_the_reference_constants():
     assert c.clamp_hi == 5.0 and c.rng_mode == sbmf.RNG_REFERENCE and c.quirks == sbmf.QUIRKS_FINAL
     assert c.precision == sbmf.F64
     assert c.method == sbmf._lib.METHOD_MCMC and c.vb_batches == 0
-    assert _lib.lib.sbmf_abi_version() == 1
+    # libfm.cpp:130 (-dim 1,1,K), :484-490 (no -regular: 0)
+    assert c.libfm_dim == 3 and (c.reg0, c.regw, c.regv) == (0.0, 0.0, 0.0)
+    assert _lib.lib.sbmf_abi_version() == 2
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure path")
@@ -87,4 +91,11 @@ def test_bad_config_rejected_before_device():
     assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG
     cfg.method = sbmf._lib.METHOD_VB
     cfg.precision = sbmf.F32  # the VB learner is f64 only
+    assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG
+    for m in (sbmf._lib.METHOD_LIBFM_MCMC, sbmf._lib.METHOD_ALS):  # so are libFM's MCMC and ALS
+        cfg.method = m
+        assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG
+    cfg = sbmf.config_default()
+    cfg.method = sbmf._lib.METHOD_ALS
+    cfg.libfm_dim = 4
     assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG
