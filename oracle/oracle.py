@@ -16,7 +16,8 @@ QUIRKS = {"final": 0, "sbpmf2": 1, "none": 2, "bias2": 3, "bias22": 4}
 class OracleConfig(C.Structure):
     _fields_ = [("K", C.c_uint32), ("iters", C.c_uint32), ("burnin", C.c_uint32), ("seed", C.c_uint),
                 ("quirks", C.c_int), ("init_stdev", C.c_double), ("clamp_lo", C.c_double),
-                ("clamp_hi", C.c_double), ("sweep_seconds_limit", C.c_double), ("rng", C.c_int)]
+                ("clamp_hi", C.c_double), ("sweep_seconds_limit", C.c_double), ("rng", C.c_int),
+                ("threads", C.c_int)]
 
 
 class OracleResult(C.Structure):
@@ -90,7 +91,7 @@ def _p(a, t):
 
 
 def run(train, test, K=20, iters=100, seed=1, quirks="final", burnin=0, num_users=0, num_items=0,
-        seconds_limit=0.0, want_factors=True, rng="ref"):
+        seconds_limit=0.0, want_factors=True, rng="ref", threads=1):
     """train/test: (user, item, rating) arrays.  Returns dict with per-sweep
     'rmse' (running mean, the reference's "rmse is"), 'rmse_this', 'tau',
     final 'U' [I][K], 'V' [J][K], 'hyper', 'pred_sum', 'seconds', and for the
@@ -103,6 +104,9 @@ def run(train, test, K=20, iters=100, seed=1, quirks="final", burnin=0, num_user
     if rng not in ("ref", "philox") or (rng == "philox" and quirks in ("bias2", "bias22")):
         raise ValueError("oracle rng %r with quirks %r" % (rng, quirks))
     cfg.rng = 1 if rng == "philox" else 0
+    if threads > 1 and rng != "philox":
+        raise ValueError("the parallel oracle needs the Philox stream (the glibc stream is sequential)")
+    cfg.threads = threads
     tu, ti, tr = (np.ascontiguousarray(train[0], np.uint32), np.ascontiguousarray(train[1], np.uint32),
                   np.ascontiguousarray(train[2], np.float64))
     su, si, sr = (np.ascontiguousarray(test[0], np.uint32), np.ascontiguousarray(test[1], np.uint32),

@@ -534,9 +534,14 @@ int oracle_run_arrays(const oracle_config *cfg, uint64_t n_train, const uint32_t
     double t_start = now_s();
     res->sweeps_done = 0;
 
+    /* Philox mode only (the glibc stream is sequential): rows of a half-sweep are
+     * independent given the partner table and touch disjoint E entries */
+    const int nth = (px && cfg->threads > 1) ? cfg->threads : 1;
+    (void)nth;
     for (uint32_t iter = 0; iter < iters; iter++) {
         /* E recompute :317-334 */
         double esq = 0.0;
+#pragma omp parallel for schedule(static) reduction(+ : esq) num_threads(nth) if (nth > 1)
         for (uint64_t c = 0; c < n_train; c++) {
             uint32_t user = tu[c], item = ti[c];
             double temp = 0.0;
@@ -586,6 +591,7 @@ int oracle_run_arrays(const oracle_config *cfg, uint64_t n_train, const uint32_t
                 mu_v[k] = o_gaussian(mv_star, qnone ? sqrt(sv_star) : sv_star);
         }
         /* users :453-491 */
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nth) if (nth > 1)
         for (uint32_t i = 0; i < I; i++) {
             uint32_t b = R.ptr[i], e = R.ptr[i + 1];
             for (uint32_t k = 0; k < D; k++) {
@@ -603,11 +609,12 @@ int oracle_run_arrays(const oracle_config *cfg, uint64_t n_train, const uint32_t
                 if (px)
                     *Uik = m_star + (qnone ? sqrt(s_star) : s_star) * px_normal(pseed, i, iter, PX_TAG_USERS, k);
                 else
-                    *Uik = o_gaussian(m_star, qnone ? sqrt(s_star) : s_star);
+                    *Uik = o_gaussian(m_star, qnone ? sqrt(s_star) : s_star); /* serial: nth == 1 */
                 for (uint32_t p = b; p < e; p++) E[R.cas[p]] += Vk[R.oth[p]] * (old - *Uik);
             }
         }
         /* items :495-535 */
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nth) if (nth > 1)
         for (uint32_t j = 0; j < J; j++) {
             uint32_t b = Rt.ptr[j], e = Rt.ptr[j + 1];
             for (uint32_t k = 0; k < D; k++) {

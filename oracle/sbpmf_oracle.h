@@ -20,6 +20,8 @@ typedef struct {
     double sweep_seconds_limit; /* >0: stop after this many seconds (bounded CPU baseline) */
     int rng;                    /* 0: glibc rand() stream (the reference's); 1: the GPU build's Philox
                                    stream mode (unbiased samplers only) */
+    int threads;                /* Philox mode: >1 = rows of each half-sweep in parallel over this many
+                                   OpenMP threads (SURVEY.md §8(d)(ii) all-core CPU baseline) */
 } oracle_config;
 
 typedef struct {

@@ -94,3 +94,39 @@ def test_cli_philox_bench_mode_matches_oracle(tmp_path, ml100k):
          "--recompute_every", "0", "-rlog", str(tmp_path / "rlog.tsv"))
     o = oracle.run(*ml100k, K=32, iters=20, seed=2015, rng="philox", want_factors=False)
     assert np.abs(_rlog(tmp_path / "rlog.tsv") - o["rmse"]).max() < 1e-6
+
+
+def _write_libfm(path, data, item_offset):
+    """users-first libFM text "r u:1 (item_offset + i):1" (Data.h:192-217)."""
+    u, i, r = data
+    with open(path, "w") as f:
+        for a, b, c in zip(u, i, r):
+            f.write("%g %d:1 %d:1\n" % (c, a, item_offset + b))
+
+
+@pytest.mark.parametrize("method", ["mcmc", "als"])
+def test_cli_libfm_methods_reproduce_libfm_output(tmp_path, ml100k, method):
+    """`sbmf` as a drop-in for `bin/libFM -method mcmc|als` on the same libFM
+    text files: the "#Iter=" lines equal libFM's own (tests/golden/ref_libfm_*,
+    libfm.cpp compiled unmodified, time() pinned to the seed), the -out file
+    and test_rmse_118_mcmc within the printed digits."""
+    I = int(max(ml100k[0][0].max(), ml100k[1][0].max())) + 1
+    tr, te = tmp_path / "train.libfm", tmp_path / "test.libfm"
+    _write_libfm(tr, ml100k[0], I)
+    _write_libfm(te, ml100k[1], I)
+    extra = ["-order", "libfm"] if method == "mcmc" else ["-regular", "0,0,10"]
+    cmd = [CLI_PATH, "-task", "r", "-train", str(tr), "-test", str(te), "-dim", "1,1,8", "-iter", "10",
+           "-method", method, "-seed", "1", "-item_offset", str(I), "-out", str(tmp_path / "pred.txt"), *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    name = "ref_libfm_%s_ml100k_d118_s1_i10" % method
+    gold_lines = open(os.path.join(os.path.dirname(__file__), "golden", name + ".txt")).read().splitlines()
+    lines = [l for l in r.stdout.splitlines() if l.startswith("#Iter")]
+    assert lines == gold_lines
+    import gzip
+    with gzip.open(os.path.join(os.path.dirname(__file__), "golden", name + "_pred.txt.gz"), "rt") as f:
+        ref_pred = np.array([float(x) for x in f.read().split()])
+    pred = np.loadtxt(tmp_path / "pred.txt")
+    assert np.abs(pred - ref_pred).max() <= 1.1e-5
+    rm = np.loadtxt(tmp_path / "test_rmse_118_mcmc")
+    assert len(rm) == 10 and abs(rm[-1] - float(gold_lines[-1].split("Test=")[1])) < 1e-5
