@@ -149,7 +149,7 @@ def measure(args, world, rank, local, precision, train, test, uid):
     return res
 
 
-def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85, max_sweeps=400):
+def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85, max_sweeps=200):
     """Wall-clock from the end of data load to the first sweep whose running-mean
     test RMSE <= target, with the reference's averaging rule."""
     from sbmf import Data, FMLearnSBPMF
@@ -176,11 +176,21 @@ def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85
             break
     n = len(L.history)
     last = L.history[-1]["rmse_avg"]
+    this = np.array([h["rmse_this"] for h in L.history])
     L.close()
-    return {"seconds": hit, "sweeps": n, "rmse": last, "burnin": burnin, "quirks": "final",
-            "average": "collected sweeps" if burnin else "sum / (sweep + 1) (reference)",
-            "target": "synthetic proxy: RMSE %.2f on the planted rank-10 set (noise floor ~0.58), not MovieLens" % target,
-            "clock": "end of data load -> first sweep with running-mean test RMSE <= %.2f" % target}
+    out = {"seconds": hit, "sweeps": n, "rmse": last, "burnin": burnin, "quirks": "final",
+           "average": "collected sweeps" if burnin else "sum / (sweep + 1) (reference)",
+           "target": "synthetic proxy: RMSE %.2f on the planted rank-10 set (noise floor ~0.58), not MovieLens" % target,
+           "clock": "end of data load -> first sweep with running-mean test RMSE <= %.2f" % target,
+           "min_rmse_this": float(np.nanmin(this)), "min_rmse_this_sweep": int(np.nanargmin(this)),
+           "rmse_this_last": float(this[-1])}
+    if hit is None:
+        out["note"] = ("not reached: the reference sampler (posterior variance used as the stdev) is under-dispersed "
+                       "and its per-sweep test RMSE climbs after sweep %d (%.3f -> %.3f at sweep %d) as the K=%d "
+                       "factors overfit this rank-10 set, so the mean of the sweeps collected after burn-in %d "
+                       "stays above the target" % (out["min_rmse_this_sweep"], out["min_rmse_this"], this[-1], n - 1,
+                                                   args.K, burnin))
+    return out
 
 
 def cpu_baseline(train, test, dims, K, seconds):

@@ -5,6 +5,8 @@
 #   bash profiles/collect.sh <tag> fetch   --pmc FETCH_SIZE      (each counter pass on its own,
 #   bash profiles/collect.sh <tag> write   --pmc WRITE_SIZE       never combined with other
 #   bash profiles/collect.sh <tag> l2      --pmc TCC_HIT/MISS     tracing domains)
+#   bash profiles/collect.sh <tag> lds     --pmc SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS (bank-conflict share)
+#   bash profiles/collect.sh <tag> gather  --pmc FETCH_SIZE over tests/hip/gather_bench (known bytes: calibration)
 # Outputs land in gpurun_out/<tag>_<pass>*.  Under rocprofv3 (ROCm 7.2) the
 # HIP runtime's exit-time teardown segfaults after the profiler has written
 # its files, so each rocprofv3 pass is the last GPU step of its gpurun call.
@@ -29,6 +31,10 @@ case "$PASS" in
            python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_l2.log" 2>&1 ;;
   sq)    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d "$O/${TAG}_pmc_sq" -o "$TAG" -- \
            python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_sq.log" 2>&1 ;;
+  lds)   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_WAVE_CYCLES -d "$O/${TAG}_pmc_lds" -o "$TAG" -- \
+           python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_lds.log" 2>&1 ;;
+  gather) timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d "$O/${TAG}_pmc_gather" -o "$TAG" -- \
+           "$R/tests/hip/gather_bench" > "$O/${TAG}_pmc_gather.log" 2>&1 ;;
   sq2)   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM -d "$O/${TAG}_pmc_sq2" -o "$TAG" -- \
            python3 "$BENCH" --steps 2 --warmup 1 $SHORT > "$O/${TAG}_pmc_sq2.log" 2>&1 ;;
   *) echo "unknown pass $PASS" >&2; exit 2 ;;

@@ -38,6 +38,9 @@ def key_of(name, order_side):
     m = re.search(r"k_gstream<(double|float), 8, 8, (true|false), (\d)>", name)
     if m:
         return ("item" if m.group(3) == "1" else "user") + "_half/gstream"
+    m = re.search(r"k_gres<(double|float), (\d+), (\d)>", name)  # the default streaming kernel
+    if m:
+        return ("item" if m.group(3) == "1" else "user") + "_half/gstream"
     m = re.search(r"k_gblock<(double|float), (\d+), (\d+), (\d+), (true|false)>", name)
     if m:
         kind = GBLOCK.get((m.group(2), m.group(3), m.group(4)))
@@ -54,7 +57,7 @@ def main():
         side = "user"
         for d in sorted(src):
             name, kb = src[d]
-            if "k_gstream" in name:  # the user half's streaming launch precedes its gblock bins ... items follow
+            if "k_gstream" in name or "k_gres" in name:  # a half's streaming launch precedes its gblock bins
                 side = "item" if re.search(r", 1>", name) else "user"
             if "k_test" in name:
                 side = "user"
