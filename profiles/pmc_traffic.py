@@ -5,9 +5,10 @@ usage: python profiles/pmc_traffic.py <fetch counter_collection.csv> <write coun
 
 Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE (kB) counts the L2's
 memory-side read requests and reports half the bytes of wide streaming reads
-on gfx950, so it is doubled; WRITE_SIZE (kB) is taken as is.  The gather
-kernels here read 8 bytes per lane (the guide leaves that width uncalibrated),
-so the x2 is an assumption noted in the output.  Counters come from separate
+on gfx950, so it is doubled; WRITE_SIZE (kB) is taken as is.  The x2 holds for the 8
+bytes-per-lane partner gathers too: one FETCH_SIZE pass over
+tests/hip/gather_bench (16.13 GB of 112-wide f64 rows gathered per launch)
+reads 7.85 GB, ratio 2.05 (profiles/r02_pmc_gather_calibration.txt).  Counters come from separate
 --pmc passes (never combined with other tracing domains).  Launches are keyed
 like bench.py's roofline kernel: "<user|item>_half/<kind>".
 """

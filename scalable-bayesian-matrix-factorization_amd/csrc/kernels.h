@@ -174,6 +174,10 @@ hipError_t launch_bias_rows(const uint32_t* ptr, uint32_t r0, uint32_t r1, T* E,
 template <typename T>
 hipError_t launch_esum2(const T* E, uint64_t n, double* part, double* out2, hipStream_t st);
 
+// out[2r] = sum(e), out[2r+1] = sum(e^2) over the ratings of rows [r0, r1) (E in their order)
+template <typename T>
+hipError_t launch_rowsum2(const uint32_t* ptr, uint32_t r0, uint32_t r1, const T* E, double* out, hipStream_t st);
+
 // E[idx[j]] = recv[j] for j < n (multi-GPU residual exchange, receiving side)
 template <typename T>
 hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, hipStream_t st);

@@ -1933,6 +1933,29 @@ __global__ __launch_bounds__(256) void k_esum2(const T* __restrict__ E, uint64_t
     }
 }
 
+// Per-row sum(e) and sum(e^2) over the rows [r0, r1) of one orientation
+// (E in its order): out[2r], out[2r+1].  One wave per row, fixed lane order;
+// summed over rows afterwards, the totals do not depend on the rank split.
+template <typename T>
+__global__ __launch_bounds__(256) void k_rowsum2(const uint32_t* __restrict__ ptr, uint32_t r0, uint32_t r1,
+                                                 const T* __restrict__ E, double* __restrict__ out) {
+    const uint32_t r = r0 + blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= r1) return;
+    const int lane = threadIdx.x & 63;
+    double s = 0.0, s2 = 0.0;
+    for (uint32_t q = ptr[r] + lane; q < ptr[r + 1]; q += 64) {
+        const double e = (double)E[q];
+        s += e;
+        s2 += e * e;
+    }
+    s = wave_sum(s);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+        out[2 * (size_t)r] = s;
+        out[2 * (size_t)r + 1] = s2;
+    }
+}
+
 // Multi-GPU residual exchange: residuals other ranks computed for this
 // rank's rows arrive packed; put each at its position in this orientation.
 template <typename T>
@@ -2246,6 +2269,13 @@ hipError_t launch_esum2(const T* E, uint64_t n, double* part, double* out2, hipS
 }
 
 template <typename T>
+hipError_t launch_rowsum2(const uint32_t* ptr, uint32_t r0, uint32_t r1, const T* E, double* out, hipStream_t st) {
+    if (r1 <= r0) return hipSuccess;
+    k_rowsum2<T><<<(r1 - r0 + 3) / 4, 256, 0, st>>>(ptr, r0, r1, E, out);
+    return hipGetLastError();
+}
+
+template <typename T>
 hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, hipStream_t st) {
     if (n == 0) return hipSuccess;
     k_unpack<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(recv, idx, n, E);
@@ -2278,7 +2308,8 @@ hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, h
     template hipError_t launch_bias_rows<T>(const uint32_t*, uint32_t, uint32_t, T*, double*, double*, double*,      \
                                             const double*, const BiasArgs&, hipStream_t);                            \
     template hipError_t launch_esum2<T>(const T*, uint64_t, double*, double*, hipStream_t);                        \
-    template hipError_t launch_unpack<T>(const T*, const uint32_t*, uint64_t, T*, hipStream_t);
+    template hipError_t launch_unpack<T>(const T*, const uint32_t*, uint64_t, T*, hipStream_t);                    \
+    template hipError_t launch_rowsum2<T>(const uint32_t*, uint32_t, uint32_t, const T*, double*, hipStream_t);
 SBMF_INST(float)
 SBMF_INST(double)
 

@@ -551,7 +551,7 @@ static void prepare_T(sbmf_ctx* c) {
         const bool refm = cf.rng_mode == SBMF_RNG_REFERENCE;
         c->d_var3u.alloc((refm ? nb : 0) * 3 * c->I * sizeof(double));
         c->d_var3v.alloc((refm ? nb : 0) * 3 * c->J * sizeof(double));
-        c->d_epart.alloc(nb * 2 * ((N + 1023) / 1024 + 1) * sizeof(double));
+        c->d_epart.alloc(nb * 2 * ((size_t)c->I + 1) * sizeof(double));  // per user row {sum e, sum e^2}
         c->b0 = c->mu_b0 = c->sig_b0 = 0.0;
         c->empty_u.clear();
         c->empty_v.clear();
@@ -968,8 +968,14 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             exchange_residuals<T>(c, false, st);
         }
         HIPCHK(launch_sum(c->d_rowsq_v.as<double>(), c->J, d_res + RES_ESQ, scratch, st));
-        // biased sampler: sum(E) and sum(E^2) of the sweep-start residuals (:342-359)
-        if (c->bias) HIPCHK(launch_esum2<T>(c->d_Eu.as<T>(), N, c->d_epart.as<double>(), d_res + RES_ES, st));
+        // biased sampler: sum(E) and sum(E^2) of the sweep-start residuals (:342-359), per
+        // own user row, rows exchanged, summed in row order (the same for any rank split)
+        if (c->bias) {
+            double* rs2 = c->d_epart.as<double>();
+            HIPCHK(launch_rowsum2<T>(c->d_uptr.as<uint32_t>(), c->users.r0, c->users.r1, c->d_Eu.as<T>(), rs2, st));
+            if (c->nranks > 1) c->comm.bcast_ranges(rs2, 2 * sizeof(double), c->users.bounds, st);
+            HIPCHK(launch_sum_cols(rs2, c->I, 2, d_res + RES_ES, st));
+        }
         // ---- column statistics with the current mu (:378-381, :397-401)
         const T* hyp = c->d_hyper.as<T>();
         double* colpart = c->d_colpart.as<double>();
@@ -1057,6 +1063,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         HIPCHK(hipEventRecord(c->ev[2], st));
         if (c->nranks > 1) {
             c->comm.bcast_ranges(c->d_U.p, c->Kp * sizeof(T), c->users.bounds, st);
+            if (c->bias) c->comm.bcast_ranges(c->d_bu.p, sizeof(double), c->users.bounds, st);
             exchange_residuals<T>(c, true, st);
         }
         HIPCHK(hipEventRecord(c->ev[3], st));
@@ -1071,6 +1078,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         HIPCHK(hipEventRecord(c->ev[4], st));
         if (c->nranks > 1) {
             c->comm.bcast_ranges(c->d_V.p, c->Kp * sizeof(T), c->items.bounds, st);
+            if (c->bias) c->comm.bcast_ranges(c->d_bv.p, sizeof(double), c->items.bounds, st);
             exchange_residuals<T>(c, false, st);
             c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
             if (cf.eval_train) c->comm.bcast_ranges(c->d_rowtr_v.p, sizeof(double), c->items.bounds, st);
@@ -1569,8 +1577,6 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
         sbmf::fail(SBMF_E_ARG, "the online VB learner runs on one GPU in this build");
     if (nranks > 1 && is_fmm(ctx))
         sbmf::fail(SBMF_E_ARG, "the libFM MCMC / ALS learner runs on one GPU in this build");
-    if (nranks > 1 && ctx->bias)
-        sbmf::fail(SBMF_E_ARG, "the biased sampler (quirks bias2/bias22) runs on one GPU in this build");
     if (nranks > 1) ctx->comm.init(nranks, rank, id);
     API_END(ctx)
 }

@@ -1,6 +1,6 @@
 """One rank of the multi-rank sampler (spawned by tests/test_gpu_multirank.py).
 
-usage: python multirank_worker.py <rank> <nranks> <id-hex> <out.npz> <K> <sweeps> <seed> <rng> [tune]
+usage: python multirank_worker.py <rank> <nranks> <id-hex> <out.npz> <K> <sweeps> <seed> <rng> [tune] [quirks]
 The ranks share one GPU and exchange their row blocks through the host comm
 backend (the id was made with SBMF_COMM=host); the result must equal a
 single-rank run in the same residual form.
@@ -30,15 +30,20 @@ def read(path):
 def main():
     rank, nranks, idhex, out, K, sweeps, seed, rng = sys.argv[1:9]
     tune = int(sys.argv[9]) if len(sys.argv) > 9 else 0
+    quirks = sys.argv[10] if len(sys.argv) > 10 else "final"
     from sbmf import Data, FMLearnSBPMF
     g = os.path.join(REPO, "tests", "golden")
     tr, te = read(os.path.join(g, "ml100k_train.tsv.gz")), read(os.path.join(g, "ml100k_test.tsv.gz"))
-    L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, tune=tune)
+    L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, tune=tune, quirks=quirks)
     L.init(comm=(int(nranks), int(rank), bytes.fromhex(idhex)))
     L.set_data(Data(*tr), Data(*te))
     L.learn(sweeps=int(sweeps))
     U, V = L.factors()
-    np.savez(out, U=U, V=V, rmse=L.rmse_trajectory, tau=np.array([h["tau"] for h in L.history]))
+    extra = {}
+    if quirks in ("bias2", "bias22"):
+        bu, bv, b0 = L.biases()
+        extra = {"bu": bu, "bv": bv, "b0": np.array([b0])}
+    np.savez(out, U=U, V=V, rmse=L.rmse_trajectory, tau=np.array([h["tau"] for h in L.history]), **extra)
     L.close()
 
 
