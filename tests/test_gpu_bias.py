@@ -84,12 +84,15 @@ def test_biased_philox_deterministic_and_statistically_equivalent(ml100k):
     b.close()
 
 
-def test_biased_sampler_is_single_gpu_in_this_build():
-    L = FMLearnSBPMF(num_factor=8, quirks="bias2")
-    with pytest.raises(sbmf.SBMFError) as ei:
-        L.init(comm=(2, 0, bytes(128)))
-    assert ei.value.code == sbmf.SBMF_E_ARG and "one GPU" in str(ei.value)
-    L.close()
+def test_libfm_and_vb_learners_are_single_gpu_in_this_build():
+    """The biased sampler runs on several GPUs (tests/test_gpu_multirank.py);
+    the online VB and libFM MCMC / ALS learners are refused for more ranks."""
+    for kw in ({"method": "als"}, {"method": "mcmc", "order": "libfm"}, {"method": "vb"}):
+        L = FMLearnSBPMF(num_factor=8, **kw)
+        with pytest.raises(sbmf.SBMFError) as ei:
+            L.init(comm=(2, 0, bytes(128)))
+        assert ei.value.code == sbmf.SBMF_E_ARG and "one GPU" in str(ei.value)
+        L.close()
 
 
 def test_get_biases_rejects_unbiased_sampler(ml100k):
