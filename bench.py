@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--method", default="mcmc", choices=["mcmc", "vb"])
+    ap.add_argument("--method", default="mcmc", choices=["mcmc", "vb", "libfm", "als"],
+                    help="mcmc: SBPMF Gibbs (headline); vb: online VB; libfm / als: libFM's own MCMC chain / ALS")
     ap.add_argument("--shape", default=None, help="ml-20m (mcmc default) | netflix (vb default) | ml-1m | ...")
     ap.add_argument("--K", type=int, default=None, help="factors (default 100 mcmc / 200 vb)")
     ap.add_argument("--precision", default="f64")
@@ -307,8 +308,64 @@ def vb_main(args):
     _lib.unload()
 
 
+def libfm_main(args):
+    """libFM's own MCMC chain (-method mcmc -order libfm) or ALS on the ML-20M
+    shape: ratings/s per iteration (draw_all + re-prediction + test RMSE)."""
+    from sbmf import Data, FMLearnSBPMF, synth
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        raise SystemExit("bench.py --method libfm|als: the libFM learner runs on one GPU in this build")
+    train, test, dims = synth.generate(args.shape)
+    n_train, n_test, K = len(train[0]), len(test[0]), args.K
+    als = args.method == "als"
+    L = FMLearnSBPMF(num_factor=K, seed=2015, rng="philox", method="als" if als else "mcmc", order="libfm",
+                     regular=(0.0, 0.0, 10.0) if als else (0.0, 0.0, 0.0), init_stdev=0.1,
+                     device=max(args.device, 0))
+    L.set_data(Data(*train), Data(*test))
+    L.learn(sweeps=args.warmup)
+    device_sync()
+    t0 = time.perf_counter()
+    L.learn(sweeps=args.steps)
+    device_sync()
+    dt = time.perf_counter() - t0
+    hist = L.history[-args.steps:]
+    gpu_ms = float(np.mean([h["ms_sweep"] + h["ms_eval"] for h in hist]))
+    # algorithmic bytes per iteration (f64): 2K + 2 passes over every case, each reading
+    # the residual (8), writing it in the other order (8), the case's partner id and
+    # position (8) and the partner value (8; the item side also the user's old value, 8);
+    # the re-prediction reads two attribute rows of K doubles per train and test case
+    # and writes the train residual
+    passes = 2 * (K + 1)
+    bytes_it = n_train * passes * 32.0 + n_train * K * 8.0 + (n_train + n_test) * (16.0 * K + 8.0)
+    out = {
+        "metric": "ratings/sec per libFM %s iteration, %s K=%d" % ("ALS" if als else "MCMC", args.shape, K),
+        "value": n_train * args.steps / dt, "unit": "ratings/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic %s-shaped (sbmf/synth.py)" % args.shape,
+        "config": {"workload": "libFM fm_learn_mcmc iteration (alpha, w0, w, f-outer v passes, re-prediction, "
+                               "test RMSE)%s" % (" without sampling (ALS)" if als else ""),
+                   "method": "als" if als else "mcmc -order libfm", "num_users": dims[0], "num_items": dims[1],
+                   "n_train": n_train, "n_test": n_test, "K": K, "rng": "philox", "gpu_ms_per_iter": gpu_ms,
+                   "launches_per_iter": int(L.timing().n_launch), "test_rmse_after": hist[-1]["rmse_avg"]},
+        "roofline": {"kernel": "iteration (all libFM-learner kernels)", "bound": "hbm",
+                     "achieved": bytes_it / (gpu_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": bytes_it / (gpu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_iter": bytes_it},
+    }
+    L.close()
+    print(json.dumps(out), flush=True)
+    from sbmf import _lib
+    _lib.unload()
+
+
 def main():
     args = parse()
+    if args.method in ("libfm", "als"):
+        if args.shape is None:
+            args.shape = "ml-20m"
+        if args.K is None:
+            args.K = 100
+        return libfm_main(args)
     if args.shape is None:
         args.shape = "netflix" if args.method == "vb" else "ml-20m"
     if args.K is None:
