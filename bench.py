@@ -393,7 +393,9 @@ def main():
     kernel = "%s_half/%s" % ("user" if s == 0 else "item", KIND_NAMES[k])
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    # the PMC pass was taken on the default single-rank ML-20M K=100 f64 run: only that config quotes it
+    profiled = world == 1 and args.shape == "ml-20m" and args.K == 100
+    if profiled and os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get(kernel)
         except Exception:
@@ -401,7 +403,7 @@ def main():
     # LDS bank-conflict share of the dominant kernel (profiles/pmc_lds.py, rocprofv3 --pmc pass)
     lds_frac = None
     pmc = os.path.join(REPO, "profiles", "pmc_lds.json")
-    if os.path.exists(pmc):
+    if profiled and os.path.exists(pmc):
         try:
             lds_frac = (json.load(open(pmc)).get(kernel) or {}).get("frac")
         except Exception:
