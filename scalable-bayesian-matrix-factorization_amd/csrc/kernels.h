@@ -92,7 +92,7 @@ struct SplitRow {
 struct SplitSync {
     double* slabs;       // [nchunk_total][nblk][16*16+16]
     double* totals;      // k_gres: [nsplit_rows * nblk][16*16+16] the chunk-ordered sum (rows > GRES_ALLREAD chunks)
-    uint32_t* counters;  // [nsplit_rows * nblk], zeroed per launch
+    uint32_t* counters;  // [nsplit_rows * nblk], zeroed per launch; then the task-queue head (dynamic order)
     uint32_t ncounters;
     uint32_t nblk;       // ceil(K/16)
     double* chunk_sq;    // [nchunk_total]
@@ -114,8 +114,12 @@ int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune);
 // All streaming tasks of a half-sweep in one cooperative persistent launch of
 // `grid` (<= residency) workgroups; workgroup w runs tasks w, w+grid, ...
 // Tasks are laid out in rounds of `grid` slots and every split row's chunks
-// share a round, so chunk hand-offs only wait on co-resident peers.  Split
-// rows are then published by k_split_finish.
+// share a round, so chunk hand-offs only wait on co-resident peers (k_gstream,
+// and k_gres with tune bit 16); k_gres by default takes one list, claimed in
+// order from a queue head by whichever workgroup is free (a split row's chunks
+// are consecutive, so a chunk only waits for peers that the next free
+// workgroups claim).  Split rows are then
+// published by k_split_finish.
 template <typename T>
 hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid, const SplitRow* srows, uint32_t nsrow,
                           const HalfArgs<T>& a, const SplitSync& sy, hipStream_t st);

@@ -1126,7 +1126,21 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
     T* const eW = eL + 4 * wr + rr;
     constexpr int JS = 4 * NW;
 
-    for (uint32_t ti = blockIdx.x; ti < ntask; ti += gridDim.x) {
+    // task order (default): a queue claimed in list order, one returning atomic
+    // per task, so a split row's chunks start as soon as enough workgroups are
+    // free; tune bit 16: static rounds (workgroup w runs w, w + grid, ...)
+    const bool dyn = !(a.tune & 0x10000u);
+    __shared__ uint32_t qti;
+    for (uint32_t it = 0;; ++it) {
+        uint32_t ti = blockIdx.x + it * gridDim.x;
+        if (dyn) {
+            if (threadIdx.x == 0)
+                qti = __hip_atomic_fetch_add(sy.counters + sy.ncounters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            ti = qti;
+            __syncthreads();  // every thread has its ticket before thread 0 claims the next
+        }
+        if (ti >= ntask) break;
         const SplitTask tk = tasks[ti];
         const uint32_t n = tk.len;
         if (n == 0) continue;  // empty round slot (uniform)
@@ -1135,10 +1149,15 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
         // optional phase profile (build with KPROF=1, run with SBMF_KPROF=1): wave 0's cycles per phase
 #ifdef SBMF_KPROF_BUILD
         unsigned long long tp = (sy.prof && threadIdx.x == 0) ? clock64() : 0ull;
+        // per chunk-count class (whole rows / 2..GRES_ALLREAD chunks / more): [32 + 24*SIDE + 8*cls]
+        unsigned long long* const pcls =
+            sy.prof ? sy.prof - 8 * SIDE + 32 + 24 * SIDE + 8 * (nch == 1 ? 0 : nch <= GRES_ALLREAD ? 1 : 2) : nullptr;
+        if (sy.prof && threadIdx.x == 0) atomicAdd(&pcls[7], 1ull);
         auto stamp = [&](int ph) {
             if (sy.prof && threadIdx.x == 0) {
                 const unsigned long long now = clock64();
                 atomicAdd(&sy.prof[ph], now - tp);
+                atomicAdd(&pcls[ph], now - tp);
                 tp = now;
             }
         };
@@ -1237,7 +1256,12 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                             val[j] += x >= GB * GB ? Cs[w][x - GB * GB] : (r0 == c0 ? Ps[w][r0] : Ls[w][r0][c0]);
                     }
                 }
-                if (nch > 1) {
+#ifdef SBMF_KPROF_BUILD
+                const bool xchg = nch > 1 && !(a.tune & 0x4000u);  // ablation (wrong results): no hand-off
+#else
+                const bool xchg = nch > 1;
+#endif
+                if (xchg) {
                     // cross-chunk sum over the row's chunks (see the header comment)
                     const size_t cstride = (size_t)nblk * SL;  // between one chunk's slabs and the next's
                     const double* pb = sy.slabs + ((size_t)tk.slab0 * nblk + t) * SL;
@@ -1267,7 +1291,11 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     // more: the last arriver sums and publishes the total (two hops, O(nch) traffic)
                     const bool allread = nch <= GRES_ALLREAD;
                     if (threadIdx.x == 0) {
-                        const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        uint32_t old = 0;
+                        if (allread)  // no return value to wait for: the poll follows at once
+                            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        else
+                            old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         lastf = !allread && old == nch - 1;
                         if (allread || old != nch - 1) {
                             const uint32_t want = allread ? nch : nch + 1;
@@ -1341,6 +1369,11 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     const T sd = a.sd_is_var ? var : tsqrt(var);
                     const T A = var * sg * mu + sd * z;
                     const T Bq = var * tau;
+#ifdef SBMF_KPROF_BUILD
+                    if (a.tune & 0x8000u)  // ablation (wrong results): no 16-step recurrence
+                        dlt = A - old + Bq * (Cr[ci] + P * old);
+                    else
+#endif
                     dlt = gblock_solve_lds(&Lr[ci][0], Bq, A - old + Bq * (Cr[ci] + P * old));
                     if (wr == 0 && lane < GB) {
                         if (kin) newS[kk] = old + dlt;
@@ -2052,7 +2085,7 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
 // workgroups (UNR 4), one per CU, instead of two 8-wave ones.
 // k_gres variant: tune bit 7 = 4-wave workgroups (4 per CU, 512-rating f64 tasks)
 static bool use_gres(uint32_t tune) { return !(tune & 64u); }
-static int gres_nw(uint32_t tune) { return (tune & 128u) ? 4 : 8; }
+static int gres_nw(uint32_t tune) { return (tune & 128u) ? 4 : (tune & 0x20000u) ? 16 : 8; }
 static int gstream_nw(uint32_t tune) { return use_gres(tune) ? gres_nw(tune) : (tune & 32u) ? 16 : 8; }
 int gstream_wg_target(uint32_t tune) { return use_gres(tune) ? 16 / gres_nw(tune) : (tune & 32u) ? 1 : 2; }
 template <typename T>
@@ -2092,6 +2125,7 @@ template <typename T>
 static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
     if (use_gres(tune)) {
         if (gres_nw(tune) == 4) return side ? (const void*)k_gres<T, 4, 1> : (const void*)k_gres<T, 4, 0>;
+        if (gres_nw(tune) == 16) return side ? (const void*)k_gres<T, 16, 1> : (const void*)k_gres<T, 16, 0>;
         return side ? (const void*)k_gres<T, 8, 1> : (const void*)k_gres<T, 8, 0>;
     }
     const bool sw = !(tune & 1u);
@@ -2134,10 +2168,8 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     if (ntask == 0) return hipSuccess;
     if (a.K > 256 || sy.cmax == 0 || grid == 0) return hipErrorInvalidValue;
     hipError_t err;
-    if (nsrow) {
-        err = hipMemsetAsync(sy.counters, 0, (size_t)sy.ncounters * sizeof(uint32_t), st);
-        if (err != hipSuccess) return err;
-    }
+    err = hipMemsetAsync(sy.counters, 0, ((size_t)sy.ncounters + 1) * sizeof(uint32_t), st);  // + queue head
+    if (err != hipSuccess) return err;
     // all chunks of a split row must be resident together: the cooperative
     // launch checks that the whole grid fits (the host sizes it to residency)
     const SplitTask* tp = tasks;

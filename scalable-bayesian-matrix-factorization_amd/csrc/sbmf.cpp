@@ -469,7 +469,7 @@ static void prepare_T(sbmf_ctx* c) {
         }
     {
         c->d_xslabs.alloc(std::max<size_t>(nx, 1) * nblk * (16 * 16 + 16) * sizeof(double));
-        c->d_xcnt.alloc(std::max<size_t>(nr, 1) * nblk * sizeof(uint32_t));
+        c->d_xcnt.alloc((nr * nblk + 1) * sizeof(uint32_t));  // + the task-queue head
         c->d_xtotals.alloc(std::max<size_t>(nr, 1) * nblk * (16 * 16 + 16) * sizeof(double));
         c->d_xchunk_sq.alloc(std::max<size_t>(nx, 1) * sizeof(double));
         c->d_xchunk_tr.alloc(std::max<size_t>(nx, 1) * sizeof(double));
@@ -586,8 +586,8 @@ static void prepare_T(sbmf_ctx* c) {
     HIPCHK(hipStreamSynchronize(st));
     c->kprof = std::getenv("SBMF_KPROF") && std::atoi(std::getenv("SBMF_KPROF")) > 0;
     if (c->kprof) {
-        c->d_kprof.alloc(32 * sizeof(unsigned long long));
-        HIPCHK(hipMemset(c->d_kprof.p, 0, 32 * sizeof(unsigned long long)));
+        c->d_kprof.alloc(96 * sizeof(unsigned long long));
+        HIPCHK(hipMemset(c->d_kprof.p, 0, 96 * sizeof(unsigned long long)));
     }
     c->sweep = 0;
     c->collected = 0;
@@ -610,12 +610,14 @@ static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vec
     if (rows.empty()) return;  // rows: degree-descending
     std::vector<std::vector<SplitTask>> rounds;
     uint32_t fill = gres;
+    // k_gres' dynamic order (default; tune bit 16: rounds): one list, heaviest rows first, no padding
+    const bool dyn = !(S.tune & 0x10000u) && !(S.tune & 64u);
     for (uint32_t r : rows) {
         const uint32_t n = s.ptr[r + 1] - s.ptr[r];
         const uint32_t nch = (n + cmax - 1) / cmax;
         if (nch > gres)
             fail(SBMF_E_ARG, "row %u has %u ratings: more than %u co-resident chunks of %u", r, n, gres, cmax);
-        if (fill + nch > gres) {
+        if (rounds.empty() || (!dyn && fill + nch > gres)) {
             rounds.emplace_back();
             fill = 0;
         }
@@ -634,7 +636,7 @@ static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vec
         }
         fill += nch;
     }
-    S.sgrid = rounds.size() > 1 ? gres : (uint32_t)rounds[0].size();
+    S.sgrid = rounds.size() > 1 ? gres : std::min<uint32_t>(gres, (uint32_t)rounds[0].size());
     for (size_t k = 0; k < rounds.size(); ++k) {
         std::vector<SplitTask>& rd = rounds[k];
         if (k + 1 < rounds.size()) rd.resize(gres, SplitTask{0, 0, 0, 1, 0, 0, 0, 0});  // empty slots
@@ -1106,7 +1108,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(hipMemcpyAsync(&split_timeout, c->d_xtimeout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (c->kprof) {
-            unsigned long long h[32];
+            unsigned long long h[96];
             HIPCHK(hipMemcpy(h, c->d_kprof.p, sizeof(h), hipMemcpyDeviceToHost));
             HIPCHK(hipMemset(c->d_kprof.p, 0, sizeof(h)));
             static const char* gn[7] = {"setup", "load+mfma", "barrier", "reduce", "solve+handoff", "e-update",
@@ -1137,6 +1139,15 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                     std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.ss[0].sgrid / 1e6,
                                  100.0 * (double)h[8 * sd + k] / tot);
                 std::fprintf(stderr, "\n");
+                if (cf.tune & 64u) continue;
+                static const char* cn[3] = {"whole rows", "2-16 chunks", ">16 chunks"};
+                for (int cl = 0; cl < 3; ++cl) {
+                    const unsigned long long* hc = h + 32 + 24 * sd + 8 * cl;
+                    if (!hc[7]) continue;
+                    std::fprintf(stderr, "[kprof]   %s: %llu tasks, kcycles per task:", cn[cl], hc[7]);
+                    for (int k = 0; k < 7; ++k) std::fprintf(stderr, " %s %.1f", nm[k], (double)hc[k] / hc[7] / 1e3);
+                    std::fprintf(stderr, "\n");
+                }
             }
         }
         if (split_timeout)  // a bounded spin in k_gstream gave up: the sweep's results are not valid
