@@ -12,7 +12,9 @@ RNG: Philox in-kernel (throughput mode); arithmetic: f64 (the reference's).
 Online VB (BASELINE config 5, `-method vb`): python bench.py --method vb
   [--shape netflix --K 200]; a step is one epoch (30 mini-batches) of the
   online variational-Bayes learner over a Netflix-shaped synthetic set of
-  100 M ratings; single GPU (the VB learner is not partitioned in this build).
+  100 M ratings.  Under torchrun (N GPUs) the users are split into N ranges
+  (one rank each, every case of those users local) and the item rows' sums
+  are all-gathered per pass (RCCL); the dataset is fixed, so scaling is strong.
 
 Single GPU:  python bench.py [--steps K --warmup W]
 Multi GPU:   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
@@ -242,30 +244,33 @@ def mk_uid(world, rank):
 def vb_main(args):
     """BASELINE config 5: online VB epochs (ratings/s per epoch)."""
     from sbmf import Data, FMLearnVBOnline, synth
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        raise SystemExit("bench.py --method vb: the online VB learner runs on one GPU in this build")
-    print("[bench vb] generating the %s-shaped set" % args.shape, file=sys.stderr, flush=True)
+    world, rank, local = dist_setup(args)
+    say = (lambda *a: print(*a, file=sys.stderr, flush=True)) if rank == 0 else (lambda *a: None)
+    say("[bench vb] generating the %s-shaped set" % args.shape)
     t0 = time.time()
     train, test, dims = synth.generate(args.shape)
-    print("[bench vb] %d train ratings in %.0f s" % (len(train[0]), time.time() - t0), file=sys.stderr, flush=True)
+    say("[bench vb] %d train ratings in %.0f s" % (len(train[0]), time.time() - t0))
     n_train = len(train[0])
-    L = FMLearnVBOnline(num_factor=args.K, seed=2015, rng="philox", device=max(args.device, 0))
+    uid = mk_uid(world, rank)
+    L = FMLearnVBOnline(num_factor=args.K, seed=2015, rng="philox", device=local)
+    L.init(comm=(world, rank, uid) if world > 1 else None)
     t0 = time.time()
     L.set_data(Data(*train), Data(*test))
     prep_s = time.time() - t0
     for _ in range(args.warmup):
         L.learn(sweeps=1)
-        print("[bench vb] warm-up epoch %.0f ms (GPU)" % L.history[-1]["ms_sweep"], file=sys.stderr, flush=True)
+        say("[bench vb] warm-up epoch %.0f ms (GPU)" % L.history[-1]["ms_sweep"])
+    barrier(world)
     device_sync()
     t0 = time.perf_counter()
-    L.learn(sweeps=args.steps, callback=lambda h: print("[bench vb] epoch %.0f ms (GPU)" % h["ms_sweep"],
-                                                          file=sys.stderr, flush=True) and False)
+    L.learn(sweeps=args.steps, callback=lambda h: say("[bench vb] epoch %.0f ms (GPU)" % h["ms_sweep"]) and False)
     device_sync()
-    dt = time.perf_counter() - t0
+    barrier(world)
+    dt = max_over_ranks(world, time.perf_counter() - t0)
     hist = L.history[-args.steps:]
     gpu_ms = float(np.mean([h["ms_sweep"] for h in hist]))
     K = args.K
+    one_device = world > 1 and (os.environ.get("SBMF_COMM") == "host" or args.device >= 0)
     # algorithmic bytes per epoch (f64): per case the two partner rows of
     # means and variances for the prediction (4 * 8K), and per factor pass
     # (2K of them) the {e,t} record read + written (32), the partner mean and
@@ -274,12 +279,17 @@ def vb_main(args):
     out = {
         "metric": "ratings/sec per online-VB epoch, %s K=%d" % ({"netflix": "synthetic 100M (Netflix-shaped)"}.get(
             args.shape, args.shape), K),
-        "value": n_train * args.steps / dt, "unit": "ratings/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
+        "value": n_train * args.steps / dt, "unit": "ratings/s", "n_gpus": 1 if one_device else world,
+        "n_ranks": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True,
+        "scaling": "not a scaling number (%d ranks on one GPU)" % world if one_device else "strong",
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic %s-shaped (sbmf/synth.py)" % args.shape,
         "config": {"workload": "online VB epoch (30 mini-batches: e/t terms, update_w0, update_w, factor-outer "
                                "update_v, hyperparameter blends) + test RMSE", "method": "vb",
+                   "parallelism": "user ranges x%d (%s)" % (world, "host-shm exchange, testing only"
+                                                             if os.environ.get("SBMF_COMM") == "host"
+                                                             else "RCCL all-gather of the item sums"),
                    "num_users": dims[0], "num_items": dims[1], "n_train": n_train, "n_test": len(test[0]), "K": K,
                    "rng": "philox", "prep_s": prep_s, "gpu_ms_per_epoch": gpu_ms,
                    "test_rmse_after": hist[-1]["rmse_avg"], "epochs_run": len(L.history)},
@@ -288,7 +298,7 @@ def vb_main(args):
                      "traffic": None, "bytes_per_epoch": bytes_epoch},
     }
     L.close()
-    if not args.no_cpu:
+    if not args.no_cpu and rank == 0 and world == 1:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle
         n = len(train[0])
@@ -303,7 +313,11 @@ def vb_main(args):
                                "sample": "oracle (vbo_oracle.c, serial C restatement of fm_learn_vb_online, f64) for "
                                          "1 epoch on a random %d-rating subsample (all %d users x %d items kept), "
                                          "K=%d, %.1f s" % (take, dims[0], dims[1], K, r["seconds"])}
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
     from sbmf import _lib
     _lib.unload()
 

@@ -194,4 +194,27 @@ void Comm::alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const
     if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
 }
 
+void Comm::allgather(const void* sendbuf, size_t bytes, void* recvbuf, hipStream_t st) {
+    if (nranks_ <= 1) {
+        if (bytes && hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            throw std::runtime_error("allgather: copy failed");
+        return;
+    }
+    if (shm_) {  // host backend: every rank writes its block into the window, then every rank reads all of it
+        if ((size_t)nranks_ * bytes > kHostWindow) throw std::runtime_error("host comm: all-gather larger than the window");
+        if (hipStreamSynchronize(st) != hipSuccess) throw std::runtime_error("hipStreamSynchronize failed");
+        unsigned char* win = shm_ + kHostHeader;
+        if (bytes && hipMemcpy(win + (size_t)rank_ * bytes, sendbuf, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+            throw std::runtime_error("host comm: D2H failed");
+        host_barrier();
+        if (bytes && hipMemcpy(recvbuf, win, (size_t)nranks_ * bytes, hipMemcpyHostToDevice) != hipSuccess)
+            throw std::runtime_error("host comm: H2D failed");
+        host_barrier();
+        return;
+    }
+    if (!comm_ || !bytes) return;
+    ncclResult_t r = ncclAllGather(sendbuf, recvbuf, bytes, ncclUint8, (ncclComm_t)comm_, st);
+    if (r != ncclSuccess) comm_fail("ncclAllGather", r);
+}
+
 }  // namespace sbmf

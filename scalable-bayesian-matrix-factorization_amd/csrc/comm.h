@@ -33,6 +33,12 @@ class Comm {
     void alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const std::vector<size_t>& scnt,
                    void* recvbuf, const std::vector<size_t>& roff, const std::vector<size_t>& rcnt, hipStream_t st);
 
+    // All-gather of equal blocks (ncclAllGather): rank k's `bytes` at sendbuf
+    // land at recvbuf + k * bytes on every rank.
+    void allgather(const void* sendbuf, size_t bytes, void* recvbuf, hipStream_t st);
+    int nranks() const { return nranks_; }
+    int rank() const { return rank_; }
+
   private:
     void host_barrier();
     void* comm_ = nullptr;  // ncclComm_t

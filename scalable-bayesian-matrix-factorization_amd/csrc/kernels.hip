@@ -29,6 +29,11 @@
 #include "kernels.h"
 #include "rng.h"
 
+// timing-only ablation switches (wrong results): KPROF=1 or ABLATE=1 builds
+#if defined(SBMF_KPROF_BUILD) || defined(SBMF_ABLATE_BUILD)
+#define SBMF_ABLATIONS 1
+#endif
+
 namespace sbmf {
 namespace {
 
@@ -476,7 +481,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
         pj[v] = q < n ? a.part[beg + q] : a.zrow;
-#ifdef SBMF_KPROF_BUILD
+#ifdef SBMF_ABLATIONS
         if (a.tune & 0x100u) pj[v] = 0;  // ablation (wrong results): every gather hits one cached row
 #endif
         pm[v] = q < n ? a.perm[beg + q] : 0u;
@@ -527,7 +532,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         }
     }
     T oldc = orow[0], sgc = a.sig[ci], muc = a.mu[ci];
-#ifdef SBMF_KPROF_BUILD
+#ifdef SBMF_ABLATIONS
     // ablation (wrong results): tune 0x800 runs the block loop twice (block index wraps)
     const uint32_t Kr = (K + GB - 1) / GB * GB;
     const uint32_t KL = (a.tune & 0x800u) ? 2 * Kr : K;
@@ -548,7 +553,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         T cc = T(0);
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-#ifdef SBMF_KPROF_BUILD
+#ifdef SBMF_ABLATIONS
             if (a.tune & 0x1000u)  // ablation (wrong results): no MFMA
                 g[v & 3] += s[v];
             else
@@ -617,7 +622,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             const T sd = a.sd_is_var ? var : tsqrt(var);
             const T A = var * sg * mu + sd * z;
             const T Bq = var * tau;
-#ifdef SBMF_KPROF_BUILD
+#ifdef SBMF_ABLATIONS
             if (a.tune & 0x200u)  // ablation (wrong results): no 16-step recurrence
                 dlt = A - old + Bq * (Cs[ws][ci] + P * old);
             else
@@ -639,7 +644,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         }
         stamp(4);  // solve + D hand-off
         // ---- 4. e -= S_B D_B (lane (r,i) holds D_i): 16-lane DPP row sums
-#ifdef SBMF_KPROF_BUILD
+#ifdef SBMF_ABLATIONS
         if (a.tune & 0x400u) {  // ablation (wrong results): residual update without the row sums
 #pragma unroll
             for (int v = 0; v < V; ++v) e[v] -= s[v] * dlt;
@@ -1216,6 +1221,12 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 const T mu = a.mu[kk];
                 if (t > 0) {
                     // apply block t-1 with the held slice, then gather slice t into it
+#ifdef SBMF_ABLATIONS
+                    if (a.tune & 0x40000u) {  // ablation (wrong results): no residual update
+#pragma unroll
+                        for (int j = 0; j < VC; ++j) s[j] = pbase[(size_t)pjW[j * JS] + t * GB];
+                    } else
+#endif
 #pragma unroll
                     for (int j = 0; j < VC; ++j) {
                         eW[j * JS] = eW[j * JS] - row16_sum_sym(s[j] * Dl);  // same value from all 16 lanes
@@ -1225,6 +1236,13 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 stamp(1);  // apply + gather issue
                 acc_t g = {T(0), T(0), T(0), T(0)};
                 T cc = T(0);
+#ifdef SBMF_ABLATIONS
+                if (a.tune & 0x80000u) {  // ablation (wrong results): no MFMA (c only, G from one vector)
+                    g = MfmaT<T>::mfma(s[0], g);
+#pragma unroll
+                    for (int j = 0; j < VC; ++j) cc += s[j] * eW[j * JS];
+                } else
+#endif
 #pragma unroll
                 for (int j = 0; j < VC; ++j) {
                     g = MfmaT<T>::mfma(s[j], g);
@@ -1256,7 +1274,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                             val[j] += x >= GB * GB ? Cs[w][x - GB * GB] : (r0 == c0 ? Ps[w][r0] : Ls[w][r0][c0]);
                     }
                 }
-#ifdef SBMF_KPROF_BUILD
+#ifdef SBMF_ABLATIONS
                 const bool xchg = nch > 1 && !(a.tune & 0x4000u);  // ablation (wrong results): no hand-off
 #else
                 const bool xchg = nch > 1;
@@ -1369,7 +1387,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     const T sd = a.sd_is_var ? var : tsqrt(var);
                     const T A = var * sg * mu + sd * z;
                     const T Bq = var * tau;
-#ifdef SBMF_KPROF_BUILD
+#ifdef SBMF_ABLATIONS
                     if (a.tune & 0x8000u)  // ablation (wrong results): no 16-step recurrence
                         dlt = A - old + Bq * (Cr[ci] + P * old);
                     else

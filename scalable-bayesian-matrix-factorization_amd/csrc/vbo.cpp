@@ -12,6 +12,18 @@
 //   4. test predictions of the means, clamped to the train target range.
 // The reference writes each epoch's 30 batches to text files and parses them
 // back (:148-203); here a batch is an index range in device memory.
+//
+// Several ranks (one process per GPU): rank k owns the users [u_k, u_k+1)
+// (contiguous, balanced by rating count) and every case of those users, so
+// user rows are local.  Every rank replays the same shuffle and keeps the
+// item tables replicated: an item row of a batch is summed over the ranks --
+// each rank writes its cases' {e1, e2} for the batch's items, an all-gather
+// delivers every rank's sums, and every rank applies the same update (rank
+// order) and forwards the deltas to its own cases.  update_w0's and the
+// blends' sums are all-gathered per rank the same way.  One all-gather per
+// item pass (2K + 4 per batch) and the owned user means broadcast once per
+// epoch (test RMSE, factors).  Results agree with one rank to rounding (the
+// item sums are added rank by rank), and are identical on every rank.
 #include "vbo.h"
 
 #include <algorithm>
@@ -22,6 +34,7 @@
 #include <thread>
 #include <vector>
 
+#include "comm.h"
 #include "common.h"
 #include "rng.h"
 
@@ -35,7 +48,11 @@ struct VBLayout {
     std::vector<uint32_t> urow0, irow0, utask0, itask0, bsize, bbase;
     std::vector<uint32_t> u2i, upart, i2u, ipart;  // [N] per entry of each order
     std::vector<float> ur;                          // [N] target per user-order entry
-    DBuf d_urows, d_irows, d_utasks, d_itasks, d_u2i, d_upart, d_i2u, d_ipart, d_ur;
+    // several ranks: bsize / bbase count this rank's cases; gbsize the whole batch;
+    // gitems the batch's items over all ranks (entries [gitem0[b], gitem0[b+1]))
+    std::vector<uint32_t> gbsize, gitem0;
+    std::vector<VGItem> gitems;
+    DBuf d_urows, d_irows, d_utasks, d_itasks, d_u2i, d_upart, d_i2u, d_ipart, d_ur, d_gitems;
 };
 
 struct VBLearner {
@@ -58,6 +75,14 @@ struct VBLearner {
     DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_ETu, d_ETv, d_part;
     DBuf d_tu, d_ti, d_tr, d_pred, d_tpart;
     VBTables tb{};
+    // several ranks
+    Comm* comm = nullptr;
+    int R = 1, rank = 0;
+    uint32_t u0 = 0, u1 = 0, NL = 0;  // owned users [u0, u1), their cases (NL)
+    std::vector<uint64_t> ubounds;     // [R + 1] user ranges of every rank
+    std::vector<uint8_t> mine;         // [N] case belongs to an owned user
+    uint32_t gmax = 0;                 // largest per-batch item count
+    DBuf d_send, d_recv, d_sums, d_recvg, d_delta;
     double last_rmse = NAN, last_alpha = NAN;
     double ms_layout = 0.0;
     uint32_t n_launch = 0;
@@ -69,16 +94,25 @@ struct VBLearner {
     }
 
     void init(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r, uint64_t nt,
-              const uint32_t* tu_, const uint32_t* ti_, const double* tr_, uint32_t I_, uint32_t J_, hipStream_t s);
+              const uint32_t* tu_, const uint32_t* ti_, const double* tr_, uint32_t I_, uint32_t J_, hipStream_t s,
+              Comm* cm);
     void build_layout(VBLayout& L, uint32_t ep);
     void run(uint32_t epochs, sbmf_sweep_cb cb, void* user);
+    void item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_, const uint32_t* i2u_,
+                   int factor, uint32_t f, double2* ETv, double2* ETu);
+    void sync_users();
 };
 
 void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r,
                      uint64_t nt, const uint32_t* tu_, const uint32_t* ti_, const double* tr_, uint32_t I_, uint32_t J_,
-                     hipStream_t s) {
+                     hipStream_t s, Comm* cm) {
     cfg = c;
     st = s;
+    if (cm && cm->nranks() > 1) {
+        comm = cm;
+        R = cm->nranks();
+        rank = cm->rank();
+    }
     K = c.num_factor;
     Kp = (K + 15) / 16 * 16;
     I = I_;
@@ -125,6 +159,29 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
         cc[tu[x]]++;
         cc[I + ti[x]]++;
     }
+    // user ranges: contiguous, cut where the running rating count passes k N / R
+    ubounds.assign(R + 1, 0);
+    {
+        uint64_t run = 0;
+        int k = 1;
+        for (uint32_t a = 0; a < I && k < R; ++a) {
+            run += cc[a];
+            while (k < R && run * R >= (uint64_t)N * k) ubounds[k++] = a + 1;
+        }
+        for (; k < R; ++k) ubounds[k] = I;
+        ubounds[R] = I;
+    }
+    u0 = (uint32_t)ubounds[rank];
+    u1 = (uint32_t)ubounds[rank + 1];
+    mine.assign(N, 1);
+    NL = N;
+    if (R > 1) {
+        NL = 0;
+        for (uint32_t x = 0; x < N; ++x) {
+            mine[x] = tu[x] >= u0 && tu[x] < u1;
+            NL += mine[x];
+        }
+    }
     upload(d_mu_v, mu_v, st);
     upload(d_sg_v, sg_v, st);
     upload(d_nm_v, nm_v, st);
@@ -154,8 +211,12 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     d_sgT.alloc((size_t)p * Kp * sizeof(double));
     HIPCHK(hipMemsetAsync(d_muT.p, 0, d_muT.bytes, st));
     HIPCHK(hipMemsetAsync(d_sgT.p, 0, d_sgT.bytes, st));
-    d_ETu.alloc((size_t)N * sizeof(double2));  // {e, t} per case, user-grouped epoch order
-    d_ETv.alloc((size_t)N * sizeof(double2));  // item-grouped epoch order
+    d_ETu.alloc((size_t)std::max(NL, 1u) * sizeof(double2));  // {e, t} per (own) case, user-grouped epoch order
+    d_ETv.alloc((size_t)std::max(NL, 1u) * sizeof(double2));  // item-grouped epoch order
+    if (R > 1) {
+        d_send.alloc((size_t)(K + 2) * sizeof(double));
+        d_recv.alloc((size_t)R * (K + 2) * sizeof(double));
+    }
     d_part.alloc(vbo_scratch_doubles(S, K, p) * sizeof(double));
     upload(d_tu, su, st);
     upload(d_ti, si, st);
@@ -249,19 +310,43 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         });
     }
     L.bsize.assign(NB, 0);
-    for (uint32_t l = 0; l < N; ++l) L.bsize[bid[l]]++;
-    L.bbase.assign(NB + 1, 0);  // a batch's cases are entries [bbase[b], bbase[b+1]) of either order
+    L.gbsize.assign(NB, 0);
+    for (uint32_t l = 0; l < N; ++l) {
+        L.gbsize[bid[l]]++;
+        L.bsize[bid[l]] += mine[l];
+    }
+    L.bbase.assign(NB + 1, 0);  // a batch's (own) cases are entries [bbase[b], bbase[b+1]) of either order
     for (uint32_t b = 0; b < NB; ++b) L.bbase[b + 1] = L.bbase[b] + L.bsize[b];
-    bcase.resize(N);  // the cases of each batch, in file order
+    bcase.resize(NL);  // the (own) cases of each batch, in file order
     {
         std::vector<uint32_t> fill(L.bbase.begin(), L.bbase.end() - 1);
-        for (uint32_t l = 0; l < N; ++l) bcase[fill[bid[l]]++] = l;
+        for (uint32_t l = 0; l < N; ++l)
+            if (mine[l]) bcase[fill[bid[l]]++] = l;
+    }
+    // several ranks: every batch's items over all ranks, and each item's index there
+    std::vector<uint32_t> gidx;
+    if (R > 1) {
+        std::vector<uint32_t> cnt((size_t)NB * J, 0);
+        for (uint32_t l = 0; l < N; ++l) cnt[(size_t)bid[l] * J + ti[l]]++;
+        L.gitems.clear();
+        L.gitem0.assign(NB + 1, 0);
+        gidx.assign((size_t)NB * J, 0);
+        for (uint32_t b = 0; b < NB; ++b) {
+            L.gitem0[b] = (uint32_t)L.gitems.size();
+            for (uint32_t a = 0; a < J; ++a)
+                if (cnt[(size_t)b * J + a]) {
+                    gidx[(size_t)b * J + a] = (uint32_t)L.gitems.size() - L.gitem0[b];
+                    L.gitems.push_back(VGItem{I + a, cnt[(size_t)b * J + a]});
+                }
+            gmax = std::max(gmax, (uint32_t)L.gitems.size() - L.gitem0[b]);
+        }
+        L.gitem0[NB] = (uint32_t)L.gitems.size();
     }
     upos.resize(N);
     ipos.resize(N);
-    L.upart.resize(N);
-    L.ipart.resize(N);
-    L.ur.resize(N);
+    L.upart.resize(NL);
+    L.ipart.resize(NL);
+    L.ur.resize(NL);
     // per batch and orientation: rows in attribute order, then stably by lane-group size
     struct Part {
         std::vector<VRow> rows;
@@ -274,16 +359,16 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         return lg;
     };
     auto group = [&](uint32_t b, bool users, std::vector<uint32_t>& off, Part& P) {
-        const uint32_t R = users ? I : J;
+        const uint32_t nattr = users ? I : J;
         const uint32_t c0 = L.bbase[b], c1 = L.bbase[b + 1];
         std::fill(off.begin(), off.end(), 0u);
         for (uint32_t x = c0; x < c1; ++x) off[users ? tu[bcase[x]] : ti[bcase[x]]]++;
         std::vector<VRow> rows;
         uint32_t run = c0;
-        for (uint32_t a = 0; a < R; ++a) {
+        for (uint32_t a = 0; a < nattr; ++a) {
             const uint32_t n = off[a];
             if (!n) continue;
-            rows.push_back(VRow{users ? a : I + a, run, n, 0});
+            rows.push_back(VRow{users ? a : I + a, run, n, (!users && R > 1) ? gidx[(size_t)b * J + a] : 0u});
             off[a] = run;  // becomes the fill position
             run += n;
         }
@@ -349,14 +434,46 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
     };
     concat(pu, L.urows, L.urow0, L.utasks, L.utask0);
     concat(pi, L.irows, L.irow0, L.itasks, L.itask0);
-    L.u2i.resize(N);
-    L.i2u.resize(N);
+    L.u2i.resize(NL);
+    L.i2u.resize(NL);
     parallel_chunks(N, [&](unsigned, uint32_t lo, uint32_t hi) {
-        for (uint32_t l = lo; l < hi; ++l) {
-            L.u2i[upos[l]] = ipos[l];
-            L.i2u[ipos[l]] = upos[l];
-        }
+        for (uint32_t l = lo; l < hi; ++l)
+            if (mine[l]) {
+                L.u2i[upos[l]] = ipos[l];
+                L.i2u[ipos[l]] = upos[l];
+            }
     });
+}
+
+// Several ranks: one item pass of a batch (the update_w biases, factor == 0,
+// or update_v of factor f): local sums -> all-gather -> the same update on
+// every rank -> deltas forwarded to the local cases.
+void VBLearner::item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_,
+                          const uint32_t* i2u_, int factor, uint32_t f, double2* ETv, double2* ETu) {
+    const uint32_t nG = L.gitem0[b + 1] - L.gitem0[b];
+    if (nG == 0) return;  // every rank sees the same global list
+    double2* sums = d_sums.as<double2>();
+    HIPCHK(hipMemsetAsync(sums, 0, (size_t)nG * sizeof(double2), st));
+    if (factor)
+        HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st, 1, sums, nullptr));
+    else
+        HIPCHK(vbo_update_w(it_, nit, ir_, i2u_, 0, tb, ETv, ETu, st, 1, sums, nullptr));
+    comm->allgather(sums, (size_t)nG * sizeof(double2), d_recvg.p, st);
+    double4* delta = d_delta.as<double4>();
+    HIPCHK(vbo_item_update(L.d_gitems.as<VGItem>() + L.gitem0[b], nG, d_recvg.as<double2>(), R, factor, f, tb, delta,
+                           st));
+    if (factor)
+        HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st, 2, nullptr, delta));
+    else
+        HIPCHK(vbo_update_w(it_, nit, ir_, i2u_, 0, tb, ETv, ETu, st, 2, nullptr, delta));
+    n_launch += 3;
+}
+
+// Several ranks: every rank's owned user means (factors and biases) to every rank
+void VBLearner::sync_users() {
+    if (R <= 1) return;
+    for (uint32_t f = 0; f < K; ++f) comm->bcast_ranges(tb.mu_v + (size_t)f * p, sizeof(double), ubounds, st);
+    comm->bcast_ranges(tb.mu_w, sizeof(double), ubounds, st);
 }
 
 void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
@@ -386,6 +503,12 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         grow(L.d_ipart, L.ipart.size() * sizeof(L.ipart[0]));
         grow(L.d_utasks, L.utasks.size() * sizeof(L.utasks[0]));
         grow(L.d_itasks, L.itasks.size() * sizeof(L.itasks[0]));
+        if (R > 1) {
+            grow(L.d_gitems, L.gitems.size() * sizeof(L.gitems[0]));
+            d_sums.ensure((size_t)std::max(gmax, 1u) * sizeof(double2));
+            d_recvg.ensure((size_t)R * std::max(gmax, 1u) * sizeof(double2));
+            d_delta.ensure((size_t)std::max(gmax, 1u) * sizeof(double4));
+        }
         const auto h2 = std::chrono::steady_clock::now();
         upload_grow(L.d_urows, L.urows, st);
         upload_grow(L.d_irows, L.irows, st);
@@ -396,6 +519,7 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         upload_grow(L.d_ipart, L.ipart, st);
         upload_grow(L.d_utasks, L.utasks, st);
         upload_grow(L.d_itasks, L.itasks, st);
+        if (R > 1) upload_grow(L.d_gitems, L.gitems, st);
         if (trace) {
             HIPCHK(hipStreamSynchronize(st));
             const auto h3 = std::chrono::steady_clock::now();
@@ -420,7 +544,13 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             HIPCHK(vbo_transpose(tb.sg_v, d_sgT.as<double>(), K, Kp, p, st));
             HIPCHK(vbo_predict(ur_ + L.urow0[b], nu, L.d_upart.as<uint32_t>(), L.d_ur.as<float>(), d_muT.as<double>(),
                                d_sgT.as<double>(), tb, Kp, ETu, st));
-            HIPCHK(vbo_update_w0(ETu + L.bbase[b], B, tb, part, st));
+            if (R > 1) {  // update_w0 from every rank's local sum
+                HIPCHK(vbo_w0_local(ETu + L.bbase[b], B, tb, part, d_send.as<double>(), st));
+                comm->allgather(d_send.p, sizeof(double), d_recv.p, st);
+                HIPCHK(vbo_w0_final(d_recv.as<double>(), R, L.gbsize[b], tb, st));
+            } else {
+                HIPCHK(vbo_update_w0(ETu + L.bbase[b], B, tb, part, st));
+            }
             const VTask* ut = L.d_utasks.as<VTask>() + L.utask0[b];
             const VTask* it_ = L.d_itasks.as<VTask>() + L.itask0[b];
             const uint32_t nut = L.utask0[b + 1] - L.utask0[b], nit = L.itask0[b + 1] - L.itask0[b];
@@ -428,12 +558,24 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             const uint32_t* u2i_ = L.d_u2i.as<uint32_t>();
             const uint32_t* i2u_ = L.d_i2u.as<uint32_t>();
             HIPCHK(vbo_update_w(ut, nut, ur_, u2i_, 1, tb, ETu, ETv, st));
-            HIPCHK(vbo_update_w(it_, nit, ir_, i2u_, 0, tb, ETv, ETu, st));
+            if (R > 1)
+                item_pass(L, b, it_, nit, ir_, i2u_, 0, 0, ETv, ETu);
+            else
+                HIPCHK(vbo_update_w(it_, nit, ir_, i2u_, 0, tb, ETv, ETu, st));
             for (uint32_t f = 0; f < K; ++f) {
                 HIPCHK(vbo_update_v(ut, nut, ur_, u2i_, L.d_upart.as<uint32_t>(), f, tb, ETu, ETv, st));
-                HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st));
+                if (R > 1)
+                    item_pass(L, b, it_, nit, ir_, i2u_, 1, f, ETv, ETu);
+                else
+                    HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st));
             }
-            HIPCHK(vbo_hyper(ETu + L.bbase[b], B, tb, part, st));
+            if (R > 1) {  // the blends from every rank's alpha sum and user-range sig sums
+                HIPCHK(vbo_hyper_local(ETu + L.bbase[b], B, tb, u0, u1, part, d_send.as<double>(), st));
+                comm->allgather(d_send.p, (K + 2) * sizeof(double), d_recv.p, st);
+                HIPCHK(vbo_hyper_final(d_recv.as<double>(), R, L.gbsize[b], tb, I, part, st));
+            } else {
+                HIPCHK(vbo_hyper(ETu + L.bbase[b], B, tb, part, st));
+            }
             n_launch += 2 * K + 12;
         }
         // the next epoch's shuffle and layout, on the host while this epoch runs
@@ -443,6 +585,7 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             const uint32_t nx = epoch + 1;
             worker = std::thread([this, nx] { build_layout(lay[nx & 1], nx); });
         }
+        sync_users();  // several ranks: owned user means to every rank (test RMSE, factors)
         HIPCHK(hipEventRecord(ev[1], st));
         // ---- test RMSE of the clamped means (fm_learn_vb_online_simultaneous.h:348-360,441-447)
         const uint64_t nt = su.size();
@@ -484,9 +627,9 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
 // ---------------------------------------------------------------- entry points used by sbmf.cpp
 VBLearner* vbo_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r,
                       uint64_t nt, const uint32_t* tu, const uint32_t* ti, const double* tr, uint32_t I, uint32_t J,
-                      hipStream_t st) {
+                      hipStream_t st, Comm* comm) {
     std::unique_ptr<VBLearner> L(new VBLearner());
-    L->init(c, n, u, i, r, nt, tu, ti, tr, I, J, st);
+    L->init(c, n, u, i, r, nt, tu, ti, tr, I, J, st, comm);
     return L.release();
 }
 void vbo_destroy(VBLearner* L) { delete L; }

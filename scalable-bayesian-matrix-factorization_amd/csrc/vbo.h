@@ -54,19 +54,41 @@ hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* part, c
 // update_w0 (:586-633): the global bias blend; its deltas are applied to e / t
 // by the user pass of vbo_update_w (apply_w0 = 1)
 hipError_t vbo_update_w0(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
+// Several ranks: an item present in a batch (any rank's cases) and its global
+// case count there; a rank's item rows carry their index in this list in VRow.pad.
+struct VGItem {
+    uint32_t attr, n;
+};
 // One 256-thread block of an update pass: rows [row0, row0 + nrows) of the
 // orientation's row list, each owned by 2^lg lanes (256 >> lg rows at most).
 struct VTask {
     uint32_t row0, nrows, lg, pad;
 };
 // update_w (:635-710) over the rows of one orientation
-// (ETin in the rows' own order, ETout in the other order: ETout[xperm[q]])
+// (ETin in the rows' own order, ETout in the other order: ETout[xperm[q]]).
+// mode 0: sums and update in one pass; several ranks, item rows: mode 1 writes
+// each row's local sums to sums[VRow.pad], mode 2 applies delta[VRow.pad]
+// (from vbo_item_update) to the row's local cases.
 hipError_t vbo_update_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm, int apply_w0,
-                        const VBTables& tb, const double2* ETin, double2* ETout, hipStream_t st);
-// update_v (:712-800) of factor f over the rows of one orientation
+                        const VBTables& tb, const double2* ETin, double2* ETout, hipStream_t st, int mode = 0,
+                        double2* sums = nullptr, const double4* delta = nullptr);
+// update_v (:712-800) of factor f over the rows of one orientation (mode as above)
 hipError_t vbo_update_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm,
                         const uint32_t* part, uint32_t f, const VBTables& tb, const double2* ETin, double2* ETout,
-                        hipStream_t st);
+                        hipStream_t st, int mode = 0, double2* sums = nullptr, const double4* delta = nullptr);
+// several ranks: the items of a batch updated from every rank's local sums
+// (recv [R][nG], rank order; factor f, or the biases when factor == 0)
+hipError_t vbo_item_update(const VGItem* gi, uint32_t nG, const double2* recv, int R, int factor, uint32_t f,
+                           const VBTables& tb, double4* delta, hipStream_t st);
+// several ranks: update_w0's local sum (out[0]) and the update from every rank's (recv[R])
+hipError_t vbo_w0_local(const double2* ET, uint32_t B, const VBTables& tb, double* part, double* out, hipStream_t st);
+hipError_t vbo_w0_final(const double* recv, int R, uint32_t B, const VBTables& tb, hipStream_t st);
+// several ranks: out = [alpha's local sum | K + 1 sig sums over the users [u0, u1)],
+// then the blends from every rank's (recv [R][K + 2]) plus the item range [I, p)
+hipError_t vbo_hyper_local(const double2* ET, uint32_t B, const VBTables& tb, uint32_t u0, uint32_t u1, double* part,
+                           double* out, hipStream_t st);
+hipError_t vbo_hyper_final(const double* recv, int R, uint32_t B, const VBTables& tb, uint32_t I, double* part,
+                           hipStream_t st);
 // step sizes of update_v (:447-453) and the hyperparameter blends (:523-580)
 hipError_t vbo_hyper(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
 // test predictions clamped to [lo, hi] and their squared errors per 256-case block
@@ -75,9 +97,13 @@ hipError_t vbo_test(const uint32_t* tu, const uint32_t* ti, const double* tr, ui
                     double* part, hipStream_t st);
 // ---- host learner (vbo.cpp), driven by the C ABI in sbmf.cpp
 struct VBLearner;
+class Comm;
+// comm: null, or a communicator of R > 1 ranks (one process per GPU): each
+// rank then owns a contiguous, rating-balanced user range and every case of
+// those users; item rows are summed over the ranks (see vbo.cpp)
 VBLearner* vbo_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r,
                       uint64_t nt, const uint32_t* tu, const uint32_t* ti, const double* tr, uint32_t I, uint32_t J,
-                      hipStream_t st);
+                      hipStream_t st, Comm* comm = nullptr);
 void vbo_destroy(VBLearner* L);
 void vbo_run(VBLearner* L, uint32_t epochs, sbmf_sweep_cb cb, void* user);
 void vbo_predict_out(VBLearner* L, double* out);  // clamped test predictions of the means

@@ -28,6 +28,7 @@
 // GPU uses the collapsed forms (same values up to rounding).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "vbo.h"
@@ -184,9 +185,16 @@ constexpr int MC = 4;  // cases a lane keeps in registers between the two passes
 
 // update_w (:635-710) for the rows of one orientation.  apply_w0: first add
 // update_w0's deltas to the row's cases (the user pass touches every case once).
+// MODE (several ranks, item rows; VRow.pad = the item's index g in the batch's
+// global item list): VB_FUSED sums and updates in one pass (one rank);
+// VB_PART writes the row's local sums {e1, e2} to sums[g]; VB_FWD applies the
+// deltas k_item_w left in delta[g] to the local cases.
+enum { VB_FUSED = 0, VB_PART = 1, VB_FWD = 2 };
+template <int MODE>
 __global__ __launch_bounds__(256, 6) void k_update_w(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
                                                    const uint32_t* __restrict__ xperm, int apply_w0, VBTables tb,
-                                                   const double2* __restrict__ ETin, double2* __restrict__ ETout) {
+                                                   const double2* __restrict__ ETin, double2* __restrict__ ETout,
+                                                   double2* __restrict__ sums, const double4* __restrict__ delta) {
     __shared__ double red[256];
     const VTask tk = tasks[blockIdx.x];
     const int G = 1 << tk.lg;
@@ -223,25 +231,40 @@ __global__ __launch_bounds__(256, 6) void k_update_w(const VTask* __restrict__ t
         e1 += ((1 - rho) * mo) + rho * cc * alpha * (e + md);
         e2 += cs;
     }
-    e1 = gsum(e1, G, red);
-    e2 = gsum(e2, G, red);
-    if (!live) return;  // after the last block-wide reduction
-    const uint32_t tw = tb.t_w[a] + n;
-    const double nm = e1 / n, ns = e2 / n;
-    const double mu = nm / ns;
-    double sigma = 1 / ns;
-    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
-    const bool ok = !(std::isnan(mu) || std::isinf(mu));
-    if (ci == 0) {
-        tb.t_w[a] = tw;
-        tb.rho_w[a] = pow((double)(1 + tw), -0.5);
-        tb.nm_w[a] = nm;
-        tb.ns_w[a] = ns;
-        tb.sg_w[a] = sigma;
-        tb.mu_w[a] = ok ? mu : md;
+    bool ok;
+    double dmu, dsg;
+    if (MODE != VB_FWD) {
+        e1 = gsum(e1, G, red);
+        e2 = gsum(e2, G, red);
     }
-    // the reference reverts a non-finite mean and leaves e, t alone (the w0 deltas stay)
-    const double dmu = ok ? md - mu : 0.0, dsg = ok ? sigma - sd : 0.0;
+    if (!live) return;  // after the last block-wide reduction
+    if (MODE == VB_PART) {
+        if (ci == 0) sums[rw.pad] = make_double2(e1, e2);
+        return;
+    } else if (MODE == VB_FWD) {
+        const double4 d = delta[rw.pad];
+        ok = d.w != 0.0;
+        dmu = d.x;
+        dsg = d.y;
+    } else {
+        const uint32_t tw = tb.t_w[a] + n;
+        const double nm = e1 / n, ns = e2 / n;
+        const double mu = nm / ns;
+        double sigma = 1 / ns;
+        if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+        ok = !(std::isnan(mu) || std::isinf(mu));
+        if (ci == 0) {
+            tb.t_w[a] = tw;
+            tb.rho_w[a] = pow((double)(1 + tw), -0.5);
+            tb.nm_w[a] = nm;
+            tb.ns_w[a] = ns;
+            tb.sg_w[a] = sigma;
+            tb.mu_w[a] = ok ? mu : md;
+        }
+        // the reference reverts a non-finite mean and leaves e, t alone (the w0 deltas stay)
+        dmu = ok ? md - mu : 0.0;
+        dsg = ok ? sigma - sd : 0.0;
+    }
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
@@ -268,11 +291,13 @@ __global__ __launch_bounds__(256, 6) void k_update_w(const VTask* __restrict__ t
     }
 }
 
-// update_v (:712-800) of factor f for the rows of one orientation
+// update_v (:712-800) of factor f for the rows of one orientation (MODE as k_update_w)
+template <int MODE>
 __global__ __launch_bounds__(256, 6) void k_update_v(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
                                                    const uint32_t* __restrict__ xperm, const uint32_t* __restrict__ part,
                                                    uint32_t f, VBTables tb, const double2* __restrict__ ETin,
-                                                   double2* __restrict__ ETout) {
+                                                   double2* __restrict__ ETout, double2* __restrict__ sums,
+                                                   const double4* __restrict__ delta) {
     __shared__ double red[256];
     const VTask tk = tasks[blockIdx.x];
     const int G = 1 << tk.lg;
@@ -311,23 +336,40 @@ __global__ __launch_bounds__(256, 6) void k_update_v(const VTask* __restrict__ t
         e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + h1));
         e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (e + md * h));
     }
-    e1 = gsum(e1, G, red);
-    e2 = gsum(e2, G, red);
-    if (!live) return;
-    const double nm = e1 / n, ns = e2 / n;
-    const double mu = nm / ns;
-    double sigma = 1 / ns;
-    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
-    const bool ok = !(std::isnan(mu) || std::isinf(mu));
-    if (ci == 0) {
-        tb.nm_v[off + a] = nm;
-        tb.ns_v[off + a] = ns;
-        s[a] = sigma;
-        v[a] = ok ? mu : md;
-        if (f == 0) tb.t_v[a] += n;  // the caller's count (:447-450)
+    bool ok;
+    double dmu, dsg, dm2;
+    if (MODE != VB_FWD) {
+        e1 = gsum(e1, G, red);
+        e2 = gsum(e2, G, red);
     }
-    // a non-finite mean: the reference returns before touching e, t -- forwarded unchanged
-    const double dmu = ok ? md - mu : 0.0, dsg = ok ? sigma - sd : 0.0, dm2 = ok ? mu * mu - md * md : 0.0;
+    if (!live) return;
+    if (MODE == VB_PART) {
+        if (ci == 0) sums[rw.pad] = make_double2(e1, e2);
+        return;
+    } else if (MODE == VB_FWD) {
+        const double4 d = delta[rw.pad];
+        ok = d.w != 0.0;
+        dmu = d.x;
+        dsg = d.y;
+        dm2 = d.z;
+    } else {
+        const double nm = e1 / n, ns = e2 / n;
+        const double mu = nm / ns;
+        double sigma = 1 / ns;
+        if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+        ok = !(std::isnan(mu) || std::isinf(mu));
+        if (ci == 0) {
+            tb.nm_v[off + a] = nm;
+            tb.ns_v[off + a] = ns;
+            s[a] = sigma;
+            v[a] = ok ? mu : md;
+            if (f == 0) tb.t_v[a] += n;  // the caller's count (:447-450)
+        }
+        // a non-finite mean: the reference returns before touching e, t -- forwarded unchanged
+        dmu = ok ? md - mu : 0.0;
+        dsg = ok ? sigma - sd : 0.0;
+        dm2 = ok ? mu * mu - md * md : 0.0;
+    }
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
@@ -356,6 +398,93 @@ __global__ __launch_bounds__(256, 6) void k_update_v(const VTask* __restrict__ t
     }
 }
 
+// Several ranks: one thread per item g of the batch's global item list; its
+// local sums from every rank (recv[r][g], rank order), its global case count,
+// then exactly k_update_v / k_update_w's update; the deltas go to delta[g] for
+// the VB_FWD pass.  Identical inputs on every rank, so identical results.
+__global__ __launch_bounds__(256) void k_item_v(const VGItem* __restrict__ gi, uint32_t nG,
+                                                 const double2* __restrict__ recv, int R, uint32_t f, VBTables tb,
+                                                 double4* __restrict__ delta) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= nG) return;
+    const uint32_t a = gi[g].attr, n = gi[g].n;
+    double e1 = 0.0, e2 = 0.0;
+    for (int r = 0; r < R; ++r) {
+        e1 += recv[(size_t)r * nG + g].x;
+        e2 += recv[(size_t)r * nG + g].y;
+    }
+    const size_t off = (size_t)f * tb.p;
+    double* __restrict__ v = tb.mu_v + off;
+    double* __restrict__ s = tb.sg_v + off;
+    const double md = v[a], sd = s[a];
+    const double nm = e1 / n, ns = e2 / n;
+    const double mu = nm / ns;
+    double sigma = 1 / ns;
+    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+    const bool ok = !(std::isnan(mu) || std::isinf(mu));
+    tb.nm_v[off + a] = nm;
+    tb.ns_v[off + a] = ns;
+    s[a] = sigma;
+    v[a] = ok ? mu : md;
+    if (f == 0) tb.t_v[a] += n;
+    delta[g] = ok ? make_double4(md - mu, sigma - sd, mu * mu - md * md, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+}
+__global__ __launch_bounds__(256) void k_item_w(const VGItem* __restrict__ gi, uint32_t nG,
+                                                 const double2* __restrict__ recv, int R, VBTables tb,
+                                                 double4* __restrict__ delta) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= nG) return;
+    const uint32_t a = gi[g].attr, n = gi[g].n;
+    double e1 = 0.0, e2 = 0.0;
+    for (int r = 0; r < R; ++r) {
+        e1 += recv[(size_t)r * nG + g].x;
+        e2 += recv[(size_t)r * nG + g].y;
+    }
+    const double md = tb.mu_w[a], sd = tb.sg_w[a];
+    const uint32_t tw = tb.t_w[a] + n;
+    const double nm = e1 / n, ns = e2 / n;
+    const double mu = nm / ns;
+    double sigma = 1 / ns;
+    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+    const bool ok = !(std::isnan(mu) || std::isinf(mu));
+    tb.t_w[a] = tw;
+    tb.rho_w[a] = pow((double)(1 + tw), -0.5);
+    tb.nm_w[a] = nm;
+    tb.ns_w[a] = ns;
+    tb.sg_w[a] = sigma;
+    tb.mu_w[a] = ok ? mu : md;
+    delta[g] = ok ? make_double4(md - mu, sigma - sd, 0.0, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+}
+
+// fixed-order sum of n doubles into out[0] (one block)
+__global__ __launch_bounds__(256) void k_sum_fixed(const double* __restrict__ in, uint32_t n, double* __restrict__ out) {
+    __shared__ double red[256];
+    double acc = 0.0;
+    for (uint32_t i = threadIdx.x; i < n; i += 256) acc += in[i];
+    acc = block_sum256(acc, red);
+    if (threadIdx.x == 0) out[0] = acc;
+}
+// out[r] = sum over c of part[r * nchunk + c], in chunk order (rows r <= K)
+__global__ __launch_bounds__(256) void k_fold_rows(const double* __restrict__ part, uint32_t nrow, uint32_t nchunk,
+                                                    double* __restrict__ out) {
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= nrow) return;
+    double t = 0.0;
+    for (uint32_t c = 0; c < nchunk; ++c) t += part[(size_t)r * nchunk + c];
+    out[r] = t;
+}
+// every rank's [alpha sum | K + 1 user-range sig sums] (recv, rank order) plus the
+// item range's sig sums (replicated) -> out = [alpha sum | K + 1 sig sums]
+__global__ __launch_bounds__(256) void k_vb_combine(const double* __restrict__ recv, int R, uint32_t K,
+                                                     const double* __restrict__ items, double* __restrict__ out) {
+    const uint32_t x = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t W = K + 2;
+    if (x >= W) return;
+    double t = 0.0;
+    for (int r = 0; r < R; ++r) t += recv[(size_t)r * W + x];
+    out[x] = x == 0 ? t : t + items[x - 1];
+}
+
 __global__ __launch_bounds__(256) void k_rho_v(VBTables tb) {
     const uint32_t a = blockIdx.x * 256 + threadIdx.x;
     if (a < tb.p) tb.rho_v[a] = pow((double)(1 + tb.t_v[a]), -0.5);
@@ -375,8 +504,9 @@ __global__ __launch_bounds__(256) void k_alpha_partial(const double2* __restrict
     if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
 
-// sum over every attribute of mean^2 + variance: row r < K = factor r, r == K = bias
-__global__ __launch_bounds__(256) void k_sig_partial(VBTables tb, double* __restrict__ part, uint32_t nchunk) {
+// sum over the attributes [a0, a1) of mean^2 + variance: row r < K = factor r, r == K = bias
+__global__ __launch_bounds__(256) void k_sig_partial(VBTables tb, uint32_t a0, uint32_t a1, double* __restrict__ part,
+                                                      uint32_t nchunk) {
     __shared__ double red[256];
     const uint32_t r = blockIdx.y, c = blockIdx.x;
     const double* m = r < tb.K ? tb.mu_v + (size_t)r * tb.p : tb.mu_w;
@@ -384,8 +514,8 @@ __global__ __launch_bounds__(256) void k_sig_partial(VBTables tb, double* __rest
     double acc = 0.0;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-        const uint32_t a = c * 2048 + u * 256 + threadIdx.x;
-        if (a < tb.p) acc += m[a] * m[a] + v[a];
+        const uint32_t a = a0 + c * 2048 + u * 256 + threadIdx.x;
+        if (a < a1) acc += m[a] * m[a] + v[a];
     }
     acc = block_sum256(acc, red);
     if (threadIdx.x == 0) part[(size_t)r * nchunk + c] = acc;
@@ -485,17 +615,38 @@ hipError_t vbo_update_w0(const double2* ET, uint32_t B, const VBTables& tb, doub
 }
 
 hipError_t vbo_update_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm, int apply_w0,
-                        const VBTables& tb, const double2* ETin, double2* ETout, hipStream_t st) {
+                        const VBTables& tb, const double2* ETin, double2* ETout, hipStream_t st, int mode,
+                        double2* sums, const double4* delta) {
     if (ntask == 0) return hipSuccess;
-    k_update_w<<<ntask, 256, 0, st>>>(tasks, rows, xperm, apply_w0, tb, ETin, ETout);
+    if (mode == VB_PART)
+        k_update_w<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, xperm, apply_w0, tb, ETin, ETout, sums, delta);
+    else if (mode == VB_FWD)
+        k_update_w<VB_FWD><<<ntask, 256, 0, st>>>(tasks, rows, xperm, apply_w0, tb, ETin, ETout, sums, delta);
+    else
+        k_update_w<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, xperm, apply_w0, tb, ETin, ETout, sums, delta);
     return hipGetLastError();
 }
 
 hipError_t vbo_update_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm,
                         const uint32_t* part, uint32_t f, const VBTables& tb, const double2* ETin, double2* ETout,
-                        hipStream_t st) {
+                        hipStream_t st, int mode, double2* sums, const double4* delta) {
     if (ntask == 0) return hipSuccess;
-    k_update_v<<<ntask, 256, 0, st>>>(tasks, rows, xperm, part, f, tb, ETin, ETout);
+    if (mode == VB_PART)
+        k_update_v<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, xperm, part, f, tb, ETin, ETout, sums, delta);
+    else if (mode == VB_FWD)
+        k_update_v<VB_FWD><<<ntask, 256, 0, st>>>(tasks, rows, xperm, part, f, tb, ETin, ETout, sums, delta);
+    else
+        k_update_v<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, xperm, part, f, tb, ETin, ETout, sums, delta);
+    return hipGetLastError();
+}
+
+hipError_t vbo_item_update(const VGItem* gi, uint32_t nG, const double2* recv, int R, int factor, uint32_t f,
+                           const VBTables& tb, double4* delta, hipStream_t st) {
+    if (nG == 0) return hipSuccess;
+    if (factor)
+        k_item_v<<<(nG + 255) / 256, 256, 0, st>>>(gi, nG, recv, R, f, tb, delta);
+    else
+        k_item_w<<<(nG + 255) / 256, 256, 0, st>>>(gi, nG, recv, R, tb, delta);
     return hipGetLastError();
 }
 
@@ -504,8 +655,51 @@ hipError_t vbo_hyper(const double2* ET, uint32_t B, const VBTables& tb, double* 
     const uint32_t nab = (B + 1023) / 1024, nchunk = (tb.p + 2047) / 2048;
     double* spart = part + nab + 8;
     k_alpha_partial<<<nab, 256, 0, st>>>(ET, B, part);
-    k_sig_partial<<<dim3(nchunk, tb.K + 1), 256, 0, st>>>(tb, spart, nchunk);
+    k_sig_partial<<<dim3(nchunk, tb.K + 1), 256, 0, st>>>(tb, 0, tb.p, spart, nchunk);
     k_hyper_final<<<1, 256, 0, st>>>(part, nab, spart, nchunk, B, tb);
+    return hipGetLastError();
+}
+
+// ---- several ranks: local partial sums, then the final steps from every rank's sums
+hipError_t vbo_w0_local(const double2* ET, uint32_t B, const VBTables& tb, double* part, double* out, hipStream_t st) {
+    if (B == 0) return hipMemsetAsync(out, 0, sizeof(double), st);
+    const uint32_t nblk = (B + 1023) / 1024;
+    k_w0_partial<<<nblk, 256, 0, st>>>(ET, B, tb, part);
+    k_sum_fixed<<<1, 256, 0, st>>>(part, nblk, out);
+    return hipGetLastError();
+}
+hipError_t vbo_w0_final(const double* recv, int R, uint32_t B, const VBTables& tb, hipStream_t st) {
+    k_w0_final<<<1, 256, 0, st>>>(recv, (uint32_t)R, B, tb);
+    return hipGetLastError();
+}
+hipError_t vbo_hyper_local(const double2* ET, uint32_t B, const VBTables& tb, uint32_t u0, uint32_t u1, double* part,
+                           double* out, hipStream_t st) {
+    k_rho_v<<<(tb.p + 255) / 256, 256, 0, st>>>(tb);
+    const uint32_t nab = (B + 1023) / 1024;
+    if (B) {
+        k_alpha_partial<<<nab, 256, 0, st>>>(ET, B, part);
+        k_sum_fixed<<<1, 256, 0, st>>>(part, nab, out);
+    } else {
+        hipError_t e = hipMemsetAsync(out, 0, sizeof(double), st);
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t nchunk = std::max(1u, (u1 - u0 + 2047) / 2048);
+    double* spart = part + nab + 8;
+    k_sig_partial<<<dim3(nchunk, tb.K + 1), 256, 0, st>>>(tb, u0, u1, spart, nchunk);
+    k_fold_rows<<<(tb.K + 1 + 255) / 256, 256, 0, st>>>(spart, tb.K + 1, nchunk, out + 1);
+    return hipGetLastError();
+}
+hipError_t vbo_hyper_final(const double* recv, int R, uint32_t B, const VBTables& tb, uint32_t I, double* part,
+                           hipStream_t st) {
+    // the item range's sums (replicated on every rank), then the combined totals
+    const uint32_t nchunk = std::max(1u, (tb.p - I + 2047) / 2048);
+    double* items = part;
+    double* spart = part + tb.K + 8;
+    double* comb = spart + (size_t)(tb.K + 1) * nchunk + 8;
+    k_sig_partial<<<dim3(nchunk, tb.K + 1), 256, 0, st>>>(tb, I, tb.p, spart, nchunk);
+    k_fold_rows<<<(tb.K + 1 + 255) / 256, 256, 0, st>>>(spart, tb.K + 1, nchunk, items);
+    k_vb_combine<<<(tb.K + 2 + 255) / 256, 256, 0, st>>>(recv, R, tb.K, items, comb);
+    k_hyper_final<<<1, 256, 0, st>>>(comb, 1, comb + 1, 1, B, tb);
     return hipGetLastError();
 }
 

@@ -13,10 +13,41 @@ import numpy as np
 import pytest
 
 from conftest import REPO
-from sbmf import Data, FMLearnSBPMF, comm_unique_id
+from conftest import golden_rmse
+from sbmf import Data, FMLearnSBPMF, FMLearnVBOnline, comm_unique_id
 
 pytestmark = pytest.mark.gpu
 WORKER = os.path.join(REPO, "tests", "workers", "multirank_worker.py")
+
+
+def _run_ranks(tmp_path, nranks, args, env=None):
+    """Spawn the ranks (host comm backend) and return their output files."""
+    old = os.environ.get("SBMF_COMM")
+    os.environ["SBMF_COMM"] = "host"
+    try:
+        uid = comm_unique_id()
+    finally:
+        if old is None:
+            del os.environ["SBMF_COMM"]
+        else:
+            os.environ["SBMF_COMM"] = old
+    outs = [str(tmp_path / ("r%d.npz" % r)) for r in range(nranks)]
+    penv = dict(os.environ, **(env or {}))
+    procs = [subprocess.Popen([sys.executable, WORKER, str(r), str(nranks), uid.hex(), outs[r]] + args,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=penv)
+             for r in range(nranks)]
+    logs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        logs.append(o.decode(errors="replace"))
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-2000:]
+    return outs
 
 
 @pytest.mark.parametrize("nranks,rng,tune,quirks", [(2, "ref", 0, "final"), (3, "philox", 0, "final"),
@@ -36,30 +67,7 @@ def test_ranks_on_one_gpu_match_single_rank(ml100k, tmp_path, nranks, rng, tune,
         bu1, bv1, b01 = L.biases()
     L.close()
 
-    old = os.environ.get("SBMF_COMM")
-    os.environ["SBMF_COMM"] = "host"
-    try:
-        uid = comm_unique_id()
-    finally:
-        if old is None:
-            del os.environ["SBMF_COMM"]
-        else:
-            os.environ["SBMF_COMM"] = old
-    outs = [str(tmp_path / ("r%d.npz" % r)) for r in range(nranks)]
-    procs = [subprocess.Popen([sys.executable, WORKER, str(r), str(nranks), uid.hex(), outs[r], str(K), str(sweeps),
-                               str(seed), rng, str(tune), quirks], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
-             for r in range(nranks)]
-    logs = []
-    for p in procs:
-        try:
-            o, _ = p.communicate(timeout=240)
-        except subprocess.TimeoutExpired:
-            for q in procs:
-                q.kill()
-            raise
-        logs.append(o.decode(errors="replace"))
-    for p, log in zip(procs, logs):
-        assert p.returncode == 0, log[-2000:]
+    outs = _run_ranks(tmp_path, nranks, [str(K), str(sweeps), str(seed), rng, str(tune), quirks])
     for r in range(nranks):
         z = np.load(outs[r])
         # every rank ends with the full, identical factor tables
@@ -68,3 +76,38 @@ def test_ranks_on_one_gpu_match_single_rank(ml100k, tmp_path, nranks, rng, tune,
         assert np.array_equal(z["rmse"], rmse1)
         if biased:
             assert np.array_equal(z["bu"], bu1) and np.array_equal(z["bv"], bv1) and z["b0"][0] == b01
+
+
+@pytest.mark.parametrize("nranks,data,K,seed,epochs,rng", [(2, "ml100k", 8, 1, 10, "ref"), (3, "ml100k", 20, 7, 5, "ref"),
+                                                           (3, "ragged", 8, 2, 20, "ref"), (2, "ml100k", 8, 5, 4, "philox")])
+def test_vb_ranks_on_one_gpu(ml100k, ragged, tmp_path, nranks, data, K, seed, epochs, rng):
+    """Online VB over several ranks (users split into ranges, the item rows'
+    sums all-gathered and added in rank order): every rank ends with the same
+    means, the per-epoch test RMSE tracks the reference learner (golden, 1e-9,
+    as one rank does) and one rank's run to rounding (item sums added rank by
+    rank instead of in one group reduction)."""
+    tr, te = ml100k if data == "ml100k" else ragged
+    L = FMLearnVBOnline(num_factor=K, seed=seed, rng=rng)
+    L.set_data(Data(*tr), Data(*te))
+    L.learn(sweeps=epochs)
+    U1, V1 = L.factors()
+    bu1, bv1, b01 = L.biases()
+    rmse1, pred1 = L.rmse_trajectory, L.predict()
+    L.close()
+    outs = _run_ranks(tmp_path, nranks, [str(K), str(epochs), str(seed), rng, "0", "final", "vb"],
+                      env={"SBMF_WORKER_DATA": data})
+    z0 = np.load(outs[0])
+    for r in range(1, nranks):  # identical on every rank
+        z = np.load(outs[r])
+        for k in ("U", "V", "bu", "bv", "b0", "rmse", "pred"):
+            assert np.array_equal(z[k], z0[k]), (r, k)
+    print("vb %d ranks %s K=%d: max|dRMSE| %.2e max|dU| %.2e max|dV| %.2e" % (
+        nranks, data, K, np.abs(z0["rmse"] - rmse1).max(), np.abs(z0["U"] - U1).max(), np.abs(z0["V"] - V1).max()))
+    assert np.abs(z0["rmse"] - rmse1).max() < 1e-11
+    assert np.abs(z0["U"] - U1).max() < 1e-9 and np.abs(z0["V"] - V1).max() < 1e-9
+    assert np.abs(z0["bu"] - bu1).max() < 1e-9 and np.abs(z0["bv"] - bv1).max() < 1e-9
+    assert abs(z0["b0"][0] - b01) < 1e-11
+    assert np.abs(z0["pred"] - pred1).max() < 1e-9
+    if rng == "ref":
+        gold = golden_rmse("ref_vbo_%s_k%d_s%d_e%d.txt" % (data, K, seed, epochs))
+        assert np.abs(z0["rmse"] - gold).max() < 1e-9

@@ -1,9 +1,10 @@
 """One rank of the multi-rank sampler (spawned by tests/test_gpu_multirank.py).
 
-usage: python multirank_worker.py <rank> <nranks> <id-hex> <out.npz> <K> <sweeps> <seed> <rng> [tune] [quirks]
+usage: python multirank_worker.py <rank> <nranks> <id-hex> <out.npz> <K> <sweeps> <seed> <rng> [tune] [quirks] [method]
 The ranks share one GPU and exchange their row blocks through the host comm
 backend (the id was made with SBMF_COMM=host); the result must equal a
-single-rank run in the same residual form.
+single-rank run in the same residual form.  method "vb": the online VB
+learner (user ranges per rank, item sums all-gathered), `sweeps` epochs.
 """
 import gzip
 import os
@@ -17,7 +18,9 @@ sys.path.insert(0, os.path.join(REPO, "scalable-bayesian-matrix-factorization_am
 
 def read(path):
     u, i, r = [], [], []
-    with gzip.open(path, "rt") as f:
+    if not os.path.exists(path):
+        path = path[:-3]  # the ragged set is plain text
+    with (gzip.open(path, "rt") if path.endswith(".gz") else open(path)) as f:
         for line in f:
             p = line.split()
             if len(p) >= 3:
@@ -31,18 +34,25 @@ def main():
     rank, nranks, idhex, out, K, sweeps, seed, rng = sys.argv[1:9]
     tune = int(sys.argv[9]) if len(sys.argv) > 9 else 0
     quirks = sys.argv[10] if len(sys.argv) > 10 else "final"
-    from sbmf import Data, FMLearnSBPMF
+    method = sys.argv[11] if len(sys.argv) > 11 else "mcmc"
+    from sbmf import Data, FMLearnSBPMF, FMLearnVBOnline
     g = os.path.join(REPO, "tests", "golden")
-    tr, te = read(os.path.join(g, "ml100k_train.tsv.gz")), read(os.path.join(g, "ml100k_test.tsv.gz"))
-    L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, tune=tune, quirks=quirks)
+    data = os.environ.get("SBMF_WORKER_DATA", "ml100k")
+    tr, te = read(os.path.join(g, data + "_train.tsv.gz")), read(os.path.join(g, data + "_test.tsv.gz"))
+    if method == "vb":
+        L = FMLearnVBOnline(num_factor=int(K), seed=int(seed), rng=rng, device=0)
+    else:
+        L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, tune=tune, quirks=quirks)
     L.init(comm=(int(nranks), int(rank), bytes.fromhex(idhex)))
     L.set_data(Data(*tr), Data(*te))
     L.learn(sweeps=int(sweeps))
     U, V = L.factors()
     extra = {}
-    if quirks in ("bias2", "bias22"):
+    if quirks in ("bias2", "bias22") or method == "vb":
         bu, bv, b0 = L.biases()
         extra = {"bu": bu, "bv": bv, "b0": np.array([b0])}
+    if method == "vb":
+        extra["pred"] = L.predict()
     np.savez(out, U=U, V=V, rmse=L.rmse_trajectory, tau=np.array([h["tau"] for h in L.history]), **extra)
     L.close()
 
