@@ -1074,14 +1074,15 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restr
 // Per block t, per vector: apply D_{t-1} with the held slice, then issue the
 // gather of slice t into the same registers; then accumulate block t.  The
 // task's partner ids, residuals, scatter targets and ratings sit in LDS.
-// Split rows hand their (G_B, c_B) partials over without fences: write-through
-// (sc1) stores, drained, then one agent-scope counter add per workgroup.  Rows
-// of up to GRES_ALLREAD chunks: every chunk polls the counter (sc1 loads) for
-// nch and sums all partials in chunk order (sc1 loads).  Longer rows: the
-// workgroup whose add returns nch-1 sums them, publishes the total the same
-// way and adds once more; the others poll for nch+1 and read the total --
-// MI355X_MICROARCH.md hand-off table, first row.  The sums never depend on
-// which chunk arrives last.
+// Split rows hand their (G_B, c_B) partials over without fences: each chunk
+// writes its packed partial (152 doubles: the lower triangle of G_B with its
+// diagonal, then c_B) with write-through (sc1) stores, drains them and adds
+// once to the block's agent-scope counter; every chunk polls the counter (sc1
+// loads) for nch and then reads all partials -- MI355X_MICROARCH.md hand-off
+// table, first row.  The chunk sum of an entry is split over the workgroup's
+// spare threads (3 per entry for 8 waves), each summing a fixed range of
+// chunks in order, the pieces added in piece order, so it never depends on
+// which chunk arrives last and every chunk gets the same bits.
 __device__ __forceinline__ void st_sc1(double* p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1091,7 +1092,9 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 struct GresSums {
     double sq, tr;
 };
-constexpr uint32_t GRES_ALLREAD = 16;  // split rows of up to this many chunks exchange in one hop
+#ifdef SBMF_KPROF_BUILD
+constexpr uint32_t GRES_ALLREAD = 16;  // phase-profile class boundary
+#endif
 template <typename T>
 struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of slices
     static constexpr int VW = sizeof(T) == 8 ? 32 : 64;
@@ -1123,8 +1126,20 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
     __shared__ T Dsh[GB];
     __shared__ T newS[256];
     __shared__ double red2[NW][2];
-    __shared__ uint32_t lastf;
+    // packed exchange entries: SLP = 136 (lower triangle incl. diagonal) + 16 (c);
+    // thread x < SLP owns entry x; XP threads per entry share a split row's chunk sum
+    constexpr int SLP = GB * (GB + 1) / 2 + GB;
+    constexpr int XP = (64 * NW) / SLP;
+    static_assert(XP >= 1 && SLP <= SL, "exchange geometry");
+    __shared__ double xsum[XP][SLP];
+    // the row's normals and old values, sigma and mu: read by the solving wave from LDS
+    // (kept out of the VGPRs the held slices need)
+    __shared__ T zL[256], oL[256], sgL[256], muL[256];
     for (int x = threadIdx.x; x < GB * GLD; x += 64 * NW) (&Lr[0][0])[x] = T(0);
+    for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {
+        sgL[k] = a.sig[k];
+        muL[k] = a.mu[k];
+    }
     // this lane's slots: vector j of wave wr is rating 4*(wr + j*NW) + rr, i.e.
     // a fixed per-lane base plus j*4*NW (an immediate LDS offset)
     const uint32_t* const pjW = pjL + 4 * wr + rr;
@@ -1180,15 +1195,9 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 if (!a.e_from_dot) eL[x] = in ? a.E_this[beg + x] : T(0);
                 if (a.row_tr) rL[x] = in ? a.r_this[beg + x] : T(0);
             }
-            T zA0, zA1, zB0 = T(0), zB1 = T(0);
-            {  // per-half normals of the row (used by the solving wave)
-                const uint32_t i0 = 2 * lane;
-                zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
-                zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
-                if (K > 128) {
-                    zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
-                    zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
-                }
+            for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {  // per-half normals and old values of the row
+                zL[k] = k < K ? a.zbuf[(size_t)row * K + k] : T(0);
+                oL[k] = a.own[(size_t)row * Kp + k];  // padding columns are zero
             }
             __syncthreads();
             if (a.e_from_dot) {  // validation mode (tune bit 1): e0 = r - own.partner
@@ -1213,12 +1222,6 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 // keep the per-vector partner offsets in LDS: hoisting them out of
                 // the block loop would hold VC 64-bit addresses in VGPRs
                 asm volatile("" ::: "memory");
-                const uint32_t kk = t * GB + ci;
-                const bool kin = kk < K;
-                // the block's old values and hyperparameters (zero padded; used by wave 0)
-                const T old = a.own[(size_t)row * Kp + kk];
-                const T sg = a.sig[kk];
-                const T mu = a.mu[kk];
                 if (t > 0) {
                     // apply block t-1 with the held slice, then gather slice t into it
 #ifdef SBMF_ABLATIONS
@@ -1260,19 +1263,24 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 if (lane < GB) Cs[wr][lane] = cc;
                 __syncthreads();
                 stamp(3);  // wait for the other waves
-                // cross-wave sum in wave order: entries x = threadIdx.x + j*64*NW of the slab image
-                constexpr int NE = (SL + 64 * NW - 1) / (64 * NW);  // entries per thread (1, or 2 for NW = 4)
-                T val[NE];
+                // cross-wave sum in wave order: thread x < SLP holds packed entry x
+                // (lower triangle incl. the diagonal, then c); the entry's geometry is
+                // recomputed here from an opaque thread id so it holds no VGPRs across
+                // the block loop
+                int tid;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
+                const int xe = tid % SLP, xpart = tid / SLP;
+                const bool xin = tid < SLP;
+                int xr = -1, xc = xe - GB * (GB + 1) / 2;  // c entry: xr = -1, xc = k
+                if (xe < GB * (GB + 1) / 2) {  // row r of the packed triangle: r (r + 1) / 2 <= xe
+                    xr = (int)((sqrtf(8.0f * (float)xe + 1.0f) - 1.0f) * 0.5f);
+                    xc = xe - xr * (xr + 1) / 2;
+                }
+                T val = T(0);
+                if (xin) {
 #pragma unroll
-                for (int j = 0; j < NE; ++j) {
-                    const int x = threadIdx.x + j * 64 * NW;
-                    val[j] = T(0);
-                    if (x < SL) {
-                        const int r0 = (x >> 4) & 15, c0 = x & 15;
-#pragma unroll
-                        for (int w = 0; w < NW; ++w)
-                            val[j] += x >= GB * GB ? Cs[w][x - GB * GB] : (r0 == c0 ? Ps[w][r0] : Ls[w][r0][c0]);
-                    }
+                    for (int w = 0; w < NW; ++w)
+                        val += xr < 0 ? Cs[w][xc] : (xr == xc ? Ps[w][xr] : Ls[w][xr][xc]);
                 }
 #ifdef SBMF_ABLATIONS
                 const bool xchg = nch > 1 && !(a.tune & 0x4000u);  // ablation (wrong results): no hand-off
@@ -1280,93 +1288,60 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 const bool xchg = nch > 1;
 #endif
                 if (xchg) {
-                    // cross-chunk sum over the row's chunks (see the header comment)
+                    // cross-chunk sum over the row's chunks (see the header comment):
+                    // every chunk stores its packed partial, adds once to the block's
+                    // counter and, once all nch have added, sums the partials in chunk
+                    // order -- XP threads per entry, each over a fixed third (or so) of
+                    // the chunks, the XP pieces added in piece order in LDS
                     const size_t cstride = (size_t)nblk * SL;  // between one chunk's slabs and the next's
                     const double* pb = sy.slabs + ((size_t)tk.slab0 * nblk + t) * SL;
-                    auto sum_chunks = [&](int x) {  // chunk order, 8 sc1 loads in flight
-                        const double* p0 = pb + x;
+                    if (xin) st_sc1(const_cast<double*>(pb) + tk.chunk * cstride + xe, (double)val);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    uint32_t* cnt = sy.counters + (size_t)tk.cnt0 + t;
+                    if (threadIdx.x == 0) {
+                        // no return value to wait for: the poll follows at once
+                        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        uint32_t spins = 0;
+                        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
+                            __builtin_amdgcn_s_sleep(1);
+                            if (++spins > (1u << 26)) {  // give up: flag, never hang the device
+                                __hip_atomic_store(sy.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                break;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    if (xpart < XP) {
+                        const uint32_t c0 = xpart * nch / XP, c1 = (xpart + 1) * nch / XP;
+                        const double* p0 = pb + xe;
                         double sum = 0.0;
-                        uint32_t c = 0;
-                        for (; c + 8 <= nch; c += 8) {
+                        uint32_t c = c0;
+                        for (; c + 8 <= c1; c += 8) {  // 8 sc1 loads in flight
                             double v[8];
 #pragma unroll
                             for (int u = 0; u < 8; ++u) v[u] = ld_sc1(p0 + (c + u) * cstride);
 #pragma unroll
                             for (int u = 0; u < 8; ++u) sum += v[u];
                         }
-                        for (; c < nch; ++c) sum += ld_sc1(p0 + c * cstride);
-                        return sum;
-                    };
-#pragma unroll
-                    for (int j = 0; j < NE; ++j) {
-                        const int x = threadIdx.x + j * 64 * NW;
-                        if (x < SL) st_sc1(const_cast<double*>(pb) + tk.chunk * cstride + x, (double)val[j]);
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __syncthreads();
-                    uint32_t* cnt = sy.counters + (size_t)tk.cnt0 + t;
-                    // up to GRES_ALLREAD chunks: every chunk reads every partial (one hop);
-                    // more: the last arriver sums and publishes the total (two hops, O(nch) traffic)
-                    const bool allread = nch <= GRES_ALLREAD;
-                    if (threadIdx.x == 0) {
-                        uint32_t old = 0;
-                        if (allread)  // no return value to wait for: the poll follows at once
-                            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        else
-                            old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        lastf = !allread && old == nch - 1;
-                        if (allread || old != nch - 1) {
-                            const uint32_t want = allread ? nch : nch + 1;
-                            uint32_t spins = 0;
-                            while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-                                __builtin_amdgcn_s_sleep(1);
-                                if (++spins > (1u << 26)) {  // give up: flag, never hang the device
-                                    __hip_atomic_store(sy.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                    break;
-                                }
-                            }
-                        }
+                        for (; c < c1; ++c) sum += ld_sc1(p0 + c * cstride);
+                        xsum[xpart][xe] = sum;
                     }
                     __syncthreads();
-                    double* tot = sy.totals + ((size_t)tk.cnt0 + t) * SL;
-                    if (allread) {
+                    if (xin) {
+                        double sum = xsum[0][xe];
 #pragma unroll
-                        for (int j = 0; j < NE; ++j) {
-                            const int x = threadIdx.x + j * 64 * NW;
-                            if (x < SL) val[j] = (T)sum_chunks(x);
-                        }
-                    } else if (lastf) {
-#pragma unroll
-                        for (int j = 0; j < NE; ++j) {
-                            const int x = threadIdx.x + j * 64 * NW;
-                            if (x < SL) {
-                                const double sum = sum_chunks(x);
-                                st_sc1(tot + x, sum);
-                                val[j] = (T)sum;
-                            }
-                        }
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        __syncthreads();
-                        if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < NE; ++j) {
-                            const int x = threadIdx.x + j * 64 * NW;
-                            if (x < SL) val[j] = (T)ld_sc1(tot + x);
-                        }
+                        for (int q = 1; q < XP; ++q) sum += xsum[q][xe];
+                        val = (T)sum;
                     }
                 }
-#pragma unroll
-                for (int j = 0; j < NE; ++j) {
-                    const int x = threadIdx.x + j * 64 * NW;
-                    if (x < SL) {
-                        if (x >= GB * GB)
-                            Cr[x - GB * GB] = val[j];
-                        else if ((x >> 4) == (x & 15))
-                            Pr[x & 15] = val[j];
-                        else if ((x & 15) < (x >> 4))
-                            Lr[x >> 4][x & 15] = val[j];
-                    }
+                if (xin) {
+                    if (xr < 0)
+                        Cr[xc] = val;
+                    else if (xr == xc)
+                        Pr[xr] = val;
+                    else
+                        Lr[xr][xc] = val;
                 }
                 __syncthreads();
                 stamp(4);  // cross-wave sum + split-row exchange
@@ -1375,14 +1350,11 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 const bool rep = a.tune & 1u;
                 T dlt = T(0);
                 if (rep || wr == 0) {
+                    const uint32_t kk = t * GB + ci;
+                    const bool kin = kk < K;
+                    // the block's old values, hyperparameters and normals (zero padded)
+                    const T old = oL[kk], sg = sgL[kk], mu = muL[kk], z = zL[kk];
                     const T P = Pr[ci];
-                    const int zl = (int)((kk >> 1) & 63);
-                    const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
-                    T z = (kk & 1) ? za1 : za0;
-                    if (K > 128) {
-                        const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
-                        z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
-                    }
                     const T var = kin ? T(1) / (sg + tau * P) : T(0);
                     const T sd = a.sd_is_var ? var : tsqrt(var);
                     const T A = var * sg * mu + sd * z;
