@@ -370,6 +370,20 @@ __device__ __forceinline__ T row16_sum_sym(T x) {
     x += dpp<0x124, 0xf>(x);  // row_ror:4
     return x;
 }
+// One level of a butterfly reduce-scatter over the 16 lanes of each DPP row:
+// values s[0..M) (M/2 pairs); the lane pairs given by CTRL (an involution)
+// split each pair by `key` (the lane's bit for this level): the lane keeps one
+// member summed with its partner's copy of that member, so s[0..M/2) then hold
+// sums over twice the lanes for this lane's half of the vectors.
+template <int CTRL, int M, typename T, int N>
+__device__ __forceinline__ void bfly_level(T (&s)[N], bool key) {
+#pragma unroll
+    for (int j = 0; j < M / 2; ++j) {
+        const T lo = s[j], hi = s[j + M / 2];
+        const T keep = key ? hi : lo, send = key ? lo : hi;
+        s[j] = keep + dpp<CTRL, 0xf>(send);
+    }
+}
 __device__ __forceinline__ float shfl_xor_t(float v, int m) { return __shfl_xor(v, m); }
 __device__ __forceinline__ double shfl_xor_t(double v, int m) { return __shfl_xor(v, m); }
 __device__ __forceinline__ float shfl_t(float v, int src) { return __shfl(v, src); }
@@ -1217,6 +1231,46 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             T s[VC];
 #pragma unroll
             for (int j = 0; j < VC; ++j) s[j] = pbase[pjW[j * JS]];
+            // Residual update e_v -= S_v D (vector v: 4 ratings x 16 columns, lane ci
+            // holding column ci): s_v *= D in place, then a butterfly reduce-scatter
+            // over the 16 lanes of each rating (row_ror:8, row_half_mirror, quad_perm
+            // xor 2, xor 1), after which lane ci holds the complete sums of
+            // max(1, VC/16) vectors and updates their residuals in LDS -- 2 (VC - 1)
+            // DPP moves instead of 4 VC row-sum steps.  The registers each level
+            // frees take their next slices at once (next(j) = the gather of vector j).
+            auto apply = [&](T D, auto&& next) {
+#pragma unroll
+                for (int j = 0; j < VC; ++j) s[j] = s[j] * D;
+                bfly_level<0x128, VC>(s, ci & 8);
+#pragma unroll
+                for (int j = VC / 2; j < VC; ++j) next(j);
+                bfly_level<0x141, VC / 2>(s, ci & 4);
+#pragma unroll
+                for (int j = VC / 4; j < VC / 2; ++j) next(j);
+                bfly_level<0x4e, VC / 4>(s, ci & 2);
+#pragma unroll
+                for (int j = VC / 8; j < VC / 4; ++j) next(j);
+                if constexpr (VC >= 16) {
+                    bfly_level<0xb1, VC / 8>(s, ci & 1);
+#pragma unroll
+                    for (int j = VC / 16; j < VC / 8; ++j) next(j);
+                } else {
+                    s[0] = s[0] + dpp<0xb1, 0xf>(s[0]);  // both lanes of the pair: the same sum
+                }
+                constexpr int RV = VC >= 16 ? VC / 16 : 1;
+                const int vb = ((ci & 8) ? VC / 2 : 0) + ((ci & 4) ? VC / 4 : 0) + ((ci & 2) ? VC / 8 : 0) +
+                               ((VC >= 16 && (ci & 1)) ? VC / 16 : 0);
+#pragma unroll
+                for (int j = 0; j < RV; ++j) {
+                    T* const pe = eW + (vb + j) * JS;
+                    *pe = *pe - s[j];
+                }
+                // other lanes of this wave read these residuals next (LDS keeps a wave's
+                // accesses in order); keep the compiler from moving reads above the writes
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int j = 0; j < RV; ++j) next(j);
+            };
             T Dl = T(0);
             for (uint32_t t = 0; t < nblk; ++t) {
                 // keep the per-vector partner offsets in LDS: hoisting them out of
@@ -1230,11 +1284,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                         for (int j = 0; j < VC; ++j) s[j] = pbase[(size_t)pjW[j * JS] + t * GB];
                     } else
 #endif
-#pragma unroll
-                    for (int j = 0; j < VC; ++j) {
-                        eW[j * JS] = eW[j * JS] - row16_sum_sym(s[j] * Dl);  // same value from all 16 lanes
-                        s[j] = pbase[(size_t)pjW[j * JS] + t * GB];
-                    }
+                    apply(Dl, [&](int j) { s[j] = pbase[(size_t)pjW[j * JS] + t * GB]; });
                 }
                 stamp(1);  // apply + gather issue
                 acc_t g = {T(0), T(0), T(0), T(0)};
@@ -1380,8 +1430,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             }
             // apply the last block; then residuals out and the per-row sums, one
             // rating per thread in rating order (no per-vector branches)
-#pragma unroll
-            for (int j = 0; j < VC; ++j) eW[j * JS] = eW[j * JS] - row16_sum_sym(s[j] * Dl);
+            apply(Dl, [](int) {});
             __syncthreads();
             double sq = 0.0, trs = 0.0;
             for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) {
