@@ -384,6 +384,21 @@ __device__ __forceinline__ void bfly_level(T (&s)[N], bool key) {
         s[j] = keep + dpp<CTRL, 0xf>(send);
     }
 }
+// Row sums of V vectors at once: s[v] (lane ci of each 16-lane row = one
+// term) -> the complete sums of vectors vb .. vb + max(1, V/16) - 1 in s[0..),
+// vb returned.  Four butterfly levels (row_ror:8, row_half_mirror, quad_perm
+// xor 2, xor 1); a level past log2(V) adds both lanes' value (every lane that
+// holds a vector ends with the same bits: the two operands of each add are
+// the same in either lane, only swapped).
+template <int V, typename T>
+__device__ __forceinline__ int row16_scatter(T (&s)[V], int ci) {
+    if constexpr (V >= 2) bfly_level<0x128, V>(s, ci & 8); else s[0] = s[0] + dpp<0x128, 0xf>(s[0]);
+    if constexpr (V >= 4) bfly_level<0x141, V / 2>(s, ci & 4); else s[0] = s[0] + dpp<0x141, 0xf>(s[0]);
+    if constexpr (V >= 8) bfly_level<0x4e, V / 4>(s, ci & 2); else s[0] = s[0] + dpp<0x4e, 0xf>(s[0]);
+    if constexpr (V >= 16) bfly_level<0xb1, V / 8>(s, ci & 1); else s[0] = s[0] + dpp<0xb1, 0xf>(s[0]);
+    return ((V >= 2 && (ci & 8)) ? V / 2 : 0) + ((V >= 4 && (ci & 4)) ? V / 4 : 0) +
+           ((V >= 8 && (ci & 2)) ? V / 8 : 0) + ((V >= 16 && (ci & 1)) ? V / 16 : 0);
+}
 __device__ __forceinline__ float shfl_xor_t(float v, int m) { return __shfl_xor(v, m); }
 __device__ __forceinline__ double shfl_xor_t(double v, int m) { return __shfl_xor(v, m); }
 __device__ __forceinline__ float shfl_t(float v, int src) { return __shfl(v, src); }
@@ -489,8 +504,12 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     // ratings of this wave: vector v covers ratings q = (wr*V + v)*4 + rr;
     // slots past the row's end gather the partner table's zero row
     uint32_t pj[V];  // partner rows (the zero row past the row's end)
-    T e[V];
+    T e[V];          // the starting residuals (then kept in LDS, eS)
     uint32_t pm[V];  // residual scatter targets, loaded now so the epilogue stores do not wait
+    // residuals of this wave's ratings: vector v, rating rr at eS[wv][4 v + rr]; read
+    // by all 16 lanes of the rating, updated by the lane whose row sum covers it
+    __shared__ T eS[NWAVE][V * 4];
+    T* const eR = &eS[wv][rr];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
@@ -525,6 +544,11 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         }
     }
 
+    if (ci == 0) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) eR[4 * v] = e[v];
+    }
+    asm volatile("" ::: "memory");  // read back by the other lanes of the wave (LDS keeps its order)
     const T tau = a.tau;
     const T* __restrict__ orow = a.own + (size_t)row * Kp + ci;
     stamp(0);  // row setup (ids, residuals, normals)
@@ -573,7 +597,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             else
 #endif
             g = MfmaT<T>::mfma(s[v], g);
-            cc += s[v] * e[v];
+            cc += s[v] * eR[4 * v];
         }
         cc += shfl_xor_t(cc, 16);
         cc += shfl_xor_t(cc, 32);
@@ -657,15 +681,17 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             dlt = Dsh[ci];
         }
         stamp(4);  // solve + D hand-off
-        // ---- 4. e -= S_B D_B (lane (r,i) holds D_i): 16-lane DPP row sums
-#ifdef SBMF_ABLATIONS
-        if (a.tune & 0x400u) {  // ablation (wrong results): residual update without the row sums
+        // ---- 4. e -= S_B D_B (lane (r,i) holds D_i): one butterfly reduce-scatter of the
+        // V row sums (row16_scatter), each lane updating the residuals its sums cover
+        {
 #pragma unroll
-            for (int v = 0; v < V; ++v) e[v] -= s[v] * dlt;
-        } else
-#endif
+            for (int v = 0; v < V; ++v) s[v] = s[v] * dlt;
+            const int vb = row16_scatter(s, ci);
+            constexpr int RV = V >= 16 ? V / 16 : 1;
 #pragma unroll
-        for (int v = 0; v < V; ++v) e[v] -= row16_sum(s[v] * dlt);
+            for (int j = 0; j < RV; ++j) eR[4 * (vb + j)] = eR[4 * (vb + j)] - s[j];
+            asm volatile("" ::: "memory");
+        }
         stamp(5);  // residual update
 #pragma unroll
         for (int v = 0; v < V; ++v) s[v] = sn[v];
@@ -680,6 +706,8 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     }
     // ---- epilogue: residuals out, per-row partial sums
     T sq = T(0), trs = T(0);
+#pragma unroll
+    for (int v = 0; v < V; ++v) e[v] = eR[4 * v];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);

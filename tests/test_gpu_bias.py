@@ -84,10 +84,11 @@ def test_biased_philox_deterministic_and_statistically_equivalent(ml100k):
     b.close()
 
 
-def test_libfm_and_vb_learners_are_single_gpu_in_this_build():
-    """The biased sampler runs on several GPUs (tests/test_gpu_multirank.py);
-    the online VB and libFM MCMC / ALS learners are refused for more ranks."""
-    for kw in ({"method": "als"}, {"method": "mcmc", "order": "libfm"}, {"method": "vb"}):
+def test_libfm_learners_are_single_gpu_in_this_build():
+    """The biased sampler and online VB run on several GPUs
+    (tests/test_gpu_multirank.py); the libFM MCMC / ALS learners are refused
+    for more ranks."""
+    for kw in ({"method": "als"}, {"method": "mcmc", "order": "libfm"}):
         L = FMLearnSBPMF(num_factor=8, **kw)
         with pytest.raises(sbmf.SBMFError) as ei:
             L.init(comm=(2, 0, bytes(128)))
