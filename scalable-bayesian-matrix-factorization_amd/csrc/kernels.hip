@@ -450,7 +450,10 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
 #ifndef SBMF_GBLOCK_OCC64
 #define SBMF_GBLOCK_OCC64 4
 #endif
-#define GBLOCK_OCC(T, V) ((V) * sizeof(T) > 64 ? 2 : (sizeof(T) == 8 ? SBMF_GBLOCK_OCC64 : 3))
+#ifndef SBMF_GBLOCK_OCC_WIDE
+#define SBMF_GBLOCK_OCC_WIDE 3
+#endif
+#define GBLOCK_OCC(T, V) ((V) * sizeof(T) > 64 ? SBMF_GBLOCK_OCC_WIDE : (sizeof(T) == 8 ? SBMF_GBLOCK_OCC64 : 3))
 template <typename T, int V, int NW, int RPW, bool SW>
 __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_gblock(const uint32_t* __restrict__ rows,
                                                                      uint32_t nrows, HalfArgs<T> a) {
