@@ -194,6 +194,17 @@ void Comm::alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const
     if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
 }
 
+void Comm::group_begin() {
+    if (!comm_) return;
+    const ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) comm_fail("ncclGroupStart", r);
+}
+void Comm::group_end() {
+    if (!comm_) return;
+    const ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
+}
+
 void Comm::allgather(const void* sendbuf, size_t bytes, void* recvbuf, hipStream_t st) {
     if (nranks_ <= 1) {
         if (bytes && hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)

@@ -33,6 +33,10 @@ class Comm {
     void alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const std::vector<size_t>& scnt,
                    void* recvbuf, const std::vector<size_t>& roff, const std::vector<size_t>& rcnt, hipStream_t st);
 
+    // Bracket several of the calls below into one RCCL group (nests; no-op for
+    // the host backend): their transfers run concurrently, started at group_end.
+    void group_begin();
+    void group_end();
     // All-gather of equal blocks (ncclAllGather): rank k's `bytes` at sendbuf
     // land at recvbuf + k * bytes on every rank.
     void allgather(const void* sendbuf, size_t bytes, void* recvbuf, hipStream_t st);

@@ -919,8 +919,11 @@ static double ev_ms(hipEvent_t a, hipEvent_t b) {
 
 // After a half (users: scatter into item order, E_v; items: into E_u): send
 // the residuals bound for other ranks' rows, unpack what arrives.
-template <typename T>
-static void exchange_residuals(sbmf_ctx* c, bool users, hipStream_t st) {
+// `with` (optional) issues the half's block broadcasts first, all in one RCCL
+// group (collectives only: they run concurrently); the residual send/receive
+// keeps a group of its own; the unpack follows it.
+template <typename T, class F>
+static void exchange_residuals(sbmf_ctx* c, bool users, hipStream_t st, F&& with) {
     if (c->nranks <= 1) return;
     const Side& s = users ? c->users : c->items;
     DBuf& E = users ? c->d_Ev : c->d_Eu;
@@ -929,10 +932,17 @@ static void exchange_residuals(sbmf_ctx* c, bool users, hipStream_t st) {
         for (size_t& x : b) x *= sizeof(T);
         return b;
     };
+    c->comm.group_begin();
+    with();
+    c->comm.group_end();
     c->comm.alltoallv(E.as<T>() + c->tu.size(), bytes(s.soff), bytes(s.scnt), c->d_xrecv.p, bytes(s.roff),
                       bytes(s.rcnt), st);
     HIPCHK(launch_unpack<T>(c->d_xrecv.as<T>(), (users ? c->d_uunpack : c->d_vunpack).as<uint32_t>(), s.nrecv,
                             E.as<T>(), st));
+}
+template <typename T>
+static void exchange_residuals(sbmf_ctx* c, bool users, hipStream_t st) {
+    exchange_residuals<T>(c, users, st, [] {});
 }
 
 template <typename T>
@@ -1063,11 +1073,11 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                                        ref ? c->d_var3u.as<double>() : nullptr, bias_args(c, true, d0), st));
         run_half<T>(c, true);
         HIPCHK(hipEventRecord(c->ev[2], st));
-        if (c->nranks > 1) {
-            c->comm.bcast_ranges(c->d_U.p, c->Kp * sizeof(T), c->users.bounds, st);
-            if (c->bias) c->comm.bcast_ranges(c->d_bu.p, sizeof(double), c->users.bounds, st);
-            exchange_residuals<T>(c, true, st);
-        }
+        if (c->nranks > 1)  // fresh U (and b_i) blocks (one RCCL group), then the residuals
+            exchange_residuals<T>(c, true, st, [&] {
+                c->comm.bcast_ranges(c->d_U.p, c->Kp * sizeof(T), c->users.bounds, st);
+                if (c->bias) c->comm.bcast_ranges(c->d_bu.p, sizeof(double), c->users.bounds, st);
+            });
         HIPCHK(hipEventRecord(c->ev[3], st));
         // ---- 4. item half-sweep
         if (!ref)
@@ -1078,13 +1088,13 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                                        ref ? c->d_var3v.as<double>() : nullptr, bias_args(c, false, 0.0), st));
         run_half<T>(c, false);
         HIPCHK(hipEventRecord(c->ev[4], st));
-        if (c->nranks > 1) {
-            c->comm.bcast_ranges(c->d_V.p, c->Kp * sizeof(T), c->items.bounds, st);
-            if (c->bias) c->comm.bcast_ranges(c->d_bv.p, sizeof(double), c->items.bounds, st);
-            exchange_residuals<T>(c, false, st);
-            c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
-            if (cf.eval_train) c->comm.bcast_ranges(c->d_rowtr_v.p, sizeof(double), c->items.bounds, st);
-        }
+        if (c->nranks > 1)  // fresh V (and b_j) blocks and the per-row sums (one RCCL group), then the residuals
+            exchange_residuals<T>(c, false, st, [&] {
+                c->comm.bcast_ranges(c->d_V.p, c->Kp * sizeof(T), c->items.bounds, st);
+                if (c->bias) c->comm.bcast_ranges(c->d_bv.p, sizeof(double), c->items.bounds, st);
+                c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
+                if (cf.eval_train) c->comm.bcast_ranges(c->d_rowtr_v.p, sizeof(double), c->items.bounds, st);
+            });
         HIPCHK(hipEventRecord(c->ev[5], st));
         // ---- 5. evaluation
         const bool collect = q2 ? true : (c->sweep >= cf.burnin);
