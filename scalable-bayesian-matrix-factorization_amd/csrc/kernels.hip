@@ -448,10 +448,10 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
 // bit 4 -> 3), 3 for 16 f32 vectors, 2 for the 16-vector f64 kind.  Partner
 // rows are kept as 32-bit ids and the block solve reads its H row from LDS.
 #ifndef SBMF_GBLOCK_OCC64
-#define SBMF_GBLOCK_OCC64 4
+#define SBMF_GBLOCK_OCC64 5
 #endif
 #ifndef SBMF_GBLOCK_OCC_WIDE
-#define SBMF_GBLOCK_OCC_WIDE 3
+#define SBMF_GBLOCK_OCC_WIDE 4
 #endif
 #define GBLOCK_OCC(T, V) ((V) * sizeof(T) > 64 ? SBMF_GBLOCK_OCC_WIDE : (sizeof(T) == 8 ? SBMF_GBLOCK_OCC64 : 3))
 template <typename T, int V, int NW, int RPW, bool SW>
@@ -492,38 +492,39 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     __shared__ T Dsh[GB];                     // SW: the block's D from the solving wave
     const int ws = NW > 1 ? 0 : wv;           // LDS slot holding this row's reduced G / c
 
-    // per-row normals: lane l holds z for k = 2l, 2l+1 (zA) and 128+2l, 129+2l (zB)
-    T zA0, zA1, zB0 = T(0), zB1 = T(0);
+    // Per-rating and per-row values live in LDS, not VGPRs (occupancy): the row's
+    // normals zS (read by the solving wave), this wave's partner-row offsets pjS
+    // (row * Kp; the host checks (P+2) Kp < 2^32), residuals eS and scatter
+    // targets pmS -- vector v, rating rr at [4 v + rr], read by all 16 lanes of the
+    // rating; a residual is updated by the lane whose row sum covers it.
+    __shared__ T zS[NW > 1 ? 1 : RPW][256];
+    __shared__ uint32_t pjS[NWAVE][V * 4];
+    __shared__ uint32_t pmS[NWAVE][V * 4];
+    __shared__ T eS[NWAVE][V * 4];
     {  // per-half normals (host reference stream or launch_philox_fill)
-        const uint32_t i0 = 2 * lane;
-        zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
-        zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
-        if (K > 128) {
-            zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
-            zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
-        }
+        const uint32_t k0 = NW > 1 ? threadIdx.x : lane, kst = NW > 1 ? 64 * NW : 64;
+        for (uint32_t k = k0; k < Kp; k += kst) zS[ws][k] = k < K ? a.zbuf[(size_t)row * K + k] : T(0);
     }
-
     // ratings of this wave: vector v covers ratings q = (wr*V + v)*4 + rr;
     // slots past the row's end gather the partner table's zero row
-    uint32_t pj[V];  // partner rows (the zero row past the row's end)
-    T e[V];          // the starting residuals (then kept in LDS, eS)
-    uint32_t pm[V];  // residual scatter targets, loaded now so the epilogue stores do not wait
-    // residuals of this wave's ratings: vector v, rating rr at eS[wv][4 v + rr]; read
-    // by all 16 lanes of the rating, updated by the lane whose row sum covers it
-    __shared__ T eS[NWAVE][V * 4];
+    T e[V];  // the starting residuals (then kept in LDS)
     T* const eR = &eS[wv][rr];
+    const uint32_t* const pjR = &pjS[wv][rr];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-        pj[v] = q < n ? a.part[beg + q] : a.zrow;
+        uint32_t pj = q < n ? a.part[beg + q] : a.zrow;
 #ifdef SBMF_ABLATIONS
-        if (a.tune & 0x100u) pj[v] = 0;  // ablation (wrong results): every gather hits one cached row
+        if (a.tune & 0x100u) pj = 0;  // ablation (wrong results): every gather hits one cached row
 #endif
-        pm[v] = q < n ? a.perm[beg + q] : 0u;
+        if (ci == 0) {
+            pjS[wv][4 * v + rr] = pj * Kp;
+            pmS[wv][4 * v + rr] = q < n ? a.perm[beg + q] : 0u;
+        }
     }
+    asm volatile("" ::: "memory");  // read back by the other lanes of the wave (LDS keeps its order)
     const T* __restrict__ pbase = a.partner + ci;
-#define PROW(v) (pbase + (size_t)pj[v] * Kp)
+#define PROW(v) (pbase + pjR[4 * (v)])
     if (a.e_from_dot) {
         T dot[V];
 #pragma unroll
@@ -649,16 +650,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         if (!(SW && NW > 1) || wr == 0) {
             const T P = Ps[ws][ci];
             const T old = oldc, sg = sgc, mu = muc;
-            // z_kk lives in lane (kk>>1)&63 of zA (kk<128) or zB
-            const int zl = (int)((kk >> 1) & 63);
-            // shuffle both registers, then pick by this lane's own parity (the
-            // source lane's select would use the source lane's k)
-            const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
-            T z = (kk & 1) ? za1 : za0;
-            if (K > 128) {
-                const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
-                z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
-            }
+            const T z = zS[ws][kk];
             const T var = kin ? T(1) / (sg + tau * P) : T(0);  // k >= K: var = 0 -> d = -old = 0
             const T sd = a.sd_is_var ? var : tsqrt(var);
             const T A = var * sg * mu + sd * z;
@@ -715,7 +707,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
         if (q < n && ci == 0) {
-            a.E_other[pm[v]] = e[v];
+            a.E_other[pmS[wv][4 * v + rr]] = e[v];
             sq += e[v] * e[v];
             if (want_r) {
                 const T r = Rs[(wv * V + v) * 4 + rr];
