@@ -444,9 +444,11 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
     return gam;
 }
 
-// Occupancy (waves/SIMD): 4 for 8 f64 vectors per wave (<= 128 VGPRs; tune
-// bit 4 -> 3), 3 for 16 f32 vectors, 2 for the 16-vector f64 kind.  Partner
-// rows are kept as 32-bit ids and the block solve reads its H row from LDS.
+// Occupancy hints (waves/SIMD): 5 for 8 f64 vectors per wave (<= 102 VGPRs),
+// 3 for the 16-vector f32 kind, 4 for the 16-vector f64 kind (<= 128).  They
+// hold because the per-rating values (partner-row offsets, residuals, scatter
+// targets) and the row's normals sit in LDS, and the block solve reads its H
+// row from LDS.
 #ifndef SBMF_GBLOCK_OCC64
 #define SBMF_GBLOCK_OCC64 5
 #endif
