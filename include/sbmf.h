@@ -122,8 +122,16 @@ typedef struct sbmf_config {
                                          of ceil(ratings / ratings-per-wave),
                                  bit 3 = f64 rows of 33..64 ratings on two 8-vector waves instead
                                          of one 16-vector wave,
-                                 bit 5 = streaming kernel on one 16-wave workgroup per CU
-                                         (default: two 8-wave workgroups)                        */
+                                 bit 5 = LDS-staged streaming kernel on 16-wave workgroups,
+                                 bit 6 = LDS-staged streaming kernel (k_gstream) instead of the
+                                         register-resident one (k_gres),
+                                 bit 7 = k_gres on 4-wave workgroups (default 8),
+                                 bits 8-10 = hybrid k_gres / k_gstream stream sets by row length,
+                                 bit 16 = k_gres tasks in static rounds (default: a queue),
+                                 bit 17 = k_gres on 16-wave workgroups,
+                                 bit 20 = every multi-wave f64 Gram-block row on 16-vector
+                                          waves (default: rows of 5-8 8-vector waves),
+                                 bit 21 = no multi-wave f64 Gram-block row on 16-vector waves  */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

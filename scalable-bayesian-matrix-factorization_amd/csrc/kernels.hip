@@ -2163,6 +2163,27 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
     if (nrows == 0) return hipSuccess;
     constexpr int V = sizeof(T) == 8 ? 8 : 16;
     const bool sw = !(a.tune & 1u);
+    // f64 rows of 5-8 waves of 8 vectors run as 3-4 waves of 16 vectors (measured faster:
+    // fewer waves meet at each block's barriers); tune bit 20: every multi-wave row so,
+    // bit 21: none
+    const bool wide = sizeof(T) == 8 && !(a.tune & 0x200000u) && (nw >= 5 || (a.tune & 0x100000u));
+    if (wide) {
+        const int nw2 = (nw + 1) / 2;
+#define SBMF_GB_NW16(NW_)                                                                        \
+    case NW_:                                                                                    \
+        k_gblock<T, 16, NW_, 1, true><<<nrows, 64 * NW_, 0, st>>>(rows, nrows, a);               \
+        break;
+        switch (nw2) {
+            SBMF_GB_NW16(1)
+            SBMF_GB_NW16(2)
+            SBMF_GB_NW16(3)
+            SBMF_GB_NW16(4)
+            default:
+                return hipErrorInvalidValue;
+        }
+#undef SBMF_GB_NW16
+        return hipGetLastError();
+    }
 #define SBMF_GB_NW(NW_)                                                                          \
     case NW_:                                                                                    \
         if (sw)                                                                                  \

@@ -121,7 +121,8 @@ def test_split_rows_match_oracle(ml100k, chunk, K):
     np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("tune", [0, 1, 4, 8, 13, 64, 65, 96, 97, 128, 1024, 1024 + 128, 65536, 65536 + 128, 65536 + 1024, 131072])
+@pytest.mark.parametrize("tune", [0, 1, 4, 8, 13, 64, 65, 96, 97, 128, 1024, 1024 + 128, 65536, 65536 + 128, 65536 + 1024, 131072,
+                                  1 << 20, 1 << 21, (1 << 20) + 4])
 def test_kernel_variants_match_oracle(ml100k, tune):
     """Kernel variants (sbmf_config.tune): block solve by one wave that hands D
     over in LDS (default, bit 0 clear) or by every wave of a row (bit 0 set);
@@ -129,8 +130,11 @@ def test_kernel_variants_match_oracle(ml100k, tune):
     bit 5 on 16-wave workgroups (LDS geometry GsGeom<16, 4>); bit 7: k_gres on
     4-wave workgroups (bit 17: 16-wave, 2048-rating tasks); bit 10: the hybrid schedule (k_gres up to 128 ratings,
     k_gstream above); bit 16: k_gres tasks in static rounds instead of
-    claimed from a queue in list order.  split_chunk 16 splits the longest rows into more than
-    16 chunks (k_gres' two-hop hand-off), 64 into fewer (one hop)."""
+    claimed from a queue in list order; bit 20: every multi-wave f64 Gram-block
+    row on 16-vector waves (default: rows of 5-8 eight-vector waves), bit 21:
+    none.  split_chunk 16 splits the longest rows into more than 16 chunks, 64
+    into fewer (the one-hop exchange splits each entry's chunk sum over 3
+    threads either way)."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=50, iters=3, seed=4)
     for kw in ({}, {"stream_threshold": 40, "split_chunk": 64}, {"stream_threshold": 40, "split_chunk": 16}):
