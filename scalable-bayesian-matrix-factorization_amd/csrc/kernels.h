@@ -57,11 +57,13 @@ static const uint32_t RK_MAXDEG[RK_NUM] = {128, 512, 2048, 4096};
 // Gram-block (MFMA) row kernels.  Max ratings per row for each kind: f64
 // holds 8 vectors (32 ratings) per wave, f32 16 (64 ratings).
 enum GblockKind { GK_W4 = 0, GK_W16 = 1, GK_B2 = 2, GK_B4 = 3, GK_B8 = 4, GK_NUM = 5 };
-inline uint32_t gk_maxdeg(int kind, bool f64, bool wide = false) {
+inline uint32_t gk_maxdeg(int kind, bool f64, bool wide = false, bool big = false) {
     static const uint32_t waves4[GK_NUM] = {1, 4, 8, 16, 32};  // (waves x vectors) / V*4 ratings
     const uint32_t per_wave = f64 ? 32 : 64;
     // wide (f64 default; tune bit 3 turns it off): the 1-wave kind holds 16 vectors (64 ratings)
     if (wide && f64 && (kind == GK_W16 || kind == GK_B2)) return 64;
+    // big (f64): the last kind takes rows up to 512 ratings, as up to 8 sixteen-vector waves
+    if (big && f64 && kind == GK_B8) return 512;
     return kind == GK_W4 ? per_wave / 4 : per_wave * waves4[kind] / 4;
 }
 

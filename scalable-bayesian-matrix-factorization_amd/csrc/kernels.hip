@@ -2178,6 +2178,10 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
             SBMF_GB_NW16(2)
             SBMF_GB_NW16(3)
             SBMF_GB_NW16(4)
+            SBMF_GB_NW16(5)
+            SBMF_GB_NW16(6)
+            SBMF_GB_NW16(7)
+            SBMF_GB_NW16(8)
             default:
                 return hipErrorInvalidValue;
         }

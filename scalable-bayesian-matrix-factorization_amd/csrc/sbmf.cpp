@@ -176,7 +176,8 @@ static const int KIND_STREAM = GK_NUM;  // 5: streaming kernel, whole rows (row 
 static const int KIND_RK0 = GK_NUM + 1;  // 6..9
 static const int KIND_GRAM = 10;         // Gram route
 
-static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr, bool f64, bool wide) {
+static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr, bool f64, bool wide,
+                       bool big = false) {
     for (auto& b : s.bin_rows) b.clear();
     s.gitems.clear();
     s.grows.clear();
@@ -204,7 +205,7 @@ static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stre
         }
         if (row_kernel == 0) {
             int kind = GK_W4;
-            while (d > gk_maxdeg(kind, f64, wide)) ++kind;
+            while (d > gk_maxdeg(kind, f64, wide, big)) ++kind;
             s.bin_rows[kind].push_back(r);
             continue;
         }
@@ -368,7 +369,9 @@ static void prepare_T(sbmf_ctx* c) {
     // streaming kernel above it, the Gram route only if a threshold is set.
     // row_kernel 1: per-coordinate kernels up to 4096 ratings, Gram route above.
     const bool f64 = sizeof(T) == 8;
-    const uint32_t gkmax = gk_maxdeg(GK_NUM - 1, f64);
+    // tune bit 22: f64 Gram-block rows up to 512 ratings (16-vector waves; not with bit 21)
+    const bool gbig = (cf.tune & 0x400000u) && !(cf.tune & 0x200000u);
+    const uint32_t gkmax = gk_maxdeg(GK_NUM - 1, f64, !(cf.tune & 8u), gbig);
     const uint32_t sthr = std::min<uint32_t>(cf.stream_threshold ? cf.stream_threshold : gkmax, gkmax);
     uint32_t thr;
     if (cf.row_kernel == 0)
@@ -376,8 +379,8 @@ static void prepare_T(sbmf_ctx* c) {
     else
         thr = cf.gram_threshold ? std::min(cf.gram_threshold, RK_MAXDEG[RK_NUM - 1]) : RK_MAXDEG[RK_NUM - 1];
     const bool wide = !(cf.tune & 8u);  // f64 rows <= 64 ratings on one wave (default)
-    build_bins(c->users, thr, (int)cf.row_kernel, sthr, f64, wide);
-    build_bins(c->items, thr, (int)cf.row_kernel, sthr, f64, wide);
+    build_bins(c->users, thr, (int)cf.row_kernel, sthr, f64, wide, gbig);
+    build_bins(c->items, thr, (int)cf.row_kernel, sthr, f64, wide, gbig);
     // multi-wave Gram-block bins: ceil(deg / ratings-per-wave) waves per row,
     // contiguous sub-ranges since each bin is degree-descending
     for (Side* sd : {&c->users, &c->items})
