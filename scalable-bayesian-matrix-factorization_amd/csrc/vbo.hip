@@ -182,6 +182,9 @@ __device__ __forceinline__ double gsum(double x, int G, double* red) {
 }
 
 constexpr int MC = 4;  // cases a lane keeps in registers between the two passes of a row
+#ifndef SBMF_VB_OCC
+#define SBMF_VB_OCC 6  // waves per SIMD the update kernels are compiled for
+#endif
 
 // update_w (:635-710) for the rows of one orientation.  apply_w0: first add
 // update_w0's deltas to the row's cases (the user pass touches every case once).
@@ -191,7 +194,7 @@ constexpr int MC = 4;  // cases a lane keeps in registers between the two passes
 // deltas k_item_w left in delta[g] to the local cases.
 enum { VB_FUSED = 0, VB_PART = 1, VB_FWD = 2 };
 template <int MODE>
-__global__ __launch_bounds__(256, 6) void k_update_w(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
+__global__ __launch_bounds__(256, SBMF_VB_OCC) void k_update_w(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
                                                    const uint32_t* __restrict__ xperm, int apply_w0, VBTables tb,
                                                    const double2* __restrict__ ETin, double2* __restrict__ ETout,
                                                    double2* __restrict__ sums, const double4* __restrict__ delta) {
@@ -293,7 +296,7 @@ __global__ __launch_bounds__(256, 6) void k_update_w(const VTask* __restrict__ t
 
 // update_v (:712-800) of factor f for the rows of one orientation (MODE as k_update_w)
 template <int MODE>
-__global__ __launch_bounds__(256, 6) void k_update_v(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
+__global__ __launch_bounds__(256, SBMF_VB_OCC) void k_update_v(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
                                                    const uint32_t* __restrict__ xperm, const uint32_t* __restrict__ part,
                                                    uint32_t f, VBTables tb, const double2* __restrict__ ETin,
                                                    double2* __restrict__ ETout, double2* __restrict__ sums,
