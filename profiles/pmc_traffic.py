@@ -18,11 +18,7 @@ import re
 import sys
 from collections import defaultdict
 
-# kernel symbol -> bench kind; k_gstream carries its half as a template argument
-GBLOCK = {("8", "1", "4"): "gblock_w16", ("2", "1", "4"): "gblock_w4", ("8", "2", "1"): "gblock_b2",
-          ("8", "4", "1"): "gblock_b4", ("8", "8", "1"): "gblock_b8",
-          ("16", "1", "4"): "gblock_w16", ("4", "1", "4"): "gblock_w4", ("16", "2", "1"): "gblock_b2",
-          ("16", "4", "1"): "gblock_b4", ("16", "8", "1"): "gblock_b8"}
+# kernel symbol -> bench key ("<user|item>_half/gstream" for the streaming launch of each half)
 
 
 def per_dispatch(path, counter):
@@ -42,10 +38,9 @@ def key_of(name, order_side):
     m = re.search(r"k_gres<(double|float), (\d+), (\d)>", name)  # the default streaming kernel
     if m:
         return ("item" if m.group(3) == "1" else "user") + "_half/gstream"
-    m = re.search(r"k_gblock<(double|float), (\d+), (\d+), (\d+), (true|false)>", name)
-    if m:
-        kind = GBLOCK.get((m.group(2), m.group(3), m.group(4)))
-        return "%s_half/%s" % (order_side, kind) if kind else None
+    # Gram-block bins are several launches each (one per waves-per-row group, and the
+    # f64 5-8-wave rows as 16-vector waves), so a per-launch figure does not match a
+    # bin: only the streaming launches (one per half, the dominant kernel) are keyed
     return None
 
 
