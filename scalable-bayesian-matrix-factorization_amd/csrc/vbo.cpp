@@ -14,7 +14,7 @@
 // back (:148-203); here a batch is an index range in device memory.
 //
 // Several ranks (one process per GPU): rank k owns the users [u_k, u_k+1)
-// (contiguous, balanced by rating count) and every case of those users, so
+// (sbmf_partition_rows over the users' rating counts) and every case of those users, so
 // user rows are local.  Every rank replays the same shuffle and keeps the
 // item tables replicated: an item row of a batch is summed over the ranks --
 // each rank writes its cases' {e1, e2} for the batch's items, an all-gather
@@ -159,17 +159,14 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
         cc[tu[x]]++;
         cc[I + ti[x]]++;
     }
-    // user ranges: contiguous, cut where the running rating count passes k N / R
+    // user ranges: the sampler's row partition (sbmf_partition_rows: contiguous,
+    // rating-balanced, 256-aligned) over the users' rating counts
     ubounds.assign(R + 1, 0);
     {
-        uint64_t run = 0;
-        int k = 1;
-        for (uint32_t a = 0; a < I && k < R; ++a) {
-            run += cc[a];
-            while (k < R && run * R >= (uint64_t)N * k) ubounds[k++] = a + 1;
-        }
-        for (; k < R; ++k) ubounds[k] = I;
-        ubounds[R] = I;
+        std::vector<uint32_t> uptr(I + 1, 0);
+        for (uint32_t a = 0; a < I; ++a) uptr[a + 1] = uptr[a] + cc[a];
+        if (sbmf_partition_rows(uptr.data(), I, R, ubounds.data()) != SBMF_OK)
+            fail(SBMF_E_ARG, "online VB: user partition failed");
     }
     u0 = (uint32_t)ubounds[rank];
     u1 = (uint32_t)ubounds[rank + 1];

@@ -93,3 +93,65 @@ def test_partition_properties_many_ranks():
         p64 = ptr.astype(np.int64)
         win = (p64[np.minimum(np.arange(len(p64)) + 384, len(p64) - 1)] - p64).max() / p64[-1]
         assert share.max() <= 1.0 / n + win + 1e-12
+
+
+def _vb_worker(rank, world, port, q):
+    """Online VB's item-pass protocol (vbo.cpp item_pass): users split by the
+    library's partition, every case local to its user's rank; per batch each
+    rank sums its cases' terms per item of the batch's global item list, the
+    per-rank sums are all-gathered and added in rank order."""
+    try:
+        sys.path.insert(0, PKG)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from sbmf import partition_rows, synth
+        train, _, dims = synth.generate("ml-100k", seed=5)
+        u, it, r = train
+        ptr = np.concatenate([[0], np.cumsum(np.bincount(u, minlength=dims[0]))]).astype(np.uint32)
+        b = partition_rows(ptr, world)
+        mine = (u >= b[rank]) & (u < b[rank + 1])
+        nb = 30
+        bid = np.random.default_rng(11).permutation(len(u)) % nb  # the same shuffle on every rank
+        x = r * np.cos(u.astype(np.float64))  # a per-case term (e1-like)
+        ok, maxerr = True, 0.0
+        for batch in range(nb):
+            inb = bid == batch
+            items, gcnt = np.unique(it[inb], return_counts=True)  # the batch's global item list
+            g = np.searchsorted(items, it)
+            send = np.zeros((len(items), 2))
+            sel = inb & mine
+            np.add.at(send[:, 0], g[sel], x[sel])
+            np.add.at(send[:, 1], g[sel], 1.0)
+            parts = [torch.zeros_like(torch.from_numpy(send)) for _ in range(world)]
+            dist.all_gather(parts, torch.from_numpy(send))
+            tot = np.zeros_like(send)
+            for p in parts:  # rank order
+                tot += p.numpy()
+            ref = np.zeros(len(items))
+            np.add.at(ref, g[inb], x[inb])
+            ok &= bool(np.array_equal(tot[:, 1], gcnt.astype(np.float64)))  # every case counted once
+            maxerr = max(maxerr, float(np.abs(tot[:, 0] - ref).max()))
+            gathered = [None] * world
+            dist.all_gather_object(gathered, tot[:, 0].tobytes())
+            ok &= all(gb == gathered[0] for gb in gathered)  # bit-identical on every rank
+        q.put((rank, ok, maxerr, int(mine.sum())))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, False, repr(e), None))
+
+
+def test_two_rank_vb_item_sums_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_vb_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, ok, maxerr, nloc in res:
+        assert ok, (rank, maxerr)
+        assert maxerr < 1e-9
+        assert nloc > 0
