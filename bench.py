@@ -326,22 +326,24 @@ def libfm_main(args):
     """libFM's own MCMC chain (-method mcmc -order libfm) or ALS on the ML-20M
     shape: ratings/s per iteration (draw_all + re-prediction + test RMSE)."""
     from sbmf import Data, FMLearnSBPMF, synth
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        raise SystemExit("bench.py --method libfm|als: the libFM learner runs on one GPU in this build")
+    world, rank, local = dist_setup(args)
     train, test, dims = synth.generate(args.shape)
     n_train, n_test, K = len(train[0]), len(test[0]), args.K
     als = args.method == "als"
+    uid = mk_uid(world, rank)
     L = FMLearnSBPMF(num_factor=K, seed=2015, rng="philox", method="als" if als else "mcmc", order="libfm",
-                     regular=(0.0, 0.0, 10.0) if als else (0.0, 0.0, 0.0), init_stdev=0.1,
-                     device=max(args.device, 0))
+                     regular=(0.0, 0.0, 10.0) if als else (0.0, 0.0, 0.0), init_stdev=0.1, device=local)
+    L.init(comm=(world, rank, uid) if world > 1 else None)
     L.set_data(Data(*train), Data(*test))
     L.learn(sweeps=args.warmup)
+    barrier(world)
     device_sync()
     t0 = time.perf_counter()
     L.learn(sweeps=args.steps)
     device_sync()
-    dt = time.perf_counter() - t0
+    barrier(world)
+    dt = max_over_ranks(world, time.perf_counter() - t0)
+    one_device = world > 1 and (os.environ.get("SBMF_COMM") == "host" or args.device >= 0)
     hist = L.history[-args.steps:]
     gpu_ms = float(np.mean([h["ms_sweep"] + h["ms_eval"] for h in hist]))
     # algorithmic bytes per iteration (f64): 2K + 2 passes over every case, each reading
@@ -353,12 +355,18 @@ def libfm_main(args):
     bytes_it = n_train * passes * 32.0 + n_train * K * 8.0 + (n_train + n_test) * (16.0 * K + 8.0)
     out = {
         "metric": "ratings/sec per libFM %s iteration, %s K=%d" % ("ALS" if als else "MCMC", args.shape, K),
-        "value": n_train * args.steps / dt, "unit": "ratings/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "weak",
+        "value": n_train * args.steps / dt, "unit": "ratings/s", "n_gpus": 1 if one_device else world,
+        "n_ranks": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
+        "higher_is_better": True,
+        "scaling": "not a scaling number (%d ranks on one GPU)" % world if one_device else "strong",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic %s-shaped (sbmf/synth.py)" % args.shape,
         "config": {"workload": "libFM fm_learn_mcmc iteration (alpha, w0, w, f-outer v passes, re-prediction, "
                                "test RMSE)%s" % (" without sampling (ALS)" if als else ""),
-                   "method": "als" if als else "mcmc -order libfm", "num_users": dims[0], "num_items": dims[1],
+                   "method": "als" if als else "mcmc -order libfm",
+                   "parallelism": "user ranges x%d (%s)" % (world, "host-shm exchange, testing only"
+                                                             if os.environ.get("SBMF_COMM") == "host"
+                                                             else "RCCL all-gather of the item sums"),
+                   "num_users": dims[0], "num_items": dims[1],
                    "n_train": n_train, "n_test": n_test, "K": K, "rng": "philox", "gpu_ms_per_iter": gpu_ms,
                    "launches_per_iter": int(L.timing().n_launch), "test_rmse_after": hist[-1]["rmse_avg"]},
         "roofline": {"kernel": "iteration (all libFM-learner kernels)", "bound": "hbm",
@@ -367,7 +375,11 @@ def libfm_main(args):
                      "bytes_per_iter": bytes_it},
     }
     L.close()
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
     from sbmf import _lib
     _lib.unload()
 

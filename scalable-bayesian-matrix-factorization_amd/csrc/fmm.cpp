@@ -18,6 +18,16 @@
 // (libFM consumes exactly one normal per drawn attribute).  Philox mode
 // fills those normals on the device.  ALS (do_sample = do_multilevel = 0)
 // draws nothing: alpha = 1, the w / v draws take their posterior means.
+//
+// Several ranks (one process per GPU), as the online VB learner: rank k owns
+// the users sbmf_partition_rows gives it and every case of those users.  User
+// rows are drawn locally; an item pass writes each item row's local sums, one
+// all-gather delivers every rank's, and every rank draws every item the same
+// way (sums added in rank order) and forwards the change to its own cases.
+// The scalar sums (alpha, w0, the train RMSE) are all-gathered per rank; the
+// owned users' w and v are broadcast after each sweep's passes, so the host
+// hyperparameter draws, the test predictions and the factors see every
+// attribute.  The host draws every variate on every rank (the same stream).
 #include "fmm.h"
 
 #include <algorithm>
@@ -26,6 +36,7 @@
 #include <memory>
 #include <vector>
 
+#include "comm.h"
 #include "common.h"
 #include "kernels.h"
 #include "rng.h"
@@ -43,7 +54,7 @@ struct FMBin {
 struct FMLearner {
     sbmf_config cfg{};
     uint32_t K = 0, Kp = 0, I = 0, J = 0, p = 0, p_train = 0, p_test = 0, RI = 0;  // RI: item-side rows (p - I)
-    uint64_t N = 0, T = 0;
+    uint64_t N = 0, T = 0, NL = 0;  // N: train cases (all ranks), NL: this rank's
     int k0 = 1, k1 = 1, do_sample = 1, do_multilevel = 1;
     double lo = 1.0, hi = 5.0;  // the train target range (min/max_target)
     double alpha = 1.0, w0 = 0.0, w_mu = 0.0, w_lambda = 0.0;
@@ -58,6 +69,32 @@ struct FMLearner {
     DBuf d_eu, d_ei, d_w, d_v, d_vT, d_vold, d_zw, d_zv, d_su, d_si, d_sy, d_pthis, d_sum, d_part, d_tpart, d_res,
         d_scratch;
     std::vector<double> h_w, h_v;
+    // several ranks
+    Comm* comm = nullptr;
+    int R = 1;
+    std::vector<uint64_t> ubounds;
+    DBuf d_sums, d_recvg, d_delta, d_recv;
+
+    // R ranks: every rank's `n` doubles at d (device) -> host, summed in rank order
+    void gather_sums(const double* d, int n, double* out) {
+        comm->allgather(d, n * sizeof(double), d_recv.p, st);
+        std::vector<double> h((size_t)R * n);
+        HIPCHK(hipMemcpyAsync(h.data(), d_recv.p, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int k = 0; k < n; ++k) {
+            double t = 0.0;
+            for (int r = 0; r < R; ++r) t += h[(size_t)r * n + k];
+            out[k] = t;
+        }
+    }
+    // R ranks: the owned users' w and v to every rank
+    void sync_users() {
+        if (R <= 1) return;
+        comm->group_begin();
+        comm->bcast_ranges(d_w.p, sizeof(double), ubounds, st);
+        for (uint32_t f = 0; f < K; ++f) comm->bcast_ranges(d_v.as<double>() + (size_t)f * p, sizeof(double), ubounds, st);
+        comm->group_end();
+    }
 
     ~FMLearner() {
         for (auto& e : ev)
@@ -150,13 +187,28 @@ struct FMLearner {
         return a;
     }
     void run_bins(FMPassArgs a, bool items, bool vpass) {
-        for (FMBin& b : items ? ibins : ubins) {
-            if (b.rows.empty()) continue;
-            a.rows = b.d_rows.as<uint32_t>();
-            a.nrows = (uint32_t)b.rows.size();
-            HIPCHK(vpass ? fmm_vpass(a, b.tpr, st) : fmm_wpass(a, b.tpr, st));
-            ++n_launch;
+        auto launch = [&](int xmode) {
+            a.xmode = xmode;
+            for (FMBin& b : items ? ibins : ubins) {
+                if (b.rows.empty()) continue;
+                a.rows = b.d_rows.as<uint32_t>();
+                a.nrows = (uint32_t)b.rows.size();
+                HIPCHK(vpass ? fmm_vpass(a, b.tpr, st) : fmm_wpass(a, b.tpr, st));
+                ++n_launch;
+            }
+        };
+        if (!(items && R > 1)) {
+            launch(0);
+            return;
         }
+        // several ranks: local sums of every item row -> all-gather -> the same draw everywhere
+        a.sums = d_sums.as<double2>();
+        launch(1);
+        comm->allgather(d_sums.p, (size_t)RI * sizeof(double2), d_recvg.p, st);
+        HIPCHK(fmm_item_update(a, d_recvg.as<double2>(), R, RI, vpass ? 1 : 0, d_delta.as<double4>(), st));
+        a.delta = d_delta.as<double4>();
+        launch(2);
+        ++n_launch;
     }
     FMPredictArgs predict_args() {
         FMPredictArgs a{};
@@ -176,7 +228,7 @@ struct FMLearner {
     // returns nothing on the host (sums land in d_res)
     void predict_train() {
         HIPCHK(fmm_transpose(d_v.as<double>(), d_vT.as<double>(), K, Kp, p, st));
-        HIPCHK(fmm_predict_train(predict_args(), d_uown.as<uint32_t>(), d_upart.as<uint32_t>(), d_uy.as<float>(), N,
+        HIPCHK(fmm_predict_train(predict_args(), d_uown.as<uint32_t>(), d_upart.as<uint32_t>(), d_uy.as<float>(), NL,
                                  d_eu.as<double>(), d_part.as<double>(), st));
         n_launch += 2;
     }
@@ -186,11 +238,18 @@ struct FMLearner {
         double* res = d_res.as<double>();
         const bool ref = cfg.rng_mode == SBMF_RNG_REFERENCE;
         // ---- alpha and w0 (fm_learn_mcmc.h:901-929, :627-668)
-        const uint64_t nb = (N + 1023) / 1024;
-        HIPCHK(fmm_esums(d_eu.as<double>(), N, w0, d_part.as<double>(), st));
-        HIPCHK(launch_sum_cols(d_part.as<double>(), (uint32_t)nb, 2, res, st));
+        const uint64_t nb = (NL + 1023) / 1024;
         double s[2];
-        HIPCHK(hipMemcpyAsync(s, res, sizeof s, hipMemcpyDeviceToHost, st));
+        if (NL) {
+            HIPCHK(fmm_esums(d_eu.as<double>(), NL, w0, d_part.as<double>(), st));
+            HIPCHK(launch_sum_cols(d_part.as<double>(), (uint32_t)nb, 2, res, st));
+        } else {
+            HIPCHK(hipMemsetAsync(res, 0, 2 * sizeof(double), st));
+        }
+        if (R > 1)
+            gather_sums(res, 2, s);  // every rank's {sum e^2, sum (e - w0)}, rank order
+        else
+            HIPCHK(hipMemcpyAsync(s, res, sizeof s, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(h_w.data(), d_w.p, (size_t)p * sizeof(double), hipMemcpyDeviceToHost, st));
         if (K) HIPCHK(hipMemcpyAsync(h_v.data(), d_v.p, (size_t)K * p * sizeof(double), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -212,7 +271,7 @@ struct FMLearner {
             if (std::isnan(w0) || std::isinf(w0)) {
                 w0 = old;
             } else {
-                HIPCHK(fmm_shift(d_eu.as<double>(), N, old - w0, st));
+                HIPCHK(fmm_shift(d_eu.as<double>(), NL, old - w0, st));
                 ++n_launch;
             }
         }
@@ -271,6 +330,7 @@ struct FMLearner {
                 }
             }
         }
+        sync_users();  // several ranks: the owned users' fresh w and v to every rank
     }
 
     void run(uint32_t iters, sbmf_sweep_cb cb, void* user) {
@@ -287,7 +347,10 @@ struct FMLearner {
             HIPCHK(hipEventRecord(ev[1], st));
             // ---- predict train and test, evaluate (fm_learn_mcmc_simultaneous.h:134-245)
             predict_train();
-            HIPCHK(launch_sum(d_part.as<double>(), (N + 255) / 256, res + 2, d_scratch.as<double>(), st));
+            if (NL)
+                HIPCHK(launch_sum(d_part.as<double>(), (NL + 255) / 256, res + 2, d_scratch.as<double>(), st));
+            else
+                HIPCHK(hipMemsetAsync(res + 2, 0, sizeof(double), st));
             const uint64_t tb = (T + 255) / 256;
             if (T) {
                 HIPCHK(fmm_predict_test(predict_args(), d_su.as<uint32_t>(), d_si.as<uint32_t>(), d_sy.as<float>(), T,
@@ -300,6 +363,7 @@ struct FMLearner {
             double h[3] = {0, 0, 0};
             HIPCHK(hipMemcpyAsync(h, res + 2, sizeof h, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
+            if (R > 1) gather_sums(res + 2, 1, h);  // the train sum of every rank (test: every rank has all)
             float ms0 = 0.f, ms1 = 0.f;
             HIPCHK(hipEventElapsedTime(&ms0, ev[0], ev[1]));
             HIPCHK(hipEventElapsedTime(&ms1, ev[1], ev[2]));
@@ -320,10 +384,14 @@ struct FMLearner {
 
 FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r,
                       uint64_t nt, const uint32_t* tu, const uint32_t* ti, const double* tr, uint32_t I, uint32_t J,
-                      hipStream_t st) {
+                      hipStream_t st, Comm* comm) {
     std::unique_ptr<FMLearner> L(new FMLearner());
     L->cfg = c;
     L->st = st;
+    if (comm && comm->nranks() > 1) {
+        L->comm = comm;
+        L->R = comm->nranks();
+    }
     L->K = c.num_factor;
     L->Kp = (L->K + 15) / 16 * 16;
     L->I = I;
@@ -357,24 +425,50 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
     for (uint64_t x = 0; x < nt; ++x) ys[x] = (float)tr[x];
     L->lo = mn;
     L->hi = mx;
-    // user order (CSR over users, cases in file order) and item order (CSC over item rows [0, RI))
+    // several ranks: the user ranges (sbmf_partition_rows over the users' rating counts);
+    // a rank keeps the cases of its users only
+    L->ubounds.assign(L->R + 1, 0);
+    L->ubounds[L->R] = I;
+    uint32_t u0 = 0, u1 = I;
+    std::vector<uint8_t> mine(n, 1);
+    L->NL = n;
+    if (L->R > 1) {
+        std::vector<uint32_t> cnt(I + 1, 0);
+        for (uint64_t x = 0; x < n; ++x) cnt[u[x] + 1]++;
+        for (uint32_t k = 0; k < I; ++k) cnt[k + 1] += cnt[k];
+        if (sbmf_partition_rows(cnt.data(), I, L->R, L->ubounds.data()) != SBMF_OK)
+            fail(SBMF_E_ARG, "libFM learner: user partition failed");
+        u0 = (uint32_t)L->ubounds[comm->rank()];
+        u1 = (uint32_t)L->ubounds[comm->rank() + 1];
+        L->NL = 0;
+        for (uint64_t x = 0; x < n; ++x) {
+            mine[x] = u[x] >= u0 && u[x] < u1;
+            L->NL += mine[x];
+        }
+    }
+    const uint64_t nl = L->NL;
+    // user order (CSR over users, cases in file order) and item order (CSC over item rows [0, RI)),
+    // over this rank's cases
     std::vector<uint32_t> uptr(I + 1, 0), iptr(L->RI + 1, 0);
     for (uint64_t x = 0; x < n; ++x) {
+        if (!mine[x]) continue;
         uptr[u[x] + 1]++;
         iptr[i[x] + 1]++;
     }
     for (uint32_t k = 0; k < I; ++k) uptr[k + 1] += uptr[k];
     for (uint32_t k = 0; k < L->RI; ++k) iptr[k + 1] += iptr[k];
-    std::vector<uint32_t> upos(n), ipos(n), uown(n), upart(n), ipart(n), uperm(n), iperm(n);
-    std::vector<float> uy(n);
+    std::vector<uint32_t> upos(n), ipos(n), uown(nl), upart(nl), ipart(nl), uperm(nl), iperm(nl);
+    std::vector<float> uy(nl);
     {
         std::vector<uint32_t> fu(uptr.begin(), uptr.end() - 1), fi(iptr.begin(), iptr.end() - 1);
         for (uint64_t x = 0; x < n; ++x) {
+            if (!mine[x]) continue;
             upos[x] = fu[u[x]]++;
             ipos[x] = fi[i[x]]++;
         }
     }
     for (uint64_t x = 0; x < n; ++x) {
+        if (!mine[x]) continue;
         uown[upos[x]] = u[x];
         upart[upos[x]] = i[x];
         uy[upos[x]] = y[x];
@@ -383,17 +477,18 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
         iperm[ipos[x]] = upos[x];
     }
     // rows binned by length: <= 256 cases 64 threads, <= 4096 256, longer 1024
-    auto bin = [](const std::vector<uint32_t>& ptr, uint32_t R, FMBin* b) {
+    // (users: this rank's range; items: every item row, each rank over its own cases)
+    auto bin = [](const std::vector<uint32_t>& ptr, uint32_t r0, uint32_t r1, FMBin* b) {
         b[0].tpr = 64;
         b[1].tpr = 256;
         b[2].tpr = 1024;
-        for (uint32_t k = 0; k < R; ++k) {
+        for (uint32_t k = r0; k < r1; ++k) {
             const uint32_t len = ptr[k + 1] - ptr[k];
             b[len <= 256 ? 0 : len <= 4096 ? 1 : 2].rows.push_back(k);
         }
     };
-    bin(uptr, I, L->ubins);
-    bin(iptr, L->RI, L->ibins);
+    bin(uptr, u0, u1, L->ubins);
+    bin(iptr, 0, L->RI, L->ibins);
     for (FMBin* bs : {L->ubins, L->ibins})
         for (int k = 0; k < 3; ++k) upload(bs[k].d_rows, bs[k].rows, st);
     upload(L->d_uptr, uptr, st);
@@ -408,8 +503,14 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
     upload(L->d_su, su, st);
     upload(L->d_si, si, st);
     upload(L->d_sy, ys, st);
-    L->d_eu.alloc(std::max<uint64_t>(n, 1) * sizeof(double));
-    L->d_ei.alloc(std::max<uint64_t>(n, 1) * sizeof(double));
+    L->d_eu.alloc(std::max<uint64_t>(nl, 1) * sizeof(double));
+    L->d_ei.alloc(std::max<uint64_t>(nl, 1) * sizeof(double));
+    if (L->R > 1) {
+        L->d_sums.alloc((size_t)std::max(L->RI, 1u) * sizeof(double2));
+        L->d_recvg.alloc((size_t)L->R * std::max(L->RI, 1u) * sizeof(double2));
+        L->d_delta.alloc((size_t)std::max(L->RI, 1u) * sizeof(double4));
+        L->d_recv.alloc((size_t)L->R * 4 * sizeof(double));
+    }
     L->d_w.alloc((size_t)p * sizeof(double));
     L->d_v.alloc(std::max<size_t>((size_t)K * p, 1) * sizeof(double));
     L->d_vT.alloc(std::max<size_t>((size_t)p * L->Kp, 1) * sizeof(double));
@@ -420,10 +521,10 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
     L->d_pthis.alloc(std::max<uint64_t>(nt, 1) * sizeof(double));
     L->d_sum.alloc(std::max<uint64_t>(nt, 1) * sizeof(double));
     HIPCHK(hipMemsetAsync(L->d_sum.p, 0, L->d_sum.bytes, st));
-    L->d_part.alloc((std::max<uint64_t>((n + 255) / 256, 2 * ((n + 1023) / 1024)) + 2) * sizeof(double));
+    L->d_part.alloc((std::max<uint64_t>((nl + 255) / 256, 2 * ((nl + 1023) / 1024)) + 2) * sizeof(double));
     L->d_tpart.alloc((2 * ((nt + 255) / 256) + 2) * sizeof(double));
     L->d_res.alloc(8 * sizeof(double));
-    L->d_scratch.alloc(((n + 255) / 256 / 1024 + 16) * 2 * sizeof(double));
+    L->d_scratch.alloc(((nl + 255) / 256 / 1024 + 16) * 2 * sizeof(double));
     L->v_mu.assign(K, 0.0);
     // fm_learn_mcmc::init (:1099-1116) and the -regular values (libfm.cpp:484-513)
     L->w_lambda = c.regw;

@@ -43,7 +43,18 @@ struct FMPassArgs {
     double alpha, mu, lambda;
     int do_sample;
     int item_side;          // factor pass: 1 = items (q carries the user pass's updates)
+    // several ranks, item rows (xmode 1): write the row's local {sum m, sum s2} to
+    // sums[row]; (xmode 2): take {old, new, keep} from delta[row] (fmm_item_update)
+    // and update the local cases' residuals; 0: one rank, sums and draw in one pass
+    int xmode;
+    double2* sums;
+    const double4* delta;
 };
+// several ranks: every item row's draw from every rank's local sums (recv
+// [R][nrows], rank order), the same on every rank; a.own / a.z / a.mu ... as for
+// the pass; writes own[a0 + row] and delta[row] = {old, new, keep}
+hipError_t fmm_item_update(const FMPassArgs& a, const double2* recv, int R, uint32_t nrows, int vpass, double4* delta,
+                           hipStream_t st);
 // draw_w (:670-719) over the rows of a bin
 hipError_t fmm_wpass(const FMPassArgs& a, int threads_per_row, hipStream_t st);
 // draw_v (:780-835) of one factor over the rows of a bin
@@ -74,9 +85,13 @@ hipError_t fmm_predict_test(const FMPredictArgs& a, const uint32_t* su, const ui
 
 // ---- host learner (fmm.cpp), driven by the C ABI in sbmf.cpp
 struct FMLearner;
+class Comm;
+// comm: null, or R > 1 ranks (one process per GPU): users split by
+// sbmf_partition_rows, every case local to its user's rank, item rows summed
+// over the ranks (as the online VB learner, vbo.cpp)
 FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r,
                       uint64_t nt, const uint32_t* tu, const uint32_t* ti, const double* tr, uint32_t I, uint32_t J,
-                      hipStream_t st);
+                      hipStream_t st, Comm* comm = nullptr);
 void fmm_destroy(FMLearner* L);
 void fmm_run(FMLearner* L, uint32_t iters, sbmf_sweep_cb cb, void* user);
 void fmm_predict_out(FMLearner* L, double* out);       // the -out predictions (fm_learn_mcmc::predict)

@@ -22,6 +22,27 @@ __device__ __forceinline__ double wsum(double x) {  // xor butterfly: bit-identi
     return x;
 }
 
+// The row's draw from its sums m = sum h e, s2 = sum h^2 (fm_learn_mcmc.h:700-719,
+// :815-835); keep: a non-finite draw restores the old value (the reference returns).
+template <int MODE>
+__device__ __forceinline__ double fmm_draw(const FMPassArgs& a, uint32_t at, double old, double m, double s2,
+                                           bool& keep) {
+    if constexpr (MODE == 1) m -= old * s2;
+    s2 = 1.0 / (a.lambda + a.alpha * s2);
+    m = -s2 * (a.alpha * m - a.mu * a.lambda);
+    double nv;
+    if (isnan(s2) || isinf(s2)) {
+        nv = 0.0;
+    } else if (a.do_sample) {  // ran_gaussian(mean, stdev), random.h:166-172
+        const double sd = sqrt(s2);
+        nv = (sd == 0.0 || isnan(sd)) ? m : m + sd * a.z[(size_t)at * a.zs + a.zoff];
+    } else {
+        nv = m;
+    }
+    keep = isnan(nv) || isinf(nv);
+    return keep ? old : nv;
+}
+
 // MODE 0: draw_w (fm_learn_mcmc.h:670-719); MODE 1: draw_v (:780-835).
 // NT threads per row; a 256-thread block holds 256 / NT rows (NT <= 256) or
 // one row (NT = 1024).
@@ -35,7 +56,9 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
     const uint32_t row = a.rows[ri];
     const uint32_t beg = a.ptr[row], n = a.ptr[row + 1] - beg;
     const uint32_t at = a.a0 + row;
-    const double old = a.own[at];
+    const int xm = a.xmode;
+    const double4 dl = xm == 2 ? a.delta[row] : make_double4(0.0, 0.0, 0.0, 0.0);
+    const double old = xm == 2 ? dl.x : a.own[at];
     const float x = 1.0f;  // one-hot value (DATA_FLOAT)
     // h of the case at position q (factor pass): x * (q_c - x * v) with the
     // case's q rebuilt from the factor column (see the file header)
@@ -51,7 +74,7 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
         return x * (qc - x * old);
     };
     double m = 0.0, s2 = 0.0;
-    for (uint32_t k = lt; k < n; k += NT) {
+    for (uint32_t k = lt; k < (xm == 2 ? 0u : n); k += NT) {
         const double e = a.e_in[beg + k];
         if constexpr (MODE == 0) {
             m += x * (e - old * x);
@@ -80,21 +103,19 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
             s2 += red[1][k];
         }
     }
-    if constexpr (MODE == 1) m -= old * s2;
-    s2 = 1.0 / (a.lambda + a.alpha * s2);
-    m = -s2 * (a.alpha * m - a.mu * a.lambda);
-    double nv;
-    if (isnan(s2) || isinf(s2)) {
-        nv = 0.0;
-    } else if (a.do_sample) {  // ran_gaussian(mean, stdev), random.h:166-172
-        const double sd = sqrt(s2);
-        nv = (sd == 0.0 || isnan(sd)) ? m : m + sd * a.z[(size_t)at * a.zs + a.zoff];
-    } else {
-        nv = m;
+    if (xm == 1) {  // several ranks: this rank's share of the row's sums
+        if (lt == 0) a.sums[row] = make_double2(m, s2);
+        return;
     }
-    const bool keep = isnan(nv) || isinf(nv);  // the reference restores the old value and returns
-    if (keep) nv = old;
-    if (lt == 0) a.own[at] = nv;
+    double nv;
+    bool keep;
+    if (xm == 2) {
+        nv = dl.y;
+        keep = dl.z != 0.0;
+    } else {
+        nv = fmm_draw<MODE>(a, at, old, m, s2, keep);
+        if (lt == 0) a.own[at] = nv;
+    }
     for (uint32_t k = lt; k < n; k += NT) {
         const uint32_t q = beg + k;
         const double e = a.e_in[q];
@@ -237,6 +258,25 @@ __global__ __launch_bounds__(256) void k_fmm_predict_test(FMPredictArgs a, const
     }
 }
 
+// several ranks: one thread per item row, sums added in rank order, then the draw
+template <int MODE>
+__global__ __launch_bounds__(256) void k_fmm_item(FMPassArgs a, const double2* __restrict__ recv, int R,
+                                                  uint32_t nrows, double4* __restrict__ delta) {
+    const uint32_t row = blockIdx.x * 256 + threadIdx.x;
+    if (row >= nrows) return;
+    double m = 0.0, s2 = 0.0;
+    for (int r = 0; r < R; ++r) {
+        m += recv[(size_t)r * nrows + row].x;
+        s2 += recv[(size_t)r * nrows + row].y;
+    }
+    const uint32_t at = a.a0 + row;
+    const double old = a.own[at];
+    bool keep;
+    const double nv = fmm_draw<MODE>(a, at, old, m, s2, keep);
+    a.own[at] = nv;
+    delta[row] = make_double4(old, nv, keep ? 1.0 : 0.0, 0.0);
+}
+
 template <int MODE>
 hipError_t launch_pass(const FMPassArgs& a, int tpr, hipStream_t st) {
     if (a.nrows == 0) return hipSuccess;
@@ -257,6 +297,16 @@ hipError_t launch_pass(const FMPassArgs& a, int tpr, hipStream_t st) {
 }
 
 }  // namespace
+
+hipError_t fmm_item_update(const FMPassArgs& a, const double2* recv, int R, uint32_t nrows, int vpass, double4* delta,
+                           hipStream_t st) {
+    if (nrows == 0) return hipSuccess;
+    if (vpass)
+        k_fmm_item<1><<<(nrows + 255) / 256, 256, 0, st>>>(a, recv, R, nrows, delta);
+    else
+        k_fmm_item<0><<<(nrows + 255) / 256, 256, 0, st>>>(a, recv, R, nrows, delta);
+    return hipGetLastError();
+}
 
 hipError_t fmm_wpass(const FMPassArgs& a, int tpr, hipStream_t st) { return launch_pass<0>(a, tpr, st); }
 hipError_t fmm_vpass(const FMPassArgs& a, int tpr, hipStream_t st) { return launch_pass<1>(a, tpr, st); }

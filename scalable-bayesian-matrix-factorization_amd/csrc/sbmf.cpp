@@ -1357,7 +1357,7 @@ static void prepare_fmm(sbmf_ctx* c) {
     c->J = std::max(c->J_req, imax + 1);
     c->K = c->cfg.num_factor;
     c->fm = fmm_create(c->cfg, c->tu.size(), c->tu.data(), c->ti.data(), c->tr.data(), c->su.size(), c->su.data(),
-                       c->si.data(), c->sr.data(), c->I, c->J, c->st);
+                       c->si.data(), c->sr.data(), c->I, c->J, c->st, c->nranks > 1 ? &c->comm : nullptr);
     c->prepared = true;
 }
 
@@ -1597,8 +1597,6 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
     HIPCHK(hipSetDevice(ctx->cfg.device));
     ctx->nranks = nranks;
     ctx->rank = rank;
-    if (nranks > 1 && is_fmm(ctx))
-        sbmf::fail(SBMF_E_ARG, "the libFM MCMC / ALS learner runs on one GPU in this build");
     if (nranks > 1) ctx->comm.init(nranks, rank, id);
     API_END(ctx)
 }

@@ -84,18 +84,6 @@ def test_biased_philox_deterministic_and_statistically_equivalent(ml100k):
     b.close()
 
 
-def test_libfm_learners_are_single_gpu_in_this_build():
-    """The biased sampler and online VB run on several GPUs
-    (tests/test_gpu_multirank.py); the libFM MCMC / ALS learners are refused
-    for more ranks."""
-    for kw in ({"method": "als"}, {"method": "mcmc", "order": "libfm"}):
-        L = FMLearnSBPMF(num_factor=8, **kw)
-        with pytest.raises(sbmf.SBMFError) as ei:
-            L.init(comm=(2, 0, bytes(128)))
-        assert ei.value.code == sbmf.SBMF_E_ARG and "one GPU" in str(ei.value)
-        L.close()
-
-
 def test_get_biases_rejects_unbiased_sampler(ml100k):
     tr, te = ml100k
     L = _run(tr, te, 1, num_factor=8)

@@ -111,3 +111,44 @@ def test_vb_ranks_on_one_gpu(ml100k, ragged, tmp_path, nranks, data, K, seed, ep
     if rng == "ref":
         gold = golden_rmse("ref_vbo_%s_k%d_s%d_e%d.txt" % (data, K, seed, epochs))
         assert np.abs(z0["rmse"] - gold).max() < 1e-9
+
+
+@pytest.mark.parametrize("nranks,run", [(2, 0), (3, 1), (2, 2), (3, 3), (2, 4)])
+def test_libfm_ranks_on_one_gpu(ml100k, ragged, tmp_path, nranks, run):
+    """libFM's own MCMC / ALS chain over several ranks (users split into
+    ranges, item rows' sums all-gathered and added in rank order, the owned
+    users' w and v broadcast after each sweep): identical on every rank, one
+    rank's run to rounding, and bin/libFM's printed digits (tests/golden)."""
+    from test_gpu_libfm import _within_printed
+    from test_oracle_libfm import RUNS, golden_name
+    method, dname, dim, seed, iters, reg = RUNS[run]
+    tr, te = ml100k if dname == "ml100k" else ragged
+    k0, k1, K = (int(x) for x in dim.split(","))
+    regular = reg or "0,0,0"
+    L = FMLearnSBPMF(num_factor=K, seed=seed, order="libfm", method="als" if method == "als" else "mcmc", k0=k0,
+                     k1=k1, regular=tuple(float(x) for x in regular.split(",")), init_stdev=0.1)
+    L.set_data(Data(*tr), Data(*te))
+    L.learn(sweeps=iters)
+    U1, V1 = L.factors()
+    test1 = L.rmse_trajectory
+    train1 = np.array([h["rmse_train"] for h in L.history])
+    pred1 = L.predict()
+    L.close()
+    outs = _run_ranks(tmp_path, nranks, [str(K), str(iters), str(seed), "ref", "0", "%d,%d;%s" % (k0, k1, regular),
+                                         "als" if method == "als" else "libfm"], env={"SBMF_WORKER_DATA": dname})
+    z0 = np.load(outs[0])
+    for r in range(1, nranks):
+        z = np.load(outs[r])
+        for k in ("U", "V", "bu", "bv", "b0", "rmse", "rmse_train", "pred"):
+            assert np.array_equal(z[k], z0[k]), (r, k)
+    print("libfm %s %d ranks: max|dTest| %.2e max|dTrain| %.2e max|dU| %.2e max|dV| %.2e" % (
+        golden_name(method, dname, dim, seed, iters), nranks, np.abs(z0["rmse"] - test1).max(),
+        np.abs(z0["rmse_train"] - train1).max(), np.abs(z0["U"] - U1).max(), np.abs(z0["V"] - V1).max()))
+    np.testing.assert_allclose(z0["rmse"], test1, rtol=1e-9, atol=0)
+    np.testing.assert_allclose(z0["rmse_train"], train1, rtol=1e-9, atol=0)
+    assert np.abs(z0["U"] - U1).max() < 1e-8 and np.abs(z0["V"] - V1).max() < 1e-8
+    assert np.abs(z0["pred"] - pred1).max() < 1e-9
+    with open(os.path.join(REPO, "tests", "golden", golden_name(method, dname, dim, seed, iters) + ".txt")) as f:
+        lines = f.read().splitlines()
+    assert _within_printed(z0["rmse_train"], [float(l.split("Train=")[1].split()[0]) for l in lines])
+    assert _within_printed(z0["rmse"], [float(l.split("Test=")[1]) for l in lines])

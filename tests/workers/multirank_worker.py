@@ -41,6 +41,12 @@ def main():
     tr, te = read(os.path.join(g, data + "_train.tsv.gz")), read(os.path.join(g, data + "_test.tsv.gz"))
     if method == "vb":
         L = FMLearnVBOnline(num_factor=int(K), seed=int(seed), rng=rng, device=0)
+    elif method in ("libfm", "als"):  # libFM's own chain: quirks carries "k0,k1;regular"
+        dim, reg = quirks.split(";")
+        k0, k1 = (int(x) for x in dim.split(","))
+        L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, order="libfm",
+                         method="als" if method == "als" else "mcmc", k0=k0, k1=k1,
+                         regular=tuple(float(x) for x in reg.split(",")), init_stdev=0.1)
     else:
         L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, tune=tune, quirks=quirks)
     L.init(comm=(int(nranks), int(rank), bytes.fromhex(idhex)))
@@ -48,11 +54,12 @@ def main():
     L.learn(sweeps=int(sweeps))
     U, V = L.factors()
     extra = {}
-    if quirks in ("bias2", "bias22") or method == "vb":
+    if quirks in ("bias2", "bias22") or method in ("vb", "libfm", "als"):
         bu, bv, b0 = L.biases()
         extra = {"bu": bu, "bv": bv, "b0": np.array([b0])}
-    if method == "vb":
+    if method in ("vb", "libfm", "als"):
         extra["pred"] = L.predict()
+        extra["rmse_train"] = np.array([h["rmse_train"] for h in L.history])
     np.savez(out, U=U, V=V, rmse=L.rmse_trajectory, tau=np.array([h["tau"] for h in L.history]), **extra)
     L.close()
 
