@@ -73,8 +73,37 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
         }
         return x * (qc - x * old);
     };
+    // a lane's first MCF cases stay in registers (residual, h, scatter target) from
+    // the sums to the residual update; the rest are reloaded (same values: the pass
+    // changes neither h nor e before the update)
+    constexpr int MCF = 4;
+    double ce[MCF], ch[MCF];
+    uint32_t cp[MCF];
     double m = 0.0, s2 = 0.0;
-    for (uint32_t k = lt; k < (xm == 2 ? 0u : n); k += NT) {
+    const uint32_t nsum = xm == 2 ? 0u : n;
+#pragma unroll
+    for (int j = 0; j < MCF; ++j) {
+        const uint32_t k = lt + j * NT;
+        ce[j] = 0.0;
+        ch[j] = x;
+        cp[j] = 0;
+        if (k < nsum) {
+            const uint32_t q = beg + k;
+            const double e = a.e_in[q];
+            ce[j] = e;
+            cp[j] = a.perm[q];
+            if constexpr (MODE == 0) {
+                m += x * (e - old * x);
+                s2 += x * x;
+            } else {
+                const double h = hval(q);
+                ch[j] = h;
+                m += h * e;
+                s2 += h * h;
+            }
+        }
+    }
+    for (uint32_t k = lt + MCF * NT; k < nsum; k += NT) {
         const double e = a.e_in[beg + k];
         if constexpr (MODE == 0) {
             m += x * (e - old * x);
@@ -116,7 +145,22 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
         nv = fmm_draw<MODE>(a, at, old, m, s2, keep);
         if (lt == 0) a.own[at] = nv;
     }
-    for (uint32_t k = lt; k < n; k += NT) {
+#pragma unroll
+    for (int j = 0; j < MCF; ++j) {
+        const uint32_t k = lt + j * NT;
+        if (k < n) {
+            const uint32_t q = beg + k;
+            const bool cached = xm != 2;  // the forwarding pass (several ranks) summed nothing
+            const double e = cached ? ce[j] : a.e_in[q];
+            double eo = e;
+            if (!keep) {
+                const double h = MODE == 0 ? (double)x : (cached ? ch[j] : hval(q));
+                eo = e - h * (old - nv);
+            }
+            a.e_out[cached ? cp[j] : a.perm[q]] = eo;
+        }
+    }
+    for (uint32_t k = lt + MCF * NT; k < n; k += NT) {
         const uint32_t q = beg + k;
         const double e = a.e_in[q];
         double eo = e;
