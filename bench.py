@@ -441,7 +441,10 @@ def main():
     pmc = os.path.join(REPO, "profiles", "pmc_lds.json")
     if profiled and os.path.exists(pmc):
         try:
-            lds_frac = (json.load(open(pmc)).get(kernel) or {}).get("frac")
+            e = json.load(open(pmc)).get(kernel) or {}
+            bc, act = e.get("bank_conflict_cycles"), e.get("lds_active_cycles")
+            # share of the LDS pipe's cycles (issuing + conflict-stalled) lost to bank conflicts
+            lds_frac = bc / (bc + act) if bc is not None and act else None
         except Exception:
             lds_frac = None
     # several ranks on one device (SBMF_COMM=host or --device): a protocol rehearsal, not a scaling point

@@ -131,7 +131,9 @@ typedef struct sbmf_config {
                                  bit 17 = k_gres on 16-wave workgroups,
                                  bit 20 = every multi-wave f64 Gram-block row on 16-vector
                                           waves (default: rows of 5-8 8-vector waves),
-                                 bit 21 = no multi-wave f64 Gram-block row on 16-vector waves  */
+                                 bit 21 = no multi-wave f64 Gram-block row on 16-vector waves,
+                                 bit 24 = k_gres (queue order) as an ordinary launch instead of
+                                          a cooperative one (measured neutral, 8.93 vs 8.95 ms)  */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

@@ -3,9 +3,12 @@
 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS pass (profiles/collect.sh lds).
 
 usage: python profiles/pmc_lds.py <counter_collection.csv> [out.json]
-frac = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS: the cycles the LDS pipe
-stalls on bank conflicts per cycle spent issuing LDS instructions, summed
-over every SIMD of the launch and averaged over the profiled sweeps.  Keys as
+conflict_per_active = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS: the cycles the
+LDS pipe stalls on bank conflicts per cycle spent issuing LDS instructions,
+summed over every SIMD of the launch and averaged over the profiled sweeps;
+frac = SQ_LDS_BANK_CONFLICT / (SQ_LDS_BANK_CONFLICT + SQ_ACTIVE_INST_LDS): the
+share of the LDS pipe's cycles lost to conflicts (bench.py's
+roofline.lds_bank_conflict_frac).  Keys as
 bench.py's roofline kernel ("<user|item>_half/<kind>").
 """
 import csv
@@ -40,11 +43,12 @@ def main():
         a[1] += per[d].get("SQ_ACTIVE_INST_LDS", 0.0)
         a[2] += per[d].get("SQ_INSTS_LDS", 0.0)
         a[3] += 1
-    out = {"_note": "frac = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS per launch (rocprofv3 --pmc, "
-                    "profiles/collect.sh lds)"}
+    out = {"_note": "conflict_per_active = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS, frac = SQ_LDS_BANK_CONFLICT / "
+                    "(SQ_LDS_BANK_CONFLICT + SQ_ACTIVE_INST_LDS), per launch (rocprofv3 --pmc, profiles/collect.sh lds)"}
     for k, (bc, act, ins, n) in sorted(acc.items()):
         out[k] = {"bank_conflict_cycles": bc / n, "lds_active_cycles": act / n, "lds_insts": ins / n,
-                  "frac": bc / act if act else None}
+                  "conflict_per_active": bc / act if act else None,
+                  "frac": bc / (bc + act) if bc + act else None}
     s = json.dumps(out, indent=1)
     print(s)
     if len(sys.argv) > 2:

@@ -2273,9 +2273,18 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     SplitSync syp = sy;
     void* args[] = {(void*)&tp, (void*)&ntask, (void*)&ap, (void*)&syp};
     const size_t dyn = gstream_dyn<T>(a.tune, sy.cmax);
-    err = hipLaunchCooperativeKernel(gstream_fn<T>(a.tune, a.tag == TAG_ITEMS ? 1u : 0u), dim3(std::min(grid, ntask)),
-                                     dim3(64 * gstream_nw(a.tune)),
-                                     args, (unsigned)dyn, st);
+    // tune bit 24 (k_gres in queue order only): an ordinary launch. A workgroup
+    // claims a task only while it runs, so only the most recently claimed row can
+    // have chunks still unclaimed, and its waiting chunks (< its chunk count,
+    // far below the resident workgroups) never block the claims that complete it.
+    const bool plain = (a.tune & 0x1000000u) && use_gres(a.tune) && !(a.tune & 0x10000u);
+    if (plain)
+        err = hipLaunchKernel(gstream_fn<T>(a.tune, a.tag == TAG_ITEMS ? 1u : 0u), dim3(std::min(grid, ntask)),
+                              dim3(64 * gstream_nw(a.tune)), args, (unsigned)dyn, st);
+    else
+        err = hipLaunchCooperativeKernel(gstream_fn<T>(a.tune, a.tag == TAG_ITEMS ? 1u : 0u), dim3(std::min(grid, ntask)),
+                                         dim3(64 * gstream_nw(a.tune)),
+                                         args, (unsigned)dyn, st);
     if (err != hipSuccess) return err;
     if (nsrow) {
         k_split_finish<T><<<nsrow, 64, 0, st>>>(srows, nsrow, a, sy);

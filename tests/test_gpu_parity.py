@@ -122,7 +122,7 @@ def test_split_rows_match_oracle(ml100k, chunk, K):
 
 
 @pytest.mark.parametrize("tune", [0, 1, 4, 8, 13, 64, 65, 96, 97, 128, 1024, 1024 + 128, 65536, 65536 + 128, 65536 + 1024, 131072,
-                                  1 << 20, 1 << 21, (1 << 20) + 4])
+                                  1 << 20, 1 << 21, (1 << 20) + 4, 1 << 24])
 def test_kernel_variants_match_oracle(ml100k, tune):
     """Kernel variants (sbmf_config.tune): block solve by one wave that hands D
     over in LDS (default, bit 0 clear) or by every wave of a row (bit 0 set);
@@ -132,7 +132,7 @@ def test_kernel_variants_match_oracle(ml100k, tune):
     k_gstream above); bit 16: k_gres tasks in static rounds instead of
     claimed from a queue in list order; bit 20: every multi-wave f64 Gram-block
     row on 16-vector waves (default: rows of 5-8 eight-vector waves), bit 21:
-    none.  split_chunk 16 splits the longest rows into more than 16 chunks, 64
+    none; bit 24: k_gres as an ordinary (not cooperative) launch.  split_chunk 16 splits the longest rows into more than 16 chunks, 64
     into fewer (the one-hop exchange splits each entry's chunk sum over 3
     threads either way)."""
     tr, te = ml100k
