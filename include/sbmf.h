@@ -133,7 +133,9 @@ typedef struct sbmf_config {
                                           waves (default: rows of 5-8 8-vector waves),
                                  bit 21 = no multi-wave f64 Gram-block row on 16-vector waves,
                                  bit 24 = k_gres (queue order) as an ordinary launch instead of
-                                          a cooperative one (measured neutral, 8.93 vs 8.95 ms)  */
+                                          a cooperative one (measured neutral, 8.93 vs 8.95 ms),
+                                 bit 25 = k_gres with double-buffered slices (slice t+1 in flight
+                                          through block t's exchange; one workgroup per CU)    */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

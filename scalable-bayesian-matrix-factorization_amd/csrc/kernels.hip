@@ -1139,9 +1139,9 @@ template <typename T>
 struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of slices
     static constexpr int VW = sizeof(T) == 8 ? 32 : 64;
 };
-template <typename T, int NW, int SIDE>
-__global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict__ tasks, uint32_t ntask,
-                                                  HalfArgs<T> a, SplitSync sy) {
+template <typename T, int NW, int SIDE, bool DB = false>
+__global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* __restrict__ tasks, uint32_t ntask,
+                                                           HalfArgs<T> a, SplitSync sy) {
     typedef typename MfmaT<T>::acc_t acc_t;
     constexpr int VW = GresW<T>::VW;
     constexpr uint32_t CAP = 4 * NW * VW;
@@ -1254,9 +1254,6 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             }
             stamp(0);  // staging
             const T* __restrict__ pbase = a.partner + ci;
-            T s[VC];
-#pragma unroll
-            for (int j = 0; j < VC; ++j) s[j] = pbase[pjW[j * JS]];
             // Residual update e_v -= S_v D (vector v: 4 ratings x 16 columns, lane ci
             // holding column ci): s_v *= D in place, then a butterfly reduce-scatter
             // over the 16 lanes of each rating (row_ror:8, row_half_mirror, quad_perm
@@ -1264,7 +1261,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             // max(1, VC/16) vectors and updates their residuals in LDS -- 2 (VC - 1)
             // DPP moves instead of 4 VC row-sum steps.  The registers each level
             // frees take their next slices at once (next(j) = the gather of vector j).
-            auto apply = [&](T D, auto&& next) {
+            auto apply = [&](auto& s, T D, auto&& next) {
                 // VC rounded up to a power of two (VP); vectors VC..VP-1 are zero
                 constexpr int VP = VC <= 8 ? 8 : VC <= 16 ? 16 : VC <= 32 ? 32 : 64;
 #pragma unroll
@@ -1302,23 +1299,9 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 for (int j = 0; j < RV; ++j) next(j);
             };
             T Dl = T(0);
-            for (uint32_t t = 0; t < nblk; ++t) {
-                // keep the per-vector partner offsets in LDS: hoisting them out of
-                // the block loop would hold VC 64-bit addresses in VGPRs
-                asm volatile("" ::: "memory");
-                if (t > 0) {
-                    // apply block t-1 with the held slice, then gather slice t into it
-#ifdef SBMF_ABLATIONS
-                    if (a.tune & 0x40000u) {  // ablation (wrong results): no residual update
-#pragma unroll
-                        for (int j = 0; j < VC; ++j) s[j] = pbase[(size_t)pjW[j * JS] + t * GB];
-                    } else
-#endif
-                    apply(Dl, [&](int j) { s[j] = pbase[(size_t)pjW[j * JS] + t * GB]; });
-                }
-                stamp(1);  // apply + gather issue
-                acc_t g = {T(0), T(0), T(0), T(0)};
-                T cc = T(0);
+            // G_t = S_t^T S_t by MFMA, c_t = S_t^T e (this lane's column, summed over
+            // the 4 ratings of each vector)
+            auto accumulate = [&](auto& s, acc_t& g, T& cc) {
 #ifdef SBMF_ABLATIONS
                 if (a.tune & 0x80000u) {  // ablation (wrong results): no MFMA (c only, G from one vector)
                     g = MfmaT<T>::mfma(s[0], g);
@@ -1333,7 +1316,11 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 }
                 cc += shfl_xor_t(cc, 16);
                 cc += shfl_xor_t(cc, 32);
-                stamp(2);  // gather wait + accumulate
+            };
+            // the block's partials into LDS, the cross-wave sum, the split-row
+            // exchange and the 16 draws: returns D_t (every lane: its column's)
+            auto finish_block = [&](const acc_t& g, T cc, uint32_t t) -> T {
+                T Dl;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int r = MfmaT<T>::row(lane, j);
@@ -1457,10 +1444,68 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     Dl = Dsh[ci];
                 }
                 stamp(5);  // solve
+                return Dl;
+            };
+            if constexpr (!DB) {
+                T s[VC];
+#pragma unroll
+                for (int j = 0; j < VC; ++j) s[j] = pbase[pjW[j * JS]];
+                for (uint32_t t = 0; t < nblk; ++t) {
+                    // keep the per-vector partner offsets in LDS: hoisting them out of
+                    // the block loop would hold VC 64-bit addresses in VGPRs
+                    asm volatile("" ::: "memory");
+                    if (t > 0) {
+                        // apply block t-1 with the held slice, then gather slice t into it
+#ifdef SBMF_ABLATIONS
+                        if (a.tune & 0x40000u) {  // ablation (wrong results): no residual update
+#pragma unroll
+                            for (int j = 0; j < VC; ++j) s[j] = pbase[(size_t)pjW[j * JS] + t * GB];
+                        } else
+#endif
+                        apply(s, Dl, [&](int j) { s[j] = pbase[(size_t)pjW[j * JS] + t * GB]; });
+                    }
+                    stamp(1);  // apply + gather issue
+                    acc_t g = {T(0), T(0), T(0), T(0)};
+                    T cc = T(0);
+                    accumulate(s, g, cc);
+                    stamp(2);  // gather wait + accumulate
+                    Dl = finish_block(g, cc, t);
+                }
+                // apply the last block
+                apply(s, Dl, [](int) {});
+            } else {
+                // double-buffered slices: slice t+1 is gathered into the second
+                // buffer right after block t's accumulate, so its loads are in flight
+                // through block t's exchange and draws (128 VGPRs of slices, one
+                // 8-wave workgroup per CU)
+                T sA[VC], sB[VC];
+#pragma unroll
+                for (int j = 0; j < VC; ++j) sA[j] = pbase[pjW[j * JS]];
+                auto dstep = [&](auto& cur, auto& prv, uint32_t t) {
+                    asm volatile("" ::: "memory");
+                    if (t > 0) apply(prv, Dl, [](int) {});  // e -= S_{t-1} D_{t-1}
+                    stamp(1);
+                    acc_t g = {T(0), T(0), T(0), T(0)};
+                    T cc = T(0);
+                    accumulate(cur, g, cc);
+                    if (t + 1 < nblk) {
+#pragma unroll
+                        for (int j = 0; j < VC; ++j) prv[j] = pbase[(size_t)pjW[j * JS] + (t + 1) * GB];
+                    }
+                    stamp(2);
+                    Dl = finish_block(g, cc, t);
+                };
+                for (uint32_t t = 0; t < nblk; t += 2) {
+                    dstep(sA, sB, t);
+                    if (t + 1 < nblk) dstep(sB, sA, t + 1);
+                }
+                if (nblk & 1u)
+                    apply(sA, Dl, [](int) {});
+                else
+                    apply(sB, Dl, [](int) {});
             }
-            // apply the last block; then residuals out and the per-row sums, one
-            // rating per thread in rating order (no per-vector branches)
-            apply(Dl, [](int) {});
+            // residuals out and the per-row sums, one rating per thread in rating
+            // order (no per-vector branches)
             __syncthreads();
             double sq = 0.0, trs = 0.0;
             for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) {
@@ -2158,7 +2203,11 @@ hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const H
 static bool use_gres(uint32_t tune) { return !(tune & 64u); }
 static int gres_nw(uint32_t tune) { return (tune & 128u) ? 4 : (tune & 0x20000u) ? 16 : 8; }
 static int gstream_nw(uint32_t tune) { return use_gres(tune) ? gres_nw(tune) : (tune & 32u) ? 16 : 8; }
-int gstream_wg_target(uint32_t tune) { return use_gres(tune) ? 16 / gres_nw(tune) : (tune & 32u) ? 1 : 2; }
+// k_gres variant: tune bit 25 = double-buffered slices (8 waves, one workgroup per CU)
+int gstream_wg_target(uint32_t tune) {
+    if (use_gres(tune)) return (tune & 0x2000000u) && gres_nw(tune) == 8 ? 1 : 16 / gres_nw(tune);
+    return (tune & 32u) ? 1 : 2;
+}
 template <typename T>
 static size_t gstream_dyn(uint32_t tune, uint32_t cmax) {
     if (use_gres(tune)) return 0;
@@ -2222,6 +2271,7 @@ static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
     if (use_gres(tune)) {
         if (gres_nw(tune) == 4) return side ? (const void*)k_gres<T, 4, 1> : (const void*)k_gres<T, 4, 0>;
         if (gres_nw(tune) == 16) return side ? (const void*)k_gres<T, 16, 1> : (const void*)k_gres<T, 16, 0>;
+        if (tune & 0x2000000u) return side ? (const void*)k_gres<T, 8, 1, true> : (const void*)k_gres<T, 8, 0, true>;
         return side ? (const void*)k_gres<T, 8, 1> : (const void*)k_gres<T, 8, 0>;
     }
     const bool sw = !(tune & 1u);
