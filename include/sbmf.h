@@ -128,14 +128,22 @@ typedef struct sbmf_config {
                                  bit 7 = k_gres on 4-wave workgroups (default 8),
                                  bits 8-10 = hybrid k_gres / k_gstream stream sets by row length,
                                  bit 16 = k_gres tasks in static rounds (default: a queue),
-                                 bit 17 = k_gres on 16-wave workgroups,
+                                 bit 17 = k_gres on 16-wave workgroups (both sides),
                                  bit 20 = every multi-wave f64 Gram-block row on 16-vector
                                           waves (default: rows of 5-8 8-vector waves),
                                  bit 21 = no multi-wave f64 Gram-block row on 16-vector waves,
                                  bit 24 = k_gres (queue order) as an ordinary launch instead of
                                           a cooperative one (measured neutral, 8.93 vs 8.95 ms),
                                  bit 25 = k_gres with double-buffered slices (slice t+1 in flight
-                                          through block t's exchange; one workgroup per CU)    */
+                                          through block t's exchange; one workgroup per CU),
+                                 bit 26 = no overlap of the next sweep's prologue (sums, column
+                                          statistics, host draws) with the test evaluation
+                                          (Philox mode; the chain is the same either way),
+                                 bit 27 = f64 item rows on 8-wave k_gres workgroups (default:
+                                          16-wave, as bit 17 does for both sides),
+                                 bit 28 = throughput mode: normals filled by a separate launch
+                                          (default: the Gram-block kernels draw their rows'
+                                          normals, the fill covers the streaming rows only)   */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

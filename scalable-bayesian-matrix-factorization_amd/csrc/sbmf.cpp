@@ -272,6 +272,15 @@ struct sbmf_ctx {
     DBuf d_bu, d_bv, d_mbu, d_mbv, d_sbu, d_sbv;  // biases b_i / b_j and their per-row (mu, sigma)
     DBuf d_var3u, d_var3v, d_epart;              // reference-mode per-row bias variates; sum(E) partials
     std::vector<double> h_res;
+    double* h_pre = nullptr;     // pinned: the prologue's sums (residual, column statistics)
+    // throughput mode: the next sweep's hyperparameters, drawn at the end of the
+    // previous sweep while its test evaluation runs (run_sweeps_T)
+    struct PreDraw {
+        bool valid = false;
+        uint32_t sweep = 0;
+        double tau = 0, b0 = 0, mu_b0 = 0, sig_b0 = 0, d0 = 0;
+        std::vector<double> sig_u, mu_u, sig_v, mu_v;
+    } pre;
     double* h_pinned = nullptr;  // pinned staging for z streams
     size_t h_pinned_bytes = 0;
     sbmf_timing timing{};
@@ -411,9 +420,16 @@ static void prepare_T(sbmf_ctx* c) {
             std::vector<uint32_t> rows[2];
             for (uint32_t r : sd->bin_rows[KIND_STREAM])  // degree-descending
                 rows[hyb && sd->ptr[r + 1] - sd->ptr[r] > hyb ? 1 : 0].push_back(r);
+            // f64 item rows (the long ones: 80 % of item ratings sit in rows split over
+            // several tasks) on 16-wave k_gres workgroups, 2048-rating tasks: half the
+            // chunks per row, a quarter of the all-read exchange (measured 4.04 -> 3.88
+            // ms; the user side stays on 8-wave workgroups, 1.59 vs 2.23 ms there).
+            // Tune bit 27, or an explicit workgroup-shape bit, keeps 8-wave items.
+            const bool item16 = sd == &c->items && sizeof(T) == 8 &&
+                                !(cf.tune & (64u | 128u | 0x20000u | 0x2000000u | 0x8000000u));
             for (int k = 0; k < 2; ++k) {
                 Side::StreamSet& S = sd->ss[k];
-                S.tune = tunes[k];
+                S.tune = k == 0 && item16 ? (tunes[k] | 0x20000u) : tunes[k];
                 // task capacity: the kernel's on-chip maximum, or smaller if split_chunk asks
                 S.cmax = gstream_cmax<T>(S.tune);
                 if (cf.split_chunk) S.cmax = std::min(S.cmax, std::max(cf.split_chunk, 1u));
@@ -526,6 +542,10 @@ static void prepare_T(sbmf_ctx* c) {
     c->d_colpart.alloc((size_t)nchunk * 2 * c->K * sizeof(double));
     c->h_res.assign(RES_COL + 4 * (size_t)c->K, 0.0);
     c->d_res.alloc(c->h_res.size() * sizeof(double));
+    if (c->h_pre) (void)hipHostFree(c->h_pre);
+    c->h_pre = nullptr;
+    HIPCHK(hipHostMalloc((void**)&c->h_pre, c->h_res.size() * sizeof(double), hipHostMallocDefault));
+    c->pre.valid = false;
     const uint64_t big = std::max<uint64_t>({(uint64_t)c->I, (uint64_t)c->J, (uint64_t)nslab, c->su.size() / 128 + 2});
     c->d_scratch.alloc((big / 1024 + 16) * 2 * sizeof(double));
     // test set
@@ -787,6 +807,19 @@ static void fill_z(sbmf_ctx* c, uint32_t R, DBuf& d) {
     HIPCHK(hipMemcpy(d.p, h, n * sizeof(T), hipMemcpyHostToDevice));
 }
 
+// Throughput mode: the Gram-block kernels draw a row's Philox normals themselves
+// (no z round trip through HBM for those rows) when the half has no
+// per-coordinate or Gram-route rows; the streaming rows still read the buffer,
+// filled for them alone (in-kernel draws cost k_gres spills).  Tune bit 28
+// keeps the whole-half fill.
+static bool zgen_side(const sbmf_ctx* c, const Side& s) {
+    if (c->cfg.rng_mode == SBMF_RNG_REFERENCE || (c->cfg.tune & 0x10000000u)) return false;
+    if (!s.gitems.empty()) return false;
+    for (int k = KIND_RK0; k < NBIN; ++k)
+        if (!s.bin_rows[k].empty()) return false;
+    return true;
+}
+
 template <typename T>
 static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     HalfArgs<T> a{};
@@ -837,6 +870,7 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     // tune bit 1: residuals from r - own.partner (the former multi-GPU form, kept for validation);
     // otherwise every rank reads the residuals the exchange delivered
     a.e_from_dot = (c->cfg.tune & 2u) ? 1 : 0;
+    a.zgen = zgen_side(c, users ? c->users : c->items) ? 1 : 0;
     return a;
 }
 
@@ -958,18 +992,18 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
     const bool q2 = cf.quirks == SBMF_QUIRKS_SBPMF2;
     double* d_res = c->d_res.as<double>();
     double* scratch = c->d_scratch.as<double>();
-    for (uint32_t it = 0; it < nsweeps; ++it) {
-        c->timing.n_launch = 0;
-        HostStream hs;
-        if (ref) {
-            draw_hyper_variates(c->grand, c, hs);
-        } else {
-            PhiloxStream ps(cf.seed, c->sweep, 0);
-            draw_hyper_variates(ps, c, hs);
-        }
-        HIPCHK(hipEventRecord(c->ev[0], st));
+    // Throughput mode (Philox: the draws of sweep s depend only on (seed, s)): the
+    // next sweep's prologue -- residual sum of squares, column statistics and the
+    // host hyperparameter draws -- is issued at the end of this sweep, its kernels
+    // before the test evaluation and its host draws while the evaluation runs, so
+    // the GPU does not wait for the host round trip at the start of the next
+    // sweep.  The inputs are the same (U, V and the residuals do not change in
+    // between), so the chain is bitwise the same.  Tune bit 26 turns it off.
+    const bool overlap = !ref && !(cf.tune & 0x4000000u);
+    // ---- 1. the prologue's kernels for sweep sw; its sums land in c->h_pre
+    auto prologue_gpu = [&](uint32_t sw) {
         // ---- 1. residual sum of squares (E recompute at sweep start, :317-334)
-        const bool recompute = c->sweep == 0 || (cf.recompute_every && c->sweep % cf.recompute_every == 0);
+        const bool recompute = sw == 0 || (cf.recompute_every && sw % cf.recompute_every == 0);
         if (recompute) {
             // residuals of every rating, scattered into user order for the user half
             HIPCHK(launch_resid<T>(c->d_rtasks.as<ResidTask>(), (uint32_t)c->items.rtasks.size(),
@@ -999,10 +1033,13 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         HIPCHK(launch_colstats<T>(c->d_V.as<T>(), K, c->Kp, 0, c->J, hyp + 3 * c->Kp, colpart, st));
         HIPCHK(launch_sum_cols(colpart, (c->J + 255) / 256, 2 * K, d_res + RES_COL + 2 * K, st));
         c->timing.n_launch += 5;
-        HIPCHK(hipMemcpyAsync(c->h_res.data(), d_res, c->h_res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        // ---- 2. host draws (:339-342, :375-414)
-        const double* Su2 = &c->h_res[RES_COL];
+        HIPCHK(hipMemcpyAsync(c->h_pre, d_res, c->h_res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    };
+    // ---- 2. host draws (:339-342, :375-414) from the prologue's sums: updates
+    // c->tau, sigma / mu (and the biased sampler's globals); returns d0
+    auto host_draw = [&](const HostStream& hs) -> double {
+        const double* res = c->h_pre;
+        const double* Su2 = &res[RES_COL];
         const double* Su1 = Su2 + K;
         const double* Sv2 = Su2 + 2 * K;
         const double* Sv1 = Su2 + 3 * K;
@@ -1010,7 +1047,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         double d0 = 0.0;  // biased sampler: global-bias delta, folded into the user half's residual pass
         if (c->bias) {
             // top-level gibbs_sbpmf2.cpp:366-467 (= src/libfm/gibbs_sbpmf22.cpp:345-446)
-            const double es = c->h_res[RES_ES], esq = c->h_res[RES_ESQ2];
+            const double es = res[RES_ES], esq = res[RES_ESQ2];
             c->tau = hs.g_tau / (cf.b0 + esq);
             c->sig_b0 = hs.g_sb0 / (cf.beta0 + (0.5 * (c->b0 - c->mu_b0) * (c->b0 - c->mu_b0)));
             const double s0 = 1.0 / (cf.nu0 + c->sig_b0);
@@ -1029,7 +1066,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 c->mu_v[k] = s1 * (cf.nu0 * cf.mu0 + c->sig_v[k] * Sv1[k]) + sd(s1) * hs.z_mv[k];
             }
         } else {
-        const double esq = c->h_res[RES_ESQ];
+        const double esq = res[RES_ESQ];
         c->tau = hs.g_tau / (cf.b0 + 0.5 * esq);
         for (uint32_t k = 0; k < K; ++k) {
             const double du = c->mu_u[k] - cf.mu0;
@@ -1048,6 +1085,35 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             c->mu_v[k] = mv_star + sd(sv_star) * hs.z_mv[k];
         }
         }
+        return d0;
+    };
+    for (uint32_t it = 0; it < nsweeps; ++it) {
+        c->timing.n_launch = 0;
+        HIPCHK(hipEventRecord(c->ev[0], st));
+        double d0;
+        if (c->pre.valid && c->pre.sweep == c->sweep) {  // drawn at the end of the previous sweep
+            c->tau = c->pre.tau;
+            c->b0 = c->pre.b0;
+            c->mu_b0 = c->pre.mu_b0;
+            c->sig_b0 = c->pre.sig_b0;
+            c->sig_u = c->pre.sig_u;
+            c->mu_u = c->pre.mu_u;
+            c->sig_v = c->pre.sig_v;
+            c->mu_v = c->pre.mu_v;
+            d0 = c->pre.d0;
+        } else {
+            HostStream hs;
+            if (ref) {
+                draw_hyper_variates(c->grand, c, hs);
+            } else {
+                PhiloxStream ps(cf.seed, c->sweep, 0);
+                draw_hyper_variates(ps, c, hs);
+            }
+            prologue_gpu(c->sweep);
+            HIPCHK(hipStreamSynchronize(st));
+            d0 = host_draw(hs);
+        }
+        c->pre.valid = false;
         {
             const size_t Kp = c->Kp;
             std::vector<T> h(4 * Kp, T(0));
@@ -1068,8 +1134,11 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         }
         HIPCHK(hipEventRecord(c->ev[1], st));
         // ---- 3. user half-sweep (throughput mode: this half's normals first)
-        if (!ref)
+        if (!ref && !zgen_side(c, c->users))
             HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep, TAG_USERS, st));
+        else if (!ref)  // the streaming rows' normals only
+            HIPCHK(launch_philox_fill_rows<T>(c->d_zU.as<T>(), K, c->d_bins_u[KIND_STREAM].as<uint32_t>(),
+                                              (uint32_t)c->users.bin_rows[KIND_STREAM].size(), cf.seed, c->sweep, TAG_USERS, st));
         if (c->bias)  // per-user bias hyperparameters + b_i draw + residual shift (:470-489, :515-530)
             HIPCHK(launch_bias_rows<T>(c->d_uptr.as<uint32_t>(), c->users.r0, c->users.r1, c->d_Eu.as<T>(),
                                        c->d_bu.as<double>(), c->d_mbu.as<double>(), c->d_sbu.as<double>(),
@@ -1083,8 +1152,11 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             });
         HIPCHK(hipEventRecord(c->ev[3], st));
         // ---- 4. item half-sweep
-        if (!ref)
+        if (!ref && !zgen_side(c, c->items))
             HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep, TAG_ITEMS, st));
+        else if (!ref)  // the streaming rows' normals only
+            HIPCHK(launch_philox_fill_rows<T>(c->d_zV.as<T>(), K, c->d_bins_v[KIND_STREAM].as<uint32_t>(),
+                                              (uint32_t)c->items.bin_rows[KIND_STREAM].size(), cf.seed, c->sweep, TAG_ITEMS, st));
         if (c->bias)  // per-item (:492-511, :563-578)
             HIPCHK(launch_bias_rows<T>(c->d_vptr.as<uint32_t>(), c->items.r0, c->items.r1, c->d_Ev.as<T>(),
                                        c->d_bv.as<double>(), c->d_mbv.as<double>(), c->d_sbv.as<double>(),
@@ -1099,6 +1171,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 if (cf.eval_train) c->comm.bcast_ranges(c->d_rowtr_v.p, sizeof(double), c->items.bounds, st);
             });
         HIPCHK(hipEventRecord(c->ev[5], st));
+        if (overlap) {  // the next sweep's prologue kernels, ahead of the evaluation
+            prologue_gpu(c->sweep + 1);
+            HIPCHK(hipEventRecord(c->ev[7], st));
+        }
         // ---- 5. evaluation
         const bool collect = q2 ? true : (c->sweep >= cf.burnin);
         if (collect) c->collected++;
@@ -1116,6 +1192,33 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         if (cf.eval_train) HIPCHK(launch_sum(c->d_rowtr_v.as<double>(), c->J, d_res + RES_TRSQ, scratch, st));
         HIPCHK(hipEventRecord(c->ev[6], st));
         HIPCHK(hipMemcpyAsync(c->h_res.data(), d_res, 8 * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (overlap) {  // the next sweep's draws while the evaluation runs; this sweep's values kept
+            HIPCHK(hipEventSynchronize(c->ev[7]));
+            HostStream hs;
+            PhiloxStream ps(cf.seed, c->sweep + 1, 0);
+            draw_hyper_variates(ps, c, hs);
+            const double tau0 = c->tau, b00 = c->b0, mb00 = c->mu_b0, sb00 = c->sig_b0;
+            std::vector<double> su0 = c->sig_u, mu0 = c->mu_u, sv0 = c->sig_v, mv0 = c->mu_v;
+            c->pre.d0 = host_draw(hs);
+            c->pre.tau = c->tau;
+            c->pre.b0 = c->b0;
+            c->pre.mu_b0 = c->mu_b0;
+            c->pre.sig_b0 = c->sig_b0;
+            c->pre.sig_u.swap(c->sig_u);
+            c->pre.mu_u.swap(c->mu_u);
+            c->pre.sig_v.swap(c->sig_v);
+            c->pre.mu_v.swap(c->mu_v);
+            c->tau = tau0;
+            c->b0 = b00;
+            c->mu_b0 = mb00;
+            c->sig_b0 = sb00;
+            c->sig_u.swap(su0);
+            c->mu_u.swap(mu0);
+            c->sig_v.swap(sv0);
+            c->mu_v.swap(mv0);
+            c->pre.sweep = c->sweep + 1;
+            c->pre.valid = true;
+        }
         uint32_t split_timeout = 0;
         if (c->d_xtimeout.p)
             HIPCHK(hipMemcpyAsync(&split_timeout, c->d_xtimeout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -1173,11 +1276,12 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         info.rmse_avg = (cf.eval_test && T_) ? std::sqrt(c->h_res[RES_TEST_AVG] / T_) : NAN;
         info.rmse_this = (cf.eval_test && T_) ? std::sqrt(c->h_res[RES_TEST_THIS] / T_) : NAN;
         info.rmse_train = cf.eval_train && N ? std::sqrt(c->h_res[RES_TRSQ] / N) : NAN;
-        c->timing.ms_hyper = ev_ms(c->ev[0], c->ev[1]);
+        // with the overlap the prologue's kernels run between ev[5] and ev[7] (for the next sweep)
+        c->timing.ms_hyper = ev_ms(c->ev[0], c->ev[1]) + (overlap ? ev_ms(c->ev[5], c->ev[7]) : 0.0);
         c->timing.ms_user_half = ev_ms(c->ev[1], c->ev[2]);
         c->timing.ms_item_half = ev_ms(c->ev[3], c->ev[4]);
         c->timing.ms_comm = ev_ms(c->ev[2], c->ev[3]) + ev_ms(c->ev[4], c->ev[5]);
-        c->timing.ms_eval = ev_ms(c->ev[5], c->ev[6]);
+        c->timing.ms_eval = ev_ms(c->ev[overlap ? 7 : 5], c->ev[6]);
         for (int sd = 0; sd < 2; ++sd) {
             const Side& sdd = sd == 0 ? c->users : c->items;
             for (int k = 0; k < SBMF_NKIND; ++k) {
@@ -1199,6 +1303,7 @@ sbmf_ctx::~sbmf_ctx() {
     vbo_destroy(vb);
     fmm_destroy(fm);
     if (h_pinned) (void)hipHostFree(h_pinned);
+    if (h_pre) (void)hipHostFree(h_pre);
     for (auto& e : ev)
         if (e) (void)hipEventDestroy(e);
     for (auto& a : kev)
@@ -1505,6 +1610,7 @@ int sbmf_set_factors(sbmf_ctx* ctx, const double* U, const double* V) {
     if (ctx->vb || ctx->fm) sbmf::fail(SBMF_E_STATE, "sbmf_set_factors is not supported by the VB / libFM learners");
     HIPCHK(hipSetDevice(ctx->cfg.device));
     HIPCHK(hipStreamSynchronize(ctx->st));
+    ctx->pre.valid = false;  // hyperparameters drawn ahead from the old tables
     if (ctx->cfg.precision == SBMF_F32) {
         if (U) sbmf::upload_table<float>(ctx, ctx->d_U, U, ctx->I);
         if (V) sbmf::upload_table<float>(ctx, ctx->d_V, V, ctx->J);

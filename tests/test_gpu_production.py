@@ -142,3 +142,36 @@ def test_ml20m_k200_reference_stream_one_sweep():
     """The single-GPU share of BASELINE config 4 (ML-20M, K=200): 13 k-blocks,
     the widest factor tables (221 MB U), reference RNG stream."""
     _check_shape("ml-20m", 200, 1, "ref", 1)
+
+
+@pytest.mark.parametrize("quirks", ["final", "bias2"])
+def test_prologue_overlap_is_bitwise_neutral(ml100k, quirks):
+    """Throughput mode draws sweep s+1's hyperparameters at the end of sweep s,
+    their kernels ahead of the test evaluation and the host draws while it runs
+    (sbmf.cpp run_sweeps_T).  The chain must be the one without the overlap
+    (tune bit 26) bit for bit: across learn() calls of one sweep each (the
+    bench's pattern), with residual recomputes on some sweeps, with biases, with
+    hyper() reporting the sweep just run, and after set_factors (which drops the
+    hyperparameters drawn ahead)."""
+    tr, te = ml100k
+    kw = dict(num_factor=20, seed=2015, rng="philox", quirks=quirks, recompute_every=3)
+    A = FMLearnSBPMF(**kw)
+    A.set_data(Data(*tr), Data(*te))
+    B = FMLearnSBPMF(tune=1 << 26, **kw)
+    B.set_data(Data(*tr), Data(*te))
+    for _ in range(5):
+        A.learn(sweeps=1)
+    B.learn(sweeps=5)
+    np.testing.assert_array_equal(A.rmse_trajectory, B.rmse_trajectory)
+    ha, hb = A.hyper(), B.hyper()
+    for k in ha:
+        np.testing.assert_array_equal(np.asarray(ha[k]), np.asarray(hb[k]))
+    U, V = A.factors()
+    for L in (A, B):
+        L.set_factors(U * 0.5, V)
+        L.learn(sweeps=2)
+    np.testing.assert_array_equal(A.rmse_trajectory, B.rmse_trajectory)
+    Ua, Va = A.factors()
+    Ub, Vb = B.factors()
+    np.testing.assert_array_equal(Ua, Ub)
+    np.testing.assert_array_equal(Va, Vb)
