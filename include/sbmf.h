@@ -140,10 +140,7 @@ typedef struct sbmf_config {
                                           statistics, host draws) with the test evaluation
                                           (Philox mode; the chain is the same either way),
                                  bit 27 = f64 item rows on 8-wave k_gres workgroups (default:
-                                          16-wave, as bit 17 does for both sides),
-                                 bit 28 = throughput mode: normals filled by a separate launch
-                                          (default: the Gram-block kernels draw their rows'
-                                          normals, the fill covers the streaming rows only)   */
+                                          16-wave, as bit 17 does for both sides)              */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

@@ -32,7 +32,7 @@ def main():
     for d in sorted(per):
         name = names[d]
         if "k_gstream" in name or "k_gres" in name:
-            side = "item" if re.search(r", 1>", name) else "user"
+            side = "item" if re.search(r"(k_gstream<\w+, \d+, \d+, \w+|k_gres<\w+, \d+), 1[,>]", name) else "user"
         if "k_test" in name:
             side = "user"
         k = key_of(name, side)

@@ -35,7 +35,7 @@ def key_of(name, order_side):
     m = re.search(r"k_gstream<(double|float), 8, 8, (true|false), (\d)>", name)
     if m:
         return ("item" if m.group(3) == "1" else "user") + "_half/gstream"
-    m = re.search(r"k_gres<(double|float), (\d+), (\d)>", name)  # the default streaming kernel
+    m = re.search(r"k_gres<(double|float), (\d+), (\d)(, (true|false))?>", name)  # the default streaming kernel
     if m:
         return ("item" if m.group(3) == "1" else "user") + "_half/gstream"
     # Gram-block bins are several launches each (one per waves-per-row group, and the
@@ -54,7 +54,7 @@ def main():
         for d in sorted(src):
             name, kb = src[d]
             if "k_gstream" in name or "k_gres" in name:  # a half's streaming launch precedes its gblock bins
-                side = "item" if re.search(r", 1>", name) else "user"
+                side = "item" if re.search(r"(k_gstream<\w+, \d+, \d+, \w+|k_gres<\w+, \d+), 1[,>]", name) else "user"
             if "k_test" in name:
                 side = "user"
             k = key_of(name, side)

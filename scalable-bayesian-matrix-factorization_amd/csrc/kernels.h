@@ -22,9 +22,6 @@ struct HalfArgs {
     const T* mu;           // [Kp] mean hyperparameter of this side (zero padded)
     uint32_t zrow;         // P: the partner table's zero row (ratings past a row's end point here)
     const T* zbuf;         // [R][K] N(0,1) variates of this half (host reference stream or launch_philox_fill)
-    int zgen;              // 1: the Gram-block kernels draw the row's Philox normals themselves
-                           // (throughput mode; the same (seed, row, sweep, tag, pair) stream as
-                           // launch_philox_fill, which then covers only the streaming rows)
     T tau;
     uint32_t K, Kp;
     int sd_is_var;         // quirk FINAL/SBPMF2: posterior variance used as stdev
@@ -203,9 +200,6 @@ hipError_t launch_sum_cols(const double* in, uint32_t nchunk, uint32_t width, do
 template <typename T>
 hipError_t launch_philox_fill(T* z, uint32_t K, uint32_t r0, uint32_t r1, uint64_t seed, uint32_t sweep, uint32_t tag,
                               hipStream_t st);
-template <typename T>
-hipError_t launch_philox_fill_rows(T* z, uint32_t K, const uint32_t* rows, uint32_t nrows, uint64_t seed,
-                                   uint32_t sweep, uint32_t tag, hipStream_t st);
 template <typename T>
 hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, double sd, uint64_t seed,
                               uint32_t tag, hipStream_t st);

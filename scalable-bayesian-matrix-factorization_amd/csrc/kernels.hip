@@ -506,16 +506,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     __shared__ T eS[NWAVE][V * 4];
     {  // per-half normals (host reference stream or launch_philox_fill)
         const uint32_t k0 = NW > 1 ? threadIdx.x : lane, kst = NW > 1 ? 64 * NW : 64;
-        if (a.zgen) {
-            for (uint32_t p = k0; 2 * p < Kp; p += kst) {
-                double z0 = 0.0, z1 = 0.0;
-                if (2 * p < K) philox_normal_pair(a.seed, row, a.sweep, a.tag, p, z0, z1);
-                zS[ws][2 * p] = (T)z0;
-                zS[ws][2 * p + 1] = 2 * p + 1 < K ? (T)z1 : T(0);
-            }
-        } else {
-            for (uint32_t k = k0; k < Kp; k += kst) zS[ws][k] = k < K ? a.zbuf[(size_t)row * K + k] : T(0);
-        }
+        for (uint32_t k = k0; k < Kp; k += kst) zS[ws][k] = k < K ? a.zbuf[(size_t)row * K + k] : T(0);
     }
     // ratings of this wave: vector v covers ratings q = (wr*V + v)*4 + rr;
     // slots past the row's end gather the partner table's zero row
@@ -1244,8 +1235,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 if (!a.e_from_dot) eL[x] = in ? a.E_this[beg + x] : T(0);
                 if (a.row_tr) rL[x] = in ? a.r_this[beg + x] : T(0);
             }
-            // per-half normals (the filled buffer: in-kernel Philox here costs spills) and old values
-            for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {
+            for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {  // per-half normals and old values of the row
                 zL[k] = k < K ? a.zbuf[(size_t)row * K + k] : T(0);
                 oL[k] = a.own[(size_t)row * Kp + k];  // padding columns are zero
             }
@@ -2026,22 +2016,6 @@ __global__ __launch_bounds__(256) void k_philox_fill(T* __restrict__ z, uint32_t
     if (2 * p + 1 < K) z[(size_t)row * K + 2 * p + 1] = (T)z1;
 }
 
-// The same normals for a list of rows (throughput mode with in-kernel normals
-// in the Gram-block kernels: only the streaming rows read the buffer).
-template <typename T>
-__global__ __launch_bounds__(256) void k_philox_fill_rows(T* __restrict__ z, uint32_t K, const uint32_t* __restrict__ rows,
-                                                          uint32_t nrows, uint64_t seed, uint32_t sweep, uint32_t tag) {
-    const uint32_t npair = (K + 1) / 2;
-    const uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t i = (uint32_t)(x / npair), p = (uint32_t)(x % npair);
-    if (i >= nrows) return;
-    const uint32_t row = rows[i];
-    double z0, z1;
-    philox_normal_pair(seed, row, sweep, tag, p, z0, z1);
-    z[(size_t)row * K + 2 * p] = (T)z0;
-    if (2 * p + 1 < K) z[(size_t)row * K + 2 * p + 1] = (T)z1;
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void k_init_philox(T* __restrict__ tab, uint32_t K, uint32_t Kp, uint32_t r0,
                                                       uint32_t r1, double sd, uint64_t seed, uint32_t tag) {
@@ -2437,15 +2411,6 @@ hipError_t launch_resid(const ResidTask* tasks, uint32_t ntask, const uint32_t* 
 }
 
 template <typename T>
-hipError_t launch_philox_fill_rows(T* z, uint32_t K, const uint32_t* rows, uint32_t nrows, uint64_t seed,
-                                   uint32_t sweep, uint32_t tag, hipStream_t st) {
-    if (nrows == 0) return hipSuccess;
-    const uint64_t n = (uint64_t)nrows * ((K + 1) / 2);
-    k_philox_fill_rows<T><<<(uint32_t)((n + 255) / 256), 256, 0, st>>>(z, K, rows, nrows, seed, sweep, tag);
-    return hipGetLastError();
-}
-
-template <typename T>
 hipError_t launch_colstats(const T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, const T* mu, double* out,
                            hipStream_t st) {
     if (r1 <= r0) return hipSuccess;
@@ -2554,8 +2519,6 @@ hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, h
                                         hipStream_t);                                                                \
     template hipError_t launch_philox_fill<T>(T*, uint32_t, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t,        \
                                               hipStream_t);                                                          \
-    template hipError_t launch_philox_fill_rows<T>(T*, uint32_t, const uint32_t*, uint32_t, uint64_t, uint32_t,     \
-                                                   uint32_t, hipStream_t);                                            \
     template hipError_t launch_colstats<T>(const T*, uint32_t, uint32_t, uint32_t, uint32_t, const T*, double*,     \
                                            hipStream_t);                                                             \
     template hipError_t launch_test<T>(const uint32_t*, const uint32_t*, const double*, uint64_t, uint64_t,         \

@@ -807,19 +807,6 @@ static void fill_z(sbmf_ctx* c, uint32_t R, DBuf& d) {
     HIPCHK(hipMemcpy(d.p, h, n * sizeof(T), hipMemcpyHostToDevice));
 }
 
-// Throughput mode: the Gram-block kernels draw a row's Philox normals themselves
-// (no z round trip through HBM for those rows) when the half has no
-// per-coordinate or Gram-route rows; the streaming rows still read the buffer,
-// filled for them alone (in-kernel draws cost k_gres spills).  Tune bit 28
-// keeps the whole-half fill.
-static bool zgen_side(const sbmf_ctx* c, const Side& s) {
-    if (c->cfg.rng_mode == SBMF_RNG_REFERENCE || (c->cfg.tune & 0x10000000u)) return false;
-    if (!s.gitems.empty()) return false;
-    for (int k = KIND_RK0; k < NBIN; ++k)
-        if (!s.bin_rows[k].empty()) return false;
-    return true;
-}
-
 template <typename T>
 static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     HalfArgs<T> a{};
@@ -870,7 +857,6 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     // tune bit 1: residuals from r - own.partner (the former multi-GPU form, kept for validation);
     // otherwise every rank reads the residuals the exchange delivered
     a.e_from_dot = (c->cfg.tune & 2u) ? 1 : 0;
-    a.zgen = zgen_side(c, users ? c->users : c->items) ? 1 : 0;
     return a;
 }
 
@@ -1134,11 +1120,8 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         }
         HIPCHK(hipEventRecord(c->ev[1], st));
         // ---- 3. user half-sweep (throughput mode: this half's normals first)
-        if (!ref && !zgen_side(c, c->users))
+        if (!ref)
             HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep, TAG_USERS, st));
-        else if (!ref)  // the streaming rows' normals only
-            HIPCHK(launch_philox_fill_rows<T>(c->d_zU.as<T>(), K, c->d_bins_u[KIND_STREAM].as<uint32_t>(),
-                                              (uint32_t)c->users.bin_rows[KIND_STREAM].size(), cf.seed, c->sweep, TAG_USERS, st));
         if (c->bias)  // per-user bias hyperparameters + b_i draw + residual shift (:470-489, :515-530)
             HIPCHK(launch_bias_rows<T>(c->d_uptr.as<uint32_t>(), c->users.r0, c->users.r1, c->d_Eu.as<T>(),
                                        c->d_bu.as<double>(), c->d_mbu.as<double>(), c->d_sbu.as<double>(),
@@ -1152,11 +1135,8 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             });
         HIPCHK(hipEventRecord(c->ev[3], st));
         // ---- 4. item half-sweep
-        if (!ref && !zgen_side(c, c->items))
+        if (!ref)
             HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep, TAG_ITEMS, st));
-        else if (!ref)  // the streaming rows' normals only
-            HIPCHK(launch_philox_fill_rows<T>(c->d_zV.as<T>(), K, c->d_bins_v[KIND_STREAM].as<uint32_t>(),
-                                              (uint32_t)c->items.bin_rows[KIND_STREAM].size(), cf.seed, c->sweep, TAG_ITEMS, st));
         if (c->bias)  // per-item (:492-511, :563-578)
             HIPCHK(launch_bias_rows<T>(c->d_vptr.as<uint32_t>(), c->items.r0, c->items.r1, c->d_Ev.as<T>(),
                                        c->d_bv.as<double>(), c->d_mbv.as<double>(), c->d_sbv.as<double>(),
