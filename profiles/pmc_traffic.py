@@ -48,23 +48,29 @@ def main():
     fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
     write = per_dispatch(sys.argv[2], "WRITE_SIZE")
     out_path = sys.argv[3] if len(sys.argv) > 3 else None
+    # a half's streaming rows may take two launches (f64 items: 8-wave tasks for rows up
+    # to 1024 ratings, 16-wave ones above): a key's bytes are summed per sweep (sweeps
+    # end at k_test) and averaged over the sweeps
     acc = {}
     for src, scale, field in ((fetch, 2.0, "fetch"), (write, 1.0, "write")):
         side = "user"
+        sweep = 0
         for d in sorted(src):
             name, kb = src[d]
             if "k_gstream" in name or "k_gres" in name:  # a half's streaming launch precedes its gblock bins
                 side = "item" if re.search(r"(k_gstream<\w+, \d+, \d+, \w+|k_gres<\w+, \d+), 1[,>]", name) else "user"
             if "k_test" in name:
                 side = "user"
+                sweep += 1
             k = key_of(name, side)
             if k is None:
                 continue
-            acc.setdefault(k, defaultdict(list))[field].append(kb * 1024.0 * scale)
+            per = acc.setdefault(k, {"fetch": defaultdict(float), "write": defaultdict(float)})[field]
+            per[sweep] += kb * 1024.0 * scale
     res = {}
     for k, v in acc.items():
-        f = sum(v["fetch"]) / max(1, len(v["fetch"]))
-        w = sum(v["write"]) / max(1, len(v["write"]))
+        f = sum(v["fetch"].values()) / max(1, len(v["fetch"]))
+        w = sum(v["write"].values()) / max(1, len(v["write"]))
         res[k] = f + w
     res["_note"] = ("bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (kB x 1024), averaged over the profiled "
                     "sweeps; x2 per MI355X_MICROARCH.md gfx950 note, checked for these 8 B/lane gathers on "

@@ -414,22 +414,31 @@ static void prepare_T(sbmf_ctx* c) {
         HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, cf.device));
         // hybrid schedule (tune bits 8/9/10): rows up to 1024 / 4096 / 128 (tests)
         // ratings in k_gres, longer ones in k_gstream's LDS-staged tasks
-        const uint32_t hyb = (cf.tune & 256u) ? 1024u : (cf.tune & 512u) ? 4096u : (cf.tune & 1024u) ? 128u : 0u;
-        const uint32_t tunes[2] = {cf.tune, cf.tune | 64u};
+        // tune bits 29/30: rows above 2048 / 1024 ratings on 16-wave k_gres workgroups,
+        // the rest on 8-wave ones (both sides), as two launches
+        const uint32_t hyb16 = (cf.tune & 0x20000000u) ? 2048u : (cf.tune & 0x40000000u) ? 1024u : 0u;
+        const uint32_t hyb = hyb16 ? hyb16
+                                   : (cf.tune & 256u) ? 1024u : (cf.tune & 512u) ? 4096u : (cf.tune & 1024u) ? 128u : 0u;
+        const uint32_t tunes[2] = {hyb16 ? cf.tune & ~0x20000u : cf.tune, hyb16 ? cf.tune | 0x20000u : cf.tune | 64u};
         for (Side* sd : {&c->users, &c->items}) {
+            // f64 item rows above 1024 ratings (75 % of the item ratings sit in rows
+            // split over several tasks) on 16-wave k_gres workgroups, 2048-rating
+            // tasks: half the chunks per split row, a quarter of the all-read
+            // exchange; shorter item rows and every user row on 8-wave workgroups
+            // (two independent tasks per CU).  Measured item launch 4.04 ms (all
+            // 8-wave) / 3.88 (all 16-wave) / 3.70 (this split); the user side is
+            // slower with any 16-wave share (1.59 / 2.23 / 1.66 ms).  Tune bit 27,
+            // or an explicit workgroup-shape or hybrid bit, keeps 8-wave items.
+            const bool item16 = sd == &c->items && sizeof(T) == 8 && !hyb &&
+                                !(cf.tune & (64u | 128u | 0x20000u | 0x2000000u | 0x8000000u));
+            const uint32_t shyb = item16 ? 1024u : hyb;
+            const uint32_t stunes[2] = {tunes[0], item16 ? cf.tune | 0x20000u : tunes[1]};
             std::vector<uint32_t> rows[2];
             for (uint32_t r : sd->bin_rows[KIND_STREAM])  // degree-descending
-                rows[hyb && sd->ptr[r + 1] - sd->ptr[r] > hyb ? 1 : 0].push_back(r);
-            // f64 item rows (the long ones: 80 % of item ratings sit in rows split over
-            // several tasks) on 16-wave k_gres workgroups, 2048-rating tasks: half the
-            // chunks per row, a quarter of the all-read exchange (measured 4.04 -> 3.88
-            // ms; the user side stays on 8-wave workgroups, 1.59 vs 2.23 ms there).
-            // Tune bit 27, or an explicit workgroup-shape bit, keeps 8-wave items.
-            const bool item16 = sd == &c->items && sizeof(T) == 8 &&
-                                !(cf.tune & (64u | 128u | 0x20000u | 0x2000000u | 0x8000000u));
+                rows[shyb && sd->ptr[r + 1] - sd->ptr[r] > shyb ? 1 : 0].push_back(r);
             for (int k = 0; k < 2; ++k) {
                 Side::StreamSet& S = sd->ss[k];
-                S.tune = k == 0 && item16 ? (tunes[k] | 0x20000u) : tunes[k];
+                S.tune = stunes[k];
                 // task capacity: the kernel's on-chip maximum, or smaller if split_chunk asks
                 S.cmax = gstream_cmax<T>(S.tune);
                 if (cf.split_chunk) S.cmax = std::min(S.cmax, std::max(cf.split_chunk, 1u));

@@ -122,7 +122,7 @@ def test_split_rows_match_oracle(ml100k, chunk, K):
 
 
 @pytest.mark.parametrize("tune", [0, 1, 4, 8, 13, 64, 65, 96, 97, 128, 1024, 1024 + 128, 65536, 65536 + 128, 65536 + 1024, 131072,
-                                  1 << 20, 1 << 21, (1 << 20) + 4, 1 << 24, 1 << 25])
+                                  1 << 20, 1 << 21, (1 << 20) + 4, 1 << 24, 1 << 25, 1 << 29])
 def test_kernel_variants_match_oracle(ml100k, tune):
     """Kernel variants (sbmf_config.tune): block solve by one wave that hands D
     over in LDS (default, bit 0 clear) or by every wave of a row (bit 0 set);
