@@ -568,8 +568,8 @@ void fmm_factors(FMLearner* L, double* U, double* V) {
     for (uint32_t f = 0; f < L->K; ++f) {
         if (U)
             for (uint32_t a = 0; a < L->I; ++a) U[(size_t)a * L->K + f] = h[(size_t)f * L->p + a];
-        if (V)
-            for (uint32_t a = 0; a < L->J; ++a) V[(size_t)a * L->K + f] = h[(size_t)f * L->p + L->I + a];
+        if (V)  // items past libFM's attribute count (sbmf_set_dims with trailing unrated ids) have no factors: 0
+            for (uint32_t a = 0; a < L->J; ++a) V[(size_t)a * L->K + f] = a < L->RI ? h[(size_t)f * L->p + L->I + a] : 0.0;
     }
 }
 void fmm_biases(FMLearner* L, double* bu, double* bv, double* b0) {
@@ -577,7 +577,11 @@ void fmm_biases(FMLearner* L, double* bu, double* bv, double* b0) {
     std::vector<double> h(L->p);
     HIPCHK(hipMemcpy(h.data(), L->d_w.p, h.size() * sizeof(double), hipMemcpyDeviceToHost));
     if (bu) std::copy(h.begin(), h.begin() + L->I, bu);
-    if (bv) std::copy(h.begin() + L->I, h.begin() + L->I + L->J, bv);
+    if (bv) {  // as fmm_factors: items past the attribute count read 0
+        const uint32_t nj = std::min(L->J, L->RI);
+        std::copy(h.begin() + L->I, h.begin() + L->I + nj, bv);
+        std::fill(bv + nj, bv + L->J, 0.0);
+    }
     if (b0) *b0 = L->w0;
 }
 // [v_lambda (K) | v_mu (K) | w_lambda, w_mu, 0... (K) | 0 (K)] and alpha

@@ -263,6 +263,7 @@ struct sbmf_ctx {
     DBuf d_colpart, d_res, d_scratch;
 
     bool kprof = false; // SBMF_KPROF=1: streaming-kernel phase cycles printed per sweep
+    int kprof_set = 0;  // SBMF_KPROF_SET: which streaming launch of a half is stamped (0: the 8-wave one)
     DBuf d_kprof;
     DBuf d_stasks[2][2], d_xrows[2][2];  // [side][stream set]
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
@@ -618,6 +619,7 @@ static void prepare_T(sbmf_ctx* c) {
     HIPCHK(hipStreamSynchronize(st));
     c->kprof = std::getenv("SBMF_KPROF") && std::atoi(std::getenv("SBMF_KPROF")) > 0;
     if (c->kprof) {
+        if (const char* e = std::getenv("SBMF_KPROF_SET")) c->kprof_set = std::atoi(e) ? 1 : 0;
         c->d_kprof.alloc(96 * sizeof(unsigned long long));
         HIPCHK(hipMemset(c->d_kprof.p, 0, 96 * sizeof(unsigned long long)));
     }
@@ -908,7 +910,7 @@ static void run_half(sbmf_ctx* c, bool users) {
                 sy.newown = c->d_xnewown.p;
                 sy.timeout = c->d_xtimeout.as<uint32_t>();
                 sy.cmax = S.cmax;
-                sy.prof = c->kprof && set == 0 ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
+                sy.prof = c->kprof && set == c->kprof_set ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
                 HalfArgs<T> as = a;
                 as.tune = S.tune;
                 HIPCHK(launch_gstream<T>(c->d_stasks[sd][set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
@@ -1238,10 +1240,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 for (int k = 0; k < 7; ++k) tot += (double)h[8 * sd + k];
                 if (tot == 0) continue;
                 std::fprintf(stderr, "[kprof] sweep %u %s %s (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep,
-                             (cf.tune & 64u) ? "gstream" : "gres", sd ? "items" : "users", S.ss[0].sgrid,
-                             S.ss[0].stasks.size());
+                             (cf.tune & 64u) ? "gstream" : "gres", sd ? "items" : "users", S.ss[c->kprof_set].sgrid,
+                             S.ss[c->kprof_set].stasks.size());
                 for (int k = 0; k < 7; ++k)
-                    std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.ss[0].sgrid / 1e6,
+                    std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.ss[c->kprof_set].sgrid / 1e6,
                                  100.0 * (double)h[8 * sd + k] / tot);
                 std::fprintf(stderr, "\n");
                 if (cf.tune & 64u) continue;

@@ -12,6 +12,7 @@
 // prediction per test line (libfm.cpp:629-634).
 // Differences, by design: -seed is honoured (libfm.cpp:124 ignores it); on
 // error the exit code is 1 (the reference prints "ERROR" and returns 0).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +20,7 @@
 #include <fstream>
 #include <iomanip>
 #include <iostream>
+#include <limits>
 #include <map>
 #include <sstream>
 #include <stdexcept>
@@ -140,12 +142,112 @@ void load(const std::string& path, const std::string& fmt, uint32_t item_offset,
 struct RunState {
     std::string rmse_file;
     bool vb = false;  // online VB prints "#Iter=..\tTest=.." (fm_learn_vb_online_simultaneous.h:447)
+    bool lfm = false;  // libFM's fm_learn_mcmc chain: one attribute group with w (fm_learn_mcmc.h:1140-1149)
+    bool k1 = false;   // -dim k1: libFM logs wmu / wlambda (fm_learn_mcmc.h:422-431)
+    bool avg_collected = false;  // the running mean divides by the collected sweeps
+    uint32_t K = 0, ncol = 0;
+    sbmf_ctx* ctx = nullptr;
+    const sbmf_ratings* test = nullptr;
+    double lo = 1.0, hi = 5.0;  // clamp of the running-mean prediction (min/max train target)
+    std::vector<double> pred, sum4;  // this sweep's running mean; the prediction sums after sweep 4
     std::ofstream* rlog = nullptr;
     int verbosity = 0;
 };
 
+// -rlog: libFM's RLog columns (rlog.h:47-90) in its field order -- fm_learn::init
+// (fm_learn.h:82-127), then fm_learn_mcmc::init (fm_learn_mcmc.h:1120-1149) or
+// fm_learn_vb_online::init (fm_learn_vb_online.h:944-970) -- written with the
+// default stream precision; fields a learner never logs print libFM's default
+// (nan).  The SBPMF sampler has two hyperprior groups (users g=0, items g=1),
+// which libFM would log as vmu[g,f] / vlambda[g,f] of two attribute groups.
+// Our own columns follow at full precision, named sbmf_*.
+void rlog_header(std::ostream& o, const RunState& rs) {
+    o << "rmse\tmae\ttime_pred\ttime_learn\ttime_learn2\ttime_learn4\talpha\trmse_mcmc_this\trmse_mcmc_all";
+    if (!rs.vb) o << "\trmse_mcmc_all_but5";
+    const int ng = (rs.lfm || rs.vb) ? 1 : 2;
+    for (int g = 0; g < ng; ++g) {
+        o << "\twmu[" << g << "]\twlambda[" << g << "]";
+        for (uint32_t f = 0; f < rs.K; ++f) o << "\tvmu[" << g << "," << f << "]\tvlambda[" << g << "," << f << "]";
+    }
+    o << "\tsbmf_iter\tsbmf_rmse_all\tsbmf_rmse_this\tsbmf_rmse_train\tsbmf_tau\tsbmf_ms_sweep\tsbmf_ms_eval\n";
+}
+
+// rmse / mae of clamp(sum * norm) against the test targets (fm_learn_mcmc_simultaneous.h:307-324)
+void eval_sums(const RunState& rs, const std::vector<double>& sum, double norm, double& rmse, double& mae) {
+    double se = 0.0, ae = 0.0;
+    const uint64_t n = rs.test->n;
+    for (uint64_t t = 0; t < n; ++t) {
+        double p = sum[t] * norm;
+        p = std::min(rs.hi, p);
+        p = std::max(rs.lo, p);
+        const double err = p - rs.test->rating[t];
+        se += err * err;
+        ae += std::abs(err);
+    }
+    rmse = std::sqrt(se / (double)n);
+    mae = ae / (double)n;
+}
+
+void rlog_line(const sbmf_sweep_info* in, RunState& rs) {
+    std::ostream& o = *rs.rlog;
+    const double nan = std::numeric_limits<double>::quiet_NaN();
+    const uint64_t n = rs.test ? rs.test->n : 0;
+    double mae = nan, rmse_but5 = nan;
+    if (n && !rs.vb) {
+        // the running mean this sweep (clamped sums / divisor); its divisor gives the sums back
+        rs.pred.resize(n);
+        if (sbmf_predict(rs.ctx, rs.pred.data()) != SBMF_OK) throw std::runtime_error(sbmf_last_error(rs.ctx));
+        const double div = rs.avg_collected ? (double)std::max(1u, rs.ncol) : (double)in->sweep + 1;
+        std::vector<double> sum(n);
+        for (uint64_t t = 0; t < n; ++t) sum[t] = rs.pred[t] * div;
+        double r;
+        eval_sums(rs, sum, 1.0 / div, r, mae);
+        // all_but5 sums the sweeps from 5 on; libFM's normalizer 1.0/(i-5+1) is an unsigned
+        // expression, so sweeps 0-3 divide by ~2^32 and sweep 4 by 0 (clamping 0 / NaN to the bounds)
+        const uint32_t i = in->sweep;
+        if (i == 4) rs.sum4 = sum;
+        std::vector<double> but5(n, 0.0);
+        if (i >= 5)
+            for (uint64_t t = 0; t < n; ++t) but5[t] = sum[t] - rs.sum4[t];
+        const double norm = 1.0 / (double)(uint32_t)(i - 5 + 1);
+        if (i == 4) {
+            std::fill(but5.begin(), but5.end(), std::numeric_limits<double>::quiet_NaN());
+            eval_sums(rs, but5, 1.0, rmse_but5, r);
+        } else {
+            eval_sums(rs, but5, norm, rmse_but5, r);
+        }
+    }
+    const double tl = in->ms_sweep / 1000.0;
+    // online VB logs time_learn* and rmse_mcmc_this only (fm_learn_vb_online_simultaneous.h:436-450)
+    o << (rs.vb ? nan : in->rmse_avg) << "\t" << mae << "\t" << nan << "\t" << tl << "\t" << tl << "\t" << tl << "\t";
+    std::vector<double> h(4 * (size_t)rs.K, nan);
+    double alpha = nan;
+    if (!rs.vb && sbmf_get_hyper(rs.ctx, h.data(), &alpha) != SBMF_OK) throw std::runtime_error(sbmf_last_error(rs.ctx));
+    o << (rs.vb ? nan : alpha) << "\t" << in->rmse_this << "\t" << (rs.vb ? nan : in->rmse_avg);
+    if (!rs.vb) o << "\t" << rmse_but5;
+    const uint32_t K = rs.K;
+    if (rs.vb) {
+        o << "\t" << nan << "\t" << nan;
+        for (uint32_t f = 0; f < K; ++f) o << "\t" << nan << "\t" << nan;
+    } else if (rs.lfm) {  // sbmf_get_hyper: [v_lambda | v_mu | w_lambda, w_mu | 0]
+        o << "\t" << (rs.k1 ? h[2 * K + (K > 1 ? 1 : 0)] : nan) << "\t" << (rs.k1 ? h[2 * K] : nan);
+        for (uint32_t f = 0; f < K; ++f) o << "\t" << h[K + f] << "\t" << h[f];
+    } else {  // [sigma_u | mu_u | sigma_v | mu_v]: users g=0, items g=1
+        for (int g = 0; g < 2; ++g) {
+            o << "\t" << nan << "\t" << nan;
+            for (uint32_t f = 0; f < K; ++f) o << "\t" << h[(2 * g + 1) * K + f] << "\t" << h[2 * g * K + f];
+        }
+    }
+    const std::streamsize pr = o.precision(17);
+    o << "\t" << in->sweep << "\t" << in->rmse_avg << "\t" << in->rmse_this << "\t" << in->rmse_train << "\t" << in->tau
+      << "\t" << in->ms_sweep << "\t" << in->ms_eval << "\n";
+    o.precision(pr);
+    o.flush();
+}
+
 int on_sweep(const sbmf_sweep_info* in, void* user) {
     RunState* rs = static_cast<RunState*>(user);
+    if (in->collected) rs->ncol++;
     if (rs->vb)
         std::cout << "#Iter=" << std::setw(3) << in->sweep << "\tTest=" << in->rmse_avg << std::endl;
     else
@@ -153,9 +255,7 @@ int on_sweep(const sbmf_sweep_info* in, void* user) {
                   << std::endl;
     std::ofstream f(rs->rmse_file, std::ios_base::app);
     f << in->rmse_avg << "\n";
-    if (rs->rlog)
-        *rs->rlog << in->sweep << "\t" << in->rmse_avg << "\t" << in->rmse_this << "\t" << in->rmse_train << "\t"
-                  << in->tau << "\t" << in->ms_sweep << "\t" << in->ms_eval << "\n";
+    if (rs->rlog) rlog_line(in, *rs);
     if (rs->verbosity > 0)
         std::cout << "  tau=" << in->tau << " sweep_ms=" << in->ms_sweep << " eval_ms=" << in->ms_eval << std::endl;
     return 0;
@@ -186,8 +286,9 @@ int main(int argc, char** argv) {
         cl.reg("method", "learning method: mcmc (SBPMF Gibbs; with -order libfm libFM's own MCMC chain) | "
                          "als (libFM's ALS) | vb (online variational Bayes, libFM's vb_online; alias vb_online); "
                          "default=mcmc");
-        cl.reg("order", "-method mcmc: sbpmf (the SBPMF sampler, default) | libfm (libFM's fm_learn_mcmc chain: "
-                        "f-outer, one hyperprior group, w0 / w per -dim k0,k1, sqrt(variance) stdev)");
+        cl.reg("order", "-method mcmc: libfm (libFM's fm_learn_mcmc chain: f-outer, one hyperprior group, w0 / w "
+                        "per -dim k0,k1, sqrt(variance) stdev; default on libFM text / binary input, as bin/libFM) | "
+                        "sbpmf (the SBPMF sampler of gibbs_sbpmf_final.cpp; default on SBPMF triple input)");
         cl.reg("verbosity", "how much infos to print; default=0");
         cl.reg("rlog", "write per-sweep measurements to a TSV file; default=''");
         cl.reg("seed", "integer seed; default=1 (glibc default seed of the reference samplers)");
@@ -219,10 +320,21 @@ int main(int argc, char** argv) {
         if (task != "r") throw std::runtime_error("only -task r (regression) is supported by the SBPMF sampler");
         const std::string method = cl.get("method", "mcmc");
         const bool vb = method == "vb" || method == "vb_online";
-        const std::string order = cl.get("order", "sbpmf");
+        const std::string fmt = cl.get("format", "auto");
+        if (fmt != "auto" && fmt != "triple" && fmt != "libfm" && fmt != "binary")
+            throw std::runtime_error("unknown -format " + fmt);
+        // bin/libFM -method mcmc runs fm_learn_mcmc on libFM data (libfm.cpp:411-419); the SBPMF
+        // sampler reads the triple files of gibbs_sbpmf_final.cpp:43
+        const std::string trainf = cl.get("train", "");
+        const bool libfm_input = fmt == "libfm" || fmt == "binary" ||
+                                 (fmt == "auto" && (has_binary(trainf) || looks_libfm(trainf)));
+        const std::string order = cl.get("order", libfm_input ? "libfm" : "sbpmf");
         if (order != "sbpmf" && order != "libfm") throw std::runtime_error("unknown -order " + order);
         const bool als = method == "als";
-        const bool lfm = als || (method == "mcmc" && order == "libfm");  // libFM's fm_learn_mcmc learner
+        const std::string q = cl.get("quirks", "final");
+        const bool biased = q == "bias2" || q == "bias22";
+        // libFM's fm_learn_mcmc learner; -quirks (the SBPMF samplers' variants) selects the SBPMF sampler
+        const bool lfm = als || (method == "mcmc" && order == "libfm" && !(cl.has("quirks") && !cl.has("order")));
         if (method != "mcmc" && !vb && !als)
             throw std::runtime_error("-method " + method + " is not supported (use mcmc, als or vb)");
         if (!cl.has("train") || !cl.has("test")) throw std::runtime_error("-train and -test are mandatory");
@@ -231,12 +343,11 @@ int main(int argc, char** argv) {
         if (dim[2] <= 0 || dim[2] > 256) throw std::runtime_error("dim k2 must be in [1,256]");
         if (vb && !(dim[0] == 1 && dim[1] == 1))
             throw std::runtime_error("the online VB learner updates w0 and the user/item w: use -dim '1,1,K'");
-        const std::string q = cl.get("quirks", "final");
-        const bool biased = q == "bias2" || q == "bias22";
         if (lfm && biased) throw std::runtime_error("-quirks bias2|bias22 selects the SBPMF biased sampler, not libFM's");
-        if (!vb && !lfm && !biased && (dim[0] || dim[1]))
-            std::cout << "note: bias terms (k0,k1) are not sampled; the reference SBPMF sampler has them compiled "
-                         "out (gibbs_sbpmf_final.cpp:276-295); -quirks bias2|bias22 selects the biased sampler"
+        if (!vb && !lfm && !biased && (dim[0] || dim[1]))  // stdout stays libFM's
+            std::cerr << "note: -order sbpmf: bias terms (k0,k1) are not sampled; the reference SBPMF sampler has "
+                         "them compiled out (gibbs_sbpmf_final.cpp:276-295); -quirks bias2|bias22 selects the biased "
+                         "sampler, -order libfm libFM's own chain"
                       << std::endl;
         if (biased && !(dim[0] == 1 && dim[1] == 1))
             throw std::runtime_error("the biased sampler (gibbs_sbpmf2.cpp) samples b0 and the user/item biases: "
@@ -295,7 +406,6 @@ int main(int argc, char** argv) {
         }
         cfg.eval_test = 1;
 
-        const std::string fmt = cl.get("format", "auto");
         const uint32_t off = (uint32_t)cl.getl("item_offset", 0);
         std::cout << "Loading train...\t" << std::endl;
         sbmf_ratings tr{}, te{};
@@ -326,12 +436,27 @@ int main(int argc, char** argv) {
         // libFM names the file after "mcmc" for als too (the als switch rewrites -method, libfm.cpp:133)
         rs.rmse_file = "test_rmse_" + nm.str() + "_" + (vb ? std::string("vb_online") : std::string("mcmc"));
         rs.vb = vb;
+        rs.lfm = lfm;
+        rs.k1 = dim[1] != 0;
+        rs.K = cfg.num_factor;
+        rs.ctx = ctx;
+        rs.test = &te;
+        rs.avg_collected = !lfm && (cfg.average == 1 || (cfg.average == 0 && cfg.quirks == SBMF_QUIRKS_NONE));  // sbmf.cpp avg_collected
+        if (lfm) {  // libFM clamps to the train target range (libfm.cpp:459-460)
+            rs.lo = *std::min_element(tr.rating, tr.rating + tr.n);
+            rs.hi = *std::max_element(tr.rating, tr.rating + tr.n);
+        } else {
+            rs.lo = cfg.clamp_lo >= 0 ? cfg.clamp_lo
+                                      : (cfg.quirks == SBMF_QUIRKS_SBPMF2 || cfg.quirks == SBMF_QUIRKS_BIAS2 ? 0.5 : 1.0);
+            rs.hi = cfg.clamp_hi;
+        }
         { std::ofstream trunc(rs.rmse_file); }
         std::ofstream rlog;
         if (cl.has("rlog") && !cl.get("rlog", "").empty()) {
             rlog.open(cl.get("rlog", ""));
-            rlog.precision(17);  // our own diagnostic file: full precision (the libFM outputs keep the default 6)
-            rlog << "iter\trmse\trmse_this\trmse_train\ttau\tms_sweep\tms_eval\n";
+            if (!rlog.is_open()) throw std::runtime_error("Unable to open file " + cl.get("rlog", ""));
+            std::cout << "logging to " << cl.get("rlog", "") << std::endl;
+            rlog_header(rlog, rs);
             rs.rlog = &rlog;
         }
         rs.verbosity = (int)cl.getl("verbosity", 0);

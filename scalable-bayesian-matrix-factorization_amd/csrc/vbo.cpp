@@ -73,6 +73,7 @@ struct VBLearner {
     // device
     DBuf d_mu_v, d_sg_v, d_nm_v, d_ns_v, d_mu_w, d_sg_w, d_nm_w, d_ns_w, d_rho_w, d_rho_v, d_t_w, d_t_v, d_cc;
     DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_ETu, d_ETv, d_part;
+    size_t part_cap = 0;  // doubles in d_part
     DBuf d_tu, d_ti, d_tr, d_pred, d_tpart;
     VBTables tb{};
     // several ranks
@@ -214,7 +215,8 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
         d_send.alloc((size_t)(K + 2) * sizeof(double));
         d_recv.alloc((size_t)R * (K + 2) * sizeof(double));
     }
-    d_part.alloc(vbo_scratch_doubles(S, K, p) * sizeof(double));
+    part_cap = vbo_scratch_doubles(S, K, p);
+    d_part.alloc(part_cap * sizeof(double));
     upload(d_tu, su, st);
     upload(d_ti, si, st);
     upload(d_tr, sr, st);
@@ -567,9 +569,9 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
                     HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st));
             }
             if (R > 1) {  // the blends from every rank's alpha sum and user-range sig sums
-                HIPCHK(vbo_hyper_local(ETu + L.bbase[b], B, tb, u0, u1, part, d_send.as<double>(), st));
+                HIPCHK(vbo_hyper_local(ETu + L.bbase[b], B, tb, u0, u1, part, part_cap, d_send.as<double>(), st));
                 comm->allgather(d_send.p, (K + 2) * sizeof(double), d_recv.p, st);
-                HIPCHK(vbo_hyper_final(d_recv.as<double>(), R, L.gbsize[b], tb, I, part, st));
+                HIPCHK(vbo_hyper_final(d_recv.as<double>(), R, L.gbsize[b], tb, I, part, part_cap, st));
             } else {
                 HIPCHK(vbo_hyper(ETu + L.bbase[b], B, tb, part, st));
             }

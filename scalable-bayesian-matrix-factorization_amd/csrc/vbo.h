@@ -13,6 +13,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "../../include/sbmf.h"
@@ -86,9 +87,9 @@ hipError_t vbo_w0_final(const double* recv, int R, uint32_t B, const VBTables& t
 // several ranks: out = [alpha's local sum | K + 1 sig sums over the users [u0, u1)],
 // then the blends from every rank's (recv [R][K + 2]) plus the item range [I, p)
 hipError_t vbo_hyper_local(const double2* ET, uint32_t B, const VBTables& tb, uint32_t u0, uint32_t u1, double* part,
-                           double* out, hipStream_t st);
+                           size_t part_cap, double* out, hipStream_t st);
 hipError_t vbo_hyper_final(const double* recv, int R, uint32_t B, const VBTables& tb, uint32_t I, double* part,
-                           hipStream_t st);
+                           size_t part_cap, hipStream_t st);
 // step sizes of update_v (:447-453) and the hyperparameter blends (:523-580)
 hipError_t vbo_hyper(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
 // test predictions clamped to [lo, hi] and their squared errors per 256-case block
@@ -113,9 +114,17 @@ void vbo_hyper_out(VBLearner* L, double* h4k, double* alpha);  // [sigma_v | 0 |
 double vbo_layout_ms(const VBLearner* L);  // host time of the last epoch's shuffle + batch layout
 uint32_t vbo_launches(const VBLearner* L);
 
-// scratch doubles vbo_update_w0 / vbo_hyper need for B cases
+// scratch doubles vbo_update_w0 / vbo_hyper (one rank) and vbo_hyper_local /
+// vbo_hyper_final (several ranks) need for B cases:
+//   vbo_hyper:       [alpha partials nab | 8 | sig partials (K+1) x nchunk(p)]
+//   vbo_hyper_final: [item sums K+1 | 7 | sig partials (K+1) x nchunk(p-I) | 8 | combined K+2]
+inline size_t vbo_hyper_final_doubles(uint32_t K, uint32_t nchunk) {
+    return (size_t)K + 8 + (size_t)(K + 1) * nchunk + 8 + (K + 2);
+}
 inline size_t vbo_scratch_doubles(uint32_t B, uint32_t K, uint32_t p) {
-    return (size_t)(B + 1023) / 1024 + 16 + (size_t)(K + 1) * ((p + 2047) / 2048 + 1);
+    const uint32_t nc = std::max(1u, (p + 2047) / 2048);
+    const size_t one = (size_t)(B + 1023) / 1024 + 16 + (size_t)(K + 1) * (nc + 1);
+    return std::max(one, vbo_hyper_final_doubles(K, nc));
 }
 
 }  // namespace sbmf

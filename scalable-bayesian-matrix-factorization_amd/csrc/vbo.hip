@@ -676,9 +676,11 @@ hipError_t vbo_w0_final(const double* recv, int R, uint32_t B, const VBTables& t
     return hipGetLastError();
 }
 hipError_t vbo_hyper_local(const double2* ET, uint32_t B, const VBTables& tb, uint32_t u0, uint32_t u1, double* part,
-                           double* out, hipStream_t st) {
-    k_rho_v<<<(tb.p + 255) / 256, 256, 0, st>>>(tb);
+                           size_t part_cap, double* out, hipStream_t st) {
     const uint32_t nab = (B + 1023) / 1024;
+    if ((size_t)nab + 8 + (size_t)(tb.K + 1) * std::max(1u, (u1 - u0 + 2047) / 2048) > part_cap)
+        return hipErrorInvalidValue;  // scratch too small for this layout
+    k_rho_v<<<(tb.p + 255) / 256, 256, 0, st>>>(tb);
     if (B) {
         k_alpha_partial<<<nab, 256, 0, st>>>(ET, B, part);
         k_sum_fixed<<<1, 256, 0, st>>>(part, nab, out);
@@ -693,9 +695,10 @@ hipError_t vbo_hyper_local(const double2* ET, uint32_t B, const VBTables& tb, ui
     return hipGetLastError();
 }
 hipError_t vbo_hyper_final(const double* recv, int R, uint32_t B, const VBTables& tb, uint32_t I, double* part,
-                           hipStream_t st) {
+                           size_t part_cap, hipStream_t st) {
     // the item range's sums (replicated on every rank), then the combined totals
     const uint32_t nchunk = std::max(1u, (tb.p - I + 2047) / 2048);
+    if (vbo_hyper_final_doubles(tb.K, nchunk) > part_cap) return hipErrorInvalidValue;  // layout below
     double* items = part;
     double* spart = part + tb.K + 8;
     double* comb = spart + (size_t)(tb.K + 1) * nchunk + 8;

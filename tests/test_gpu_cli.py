@@ -46,9 +46,22 @@ def _cli(tmp_path, ml100k, *args):
     return r
 
 
-def _rlog(path):
-    rows = [l.split("\t") for l in open(path).read().splitlines()[1:]]
-    return np.array([float(x[1]) for x in rows])
+def _rlog(path, col="sbmf_rmse_all"):
+    lines = open(path).read().splitlines()
+    head = lines[0].split("\t")
+    return np.array([float(l.split("\t")[head.index(col)]) for l in lines[1:]])
+
+
+def _libfm_rlog_header(K, groups=1, but5=True):
+    """libFM's RLog field order for regression MCMC: fm_learn::init (fm_learn.h:82-127),
+    then fm_learn_mcmc::init (fm_learn_mcmc.h:1121-1148)."""
+    h = ["rmse", "mae", "time_pred", "time_learn", "time_learn2", "time_learn4", "alpha", "rmse_mcmc_this",
+         "rmse_mcmc_all"] + (["rmse_mcmc_all_but5"] if but5 else [])
+    for g in range(groups):
+        h += ["wmu[%d]" % g, "wlambda[%d]" % g]
+        for f in range(K):
+            h += ["vmu[%d,%d]" % (g, f), "vlambda[%d,%d]" % (g, f)]
+    return h
 
 
 def test_cli_mcmc_k20_matches_reference_golden(tmp_path, ml100k):
@@ -69,10 +82,20 @@ def test_cli_mcmc_k20_matches_reference_golden(tmp_path, ml100k):
     assert vals.shape == gold.shape
     assert _close6(vals, gold)
     assert np.abs(_rlog(tmp_path / "rlog.tsv") - gold).max() < 1e-6
+    # libFM's -rlog columns first (the SBPMF sampler's two hyperprior groups), ours after them
+    head = (tmp_path / "rlog.tsv").read_text().splitlines()[0].split("\t")
+    assert head[:len(_libfm_rlog_header(20, groups=2))] == _libfm_rlog_header(20, groups=2)
+    assert _close6(_rlog(tmp_path / "rlog.tsv", "rmse"), gold)
+    assert _close6(_rlog(tmp_path / "rlog.tsv", "rmse_mcmc_all"), gold)
+    tau = _rlog(tmp_path / "rlog.tsv", "sbmf_tau")
+    assert _close6(_rlog(tmp_path / "rlog.tsv", "alpha"), tau)
     o = oracle.run(*ml100k, K=20, iters=100, seed=1, want_factors=False)
     pred = np.array([float(x) for x in (tmp_path / "pred.txt").read_text().split()])
     assert pred.shape == (len(ml100k[1][0]),)
     assert _close6(pred, o["pred_sum"] / 100)
+    # mae of the running mean after the last sweep, from the same predictions
+    mae = _rlog(tmp_path / "rlog.tsv", "mae")
+    assert _close6(mae[-1], np.mean(np.abs(pred - ml100k[1][2])))
 
 
 def test_cli_truncates_rmse_file_and_runs_config1_k8(tmp_path, ml100k):
@@ -130,3 +153,31 @@ def test_cli_libfm_methods_reproduce_libfm_output(tmp_path, ml100k, method):
     assert np.abs(pred - ref_pred).max() <= 1.1e-5
     rm = np.loadtxt(tmp_path / "test_rmse_118_mcmc")
     assert len(rm) == 10 and abs(rm[-1] - float(gold_lines[-1].split("Test=")[1])) < 1e-5
+
+
+def test_cli_mcmc_on_libfm_input_is_libfms_chain(tmp_path, ml100k):
+    """`bin/libFM -method mcmc -dim 1,1,8` on libFM text runs fm_learn_mcmc (libfm.cpp:411-419):
+    without -order, sbmf does the same (no note on stdout), and -rlog carries libFM's
+    one-group field set with rmse_mcmc_all_but5 per fm_learn_mcmc_simultaneous.h:158-161,241."""
+    I = int(max(ml100k[0][0].max(), ml100k[1][0].max())) + 1
+    tr, te = tmp_path / "train.libfm", tmp_path / "test.libfm"
+    _write_libfm(tr, ml100k[0], I)
+    _write_libfm(te, ml100k[1], I)
+    cmd = [CLI_PATH, "-task", "r", "-train", str(tr), "-test", str(te), "-dim", "1,1,8", "-iter", "10",
+           "-method", "mcmc", "-seed", "1", "-item_offset", str(I), "-rlog", str(tmp_path / "rlog.tsv")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    assert "note" not in r.stdout
+    name = "ref_libfm_mcmc_ml100k_d118_s1_i10"
+    gold_lines = open(os.path.join(os.path.dirname(__file__), "golden", name + ".txt")).read().splitlines()
+    assert [l for l in r.stdout.splitlines() if l.startswith("#Iter")] == gold_lines
+    head = (tmp_path / "rlog.tsv").read_text().splitlines()[0].split("\t")
+    assert head[:len(_libfm_rlog_header(8))] == _libfm_rlog_header(8)
+    b5 = _rlog(tmp_path / "rlog.tsv", "rmse_mcmc_all_but5")
+    allr = _rlog(tmp_path / "rlog.tsv", "rmse_mcmc_all")
+    assert np.all(np.isfinite(b5)) and b5[5] == pytest.approx(_rlog(tmp_path / "rlog.tsv", "rmse_mcmc_this")[5], abs=1e-5)
+    assert abs(allr[-1] - float(gold_lines[-1].split("Test=")[1])) < 1e-5
+    # the explicit SBPMF order on the same file keeps its note off stdout
+    r2 = subprocess.run(cmd[:-2] + ["-order", "sbpmf"], capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r2.returncode == 0, r2.stderr
+    assert "note" in r2.stderr and "note" not in r2.stdout

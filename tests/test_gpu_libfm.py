@@ -84,3 +84,25 @@ def test_libfm_philox_mode_deterministic_and_learns(ml100k):
     assert np.array_equal(ra, np.array([h["rmse_avg"] for h in b.history]))
     # the running mean of the reference chain on ML-100k K=8 settles near 0.93-0.95 within 10 iterations
     assert ra[-1] < 0.97 and ra[-1] < ra[0]
+
+
+def test_libfm_trailing_unrated_items_read_zero(ml100k):
+    """sbmf_set_dims with more items than libFM's attribute count (ids past every
+    rated one): those items have no attribute, so factors and biases read 0 and
+    the rated items are unchanged (no read past the attribute table)."""
+    tr, te = ml100k
+    I = int(max(tr[0].max(), te[0].max())) + 1
+    J = int(max(tr[1].max(), te[1].max())) + 1
+    extra = 37
+    runs = []
+    for nj in (0, J + extra):
+        L = FMLearnSBPMF(num_factor=4, seed=2, method="mcmc", order="libfm", init_stdev=0.1)
+        L.set_data(Data(*tr), Data(*te), num_users=I, num_items=nj)
+        L.learn(sweeps=2)
+        runs.append((L.factors(), L.biases()))
+    (U0, V0), (bu0, bv0, _) = runs[0]
+    (U1, V1), (bu1, bv1, _) = runs[1]
+    assert V1.shape[0] == J + extra and bv1.shape[0] == J + extra
+    assert np.array_equal(U0, U1) and np.array_equal(bu0, bu1)
+    assert np.array_equal(V0, V1[:V0.shape[0]]) and np.array_equal(bv0, bv1[:bv0.shape[0]])
+    assert not V1[V0.shape[0]:].any() and not bv1[bv0.shape[0]:].any()
