@@ -447,6 +447,22 @@ def main():
             lds_frac = bc / (bc + act) if bc is not None and act else None
         except Exception:
             lds_frac = None
+    # every launch kind of both halves against its own bound: algorithmic bytes (per
+    # launch) / HIP-event time; the user side gathers from the 24 MB V table (measured random-row
+    # gather ceiling 8.1 TB/s), the item side from the 124 MB U table (6.3 TB/s;
+    # profiles/r01_gather_ceiling.txt), both quoted as fractions of the 8 TB/s spec too
+    ceil = {0: 8100.0, 1: 6300.0}
+    bins = {}
+    for s_ in range(2):
+        for k_ in range(NKIND):
+            if km[s_, k_] <= 0:
+                continue
+            gbs = main_res["kern_bytes"][s_, k_] / (km[s_, k_] * 1e-3) / 1e9
+            bins[("user_" if s_ == 0 else "item_") + KIND_NAMES[k_]] = {
+                "ms": round(float(km[s_, k_]), 4), "rows": int(main_res["kern_rows"][s_, k_]),
+                "GB": round(float(main_res["kern_bytes"][s_, k_]) / 1e9, 4), "GB/s": round(float(gbs), 1),
+                "frac_peak": round(float(gbs / HBM_PEAK_GBS), 4),
+                "frac_gather_ceiling": round(float(gbs / ceil[s_]), 4)}
     # several ranks on one device (SBMF_COMM=host or --device): a protocol rehearsal, not a scaling point
     one_device = world > 1 and (os.environ.get("SBMF_COMM") == "host" or args.device >= 0)
     out = {
@@ -476,7 +492,8 @@ def main():
                      "bytes_per_launch": float(main_res["kern_bytes"][s, k]),
                      "rows_per_launch": int(main_res["kern_rows"][s, k]),
                      "ms_per_launch": float(km[s, k]),
-                     "sweep_alg_GBs": main_res["bytes_alg"] / (main_res["seconds"] / args.steps) / 1e9},
+                     "sweep_alg_GBs": main_res["bytes_alg"] / (main_res["seconds"] / args.steps) / 1e9,
+                     "bins": bins},
     }
     if f32 is not None:
         out["f32_value"] = n_train * args.steps / f32["seconds"]

@@ -18,7 +18,7 @@ import re
 import sys
 from collections import defaultdict
 
-# kernel symbol -> bench key ("<user|item>_half/gstream" for the streaming launch of each half)
+# kernel symbol -> bench key ("<user|item>_half/gres_stage" for the streaming launch of each half)
 
 
 def per_dispatch(path, counter):
@@ -34,10 +34,10 @@ def per_dispatch(path, counter):
 def key_of(name, order_side):
     m = re.search(r"k_gstream<(double|float), 8, 8, (true|false), (\d)>", name)
     if m:
-        return ("item" if m.group(3) == "1" else "user") + "_half/gstream"
+        return ("item" if m.group(3) == "1" else "user") + "_half/gres_stage"
     m = re.search(r"k_gres<(double|float), (\d+), (\d)(, (true|false))?>", name)  # the default streaming kernel
     if m:
-        return ("item" if m.group(3) == "1" else "user") + "_half/gstream"
+        return ("item" if m.group(3) == "1" else "user") + "_half/gres_stage"
     # Gram-block bins are several launches each (one per waves-per-row group, and the
     # f64 5-8-wave rows as 16-vector waves), so a per-launch figure does not match a
     # bin: only the streaming launches (one per half, the dominant kernel) are keyed

@@ -10,5 +10,5 @@ for set in 0 1; do
     python3 bench.py --steps 3 --warmup 1 $SHORT > $O/r03a_kprof$set.json 2> $O/r03a_kprof$set.err
 done
 timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 $SHORT > $O/r03a_bench.json 2> $O/r03a_bench.err
-timeout -k 10 500 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/r03a_pytest.log 2>&1
+timeout -k 10 800 python3 -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $O/r03a_pytest.log 2>&1
 echo probe done

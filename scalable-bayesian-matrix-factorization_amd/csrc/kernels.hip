@@ -1135,6 +1135,24 @@ struct GresSums {
 #ifdef SBMF_KPROF_BUILD
 constexpr uint32_t GRES_ALLREAD = 16;  // phase-profile class boundary
 #endif
+// Residual slot of rating q (of a task) in LDS.  The butterfly residual update
+// has lane ci of a rating write the residuals of vectors vb(ci) + j, whose
+// slots are 4*NW apart: plain slots put all 16 lanes of a rating on one bank
+// pair (16-way conflicts).  XOR-ing bits 1-4 of the slot with a 4-bit hash of
+// the vector index J = q / (4 NW) spreads them over 16 bank pairs; the map is a
+// permutation inside each aligned group of 32 slots, so the staging and the
+// epilogue (consecutive slots per lane) stay conflict-free as well.
+#ifndef SBMF_GRES_SWZ
+#define SBMF_GRES_SWZ 1
+#endif
+template <int NW>
+__device__ __forceinline__ uint32_t gres_swz(uint32_t J) {
+    return SBMF_GRES_SWZ ? (((J ^ (J >> 4)) & 15u) << 1) : 0u;
+}
+template <int NW>
+__device__ __forceinline__ uint32_t gres_slot(uint32_t q) {
+    return q ^ gres_swz<NW>(q / (4 * NW));
+}
 template <typename T>
 struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of slices
     static constexpr int VW = sizeof(T) == 8 ? 32 : 64;
@@ -1183,8 +1201,19 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
     // this lane's slots: vector j of wave wr is rating 4*(wr + j*NW) + rr, i.e.
     // a fixed per-lane base plus j*4*NW (an immediate LDS offset)
     const uint32_t* const pjW = pjL + 4 * wr + rr;
-    T* const eW = eL + 4 * wr + rr;
+    const uint32_t lb = 4 * wr + rr;  // this lane's slot in every vector (before the swizzle)
     constexpr int JS = 4 * NW;
+    // residual slot of this lane's rating in vector j of its wave (j = vector index / NW)
+    // (lb is re-read through an opaque move at each use so the compiler does not hoist
+    // VC swizzled addresses out of the block loop into VGPRs)
+    auto eS = [&](uint32_t j) -> T& {
+        uint32_t lbo = lb;
+        if constexpr (SBMF_GRES_SWZ) asm volatile("v_mov_b32 %0, %1" : "=v"(lbo) : "v"(lb));
+        if constexpr (JS % 32 == 0)  // the XOR stays inside the lane-slot field: an immediate offset per j
+            return eL[j * JS + (lbo ^ gres_swz<NW>(j))];
+        else
+            return eL[gres_slot<NW>(j * JS + lbo)];
+    };
 
     // task order (default): a queue claimed in list order, one returning atomic
     // per task, so a split row's chunks start as soon as enough workgroups are
@@ -1232,7 +1261,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 const bool in = x < n;
                 pjL[x] = (in ? a.part[beg + x] : a.zrow) * Kp;  // host checks (P+2)*Kp < 2^32
                 pmL[x] = in ? a.perm[beg + x] : 0u;
-                if (!a.e_from_dot) eL[x] = in ? a.E_this[beg + x] : T(0);
+                if (!a.e_from_dot) eL[gres_slot<NW>(x)] = in ? a.E_this[beg + x] : T(0);
                 if (a.row_tr) rL[x] = in ? a.r_this[beg + x] : T(0);
             }
             for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {  // per-half normals and old values of the row
@@ -1248,7 +1277,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                     for (uint32_t k0 = 0; k0 < K; k0 += GB)
                         d += a.partner[(size_t)pj + k0 + ci] * a.own[(size_t)row * Kp + k0 + ci];
                     d = row16_sum(d);
-                    if (ci == 0) eL[q] = q < n ? a.r_this[beg + q] - d : T(0);
+                    if (ci == 0) eL[gres_slot<NW>(q)] = q < n ? a.r_this[beg + q] - d : T(0);
                 }
                 __syncthreads();
             }
@@ -1288,8 +1317,8 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
 #pragma unroll
                 for (int j = 0; j < RV; ++j) {
                     if (VP == VC || vb + j < VC) {  // a zero vector's sum updates nothing
-                        T* const pe = eW + (vb + j) * JS;
-                        *pe = *pe - s[j];
+                        T& pe = eS(vb + j);
+                        pe = pe - s[j];
                     }
                 }
                 // other lanes of this wave read these residuals next (LDS keeps a wave's
@@ -1306,13 +1335,13 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 if (a.tune & 0x80000u) {  // ablation (wrong results): no MFMA (c only, G from one vector)
                     g = MfmaT<T>::mfma(s[0], g);
 #pragma unroll
-                    for (int j = 0; j < VC; ++j) cc += s[j] * eW[j * JS];
+                    for (int j = 0; j < VC; ++j) cc += s[j] * eS(j);
                 } else
 #endif
 #pragma unroll
                 for (int j = 0; j < VC; ++j) {
                     g = MfmaT<T>::mfma(s[j], g);
-                    cc += s[j] * eW[j * JS];
+                    cc += s[j] * eS(j);
                 }
                 cc += shfl_xor_t(cc, 16);
                 cc += shfl_xor_t(cc, 32);
@@ -1320,6 +1349,10 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
             // the block's partials into LDS, the cross-wave sum, the split-row
             // exchange and the 16 draws: returns D_t (every lane: its column's)
             auto finish_block = [&](const acc_t& g, T cc, uint32_t t) -> T {
+                // tune bit 28: the block's critical path (partials, cross-wave sum, split-row
+                // exchange, draws) at raised wave priority over a co-resident workgroup's stream
+                const bool prio = a.tune & 0x10000000u;
+                if (prio) __builtin_amdgcn_s_setprio(2);
                 T Dl;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -1444,6 +1477,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                     Dl = Dsh[ci];
                 }
                 stamp(5);  // solve
+                if (prio) __builtin_amdgcn_s_setprio(0);
                 return Dl;
             };
             if constexpr (!DB) {
@@ -1509,7 +1543,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
             __syncthreads();
             double sq = 0.0, trs = 0.0;
             for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) {
-                const T e = eL[x];
+                const T e = eL[gres_slot<NW>(x)];
                 a.E_other[pmL[x]] = e;
                 sq += (double)(e * e);
                 if (a.row_tr) {

@@ -17,7 +17,7 @@ QUIRKS_FINAL, QUIRKS_SBPMF2, QUIRKS_NONE, QUIRKS_BIAS2, QUIRKS_BIAS22 = 0, 1, 2,
 F64, F32 = 0, 1
 METHOD_MCMC, METHOD_VB, METHOD_LIBFM_MCMC, METHOD_ALS = 0, 1, 2, 3
 NKIND = 11  # SBMF_NKIND
-KIND_NAMES = ['gblock_w4', 'gblock_w16', 'gblock_b2', 'gblock_b4', 'gblock_b8', 'gstream', 'rows_w2', 'rows_w8',
+KIND_NAMES = ['gblock_w4', 'gblock_w16', 'gblock_b2', 'gblock_b4', 'gblock_b8', 'gres_stage', 'rows_w2', 'rows_w8',
               'rows_b4', 'rows_b8', 'gram']
 
 

@@ -105,4 +105,7 @@ def test_libfm_trailing_unrated_items_read_zero(ml100k):
     assert V1.shape[0] == J + extra and bv1.shape[0] == J + extra
     assert np.array_equal(U0, U1) and np.array_equal(bu0, bu1)
     assert np.array_equal(V0, V1[:V0.shape[0]]) and np.array_equal(bv0, bv1[:bv0.shape[0]])
-    assert not V1[V0.shape[0]:].any() and not bv1[bv0.shape[0]:].any()
+    # item J is libFM's phantom attribute (num_all_attribute = max feature id + 1 + 1,
+    # libfm.cpp:328): it exists, is drawn from its prior and keeps its value; past it, nothing
+    assert V1[J].any()
+    assert not V1[J + 1:].any() and not bv1[J + 1:].any()

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 WORKER = os.path.join(REPO, "tests", "workers", "multirank_worker.py")
 
 
-def _run_ranks(tmp_path, nranks, args, env=None):
+def _run_ranks(tmp_path, nranks, args, env=None, timeout=240):
     """Spawn the ranks (host comm backend) and return their output files."""
     old = os.environ.get("SBMF_COMM")
     os.environ["SBMF_COMM"] = "host"
@@ -39,7 +39,7 @@ def _run_ranks(tmp_path, nranks, args, env=None):
     logs = []
     for p in procs:
         try:
-            o, _ = p.communicate(timeout=240)
+            o, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
@@ -152,3 +152,58 @@ def test_libfm_ranks_on_one_gpu(ml100k, ragged, tmp_path, nranks, run):
         lines = f.read().splitlines()
     assert _within_printed(z0["rmse_train"], [float(l.split("Train=")[1].split()[0]) for l in lines])
     assert _within_printed(z0["rmse"], [float(l.split("Test=")[1]) for l in lines])
+
+
+@pytest.mark.timeout(900)
+def test_config4_ml20m_k200_two_ranks_match_single_rank(tmp_path):
+    """BASELINE config 4's split (ML-20M K=200, user and item row blocks over ranks)
+    at its own shape, reference stream, one sweep: two ranks on one GPU (host comm
+    backend) end with the single-rank U, V, tau and RMSE bit for bit.  The
+    single-rank run is pinned to the oracle by test_gpu_production.py::
+    test_ml20m_k200_reference_stream_one_sweep.  At this shape both ranks own
+    split item rows (over 1024 ratings: several co-resident chunks per row) and
+    the residual exchange carries tens of MB across the cut."""
+    import hashlib
+    from sbmf import partition_rows, synth
+    K, sweeps, seed = 200, 1, 1
+    cache = str(tmp_path / "synth")  # generated once here, read back by the ranks
+    old = os.environ.get("SBMF_SYNTH_CACHE")
+    os.environ["SBMF_SYNTH_CACHE"] = cache
+    try:
+        tr, te, dims = synth.generate("ml-20m")
+    finally:
+        if old is None:
+            del os.environ["SBMF_SYNTH_CACHE"]
+        else:
+            os.environ["SBMF_SYNTH_CACHE"] = old
+    I, J = dims
+    # the item row blocks of the 2-rank cut: split rows on both sides, ratings crossing it
+    iptr = np.concatenate([[0], np.cumsum(np.bincount(tr[1], minlength=J))]).astype(np.uint64)
+    uptr = np.concatenate([[0], np.cumsum(np.bincount(tr[0], minlength=I))]).astype(np.uint64)
+    ib, ub = partition_rows(iptr, 2), partition_rows(uptr, 2)
+    deg = np.diff(iptr)
+    for r in range(2):
+        assert deg[ib[r]:ib[r + 1]].max() > 1024, (r, ib)
+    user_rank = (tr[0] >= ub[1]).astype(np.int8)
+    item_rank = (tr[1] >= ib[1]).astype(np.int8)
+    cross = int((user_rank != item_rank).sum())
+    assert cross > 1_000_000  # residuals of > 1 M ratings cross the cut each half (8 B each)
+    L = FMLearnSBPMF(num_factor=K, seed=seed, rng="ref")
+    L.set_data(Data(*tr), Data(*te), num_users=I, num_items=J)
+    L.learn(sweeps=sweeps)
+    U1, V1 = L.factors()
+    rmse1 = L.rmse_trajectory
+    tau1 = np.array([h["tau"] for h in L.history])
+    L.close()
+    hU = np.frombuffer(hashlib.sha256(np.ascontiguousarray(U1).tobytes()).digest(), np.uint8)
+    hV = np.frombuffer(hashlib.sha256(np.ascontiguousarray(V1).tobytes()).digest(), np.uint8)
+    del U1, V1
+    outs = _run_ranks(tmp_path, 2, [str(K), str(sweeps), str(seed), "ref", "0", "final"],
+                      env={"SBMF_WORKER_DATA": "synth:ml-20m", "SBMF_WORKER_DIGEST": "1", "SBMF_SYNTH_CACHE": cache},
+                      timeout=600)
+    for r in range(2):
+        z = np.load(outs[r])
+        assert np.array_equal(z["U"], hU) and np.array_equal(z["V"], hV), r
+        assert np.array_equal(z["rmse"], rmse1) and np.array_equal(z["tau"], tau1), r
+    print("config 4 split: item blocks %s, user blocks %s, %d ratings cross the cut, rmse %s" % (
+        list(ib), list(ub), cross, rmse1))

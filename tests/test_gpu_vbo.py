@@ -77,3 +77,52 @@ def test_vbo_continues_across_learn_calls(ml100k):
     assert np.array_equal(a.rmse_trajectory, b.rmse_trajectory)
     a.close()
     b.close()
+
+
+@pytest.mark.timeout(900)
+def test_vbo_ml1m_k200_matches_oracle():
+    """BASELINE config 5's factor count (K=200) on the ML-1M shape (sbmf/synth.py), two
+    epochs, reference RNG: per-epoch test RMSE within 1e-9 and the posterior means
+    within 1e-8 of the oracle (fm_learn_vb_online.h:712-800 update_v, :391-583
+    update_all; fm_learn_vb_online_simultaneous.h:148-299 the epoch loop)."""
+    from sbmf import synth
+    tr, te, dims = synth.generate("ml-1m")
+    K, epochs, seed = 200, 2, 3
+    o = oracle.run_vbo(tr, te, K=K, epochs=epochs, seed=seed, num_users=dims[0], num_items=dims[1])
+    L = FMLearnVBOnline(num_factor=K, seed=seed)
+    L.set_data(Data(*tr), Data(*te), num_users=dims[0], num_items=dims[1])
+    L.learn(sweeps=epochs)
+    err = np.abs(L.rmse_trajectory - o["rmse"])
+    U, V = L.factors()
+    bu, bv, b0 = L.biases()
+    I = U.shape[0]
+    print("vbo ml-1m K=200: rmse %s, max|dRMSE| %.2e max|dU| %.2e max|dV| %.2e" % (
+        L.rmse_trajectory, err.max(), np.abs(U - o["mu_v"][:I]).max(), np.abs(V - o["mu_v"][I:]).max()))
+    assert err.max() < 1e-9
+    assert np.abs(U - o["mu_v"][:I]).max() < 1e-8
+    assert np.abs(V - o["mu_v"][I:]).max() < 1e-8
+    assert np.abs(bu - o["mu_w"][:I]).max() < 1e-8 and np.abs(bv - o["mu_w"][I:]).max() < 1e-8
+    assert abs(b0 - o["mu0"]) < 1e-10
+    L.close()
+
+
+@pytest.mark.timeout(900)
+def test_vbo_netflix_k200_full_size():
+    """BASELINE config 5 at its own size: the Netflix-shaped synthetic set (90.4 M
+    train ratings, 480,189 x 17,770), K=200, throughput mode (bench.py --method vb).
+    Two epochs: finite test RMSE that falls from epoch 1 to 2, and a second run's
+    first epoch bitwise equal to the first run's (the Philox shuffle, the batch
+    layout and every reduction are fixed-order)."""
+    from sbmf import synth
+    tr, te, dims = synth.generate("netflix")
+    runs = []
+    for epochs in (2, 1):
+        L = FMLearnVBOnline(num_factor=200, seed=2015, rng="philox")
+        L.set_data(Data(*tr), Data(*te), num_users=dims[0], num_items=dims[1])
+        L.learn(sweeps=epochs)
+        runs.append(L.rmse_trajectory.copy())
+        L.close()
+    a, b = runs
+    print("vbo netflix K=200: rmse %s / %s" % (a, b))
+    assert np.all(np.isfinite(a)) and a[1] < a[0] < 1.5
+    assert np.array_equal(a[:1], b)

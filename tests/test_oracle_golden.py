@@ -39,3 +39,15 @@ def test_vbo_oracle_bitwise_equals_reference(data, K, seed, epochs, ml100k, ragg
     gold = golden_rmse("ref_vbo_%s_k%d_s%d_e%d.txt" % (data, K, seed, epochs))
     o = oracle.run_vbo(tr, te, K=K, epochs=epochs, seed=seed, want_params=False)
     assert np.array_equal(o["rmse"], gold), np.abs(o["rmse"] - gold).max()
+
+
+def test_oracle_follows_reference_through_collapse():
+    """gibbs_sbpmf_final on the ML-1M-shaped synthetic set (K=20, seed 1): the
+    reference's 100-sweep trajectory bottoms at sweep 36 and rises as tau falls
+    to 0 and turns NaN; the oracle reproduces all 100 lines bit for bit."""
+    from sbmf import synth
+    tr, te, _ = synth.generate("ml-1m")
+    gold = golden_rmse("ref_final_ml1msynth_k20_s1.txt")
+    o = oracle.run(tr, te, K=20, iters=100, seed=1, want_factors=False)
+    assert np.array_equal(o["rmse"], gold)
+    assert int(np.argmin(gold)) == 36 and np.isnan(o["tau"][43:]).all()

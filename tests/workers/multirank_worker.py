@@ -38,7 +38,12 @@ def main():
     from sbmf import Data, FMLearnSBPMF, FMLearnVBOnline
     g = os.path.join(REPO, "tests", "golden")
     data = os.environ.get("SBMF_WORKER_DATA", "ml100k")
-    tr, te = read(os.path.join(g, data + "_train.tsv.gz")), read(os.path.join(g, data + "_test.tsv.gz"))
+    dims = (0, 0)
+    if data.startswith("synth:"):  # a full-size synthetic shape (sbmf/synth.py), identical in every rank
+        from sbmf import synth
+        tr, te, dims = synth.generate(data[6:])
+    else:
+        tr, te = read(os.path.join(g, data + "_train.tsv.gz")), read(os.path.join(g, data + "_test.tsv.gz"))
     if method == "vb":
         L = FMLearnVBOnline(num_factor=int(K), seed=int(seed), rng=rng, device=0)
     elif method in ("libfm", "als"):  # libFM's own chain: quirks carries "k0,k1;regular"
@@ -50,9 +55,13 @@ def main():
     else:
         L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, tune=tune, quirks=quirks)
     L.init(comm=(int(nranks), int(rank), bytes.fromhex(idhex)))
-    L.set_data(Data(*tr), Data(*te))
+    L.set_data(Data(*tr), Data(*te), num_users=dims[0], num_items=dims[1])
     L.learn(sweeps=int(sweeps))
     U, V = L.factors()
+    if os.environ.get("SBMF_WORKER_DIGEST"):  # full-size tables: digests instead of the arrays
+        import hashlib
+        U = np.frombuffer(hashlib.sha256(np.ascontiguousarray(U).tobytes()).digest(), np.uint8)
+        V = np.frombuffer(hashlib.sha256(np.ascontiguousarray(V).tobytes()).digest(), np.uint8)
     extra = {}
     if quirks in ("bias2", "bias22") or method in ("vb", "libfm", "als"):
         bu, bv, b0 = L.biases()
