@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--shape", default=None, help="ml-20m (mcmc default) | netflix (vb default) | ml-1m | ...")
     ap.add_argument("--K", type=int, default=None, help="factors (default 100 mcmc / 200 vb)")
     ap.add_argument("--precision", default="f64")
+    ap.add_argument("--quirks", default="final",
+                    help="final (gibbs_sbpmf_final.cpp, headline) | bias2 (the biased sampler of the top-level "
+                         "gibbs_sbpmf2.cpp: the paper's SBMF-P model) | bias22 | sbpmf2 | none")
     ap.add_argument("--no-f32", action="store_true", help="skip the extra f32 measurement")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
@@ -122,7 +125,7 @@ def device_sync():
 def make_learner(args, world, rank, local, precision, uid):
     from sbmf import Data, FMLearnSBPMF
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=precision, device=local,
-                     recompute_every=0, eval_train=False, gram_threshold=args.gram_threshold,
+                     quirks=args.quirks, recompute_every=0, eval_train=False, gram_threshold=args.gram_threshold,
                      row_kernel=args.row_kernel, tune=args.tune, split_chunk=args.split_chunk,
                      stream_threshold=args.stream_threshold)
     L.init(comm=(world, rank, uid) if world > 1 else None)
@@ -414,6 +417,8 @@ def main():
     from sbmf._lib import KIND_NAMES, NKIND
     train, test, dims = synth.generate(args.shape)
     main_res = measure(args, world, rank, local, args.precision, train, test, mk_uid(world, rank))
+    if args.quirks != "final":  # the extra legs (f32, time-to-RMSE) belong to the headline sampler
+        args.no_f32 = args.no_ttr = True
     f32 = None
     if not args.no_f32 and args.precision != "f32":
         f32 = measure(args, world, rank, local, "f32", train, test, mk_uid(world, rank))
@@ -430,7 +435,7 @@ def main():
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     # the PMC pass was taken on the default single-rank ML-20M K=100 f64 run: only that config quotes it
-    profiled = world == 1 and args.shape == "ml-20m" and args.K == 100
+    profiled = world == 1 and args.shape == "ml-20m" and args.K == 100 and args.quirks == "final"
     if profiled and os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get(kernel)
@@ -476,10 +481,10 @@ def main():
         "vs_baseline": None if one_device else value / BASELINE_RPS,
         "dtype": args.precision,
         "data": "synthetic ML-20M-shaped (sbmf/synth.py: planted rank-10, Pareto users, log-normal items)",
-        "config": {"workload": "%s K=%d SBPMF Gibbs sweep (user+item half-sweeps, hyperparameters, test RMSE)"
-                               % (args.shape, args.K),
+        "config": {"workload": "%s K=%d SBPMF Gibbs sweep (%suser+item half-sweeps, hyperparameters, test RMSE)"
+                               % (args.shape, args.K, "bias draws + " if args.quirks.startswith("bias") else ""),
                    "num_users": dims[0], "num_items": dims[1], "n_train": n_train, "n_test": len(test[0]),
-                   "K": args.K, "rng": "philox", "quirks": "final",
+                   "K": args.K, "rng": "philox", "quirks": args.quirks,
                    "parallelism": "rows x%d (%s)" % (world, "host-shm exchange, testing only" if os.environ.get("SBMF_COMM") == "host" else "RCCL block broadcast + p2p residual exchange"),
                    "test_rmse_after": main_res["rmse"], "sweeps_run": main_res["sweeps_run"],
                    "time_to_test_rmse_0.85": ttr,

@@ -414,6 +414,21 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory operations are done
+// (the counter holds at most 63: a larger N waits for the oldest N - 63 of them too)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0, "vmcnt range");
+    if constexpr (N >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+    else if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if constexpr (N == 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else static_assert(N == 0, "add the count");
+}
+
 constexpr int GB = 16;      // k per block
 constexpr int GLD = GB + 1; // padded LDS row (conflict-free row reads)
 
@@ -441,6 +456,20 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
     for (int j = 0; j < GB; ++j) {
         const T dj = readlane(gam, j);
         gam -= (Bq * hrow[j]) * dj;
+    }
+    return gam;
+}
+
+// Same recurrence over a full 16x17 image of G (row `hrow`): only the strictly
+// lower entries j < c take part (the diagonal and the upper part hold other data);
+// a masked entry contributes (Bq * 0) * d_j, exactly as the zero-filled image did.
+template <typename T>
+__device__ __forceinline__ T gblock_solve_lds_lower(const T* __restrict__ hrow, T Bq, T gam, int c) {
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+        const T dj = readlane(gam, j);
+        const T h = j < c ? hrow[j] : T(0);
+        gam -= (Bq * h) * dj;
     }
     return gam;
 }
@@ -1143,7 +1172,7 @@ constexpr uint32_t GRES_ALLREAD = 16;  // phase-profile class boundary
 // permutation inside each aligned group of 32 slots, so the staging and the
 // epilogue (consecutive slots per lane) stay conflict-free as well.
 #ifndef SBMF_GRES_SWZ
-#define SBMF_GRES_SWZ 1
+#define SBMF_GRES_SWZ 0  // measured 5 % slower on the item stage (r03b): off
 #endif
 template <int NW>
 __device__ __forceinline__ uint32_t gres_swz(uint32_t J) {
@@ -1175,12 +1204,12 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
     __shared__ uint32_t pmL[CAP];      // residual scatter target per rating
     __shared__ T eL[CAP];              // residuals (bit-identical in the 16 lanes of a rating)
     __shared__ T rL[CAP];              // ratings (train error), when requested
-    __shared__ T Ls[NW][GB][GLD];      // per-wave strictly lower part of G_B
-    __shared__ T Ps[NW][GB];           // per-wave diagonal
-    __shared__ T Cs[NW][GB];           // per-wave c_B
-    __shared__ T Lr[GB][GLD];          // reduced: strictly lower part (diagonal and upper stay 0)
-    __shared__ T Pr[GB];
-    __shared__ T Cr[GB];
+    // per-wave block partials: the 16x17 image of G_B (row r, column c at r*GLD + c, all 256
+    // entries as the MFMA leaves them) followed by c_B; Rr: the reduced entries (lower triangle
+    // with the diagonal, and c_B) in the same layout
+    constexpr int PW = GB * GLD + GB;
+    __shared__ T Pw[NW][PW];
+    __shared__ T Rr[PW];
     __shared__ T Dsh[GB];
     __shared__ T newS[256];
     __shared__ double red2[NW][2];
@@ -1190,10 +1219,19 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
     constexpr int XP = (64 * NW) / SLP;
     static_assert(XP >= 1 && SLP <= SL, "exchange geometry");
     __shared__ double xsum[XP][SLP];
+    // packed entry x -> its offset in a partial image (computed once: no per-block geometry)
+    __shared__ uint16_t xoff[SLP];
     // the row's normals and old values, sigma and mu: read by the solving wave from LDS
     // (kept out of the VGPRs the held slices need)
     __shared__ T zL[256], oL[256], sgL[256], muL[256];
-    for (int x = threadIdx.x; x < GB * GLD; x += 64 * NW) (&Lr[0][0])[x] = T(0);
+    for (int x = threadIdx.x; x < SLP; x += 64 * NW) {
+        int r = 0;
+        while ((r + 1) * (r + 2) / 2 <= x && r < GB) ++r;  // row of the packed triangle
+        xoff[x] = (uint16_t)(x < GB * (GB + 1) / 2 ? r * GLD + (x - r * (r + 1) / 2) : GB * GLD + (x - GB * (GB + 1) / 2));
+    }
+    // this wave's index as a scalar, and the lane: the thread id is rebuilt from them in the
+    // block loop (no VGPR held across it, no spill slot to reload)
+    const int wr_s = __builtin_amdgcn_readfirstlane(wr);
     for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {
         sgL[k] = a.sig[k];
         muL[k] = a.mu[k];
@@ -1348,39 +1386,40 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
             };
             // the block's partials into LDS, the cross-wave sum, the split-row
             // exchange and the 16 draws: returns D_t (every lane: its column's)
-            auto finish_block = [&](const acc_t& g, T cc, uint32_t t) -> T {
+            // pf: the double-buffered kernel's gather of the next block's slices (NPF loads per
+            // wave), issued here so that it stays in flight through the block's exchange and
+            // draws.  Every barrier below is an LDS-only barrier (lds_barrier: __syncthreads()
+            // would wait vmcnt(0) and drain the prefetch); a split row's partial stores are
+            // issued before the prefetch and waited for with vmcnt(NPF).
+            auto finish_block = [&](const acc_t& g, T cc, uint32_t t, auto&& pf, auto npf) -> T {
+                constexpr int NPF = decltype(npf)::value;
                 // tune bit 28: the block's critical path (partials, cross-wave sum, split-row
                 // exchange, draws) at raised wave priority over a co-resident workgroup's stream
                 const bool prio = a.tune & 0x10000000u;
                 if (prio) __builtin_amdgcn_s_setprio(2);
                 T Dl;
+                if (nch == 1) pf();
+                {
+                    T* const pw = &Pw[wr_s][0];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int r = MfmaT<T>::row(lane, j);
-                    Ls[wr][r][ci] = ci < r ? g[j] : T(0);
-                    if (r == ci) Ps[wr][ci] = g[j];
+                    for (int j = 0; j < 4; ++j) pw[MfmaT<T>::row(lane, j) * GLD + ci] = g[j];
+                    if (lane < GB) pw[GB * GLD + lane] = cc;
                 }
-                if (lane < GB) Cs[wr][lane] = cc;
-                __syncthreads();
+                lds_barrier();
                 stamp(3);  // wait for the other waves
                 // cross-wave sum in wave order: thread x < SLP holds packed entry x
                 // (lower triangle incl. the diagonal, then c); the entry's geometry is
                 // recomputed here from an opaque thread id so it holds no VGPRs across
                 // the block loop
-                int tid;
-                asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
+                const int tid = wr_s * 64 + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
                 const int xe = tid % SLP, xpart = tid / SLP;
                 const bool xin = tid < SLP;
-                int xr = -1, xc = xe - GB * (GB + 1) / 2;  // c entry: xr = -1, xc = k
-                if (xe < GB * (GB + 1) / 2) {  // row r of the packed triangle: r (r + 1) / 2 <= xe
-                    xr = (int)((sqrtf(8.0f * (float)xe + 1.0f) - 1.0f) * 0.5f);
-                    xc = xe - xr * (xr + 1) / 2;
-                }
+                const int xo = xin ? (int)xoff[xe] : 0;  // the entry's offset in every partial image
                 T val = T(0);
                 if (xin) {
 #pragma unroll
                     for (int w = 0; w < NW; ++w)
-                        val += xr < 0 ? Cs[w][xc] : (xr == xc ? Ps[w][xr] : Ls[w][xr][xc]);
+                        val += Pw[w][xo];
                 }
 #ifdef SBMF_ABLATIONS
                 const bool xchg = nch > 1 && !(a.tune & 0x4000u);  // ablation (wrong results): no hand-off
@@ -1396,8 +1435,16 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                     const size_t cstride = (size_t)nblk * SL;  // between one chunk's slabs and the next's
                     const double* pb = sy.slabs + ((size_t)tk.slab0 * nblk + t) * SL;
                     if (xin) st_sc1(const_cast<double*>(pb) + tk.chunk * cstride + xe, (double)val);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __syncthreads();
+                    asm volatile("" ::: "memory");
+                    pf();
+                    asm volatile("" ::: "memory");
+                    // this wave's partial stores (older than the prefetch) are done; the last block
+                    // prefetches nothing, so it waits for everything
+                    if (NPF > 0 && t + 1 < nblk)
+                        wait_vmcnt<NPF>();
+                    else
+                        wait_vmcnt<0>();
+                    lds_barrier();
                     uint32_t* cnt = sy.counters + (size_t)tk.cnt0 + t;
                     if (threadIdx.x == 0) {
                         // no return value to wait for: the poll follows at once
@@ -1411,7 +1458,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                             }
                         }
                     }
-                    __syncthreads();
+                    lds_barrier();
                     if (xpart < XP) {
                         const uint32_t c0 = xpart * nch / XP, c1 = (xpart + 1) * nch / XP;
                         const double* p0 = pb + xe;
@@ -1427,7 +1474,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                         for (; c < c1; ++c) sum += ld_sc1(p0 + c * cstride);
                         xsum[xpart][xe] = sum;
                     }
-                    __syncthreads();
+                    lds_barrier();
                     if (xin) {
                         double sum = xsum[0][xe];
 #pragma unroll
@@ -1435,15 +1482,8 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                         val = (T)sum;
                     }
                 }
-                if (xin) {
-                    if (xr < 0)
-                        Cr[xc] = val;
-                    else if (xr == xc)
-                        Pr[xr] = val;
-                    else
-                        Lr[xr][xc] = val;
-                }
-                __syncthreads();
+                if (xin) Rr[xo] = val;
+                lds_barrier();
                 stamp(4);  // cross-wave sum + split-row exchange
                 // the 16 draws: wave 0, D handed over in LDS (default), or -- tune bit 0 --
                 // every wave redundantly (identical inputs, identical results; one barrier less)
@@ -1454,26 +1494,28 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                     const bool kin = kk < K;
                     // the block's old values, hyperparameters and normals (zero padded)
                     const T old = oL[kk], sg = sgL[kk], mu = muL[kk], z = zL[kk];
-                    const T P = Pr[ci];
+                    const T P = Rr[ci * GLD + ci];
+                    const T Cc = Rr[GB * GLD + ci];
                     const T var = kin ? T(1) / (sg + tau * P) : T(0);
-                    const T sd = a.sd_is_var ? var : tsqrt(var);
+                    T sd = var;  // a uniform branch: no square root under the variance-as-stdev quirk
+                    if (!a.sd_is_var) sd = tsqrt(var);
                     const T A = var * sg * mu + sd * z;
                     const T Bq = var * tau;
 #ifdef SBMF_ABLATIONS
                     if (a.tune & 0x8000u)  // ablation (wrong results): no 16-step recurrence
-                        dlt = A - old + Bq * (Cr[ci] + P * old);
+                        dlt = A - old + Bq * (Cc + P * old);
                     else
 #endif
-                    dlt = gblock_solve_lds(&Lr[ci][0], Bq, A - old + Bq * (Cr[ci] + P * old));
+                    dlt = gblock_solve_lds_lower(&Rr[ci * GLD], Bq, A - old + Bq * (Cc + P * old), ci);
                     if (wr == 0 && lane < GB) {
                         if (kin) newS[kk] = old + dlt;
                         Dsh[lane] = dlt;
                     }
                 }
                 if (rep) {
-                    Dl = dlt;  // the next block's barrier keeps Lr / Pr / Cr until every wave has solved
+                    Dl = dlt;  // the next block's barrier keeps Rr until every wave has solved
                 } else {
-                    __syncthreads();
+                    lds_barrier();
                     Dl = Dsh[ci];
                 }
                 stamp(5);  // solve
@@ -1503,7 +1545,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                     T cc = T(0);
                     accumulate(s, g, cc);
                     stamp(2);  // gather wait + accumulate
-                    Dl = finish_block(g, cc, t);
+                    Dl = finish_block(g, cc, t, [] {}, std::integral_constant<int, 0>{});
                 }
                 // apply the last block
                 apply(s, Dl, [](int) {});
@@ -1522,12 +1564,16 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                     acc_t g = {T(0), T(0), T(0), T(0)};
                     T cc = T(0);
                     accumulate(cur, g, cc);
-                    if (t + 1 < nblk) {
-#pragma unroll
-                        for (int j = 0; j < VC; ++j) prv[j] = pbase[(size_t)pjW[j * JS] + (t + 1) * GB];
-                    }
                     stamp(2);
-                    Dl = finish_block(g, cc, t);
+                    // slice t+1 into the registers slice t-1 held, in flight through this block's
+                    // exchange and draws (a block without a successor issues nothing: NPF stays
+                    // an upper bound of the loads in flight)
+                    Dl = finish_block(g, cc, t, [&] {
+                        if (t + 1 < nblk) {
+#pragma unroll
+                            for (int j = 0; j < VC; ++j) prv[j] = pbase[(size_t)pjW[j * JS] + (t + 1) * GB];
+                        }
+                    }, std::integral_constant<int, VC>{});
                 };
                 for (uint32_t t = 0; t < nblk; t += 2) {
                     dstep(sA, sB, t);

@@ -18,9 +18,10 @@ LDS-capacity task size) and f64.  These tests run exactly that configuration:
     single-GPU half of the 8-GPU config), one or two sweeps each against the
     oracle: U and V within 1e-7, RMSE and tau within 1e-9 (relative for tau).
     The item side at these sizes takes the production schedule: thousands of
-    streaming tasks in rounds of the full cooperative grid, rows longer than
-    the 4096-rating task split over co-resident workgroups.  A split-row
-    hand-off that timed out raises inside learn() (sbmf_run fails).
+    streaming tasks claimed from a queue by the persistent k_gres launches,
+    item rows longer than 1024 ratings split into 2048-rating tasks (16-wave
+    workgroups, f64) over co-resident workgroups.  A split-row hand-off that
+    timed out raises inside learn() (sbmf_run fails).
 
 Reference: gibbs_sbpmf_final.cpp:317-334 (E recompute), :453-535 (halves).
 """
