@@ -517,3 +517,9 @@ def main():
 
 if __name__ == "__main__":
     main()
+    # every result is printed and the library unloaded: leave without the interpreter's
+    # exit-time teardown (under rocprofv3 the HIP runtime's exit-time destructors fault after
+    # the profiler has finalized -- profiles/r03_rocprof_teardown.txt)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)

@@ -143,6 +143,41 @@ void Comm::bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_
     if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
 }
 
+void Comm::bcast_blocks(void* base, size_t unit_bytes, const std::vector<uint64_t>& starts,
+                        const std::vector<uint64_t>& ends, hipStream_t st) {
+    if (nranks_ <= 1) return;
+    char* dev = static_cast<char*>(base);
+    if (shm_) {  // host backend: each owner's block through the window, window by window
+        if (hipStreamSynchronize(st) != hipSuccess) throw std::runtime_error("hipStreamSynchronize failed");
+        unsigned char* win = shm_ + kHostHeader;
+        for (int k = 0; k < nranks_; ++k) {
+            const size_t lo = (size_t)starts[k] * unit_bytes, hi = (size_t)ends[k] * unit_bytes;
+            for (size_t w0 = lo; w0 < hi; w0 += kHostWindow) {
+                const size_t w1 = std::min(hi, w0 + kHostWindow);
+                if (k == rank_ && hipMemcpy(win, dev + w0, w1 - w0, hipMemcpyDeviceToHost) != hipSuccess)
+                    throw std::runtime_error("host comm: D2H failed");
+                host_barrier();
+                if (k != rank_ && hipMemcpy(dev + w0, win, w1 - w0, hipMemcpyHostToDevice) != hipSuccess)
+                    throw std::runtime_error("host comm: H2D failed");
+                host_barrier();
+            }
+        }
+        return;
+    }
+    if (!comm_) return;
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) comm_fail("ncclGroupStart", r);
+    for (int k = 0; k < nranks_; ++k) {
+        const size_t bytes = (size_t)(ends[k] - starts[k]) * unit_bytes;
+        if (bytes == 0) continue;
+        char* p = dev + (size_t)starts[k] * unit_bytes;
+        r = ncclBroadcast(p, p, bytes, ncclUint8, k, (ncclComm_t)comm_, st);
+        if (r != ncclSuccess) comm_fail("ncclBroadcast", r);
+    }
+    r = ncclGroupEnd();
+    if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
+}
+
 void Comm::alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const std::vector<size_t>& scnt,
                      void* recvbuf, const std::vector<size_t>& roff, const std::vector<size_t>& rcnt, hipStream_t st) {
     if (nranks_ <= 1) return;

@@ -27,6 +27,10 @@ class Comm {
     // Rank k owns units [bounds[k], bounds[k+1]) of unit_bytes each, starting
     // at base; after the call every rank holds every rank's units.
     void bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_t>& bounds, hipStream_t st);
+    // The same for blocks that need not tile a range: rank k owns units
+    // [starts[k], ends[k]) (a pipelined stage of every rank's block).
+    void bcast_blocks(void* base, size_t unit_bytes, const std::vector<uint64_t>& starts,
+                      const std::vector<uint64_t>& ends, hipStream_t st);
     // Point-to-point exchange (grouped ncclSend / ncclRecv): to every other
     // rank k, send [soff[k], soff[k] + scnt[k]) of sendbuf, and receive
     // rcnt[k] bytes from it at recvbuf + roff[k] (byte offsets and counts).

@@ -59,9 +59,6 @@ struct Side {
     std::vector<double> r;              // [N] ratings
     uint32_t r0 = 0, r1 = 0;            // owned row range (multi-GPU)
     std::vector<uint64_t> bounds;       // [nranks+1] row ranges of every rank
-    std::vector<uint32_t> bin_rows[NBIN];  // kinds: GK_* (0..4), KIND_STREAM (5), KIND_RK0 + RK_* (6..9)
-    std::vector<GramItem> gitems;
-    std::vector<GramRow> grows;
     // streaming rows: set 0 (k_gres, or k_gstream with tune bit 6) and, in the
     // hybrid schedule, set 1 = the rows above the hybrid threshold (k_gstream)
     struct StreamSet {
@@ -71,15 +68,32 @@ struct Side {
         uint32_t sgrid = 0;             // persistent grid of the launch
         uint32_t cmax = 0;              // task capacity (ratings)
         uint32_t tune = 0;              // kernel variant bits of the launch
-    } ss[2];
-    std::vector<std::array<uint32_t, 3>> gsub[GK_NUM];  // multi-wave bins: (waves, offset, count) sub-ranges
+    };
+    // A stage: the rows [r0, r1) of this rank's block, binned for their own launches.
+    // One stage per half unless the multi-GPU exchange is pipelined: then the block is
+    // cut into nnz-balanced stages and stage s's fresh rows and residuals travel while
+    // stage s+1 computes (run_sweeps_T).  Results do not depend on the cut: every row's
+    // draws are the same in any launch.
+    struct Stage {
+        uint32_t r0 = 0, r1 = 0;
+        std::vector<uint32_t> bin_rows[NBIN];  // kinds: GK_* (0..4), KIND_STREAM (5), KIND_RK0 + RK_* (6..9)
+        std::vector<GramItem> gitems;
+        std::vector<GramRow> grows;
+        StreamSet ss[2];
+        std::vector<std::array<uint32_t, 3>> gsub[GK_NUM];  // multi-wave bins: (waves, offset, count) sub-ranges
+        DBuf d_bins[NBIN], d_stasks[2], d_xrows[2], d_gitems, d_grows;
+        // multi-GPU residual exchange of this stage: [peer] segments of the send / receive areas
+        std::vector<size_t> soff, scnt, roff, rcnt;
+        size_t rbeg = 0, rend = 0;  // this stage's receive elements [rbeg, rend)
+    };
+    std::vector<std::unique_ptr<Stage>> stg;
+    std::vector<std::vector<uint64_t>> sbounds;  // [rank][stage + 1]: every rank's stage cuts
     std::vector<ResidTask> rtasks;   // residual recompute: own rows in chunks of <= RESID_CHUNK
     std::vector<uint32_t> rtptr;     // [r1-r0+1] first task of each own row
     // multi-GPU residual exchange (see build_exchange): where this rank's rows
     // scatter their residuals (the other orientation's position, or a send slot
     // past its end), and where the residuals other ranks send land
     std::vector<uint32_t> perm2, unpack;
-    std::vector<size_t> soff, scnt, roff, rcnt;  // elements, per peer
     size_t nsend = 0, nrecv = 0;
 };
 
@@ -96,39 +110,52 @@ struct Side {
 // r - own.partner, which re-reads every partner row.
 static void build_exchange(Side& s, const Side& other, int nranks, int rank) {
     const uint64_t N = s.perm.size();
+    const size_t P = s.stg.size();
     std::vector<uint64_t> obase(nranks + 1);
     for (int k = 0; k <= nranks; ++k) obase[k] = other.ptr[other.bounds[k]];
     auto owner = [&](uint32_t pos) {
         return (int)(std::upper_bound(obase.begin(), obase.end(), (uint64_t)pos) - obase.begin()) - 1;
     };
-    s.scnt.assign(nranks, 0);
-    s.rcnt.assign(nranks, 0);
-    const uint64_t m0 = s.ptr[s.bounds[rank]], m1 = s.ptr[s.bounds[rank + 1]];
-    for (uint64_t idx = m0; idx < m1; ++idx) {
-        const int q = owner(s.perm[idx]);
-        if (q != rank) s.scnt[q]++;
-    }
-    s.soff.assign(nranks, 0);
+    // send area: [stage][peer] segments, each in rating order
     size_t off = 0;
-    for (int k = 0; k < nranks; ++k) {
-        s.soff[k] = off;
-        off += s.scnt[k];
+    for (size_t p = 0; p < P; ++p) {
+        Side::Stage& g = *s.stg[p];
+        g.scnt.assign(nranks, 0);
+        for (uint64_t idx = s.ptr[g.r0]; idx < s.ptr[g.r1]; ++idx) {
+            const int q = owner(s.perm[idx]);
+            if (q != rank) g.scnt[q]++;
+        }
+        g.soff.assign(nranks, 0);
+        for (int k = 0; k < nranks; ++k) {
+            g.soff[k] = off;
+            off += g.scnt[k];
+        }
     }
     s.nsend = off;
     s.perm2.assign(s.perm.begin(), s.perm.end());
-    std::vector<size_t> fill(s.soff);
-    for (uint64_t idx = m0; idx < m1; ++idx) {
-        const int q = owner(s.perm[idx]);
-        if (q != rank) s.perm2[idx] = (uint32_t)(N + fill[q]++);
+    for (size_t p = 0; p < P; ++p) {
+        Side::Stage& g = *s.stg[p];
+        std::vector<size_t> fill(g.soff);
+        for (uint64_t idx = s.ptr[g.r0]; idx < s.ptr[g.r1]; ++idx) {
+            const int q = owner(s.perm[idx]);
+            if (q != rank) s.perm2[idx] = (uint32_t)(N + fill[q]++);
+        }
     }
+    // receive area: what rank k's stage p sends here, in k's rating order, [stage][peer]
     s.unpack.clear();
-    s.roff.assign(nranks, 0);
-    for (int k = 0; k < nranks; ++k) {  // what rank k sends here, in k's rating order
-        s.roff[k] = s.unpack.size();
-        if (k == rank) continue;
-        for (uint64_t idx = s.ptr[s.bounds[k]]; idx < s.ptr[s.bounds[k + 1]]; ++idx)
-            if (owner(s.perm[idx]) == rank) s.unpack.push_back(s.perm[idx]);
-        s.rcnt[k] = s.unpack.size() - s.roff[k];
+    for (size_t p = 0; p < P; ++p) {
+        Side::Stage& g = *s.stg[p];
+        g.roff.assign(nranks, 0);
+        g.rcnt.assign(nranks, 0);
+        g.rbeg = s.unpack.size();
+        for (int k = 0; k < nranks; ++k) {
+            g.roff[k] = s.unpack.size();
+            if (k == rank) continue;
+            for (uint64_t idx = s.ptr[s.sbounds[k][p]]; idx < s.ptr[s.sbounds[k][p + 1]]; ++idx)
+                if (owner(s.perm[idx]) == rank) s.unpack.push_back(s.perm[idx]);
+            g.rcnt[k] = s.unpack.size() - g.roff[k];
+        }
+        g.rend = s.unpack.size();
     }
     s.nrecv = s.unpack.size();
     if (N + s.nsend >= 0xffffffffull) fail(SBMF_E_ARG, "too many ratings for the 32-bit residual exchange");
@@ -165,24 +192,48 @@ static void partition_bounds(const uint32_t* ptr, uint32_t R, int nranks, uint64
         bounds[k] = std::max<uint64_t>(bounds[k - 1], row);
     }
 }
-static void partition(Side& s, int nranks, int rank) {
+static void partition(Side& s, int nranks, int rank, uint32_t nstages) {
     s.bounds.assign(nranks + 1, 0);
     partition_bounds(s.ptr.data(), (uint32_t)s.ptr.size() - 1, nranks, s.bounds.data());
     s.r0 = (uint32_t)s.bounds[rank];
     s.r1 = (uint32_t)s.bounds[rank + 1];
+    // every rank's block cut into nstages nnz-balanced stages (known to every rank:
+    // the exchange of stage p involves every rank's stage p)
+    s.sbounds.assign(nranks, std::vector<uint64_t>(nstages + 1, 0));
+    for (int k = 0; k < nranks; ++k) {
+        const uint64_t b0 = s.bounds[k], b1 = s.bounds[k + 1];
+        std::vector<uint64_t>& sb = s.sbounds[k];
+        sb[0] = b0;
+        for (uint32_t p = 1; p <= nstages; ++p) {
+            uint64_t row = b1;
+            if (p < nstages) {
+                const double target = s.ptr[b0] + (double)(s.ptr[b1] - s.ptr[b0]) * p / nstages;
+                row = (uint64_t)(std::lower_bound(s.ptr.begin() + b0, s.ptr.begin() + b1 + 1,
+                                                  (uint32_t)std::llround(target)) - s.ptr.begin());
+                row = std::min<uint64_t>(std::max<uint64_t>(row, b0), b1);
+            }
+            sb[p] = std::max<uint64_t>(sb[p - 1], row);
+        }
+    }
+    s.stg.clear();
+    for (uint32_t p = 0; p < nstages; ++p) {
+        s.stg.emplace_back(new Side::Stage);
+        s.stg.back()->r0 = (uint32_t)s.sbounds[rank][p];
+        s.stg.back()->r1 = (uint32_t)s.sbounds[rank][p + 1];
+    }
 }
 
 static const int KIND_STREAM = GK_NUM;  // 5: streaming kernel, whole rows (row bin: every streaming row)
 static const int KIND_RK0 = GK_NUM + 1;  // 6..9
 static const int KIND_GRAM = 10;         // Gram route
 
-static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stream_thr, bool f64, bool wide,
-                       bool big = false) {
-    for (auto& b : s.bin_rows) b.clear();
-    s.gitems.clear();
-    s.grows.clear();
-    std::vector<uint32_t> order(s.r1 - s.r0);
-    std::iota(order.begin(), order.end(), s.r0);
+static void build_bins(const Side& s, Side::Stage& g, uint32_t gram_thr, int row_kernel, uint32_t stream_thr,
+                       bool f64, bool wide, bool big = false) {
+    for (auto& b : g.bin_rows) b.clear();
+    g.gitems.clear();
+    g.grows.clear();
+    std::vector<uint32_t> order(g.r1 - g.r0);
+    std::iota(order.begin(), order.end(), g.r0);
     auto deg = [&](uint32_t r) { return s.ptr[r + 1] - s.ptr[r]; };
     // heaviest first: blocks are dispatched roughly in index order, so the
     // longest rows start earliest (LPT)
@@ -191,27 +242,27 @@ static void build_bins(Side& s, uint32_t gram_thr, int row_kernel, uint32_t stre
     for (uint32_t r : order) {
         const uint32_t d = deg(r);
         if (row_kernel == 0 && d > stream_thr && d <= gram_thr) {
-            s.bin_rows[KIND_STREAM].push_back(r);
+            g.bin_rows[KIND_STREAM].push_back(r);
             continue;
         }
         if (d > gram_thr || d > RK_MAXDEG[RK_NUM - 1]) {
-            GramRow gr{r, (uint32_t)s.gitems.size(), 0};
+            GramRow gr{r, (uint32_t)g.gitems.size(), 0};
             for (uint32_t o = 0; o < d; o += chunk) {
-                s.gitems.push_back(GramItem{r, s.ptr[r] + o, std::min(chunk, d - o), (uint32_t)s.gitems.size()});
+                g.gitems.push_back(GramItem{r, s.ptr[r] + o, std::min(chunk, d - o), (uint32_t)g.gitems.size()});
                 gr.nslab++;
             }
-            s.grows.push_back(gr);
+            g.grows.push_back(gr);
             continue;
         }
         if (row_kernel == 0) {
             int kind = GK_W4;
             while (d > gk_maxdeg(kind, f64, wide, big)) ++kind;
-            s.bin_rows[kind].push_back(r);
+            g.bin_rows[kind].push_back(r);
             continue;
         }
         int kind = RK_W2;
         while (d > RK_MAXDEG[kind]) ++kind;
-        s.bin_rows[KIND_RK0 + kind].push_back(r);
+        g.bin_rows[KIND_RK0 + kind].push_back(r);
     }
 }
 
@@ -254,18 +305,23 @@ struct sbmf_ctx {
     // device
     hipStream_t st = nullptr;
     hipEvent_t ev[8] = {};
-    hipEvent_t kev[2][SBMF_NKIND][2] = {};
+    std::vector<hipEvent_t> kevs;  // [stage][side][kind][begin, end] launch timing
+    hipEvent_t& kev(uint32_t stage, int side, int kind, int e) {
+        return kevs[(((size_t)stage * 2 + side) * SBMF_NKIND + kind) * 2 + e];
+    }
+    uint32_t nstages = 1;          // stages per half (see Side::Stage); > 1 only with several ranks
+    hipStream_t stc = nullptr;     // multi-GPU: the exchange of stage p runs here while stage p+1 computes
+    std::vector<hipEvent_t> sev;   // [side][stage]: stage computed (compute stream)
+    hipEvent_t cev[2] = {};        // [side]: the half's exchange done (comm stream)
     DBuf d_uptr, d_upart, d_uperm, d_ur, d_vptr, d_vpart, d_vperm, d_vr;
     DBuf d_U, d_V, d_Eu, d_Ev, d_zU, d_zV, d_hyper;
     DBuf d_rowsq_u, d_rowtr_u, d_rowsq_v, d_rowtr_v;
-    DBuf d_bins_u[NBIN], d_bins_v[NBIN];
-    DBuf d_gitems_u, d_grows_u, d_gitems_v, d_grows_v, d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
+    DBuf d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
     DBuf d_colpart, d_res, d_scratch;
 
     bool kprof = false; // SBMF_KPROF=1: streaming-kernel phase cycles printed per sweep
     int kprof_set = 0;  // SBMF_KPROF_SET: which streaming launch of a half is stamped (0: the 8-wave one)
     DBuf d_kprof;
-    DBuf d_stasks[2][2], d_xrows[2][2];  // [side][stream set]
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
     DBuf d_xslabs, d_xtotals, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
@@ -369,8 +425,12 @@ static void prepare_T(sbmf_ctx* c) {
         c->users.perm[pos_u[x]] = pos_v[x];
         c->items.perm[pos_v[x]] = pos_u[x];
     }
-    partition(c->users, c->nranks, c->rank);
-    partition(c->items, c->nranks, c->rank);
+    // stages per half: the multi-GPU exchange of a stage overlaps the next stage's
+    // compute; one rank needs no exchange (SBMF_STAGES overrides, for tests)
+    c->nstages = c->nranks > 1 ? 4u : 1u;
+    if (const char* e = std::getenv("SBMF_STAGES")) c->nstages = std::max(1, std::min(16, std::atoi(e)));
+    partition(c->users, c->nranks, c->rank, c->nstages);
+    partition(c->items, c->nranks, c->rank, c->nstages);
     if (c->nranks > 1) {
         build_exchange(c->users, c->items, c->nranks, c->rank);  // user half -> item order
         build_exchange(c->items, c->users, c->nranks, c->rank);  // item half -> user order
@@ -389,14 +449,16 @@ static void prepare_T(sbmf_ctx* c) {
     else
         thr = cf.gram_threshold ? std::min(cf.gram_threshold, RK_MAXDEG[RK_NUM - 1]) : RK_MAXDEG[RK_NUM - 1];
     const bool wide = !(cf.tune & 8u);  // f64 rows <= 64 ratings on one wave (default)
-    build_bins(c->users, thr, (int)cf.row_kernel, sthr, f64, wide, gbig);
-    build_bins(c->items, thr, (int)cf.row_kernel, sthr, f64, wide, gbig);
+    for (Side* sd : {&c->users, &c->items})
+        for (auto& g : sd->stg) build_bins(*sd, *g, thr, (int)cf.row_kernel, sthr, f64, wide, gbig);
     // multi-wave Gram-block bins: ceil(deg / ratings-per-wave) waves per row,
     // contiguous sub-ranges since each bin is degree-descending
     for (Side* sd : {&c->users, &c->items})
+        for (auto& gp : sd->stg)
         for (int k = GK_B2; k < GK_NUM; ++k) {
-            sd->gsub[k].clear();
-            const std::vector<uint32_t>& rows = sd->bin_rows[k];
+            Side::Stage& g = *gp;
+            g.gsub[k].clear();
+            const std::vector<uint32_t>& rows = g.bin_rows[k];
             const uint32_t per_wave = f64 ? 32 : 64;
             for (uint32_t i = 0; i < rows.size();) {
                 const uint32_t d = sd->ptr[rows[i] + 1] - sd->ptr[rows[i]];
@@ -405,7 +467,7 @@ static void prepare_T(sbmf_ctx* c) {
                 while (j < rows.size() &&
                        std::max(2u, (sd->ptr[rows[j] + 1] - sd->ptr[rows[j]] + per_wave - 1) / per_wave) == nw)
                     ++j;
-                sd->gsub[k].push_back({nw, i, j - i});
+                g.gsub[k].push_back({nw, i, j - i});
                 i = j;
             }
         }
@@ -434,11 +496,12 @@ static void prepare_T(sbmf_ctx* c) {
                                 !(cf.tune & (64u | 128u | 0x20000u | 0x2000000u | 0x8000000u));
             const uint32_t shyb = item16 ? 1024u : hyb;
             const uint32_t stunes[2] = {tunes[0], item16 ? cf.tune | 0x20000u : tunes[1]};
+            for (auto& gp : sd->stg) {
             std::vector<uint32_t> rows[2];
-            for (uint32_t r : sd->bin_rows[KIND_STREAM])  // degree-descending
+            for (uint32_t r : gp->bin_rows[KIND_STREAM])  // degree-descending
                 rows[shyb && sd->ptr[r + 1] - sd->ptr[r] > shyb ? 1 : 0].push_back(r);
             for (int k = 0; k < 2; ++k) {
-                Side::StreamSet& S = sd->ss[k];
+                Side::StreamSet& S = gp->ss[k];
                 S.tune = stunes[k];
                 // task capacity: the kernel's on-chip maximum, or smaller if split_chunk asks
                 S.cmax = gstream_cmax<T>(S.tune);
@@ -446,6 +509,7 @@ static void prepare_T(sbmf_ctx* c) {
                 const int per_cu =
                     std::max(1, std::min(gstream_wg_target(S.tune), gstream_blocks_per_cu<T>(S.cmax, S.tune)));
                 build_stream_tasks(*sd, S, rows[k], (uint32_t)(dev_cus * per_cu), nblk);
+            }
             }
         }
     }
@@ -470,10 +534,9 @@ static void prepare_T(sbmf_ctx* c) {
     upload(c->d_vpart, c->items.part, st);
     upload(c->d_vperm, c->items.perm, st);
     upload(c->d_vr, to_T<T>(c->items.r), st);
-    for (int k = 0; k < NBIN; ++k) {
-        upload(c->d_bins_u[k], c->users.bin_rows[k], st);
-        upload(c->d_bins_v[k], c->items.bin_rows[k], st);
-    }
+    for (Side* sd : {&c->users, &c->items})
+        for (auto& g : sd->stg)
+            for (int k = 0; k < NBIN; ++k) upload(g->d_bins[k], g->bin_rows[k], st);
     {  // residual recompute tasks over the own item rows
         Side& s = c->items;
         s.rtasks.clear();
@@ -488,14 +551,15 @@ static void prepare_T(sbmf_ctx* c) {
         c->d_rtsq.alloc(std::max<size_t>(s.rtasks.size(), 1) * sizeof(double));
     }
     size_t nx = 0, nr = 0;  // split-row slots of the largest stream set (the sets run one after another)
-    for (int sd = 0; sd < 2; ++sd)
-        for (int k = 0; k < 2; ++k) {
-            const Side::StreamSet& S = (sd ? c->items : c->users).ss[k];
-            upload(c->d_stasks[sd][k], S.stasks, st);
-            upload(c->d_xrows[sd][k], S.xrows, st);
-            nx = std::max<size_t>(nx, S.nxchunk);
-            nr = std::max<size_t>(nr, S.xrows.size());
-        }
+    for (Side* sd : {&c->users, &c->items})
+        for (auto& g : sd->stg)
+            for (int k = 0; k < 2; ++k) {
+                const Side::StreamSet& S = g->ss[k];
+                upload(g->d_stasks[k], S.stasks, st);
+                upload(g->d_xrows[k], S.xrows, st);
+                nx = std::max<size_t>(nx, S.nxchunk);
+                nr = std::max<size_t>(nr, S.xrows.size());
+            }
     {
         c->d_xslabs.alloc(std::max<size_t>(nx, 1) * nblk * (16 * 16 + 16) * sizeof(double));
         c->d_xcnt.alloc((nr * nblk + 1) * sizeof(uint32_t));  // + the task-queue head
@@ -507,14 +571,16 @@ static void prepare_T(sbmf_ctx* c) {
         c->d_xtimeout.alloc(sizeof(uint32_t));
         HIPCHK(hipMemsetAsync(c->d_xtimeout.p, 0, sizeof(uint32_t), st));
     }
-    upload(c->d_gitems_u, c->users.gitems, st);
-    upload(c->d_grows_u, c->users.grows, st);
-    upload(c->d_gitems_v, c->items.gitems, st);
-    upload(c->d_grows_v, c->items.grows, st);
+    size_t nslab = 0, ngrow = 0;  // Gram-route slabs of the largest stage (the stages run one after another)
+    for (Side* sd : {&c->users, &c->items})
+        for (auto& g : sd->stg) {
+            upload(g->d_gitems, g->gitems, st);
+            upload(g->d_grows, g->grows, st);
+            nslab = std::max(nslab, g->gitems.size());
+            ngrow = std::max(ngrow, g->grows.size());
+        }
     const uint32_t Kt = (c->K + 15) / 16 * 16;
     const size_t SL = (size_t)Kt * Kt + Kt;
-    const size_t nslab = std::max(c->users.gitems.size(), c->items.gitems.size());
-    const size_t ngrow = std::max(c->users.grows.size(), c->items.grows.size());
     c->d_slabs.alloc((nslab + ngrow) * SL * sizeof(double));
     c->d_delta.alloc(std::max<size_t>(ngrow, 1) * c->Kp * sizeof(T));
     c->d_chunk_sq.alloc(std::max<size_t>(nslab, 1) * sizeof(double));
@@ -623,6 +689,12 @@ static void prepare_T(sbmf_ctx* c) {
         c->d_kprof.alloc(96 * sizeof(unsigned long long));
         HIPCHK(hipMemset(c->d_kprof.p, 0, 96 * sizeof(unsigned long long)));
     }
+    for (hipEvent_t e : c->kevs) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->sev) (void)hipEventDestroy(e);
+    c->kevs.assign((size_t)c->nstages * 2 * SBMF_NKIND * 2, nullptr);
+    c->sev.assign((size_t)2 * c->nstages, nullptr);
+    for (hipEvent_t& e : c->kevs) HIPCHK(hipEventCreate(&e));
+    for (hipEvent_t& e : c->sev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->sweep = 0;
     c->collected = 0;
     fill_kernel_bytes(c);
@@ -872,32 +944,31 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
 }
 
 template <typename T>
-static void run_half(sbmf_ctx* c, bool users) {
+static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     Side& s = users ? c->users : c->items;
+    Side::Stage& g = *s.stg[stage];
     HalfArgs<T> a = half_args<T>(c, users);
     hipStream_t st = c->st;
-    DBuf* bins = users ? c->d_bins_u : c->d_bins_v;
     const int sd = users ? 0 : 1;
-    if (!s.gitems.empty()) {
-        HIPCHK(hipEventRecord(c->kev[sd][KIND_GRAM][0], st));
-        HIPCHK(launch_gram<T>((users ? c->d_gitems_u : c->d_gitems_v).as<GramItem>(), (uint32_t)s.gitems.size(),
-                              (users ? c->d_grows_u : c->d_grows_v).as<GramRow>(), (uint32_t)s.grows.size(),
-                              c->d_slabs.as<double>(), c->d_delta.as<T>(), c->d_chunk_sq.as<double>(),
-                              a.row_tr ? c->d_chunk_tr.as<double>() : nullptr, a, st));
-        HIPCHK(hipEventRecord(c->kev[sd][KIND_GRAM][1], st));
+    if (!g.gitems.empty()) {
+        HIPCHK(hipEventRecord(c->kev(stage, sd, KIND_GRAM, 0), st));
+        HIPCHK(launch_gram<T>(g.d_gitems.as<GramItem>(), (uint32_t)g.gitems.size(), g.d_grows.as<GramRow>(),
+                              (uint32_t)g.grows.size(), c->d_slabs.as<double>(), c->d_delta.as<T>(),
+                              c->d_chunk_sq.as<double>(), a.row_tr ? c->d_chunk_tr.as<double>() : nullptr, a, st));
+        HIPCHK(hipEventRecord(c->kev(stage, sd, KIND_GRAM, 1), st));
         c->timing.n_launch += 4;
     }
     for (int k = NBIN - 1; k >= 0; --k) {
-        if (s.bin_rows[k].empty()) continue;
-        HIPCHK(hipEventRecord(c->kev[sd][k][0], st));
+        if (g.bin_rows[k].empty()) continue;
+        HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
         if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
-            for (const auto& g : s.gsub[k])
-                HIPCHK(launch_gblock_nw<T>((int)g[0], bins[k].as<uint32_t>() + g[1], g[2], a, st));
+            for (const auto& gs : g.gsub[k])
+                HIPCHK(launch_gblock_nw<T>((int)gs[0], g.d_bins[k].as<uint32_t>() + gs[1], gs[2], a, st));
         } else if (k < GK_NUM)
-            HIPCHK(launch_gblock<T>(k, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
+            HIPCHK(launch_gblock<T>(k, g.d_bins[k].as<uint32_t>(), (uint32_t)g.bin_rows[k].size(), a, st));
         else if (k == KIND_STREAM) {
             for (int set = 0; set < 2; ++set) {
-                const Side::StreamSet& S = s.ss[set];
+                const Side::StreamSet& S = g.ss[set];
                 if (S.stasks.empty()) continue;
                 SplitSync sy{};
                 sy.slabs = c->d_xslabs.as<double>();
@@ -913,13 +984,13 @@ static void run_half(sbmf_ctx* c, bool users) {
                 sy.prof = c->kprof && set == c->kprof_set ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
                 HalfArgs<T> as = a;
                 as.tune = S.tune;
-                HIPCHK(launch_gstream<T>(c->d_stasks[sd][set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
-                                         c->d_xrows[sd][set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, st));
+                HIPCHK(launch_gstream<T>(g.d_stasks[set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
+                                         g.d_xrows[set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, st));
             }
         }
         else
-            HIPCHK(launch_rows<T>(k - KIND_RK0, bins[k].as<uint32_t>(), (uint32_t)s.bin_rows[k].size(), a, st));
-        HIPCHK(hipEventRecord(c->kev[sd][k][1], st));
+            HIPCHK(launch_rows<T>(k - KIND_RK0, g.d_bins[k].as<uint32_t>(), (uint32_t)g.bin_rows[k].size(), a, st));
+        HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
         c->timing.n_launch++;
     }
 }
@@ -934,14 +1005,20 @@ static void fill_kernel_bytes(sbmf_ctx* c) {
     const uint64_t tsz = tsize(c);
     for (int sd = 0; sd < 2; ++sd) {
         const Side& s = sd == 0 ? c->users : c->items;
-        for (int k = 0; k < NBIN; ++k) {
-            c->timing.kern_bytes[sd][k] = alg_bytes(s, s.bin_rows[k], c->K, tsz);
-            c->timing.kern_rows[sd][k] = (uint32_t)s.bin_rows[k].size();
+        for (int k = 0; k < SBMF_NKIND; ++k) {
+            c->timing.kern_bytes[sd][k] = 0;
+            c->timing.kern_rows[sd][k] = 0;
         }
-        std::vector<uint32_t> gr;
-        for (const GramRow& g : s.grows) gr.push_back(g.row);
-        c->timing.kern_bytes[sd][KIND_GRAM] = alg_bytes(s, gr, c->K, tsz);
-        c->timing.kern_rows[sd][KIND_GRAM] = (uint32_t)gr.size();
+        for (const auto& g : s.stg) {  // a kind's launches summed over the stages
+            for (int k = 0; k < NBIN; ++k) {
+                c->timing.kern_bytes[sd][k] += alg_bytes(s, g->bin_rows[k], c->K, tsz);
+                c->timing.kern_rows[sd][k] += (uint32_t)g->bin_rows[k].size();
+            }
+            std::vector<uint32_t> gr;
+            for (const GramRow& x : g->grows) gr.push_back(x.row);
+            c->timing.kern_bytes[sd][KIND_GRAM] += alg_bytes(s, gr, c->K, tsz);
+            c->timing.kern_rows[sd][KIND_GRAM] += (uint32_t)gr.size();
+        }
     }
 }
 
@@ -951,32 +1028,69 @@ static double ev_ms(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
-// After a half (users: scatter into item order, E_v; items: into E_u): send
-// the residuals bound for other ranks' rows, unpack what arrives.
-// `with` (optional) issues the half's block broadcasts first, all in one RCCL
-// group (collectives only: they run concurrently); the residual send/receive
-// keeps a group of its own; the unpack follows it.
+// After a stage of a half (users: scatter into item order, E_v; items: into
+// E_u): send the stage's residuals bound for other ranks' rows, unpack what
+// every rank's same stage sends here.  `with(p)` (optional) issues the stage's
+// block broadcasts first, all in one RCCL group (collectives only: they run
+// concurrently); the residual send/receive keeps a group of its own; the
+// unpack follows it.  Offsets are taken relative to the stage's segments, so a
+// transfer touches only this stage's part of the send and receive areas.
 template <typename T, class F>
-static void exchange_residuals(sbmf_ctx* c, bool users, hipStream_t st, F&& with) {
+static void exchange_stage(sbmf_ctx* c, bool users, uint32_t p, hipStream_t st, F&& with) {
     if (c->nranks <= 1) return;
     const Side& s = users ? c->users : c->items;
+    const Side::Stage& g = *s.stg[p];
     DBuf& E = users ? c->d_Ev : c->d_Eu;
+    auto rel = [](const std::vector<size_t>& v, size_t base) {
+        std::vector<size_t> b(v);
+        for (size_t& x : b) x = (x - base) * sizeof(T);
+        return b;
+    };
     auto bytes = [](const std::vector<size_t>& v) {
         std::vector<size_t> b(v);
         for (size_t& x : b) x *= sizeof(T);
         return b;
     };
     c->comm.group_begin();
-    with();
+    with(p);
     c->comm.group_end();
-    c->comm.alltoallv(E.as<T>() + c->tu.size(), bytes(s.soff), bytes(s.scnt), c->d_xrecv.p, bytes(s.roff),
-                      bytes(s.rcnt), st);
-    HIPCHK(launch_unpack<T>(c->d_xrecv.as<T>(), (users ? c->d_uunpack : c->d_vunpack).as<uint32_t>(), s.nrecv,
-                            E.as<T>(), st));
+    const size_t s0 = g.soff.empty() ? 0 : g.soff[0];
+    c->comm.alltoallv(E.as<T>() + c->tu.size() + s0, rel(g.soff, s0), bytes(g.scnt), c->d_xrecv.as<T>() + g.rbeg,
+                      rel(g.roff, g.rbeg), bytes(g.rcnt), st);
+    HIPCHK(launch_unpack<T>(c->d_xrecv.as<T>() + g.rbeg, (users ? c->d_uunpack : c->d_vunpack).as<uint32_t>() + g.rbeg,
+                            g.rend - g.rbeg, E.as<T>(), st));
 }
+// Every stage's residual exchange, on `st` (no broadcasts: the prologue's recompute)
 template <typename T>
 static void exchange_residuals(sbmf_ctx* c, bool users, hipStream_t st) {
-    exchange_residuals<T>(c, users, st, [] {});
+    for (uint32_t p = 0; p < c->nstages; ++p) exchange_stage<T>(c, users, p, st, [](uint32_t) {});
+}
+// Every rank's units of stage p of `s` (its rows [sbounds[k][p], sbounds[k][p+1]))
+static void bcast_stage(sbmf_ctx* c, const Side& s, uint32_t p, void* base, size_t unit_bytes) {
+    std::vector<uint64_t> lo(c->nranks), hi(c->nranks);
+    for (int k = 0; k < c->nranks; ++k) {
+        lo[k] = s.sbounds[k][p];
+        hi[k] = s.sbounds[k][p + 1];
+    }
+    c->comm.bcast_blocks(base, unit_bytes, lo, hi, c->stc);
+}
+// A half's stages, each followed -- on the comm stream, while the next stage
+// computes -- by its exchange; the compute stream then waits for the last one.
+template <typename T, class F>
+static void run_half_pipelined(sbmf_ctx* c, bool users, F&& bcasts) {
+    const int sd = users ? 0 : 1;
+    for (uint32_t p = 0; p < c->nstages; ++p) {
+        run_half<T>(c, users, p);
+        if (c->nranks > 1) HIPCHK(hipEventRecord(c->sev[(size_t)sd * c->nstages + p], c->st));
+    }
+    HIPCHK(hipEventRecord(c->ev[users ? 2 : 4], c->st));
+    if (c->nranks <= 1) return;
+    for (uint32_t p = 0; p < c->nstages; ++p) {
+        HIPCHK(hipStreamWaitEvent(c->stc, c->sev[(size_t)sd * c->nstages + p], 0));
+        exchange_stage<T>(c, users, p, c->stc, bcasts);
+    }
+    HIPCHK(hipEventRecord(c->cev[sd], c->stc));
+    HIPCHK(hipStreamWaitEvent(c->st, c->cev[sd], 0));
 }
 
 template <typename T>
@@ -1137,13 +1251,12 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(launch_bias_rows<T>(c->d_uptr.as<uint32_t>(), c->users.r0, c->users.r1, c->d_Eu.as<T>(),
                                        c->d_bu.as<double>(), c->d_mbu.as<double>(), c->d_sbu.as<double>(),
                                        ref ? c->d_var3u.as<double>() : nullptr, bias_args(c, true, d0), st));
-        run_half<T>(c, true);
-        HIPCHK(hipEventRecord(c->ev[2], st));
-        if (c->nranks > 1)  // fresh U (and b_i) blocks (one RCCL group), then the residuals
-            exchange_residuals<T>(c, true, st, [&] {
-                c->comm.bcast_ranges(c->d_U.p, c->Kp * sizeof(T), c->users.bounds, st);
-                if (c->bias) c->comm.bcast_ranges(c->d_bu.p, sizeof(double), c->users.bounds, st);
-            });
+        // several ranks: each stage's fresh U (and b_i) blocks (one RCCL group), then its
+        // residuals, while the next stage computes
+        run_half_pipelined<T>(c, true, [&](uint32_t p) {
+            bcast_stage(c, c->users, p, c->d_U.p, c->Kp * sizeof(T));
+            if (c->bias) bcast_stage(c, c->users, p, c->d_bu.p, sizeof(double));
+        });
         HIPCHK(hipEventRecord(c->ev[3], st));
         // ---- 4. item half-sweep
         if (!ref)
@@ -1152,15 +1265,13 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(launch_bias_rows<T>(c->d_vptr.as<uint32_t>(), c->items.r0, c->items.r1, c->d_Ev.as<T>(),
                                        c->d_bv.as<double>(), c->d_mbv.as<double>(), c->d_sbv.as<double>(),
                                        ref ? c->d_var3v.as<double>() : nullptr, bias_args(c, false, 0.0), st));
-        run_half<T>(c, false);
-        HIPCHK(hipEventRecord(c->ev[4], st));
-        if (c->nranks > 1)  // fresh V (and b_j) blocks and the per-row sums (one RCCL group), then the residuals
-            exchange_residuals<T>(c, false, st, [&] {
-                c->comm.bcast_ranges(c->d_V.p, c->Kp * sizeof(T), c->items.bounds, st);
-                if (c->bias) c->comm.bcast_ranges(c->d_bv.p, sizeof(double), c->items.bounds, st);
-                c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
-                if (cf.eval_train) c->comm.bcast_ranges(c->d_rowtr_v.p, sizeof(double), c->items.bounds, st);
-            });
+        // fresh V (and b_j) blocks and the per-row sums (one RCCL group), then the residuals
+        run_half_pipelined<T>(c, false, [&](uint32_t p) {
+            bcast_stage(c, c->items, p, c->d_V.p, c->Kp * sizeof(T));
+            if (c->bias) bcast_stage(c, c->items, p, c->d_bv.p, sizeof(double));
+            bcast_stage(c, c->items, p, c->d_rowsq_v.p, sizeof(double));
+            if (cf.eval_train) bcast_stage(c, c->items, p, c->d_rowtr_v.p, sizeof(double));
+        });
         HIPCHK(hipEventRecord(c->ev[5], st));
         if (overlap) {  // the next sweep's prologue kernels, ahead of the evaluation
             prologue_gpu(c->sweep + 1);
@@ -1240,10 +1351,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 for (int k = 0; k < 7; ++k) tot += (double)h[8 * sd + k];
                 if (tot == 0) continue;
                 std::fprintf(stderr, "[kprof] sweep %u %s %s (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep,
-                             (cf.tune & 64u) ? "gstream" : "gres", sd ? "items" : "users", S.ss[c->kprof_set].sgrid,
-                             S.ss[c->kprof_set].stasks.size());
+                             (cf.tune & 64u) ? "gstream" : "gres", sd ? "items" : "users", S.stg[0]->ss[c->kprof_set].sgrid,
+                             S.stg[0]->ss[c->kprof_set].stasks.size());
                 for (int k = 0; k < 7; ++k)
-                    std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.ss[c->kprof_set].sgrid / 1e6,
+                    std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.stg[0]->ss[c->kprof_set].sgrid / 1e6,
                                  100.0 * (double)h[8 * sd + k] / tot);
                 std::fprintf(stderr, "\n");
                 if (cf.tune & 64u) continue;
@@ -1276,8 +1387,13 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         for (int sd = 0; sd < 2; ++sd) {
             const Side& sdd = sd == 0 ? c->users : c->items;
             for (int k = 0; k < SBMF_NKIND; ++k) {
-                const bool ran = k == KIND_GRAM ? !sdd.gitems.empty() : !sdd.bin_rows[k].empty();
-                c->timing.kern_ms[sd][k] = ran ? ev_ms(c->kev[sd][k][0], c->kev[sd][k][1]) : 0.0;
+                double ms = 0.0;
+                for (uint32_t p = 0; p < c->nstages; ++p) {
+                    const Side::Stage& g = *sdd.stg[p];
+                    const bool ran = k == KIND_GRAM ? !g.gitems.empty() : !g.bin_rows[k].empty();
+                    if (ran) ms += ev_ms(c->kev(p, sd, k, 0), c->kev(p, sd, k, 1));
+                }
+                c->timing.kern_ms[sd][k] = ms;
             }
         }
         info.ms_sweep = ev_ms(c->ev[0], c->ev[5]);
@@ -1297,10 +1413,13 @@ sbmf_ctx::~sbmf_ctx() {
     if (h_pre) (void)hipHostFree(h_pre);
     for (auto& e : ev)
         if (e) (void)hipEventDestroy(e);
-    for (auto& a : kev)
-        for (auto& b : a)
-            for (auto& e : b)
-                if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : kevs)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : sev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : cev)
+        if (e) (void)hipEventDestroy(e);
+    if (stc) (void)hipStreamDestroy(stc);
     if (st) (void)hipStreamDestroy(st);
 }
 
@@ -1398,10 +1517,9 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     c->hi = cfg->clamp_hi;
     c->sd_is_var = cfg->quirks == SBMF_QUIRKS_NONE ? 0 : 1;
     HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->stc, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
-    for (auto& a : c->kev)
-        for (auto& b : a)
-            for (auto& e : b) HIPCHK(hipEventCreate(&e));
+    for (auto& e : c->cev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     *out = c.release();
     API_END(ctx)
 }

@@ -261,6 +261,18 @@ int on_sweep(const sbmf_sweep_info* in, void* user) {
     return 0;
 }
 
+// Every output file is closed and the context destroyed by now: leave without the
+// exit-time destructors.  Under rocprofv3 (ROCm 7.2) the HIP module destructors run
+// from __cxa_finalize after the profiler has finalized and fault (SIGSEGV after the
+// profile is written: profiles/r03_rocprof_teardown.txt); skipping them changes
+// nothing else -- the process's device memory goes with it.
+int quick_exit_after_flush(int rc) {
+    std::cout.flush();
+    std::cerr.flush();
+    std::fflush(nullptr);
+    std::_Exit(rc);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -472,7 +484,7 @@ int main(int argc, char** argv) {
         sbmf_free_ratings(&te);
     } catch (const std::exception& e) {
         std::cerr << "ERROR: " << e.what() << std::endl;
-        return 1;
+        return quick_exit_after_flush(1);
     }
-    return 0;
+    return quick_exit_after_flush(0);
 }

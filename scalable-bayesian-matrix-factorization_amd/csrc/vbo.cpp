@@ -352,9 +352,13 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         std::vector<VTask> tasks;  // row0 relative to the batch's first row
     };
     std::vector<Part> pu(NB), pi(NB);
+    // lane-group size of a row: the fewest lanes (a power of two, 1..256) that hold its
+    // cases at VB_CASES_PER_LANE per lane in registers -- a user row of a batch (a few
+    // cases) takes one lane, so a task covers up to 256 rows and every lane has several
+    // independent loads in flight
     auto lg_of = [](uint32_t n) {
-        uint32_t lg = 2;
-        while (lg < 8 && (1u << lg) < n) ++lg;
+        uint32_t lg = 0;
+        while (lg < 8 && (VB_CASES_PER_LANE << lg) < n) ++lg;
         return lg;
     };
     auto group = [&](uint32_t b, bool users, std::vector<uint32_t>& off, Part& P) {
@@ -385,7 +389,7 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         for (const VRow& r : rows) cls[lg_of(r.len)]++;
         uint32_t at = 0;
         std::vector<uint32_t> first(10, 0);
-        for (int lg = 8; lg >= 2; --lg) {
+        for (int lg = 8; lg >= 0; --lg) {
             first[lg] = at;
             at += cls[lg];
         }

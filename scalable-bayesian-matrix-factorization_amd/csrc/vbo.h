@@ -61,7 +61,9 @@ struct VGItem {
     uint32_t attr, n;
 };
 // One 256-thread block of an update pass: rows [row0, row0 + nrows) of the
-// orientation's row list, each owned by 2^lg lanes (256 >> lg rows at most).
+// orientation's row list, each owned by 2^lg lanes (256 >> lg rows at most);
+// a lane keeps up to VB_CASES_PER_LANE of its row's cases in registers.
+constexpr uint32_t VB_CASES_PER_LANE = 4;
 struct VTask {
     uint32_t row0, nrows, lg, pad;
 };

@@ -169,19 +169,19 @@ __device__ __forceinline__ double gsum(double x, int G, double* red) {
         for (int m = G >> 1; m > 0; m >>= 1) x += __shfl_xor(x, m, G);
         return __shfl(x, 0, G);
     }
-    const int base = threadIdx.x & ~(G - 1), li = threadIdx.x & (G - 1);
-    red[threadIdx.x] = x;
+    // 128 / 256 lanes: each wave's butterfly sum, then the waves' sums in wave order
+    // (one barrier pair instead of one per tree level)
+    for (int m = 32; m > 0; m >>= 1) x += __shfl_xor(x, m, 64);
+    const int w = threadIdx.x >> 6, w0 = (threadIdx.x & ~(G - 1)) >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = x;
     __syncthreads();
-    for (int m = G >> 1; m > 0; m >>= 1) {
-        if (li < m) red[threadIdx.x] += red[threadIdx.x + m];
-        __syncthreads();
-    }
-    const double t = red[base];
+    double t = red[w0];
+    for (int k = 1; k < G / 64; ++k) t += red[w0 + k];
     __syncthreads();
     return t;
 }
 
-constexpr int MC = 4;  // cases a lane keeps in registers between the two passes of a row
+constexpr int MC = VB_CASES_PER_LANE;  // cases a lane keeps in registers between the two passes of a row
 #ifndef SBMF_VB_OCC
 #define SBMF_VB_OCC 6  // waves per SIMD the update kernels are compiled for
 #endif

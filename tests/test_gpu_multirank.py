@@ -207,3 +207,50 @@ def test_config4_ml20m_k200_two_ranks_match_single_rank(tmp_path):
         assert np.array_equal(z["rmse"], rmse1) and np.array_equal(z["tau"], tau1), r
     print("config 4 split: item blocks %s, user blocks %s, %d ratings cross the cut, rmse %s" % (
         list(ib), list(ub), cross, rmse1))
+
+
+@pytest.mark.parametrize("stages", [2, 3])
+def test_stages_do_not_change_the_chain(ml100k, stages):
+    """One rank with its half-sweeps cut into stages (the multi-GPU pipeline's unit:
+    each stage's launches, then its exchange while the next stage computes) gives the
+    single-stage chain bit for bit: a row's draws do not depend on which launch runs it."""
+    tr, te = ml100k
+    out = []
+    for st in (1, stages):
+        old = os.environ.get("SBMF_STAGES")
+        os.environ["SBMF_STAGES"] = str(st)
+        try:
+            L = FMLearnSBPMF(num_factor=30, seed=6, rng="philox", quirks="bias2", stream_threshold=40, split_chunk=64)
+            L.set_data(Data(*tr), Data(*te))
+        finally:
+            if old is None:
+                del os.environ["SBMF_STAGES"]
+            else:
+                os.environ["SBMF_STAGES"] = old
+        L.learn(sweeps=3)
+        out.append((L.factors(), L.biases(), L.rmse_trajectory, L.timing().kern_rows[1][5]))
+        L.close()
+    (U1, V1), b1, r1, n1 = out[0]
+    (U2, V2), b2, r2, n2 = out[1]
+    assert np.array_equal(U1, U2) and np.array_equal(V1, V2) and np.array_equal(r1, r2)
+    assert np.array_equal(b1[0], b2[0]) and np.array_equal(b1[1], b2[1]) and b1[2] == b2[2]
+    assert n1 == n2 > 0  # the streaming rows are counted over the stages
+
+
+@pytest.mark.parametrize("stages", [1, 3])
+def test_ranks_with_stage_count(ml100k, tmp_path, stages):
+    """2 ranks (host comm backend) with the exchange unpipelined (1 stage) and cut into 3
+    stages: both equal the single-rank chain bit for bit."""
+    K, sweeps, seed = 30, 3, 6
+    tr, te = ml100k
+    L = FMLearnSBPMF(num_factor=K, seed=seed, rng="philox")
+    L.set_data(Data(*tr), Data(*te))
+    L.learn(sweeps=sweeps)
+    U1, V1 = L.factors()
+    rmse1 = L.rmse_trajectory
+    L.close()
+    outs = _run_ranks(tmp_path, 2, [str(K), str(sweeps), str(seed), "philox", "0", "final"],
+                      env={"SBMF_STAGES": str(stages)})
+    for r in range(2):
+        z = np.load(outs[r])
+        assert np.array_equal(z["U"], U1) and np.array_equal(z["V"], V1) and np.array_equal(z["rmse"], rmse1)
