@@ -516,10 +516,14 @@ def main():
 
 
 if __name__ == "__main__":
+    from sbmf import _lib as _sbmf_lib
+    if os.environ.get("SBMF_EXIT") != "normal":
+        # before anything starts the HIP runtime: leave through libsbmf's exit handler
+        # after rocprofv3's (if any) has written its output -- the HIP runtime's library
+        # finalizer faults under rocprofv3 (ROCm 7.2, profiles/r03_rocprof_teardown.txt)
+        _sbmf_lib.exit_guard(1)
     main()
-    # every result is printed and the library unloaded: leave without the interpreter's
-    # exit-time teardown (under rocprofv3 the HIP runtime's exit-time destructors fault after
-    # the profiler has finalized -- profiles/r03_rocprof_teardown.txt)
     sys.stdout.flush()
     sys.stderr.flush()
-    os._exit(0)
+    if os.environ.get("SBMF_EXIT") != "normal":
+        _sbmf_lib.exit_guard(0)

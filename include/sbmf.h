@@ -281,6 +281,15 @@ void sbmf_free_ratings(sbmf_ratings* r);
  * bounds: [nranks+1]; rank k owns rows [bounds[k], bounds[k+1]). */
 int sbmf_partition_rows(const uint32_t* ptr, uint32_t R, int nranks, uint64_t* bounds);
 
+/* --- process exit (host only; not a reference interface) -------------------------------- */
+/* First call: registers an exit handler that ends the process with _Exit(rc) once
+ * the exit handlers registered after it (a profiler's, e.g. rocprofv3's output
+ * writer) have run, skipping the shared-library finalizers -- under rocprofv3
+ * (ROCm 7.2) the HIP runtime's finalizer faults after the profiler has finished
+ * (profiles/r03_rocprof_teardown.txt).  Call it before the first HIP call; later
+ * calls only set rc.  The handler belongs to libsbmf: do not dlclose it after. */
+int sbmf_exit_guard(int rc);
+
 /* --- test hooks ---------------------------------------------------------------------------- */
 /* The host glibc-compatible stream (reference mode): n values of rand(),
  * ran_gaussian() and ran_gamma(shape) for seed. */

@@ -1447,6 +1447,25 @@ extern "C" {
 
 int sbmf_abi_version(void) { return SBMF_ABI_VERSION; }
 
+namespace {
+int g_exit_rc = 1;
+bool g_exit_guarded = false;
+void exit_guard_handler() {
+    std::fflush(nullptr);
+    std::_Exit(g_exit_rc);
+}
+}  // namespace
+int sbmf_exit_guard(int rc) {
+    g_exit_rc = rc;
+    if (g_exit_guarded) return SBMF_OK;
+    if (std::atexit(exit_guard_handler) != 0) {
+        g_err = "sbmf_exit_guard: atexit failed";
+        return SBMF_E_STATE;
+    }
+    g_exit_guarded = true;
+    return SBMF_OK;
+}
+
 int sbmf_config_default(sbmf_config* c) {
     if (!c) return SBMF_E_ARG;
     std::memset(c, 0, sizeof *c);

@@ -261,21 +261,24 @@ int on_sweep(const sbmf_sweep_info* in, void* user) {
     return 0;
 }
 
-// Every output file is closed and the context destroyed by now: leave without the
-// exit-time destructors.  Under rocprofv3 (ROCm 7.2) the HIP module destructors run
-// from __cxa_finalize after the profiler has finalized and fault (SIGSEGV after the
-// profile is written: profiles/r03_rocprof_teardown.txt); skipping them changes
-// nothing else -- the process's device memory goes with it.
-int quick_exit_after_flush(int rc) {
+// Leave through sbmf_exit_guard's handler (registered at main's start, before the
+// first HIP call): a profiler's exit handlers (rocprofv3 writes its output there)
+// still run, the HIP runtime's library finalizer -- which faults under rocprofv3
+// on ROCm 7.2 -- does not (profiles/r03_rocprof_teardown.txt).  Every file is
+// closed and the context destroyed by then.  SBMF_EXIT=normal: plain exit.
+bool g_guarded = false;
+int leave(int rc) {
     std::cout.flush();
     std::cerr.flush();
-    std::fflush(nullptr);
-    std::_Exit(rc);
+    if (g_guarded) (void)sbmf_exit_guard(rc);
+    return rc;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
+    const char* em = std::getenv("SBMF_EXIT");
+    g_guarded = !(em && std::strcmp(em, "normal") == 0) && sbmf_exit_guard(1) == SBMF_OK;
     try {
         CmdLine cl(argc, argv);
         std::cout << "----------------------------------------------------------------------------\n"
@@ -325,7 +328,7 @@ int main(int argc, char** argv) {
         cl.reg("row_kernel", "0: MFMA Gram-block kernels (default) | 1: per-coordinate wave-reduction kernels");
         if (cl.has("help") || argc == 1) {
             cl.print_help();
-            return 0;
+            return leave(0);
         }
         cl.check();
         const std::string task = cl.get("task", "");
@@ -484,7 +487,7 @@ int main(int argc, char** argv) {
         sbmf_free_ratings(&te);
     } catch (const std::exception& e) {
         std::cerr << "ERROR: " << e.what() << std::endl;
-        return quick_exit_after_flush(1);
+        return leave(1);
     }
-    return quick_exit_after_flush(0);
+    return leave(0);
 }

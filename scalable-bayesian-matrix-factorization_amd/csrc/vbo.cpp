@@ -46,13 +46,13 @@ struct VBLayout {
     std::vector<VRow> urows, irows;    // every batch's rows, batch-major
     std::vector<VTask> utasks, itasks; // 256-thread tasks over those rows
     std::vector<uint32_t> urow0, irow0, utask0, itask0, bsize, bbase;
-    std::vector<uint32_t> u2i, upart, i2u, ipart;  // [N] per entry of each order
+    std::vector<uint32_t> upart, i2u, ipart;  // [N] per entry of each order (i2u: the user-order position)
     std::vector<float> ur;                          // [N] target per user-order entry
     // several ranks: bsize / bbase count this rank's cases; gbsize the whole batch;
     // gitems the batch's items over all ranks (entries [gitem0[b], gitem0[b+1]))
     std::vector<uint32_t> gbsize, gitem0;
     std::vector<VGItem> gitems;
-    DBuf d_urows, d_irows, d_utasks, d_itasks, d_u2i, d_upart, d_i2u, d_ipart, d_ur, d_gitems;
+    DBuf d_urows, d_irows, d_utasks, d_itasks, d_upart, d_i2u, d_ipart, d_ur, d_gitems;
 };
 
 struct VBLearner {
@@ -72,7 +72,8 @@ struct VBLearner {
     uint32_t built = 0;              // epochs whose layout exists (ready or being built)
     // device
     DBuf d_mu_v, d_sg_v, d_nm_v, d_ns_v, d_mu_w, d_sg_w, d_nm_w, d_ns_w, d_rho_w, d_rho_v, d_t_w, d_t_v, d_cc;
-    DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_ETu, d_ETv, d_part;
+    DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_ETu, d_part;
+    DBuf d_D, d_VS;  // per item: the last item pass's pending deltas; per user: fresh {mean, variance} of f
     size_t part_cap = 0;  // doubles in d_part
     DBuf d_tu, d_ti, d_tr, d_pred, d_tpart;
     VBTables tb{};
@@ -83,7 +84,7 @@ struct VBLearner {
     std::vector<uint64_t> ubounds;     // [R + 1] user ranges of every rank
     std::vector<uint8_t> mine;         // [N] case belongs to an owned user
     uint32_t gmax = 0;                 // largest per-batch item count
-    DBuf d_send, d_recv, d_sums, d_recvg, d_delta;
+    DBuf d_send, d_recv, d_sums, d_recvg;
     double last_rmse = NAN, last_alpha = NAN;
     double ms_layout = 0.0;
     uint32_t n_launch = 0;
@@ -100,7 +101,7 @@ struct VBLearner {
     void build_layout(VBLayout& L, uint32_t ep);
     void run(uint32_t epochs, sbmf_sweep_cb cb, void* user);
     void item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_, const uint32_t* i2u_,
-                   int factor, uint32_t f, double2* ETv, double2* ETu);
+                   int factor, uint32_t f, const double2* ETu);
     void sync_users();
 };
 
@@ -210,7 +211,9 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     HIPCHK(hipMemsetAsync(d_muT.p, 0, d_muT.bytes, st));
     HIPCHK(hipMemsetAsync(d_sgT.p, 0, d_sgT.bytes, st));
     d_ETu.alloc((size_t)std::max(NL, 1u) * sizeof(double2));  // {e, t} per (own) case, user-grouped epoch order
-    d_ETv.alloc((size_t)std::max(NL, 1u) * sizeof(double2));  // item-grouped epoch order
+    d_D.alloc((size_t)std::max(J, 1u) * sizeof(double4));
+    d_VS.alloc((size_t)std::max(I, 1u) * sizeof(double2));
+    HIPCHK(hipMemsetAsync(d_D.p, 0, d_D.bytes, st));
     if (R > 1) {
         d_send.alloc((size_t)(K + 2) * sizeof(double));
         d_recv.alloc((size_t)R * (K + 2) * sizeof(double));
@@ -240,6 +243,7 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     tb.K = K;
     tb.p = p;
     tb.N = N;
+    tb.I = I;
     shuffle.resize(N);
     for (uint32_t x = 0; x < N; ++x) shuffle[x] = x + 1;
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
@@ -346,7 +350,7 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
     L.upart.resize(NL);
     L.ipart.resize(NL);
     L.ur.resize(NL);
-    // per batch and orientation: rows in attribute order, then stably by lane-group size
+    // per batch and orientation: rows stably sorted by lane-group size, records in row order
     struct Part {
         std::vector<VRow> rows;
         std::vector<VTask> tasks;  // row0 relative to the batch's first row
@@ -366,25 +370,12 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         const uint32_t c0 = L.bbase[b], c1 = L.bbase[b + 1];
         std::fill(off.begin(), off.end(), 0u);
         for (uint32_t x = c0; x < c1; ++x) off[users ? tu[bcase[x]] : ti[bcase[x]]]++;
-        std::vector<VRow> rows;
-        uint32_t run = c0;
-        for (uint32_t a = 0; a < nattr; ++a) {
-            const uint32_t n = off[a];
-            if (!n) continue;
-            rows.push_back(VRow{users ? a : I + a, run, n, (!users && R > 1) ? gidx[(size_t)b * J + a] : 0u});
-            off[a] = run;  // becomes the fill position
-            run += n;
-        }
-        std::vector<uint32_t>& pos = users ? upos : ipos;
-        std::vector<uint32_t>& part = users ? L.upart : L.ipart;
-        for (uint32_t x = c0; x < c1; ++x) {
-            const uint32_t l = bcase[x];
-            const uint32_t q = off[users ? tu[l] : ti[l]]++;
-            pos[l] = q;
-            part[q] = users ? I + ti[l] : tu[l];
-            if (users) L.ur[q] = (float)tr[l];
-        }
-        // counting sort by lane-group size, largest first
+        std::vector<VRow> rows;  // attribute order; positions assigned after the sort
+        for (uint32_t a = 0; a < nattr; ++a)
+            if (off[a]) rows.push_back(VRow{users ? a : I + a, 0u, off[a], (!users && R > 1) ? gidx[(size_t)b * J + a] : 0u});
+        // counting sort by lane-group size, largest first (stable: attribute order within
+        // a size); the rows' records follow the sorted order, so a task's rows are one
+        // contiguous run of records (coalesced reads, whole-line writes from one block)
         std::vector<uint32_t> cls(10, 0);
         for (const VRow& r : rows) cls[lg_of(r.len)]++;
         uint32_t at = 0;
@@ -395,6 +386,21 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         }
         P.rows.resize(rows.size());
         for (const VRow& r : rows) P.rows[first[lg_of(r.len)]++] = r;
+        uint32_t run = c0;
+        for (VRow& r : P.rows) {
+            r.start = run;
+            off[users ? r.attr : r.attr - I] = run;  // becomes the fill position
+            run += r.len;
+        }
+        std::vector<uint32_t>& pos = users ? upos : ipos;
+        std::vector<uint32_t>& part = users ? L.upart : L.ipart;
+        for (uint32_t x = c0; x < c1; ++x) {
+            const uint32_t l = bcase[x];
+            const uint32_t q = off[users ? tu[l] : ti[l]]++;
+            pos[l] = q;
+            part[q] = users ? I + ti[l] : tu[l];
+            if (users) L.ur[q] = (float)tr[l];
+        }
         P.tasks.clear();
         for (uint32_t r = 0; r < P.rows.size();) {
             const uint32_t lg = lg_of(P.rows[r].len);
@@ -437,39 +443,31 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
     };
     concat(pu, L.urows, L.urow0, L.utasks, L.utask0);
     concat(pi, L.irows, L.irow0, L.itasks, L.itask0);
-    L.u2i.resize(NL);
     L.i2u.resize(NL);
     parallel_chunks(N, [&](unsigned, uint32_t lo, uint32_t hi) {
         for (uint32_t l = lo; l < hi; ++l)
-            if (mine[l]) {
-                L.u2i[upos[l]] = ipos[l];
-                L.i2u[ipos[l]] = upos[l];
-            }
+            if (mine[l]) L.i2u[ipos[l]] = upos[l];
     });
 }
 
 // Several ranks: one item pass of a batch (the update_w biases, factor == 0,
 // or update_v of factor f): local sums -> all-gather -> the same update on
-// every rank -> deltas forwarded to the local cases.
+// every rank, its deltas to D for the next user pass.
 void VBLearner::item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_,
-                          const uint32_t* i2u_, int factor, uint32_t f, double2* ETv, double2* ETu) {
+                          const uint32_t* i2u_, int factor, uint32_t f, const double2* ETu) {
     const uint32_t nG = L.gitem0[b + 1] - L.gitem0[b];
     if (nG == 0) return;  // every rank sees the same global list
     double2* sums = d_sums.as<double2>();
     HIPCHK(hipMemsetAsync(sums, 0, (size_t)nG * sizeof(double2), st));
     if (factor)
-        HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st, 1, sums, nullptr));
+        HIPCHK(vbo_item_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETu, d_VS.as<double2>(),
+                          d_D.as<double4>(), sums, st));
     else
-        HIPCHK(vbo_update_w(it_, nit, ir_, i2u_, 0, tb, ETv, ETu, st, 1, sums, nullptr));
+        HIPCHK(vbo_item_w(it_, nit, ir_, i2u_, tb, ETu, d_D.as<double4>(), sums, st));
     comm->allgather(sums, (size_t)nG * sizeof(double2), d_recvg.p, st);
-    double4* delta = d_delta.as<double4>();
-    HIPCHK(vbo_item_update(L.d_gitems.as<VGItem>() + L.gitem0[b], nG, d_recvg.as<double2>(), R, factor, f, tb, delta,
-                           st));
-    if (factor)
-        HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st, 2, nullptr, delta));
-    else
-        HIPCHK(vbo_update_w(it_, nit, ir_, i2u_, 0, tb, ETv, ETu, st, 2, nullptr, delta));
-    n_launch += 3;
+    HIPCHK(vbo_item_update(L.d_gitems.as<VGItem>() + L.gitem0[b], nG, d_recvg.as<double2>(), R, factor, f, tb,
+                           d_D.as<double4>(), st));
+    n_launch += 1;  // vbo_item_update (the item pass itself is counted by run)
 }
 
 // Several ranks: every rank's owned user means (factors and biases) to every rank
@@ -499,7 +497,6 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         auto grow = [](DBuf& d, size_t bytes) { d.ensure(std::max<size_t>(bytes, 1)); };
         grow(L.d_urows, L.urows.size() * sizeof(L.urows[0]));
         grow(L.d_irows, L.irows.size() * sizeof(L.irows[0]));
-        grow(L.d_u2i, L.u2i.size() * sizeof(L.u2i[0]));
         grow(L.d_upart, L.upart.size() * sizeof(L.upart[0]));
         grow(L.d_ur, L.ur.size() * sizeof(L.ur[0]));
         grow(L.d_i2u, L.i2u.size() * sizeof(L.i2u[0]));
@@ -510,12 +507,10 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             grow(L.d_gitems, L.gitems.size() * sizeof(L.gitems[0]));
             d_sums.ensure((size_t)std::max(gmax, 1u) * sizeof(double2));
             d_recvg.ensure((size_t)R * std::max(gmax, 1u) * sizeof(double2));
-            d_delta.ensure((size_t)std::max(gmax, 1u) * sizeof(double4));
         }
         const auto h2 = std::chrono::steady_clock::now();
         upload_grow(L.d_urows, L.urows, st);
         upload_grow(L.d_irows, L.irows, st);
-        upload_grow(L.d_u2i, L.u2i, st);
         upload_grow(L.d_upart, L.upart, st);
         upload_grow(L.d_ur, L.ur, st);
         upload_grow(L.d_i2u, L.i2u, st);
@@ -536,7 +531,8 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         n_launch = 0;
         HIPCHK(hipEventRecord(ev[0], st));
         double2* ETu = d_ETu.as<double2>();
-        double2* ETv = d_ETv.as<double2>();
+        double4* D = d_D.as<double4>();
+        double2* VS = d_VS.as<double2>();
         double* part = d_part.as<double>();
         const VRow* ur_ = L.d_urows.as<VRow>();
         const VRow* ir_ = L.d_irows.as<VRow>();
@@ -557,21 +553,26 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             const VTask* ut = L.d_utasks.as<VTask>() + L.utask0[b];
             const VTask* it_ = L.d_itasks.as<VTask>() + L.itask0[b];
             const uint32_t nut = L.utask0[b + 1] - L.utask0[b], nit = L.itask0[b + 1] - L.itask0[b];
-            // every pass reads its own order and writes the other one: users ETu -> ETv, items ETv -> ETu
-            const uint32_t* u2i_ = L.d_u2i.as<uint32_t>();
+            const uint32_t* upart_ = L.d_upart.as<uint32_t>();
+            const uint32_t* ipart_ = L.d_ipart.as<uint32_t>();
             const uint32_t* i2u_ = L.d_i2u.as<uint32_t>();
-            HIPCHK(vbo_update_w(ut, nut, ur_, u2i_, 1, tb, ETu, ETv, st));
+            // users update their records in place; items read them (through i2u) and leave
+            // their updates in D, which the next user pass (or the flush) applies
+            HIPCHK(vbo_user_w(ut, nut, ur_, tb, ETu, st));
             if (R > 1)
-                item_pass(L, b, it_, nit, ir_, i2u_, 0, 0, ETv, ETu);
+                item_pass(L, b, it_, nit, ir_, i2u_, 0, 0, ETu);
             else
-                HIPCHK(vbo_update_w(it_, nit, ir_, i2u_, 0, tb, ETv, ETu, st));
+                HIPCHK(vbo_item_w(it_, nit, ir_, i2u_, tb, ETu, D, nullptr, st));
+            int pend = VB_PEND_W;
             for (uint32_t f = 0; f < K; ++f) {
-                HIPCHK(vbo_update_v(ut, nut, ur_, u2i_, L.d_upart.as<uint32_t>(), f, tb, ETu, ETv, st));
+                HIPCHK(vbo_user_v(ut, nut, ur_, upart_, f, pend, f - 1, tb, D, ETu, VS, st));
                 if (R > 1)
-                    item_pass(L, b, it_, nit, ir_, i2u_, 1, f, ETv, ETu);
+                    item_pass(L, b, it_, nit, ir_, i2u_, 1, f, ETu);
                 else
-                    HIPCHK(vbo_update_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETv, ETu, st));
+                    HIPCHK(vbo_item_v(it_, nit, ir_, i2u_, ipart_, f, tb, ETu, VS, D, nullptr, st));
+                pend = VB_PEND_V;
             }
+            HIPCHK(vbo_user_flush(ut, nut, ur_, upart_, pend, K - 1, tb, D, ETu, st));
             if (R > 1) {  // the blends from every rank's alpha sum and user-range sig sums
                 HIPCHK(vbo_hyper_local(ETu + L.bbase[b], B, tb, u0, u1, part, part_cap, d_send.as<double>(), st));
                 comm->allgather(d_send.p, (K + 2) * sizeof(double), d_recv.p, st);
@@ -579,7 +580,7 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             } else {
                 HIPCHK(vbo_hyper(ETu + L.bbase[b], B, tb, part, st));
             }
-            n_launch += 2 * K + 12;
+            n_launch += 2 * K + 12;  // transposes 2, predict, w0 2, bias passes 2, factor passes 2K, flush, hyper 4
         }
         // the next epoch's shuffle and layout, on the host while this epoch runs
         // (the reference stream after this epoch's shuffle is exactly the next one's)

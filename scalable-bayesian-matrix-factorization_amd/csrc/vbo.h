@@ -44,6 +44,7 @@ struct VBTables {
     double* sigma_v;                    // [K] prior precisions of the factors
     VBScal* scal;
     uint32_t K, p, N;                   // N: train ratings (the reference's _size)
+    uint32_t I;                         // users (attributes [0, I)); items are [I, p)
 };
 
 // [K][p] -> [p][Kp] (attribute-major rows for the prediction gathers)
@@ -53,7 +54,7 @@ hipError_t vbo_transpose(const double* src, double* dst, uint32_t K, uint32_t Kp
 hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* part, const float* r, const double* muT,
                        const double* sgT, const VBTables& tb, uint32_t Kp, double2* ET, hipStream_t st);
 // update_w0 (:586-633): the global bias blend; its deltas are applied to e / t
-// by the user pass of vbo_update_w (apply_w0 = 1)
+// by vbo_user_w
 hipError_t vbo_update_w0(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
 // Several ranks: an item present in a batch (any rank's cases) and its global
 // case count there; a rank's item rows carry their index in this list in VRow.pad.
@@ -67,22 +68,33 @@ constexpr uint32_t VB_CASES_PER_LANE = 4;
 struct VTask {
     uint32_t row0, nrows, lg, pad;
 };
-// update_w (:635-710) over the rows of one orientation
-// (ETin in the rows' own order, ETout in the other order: ETout[xperm[q]]).
-// mode 0: sums and update in one pass; several ranks, item rows: mode 1 writes
-// each row's local sums to sums[VRow.pad], mode 2 applies delta[VRow.pad]
-// (from vbo_item_update) to the row's local cases.
-hipError_t vbo_update_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm, int apply_w0,
-                        const VBTables& tb, const double2* ETin, double2* ETout, hipStream_t st, int mode = 0,
-                        double2* sums = nullptr, const double4* delta = nullptr);
-// update_v (:712-800) of factor f over the rows of one orientation (mode as above)
-hipError_t vbo_update_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm,
-                        const uint32_t* part, uint32_t f, const VBTables& tb, const double2* ETin, double2* ETout,
-                        hipStream_t st, int mode = 0, double2* sums = nullptr, const double4* delta = nullptr);
+// The passes of a batch keep one {e, t} record per case, in the batch's
+// user-grouped order (ET).  A user pass reads and writes its rows' records in
+// place; an item pass gathers e through i2u (a case's user-grouped position)
+// and writes nothing per case: its e / t updates are left per item in D
+// (double4 {dmu, dsg, dm2, ok}, indexed by item) and applied by the next user
+// pass (pend) or by vbo_user_flush before the hyperparameter sums.
+enum { VB_PEND_NONE = 0, VB_PEND_W = 1, VB_PEND_V = 2 };  // pending: none | bias pass | factor pass
+// update_w (:635-710) of the users (update_w0's deltas applied first)
+hipError_t vbo_user_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const VBTables& tb, double2* ET,
+                      hipStream_t st);
+// update_v (:712-800) of factor f for the users, after the pending item updates
+// (pend; factor fp for VB_PEND_V); VS[user] = its new {mean, variance} of f
+hipError_t vbo_user_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, uint32_t f, int pend,
+                      uint32_t fp, const VBTables& tb, const double4* D, double2* ET, double2* VS, hipStream_t st);
+hipError_t vbo_user_flush(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, int pend,
+                          uint32_t fp, const VBTables& tb, const double4* D, double2* ET, hipStream_t st);
+// update_w / update_v of factor f for the items (D[item] = the deltas); several
+// ranks: sums != null -> each row's local sums to sums[VRow.pad] only
+hipError_t vbo_item_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const VBTables& tb,
+                      const double2* ET, double4* D, double2* sums, hipStream_t st);
+hipError_t vbo_item_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const uint32_t* part,
+                      uint32_t f, const VBTables& tb, const double2* ET, const double2* VS, double4* D, double2* sums,
+                      hipStream_t st);
 // several ranks: the items of a batch updated from every rank's local sums
 // (recv [R][nG], rank order; factor f, or the biases when factor == 0)
 hipError_t vbo_item_update(const VGItem* gi, uint32_t nG, const double2* recv, int R, int factor, uint32_t f,
-                           const VBTables& tb, double4* delta, hipStream_t st);
+                           const VBTables& tb, double4* D, hipStream_t st);
 // several ranks: update_w0's local sum (out[0]) and the update from every rank's (recv[R])
 hipError_t vbo_w0_local(const double2* ET, uint32_t B, const VBTables& tb, double* part, double* out, hipStream_t st);
 hipError_t vbo_w0_final(const double* recv, int R, uint32_t B, const VBTables& tb, hipStream_t st);

@@ -3,23 +3,24 @@
 //
 // The work unit is an attribute row of one batch: a user (or an item) and the
 // batch's cases that carry it.  A group of G lanes owns a row, G the power of
-// two (4..256) that covers the row's cases one per lane, so a 256-thread
-// block holds 64 four-case user rows or one popular item; rows longer than
-// 4 x 256 loop.  Each block reads a task {first row, rows, log2 G} built on
-// the host.  A lane keeps its cases' values in registers between the
-// row's two passes (sums, then residual updates).  The row's
-// natural-parameter sums are fixed-order group reductions.  A case's
-// residual e and variance term t travel as one 16-byte {e, t} record in two
-// copies: ETu in the epoch's user-grouped order and ETv in its item-grouped
-// order.  A pass reads its own order (consecutive lanes, consecutive
-// records) and writes the other order through the case's position there
-// (xperm), which is the order the next pass reads -- the same scatter
-// scheme as the Gibbs half-sweeps.  Every case belongs to exactly one user
-// row and one item row, so the rows of one pass never share a case.
-// In an update_v pass the partner values (item factors for user rows, the
-// fresh user factors for item rows) are read from the factor column f of the
-// f-major tables, which stays in L2.  Every reduction has a fixed order, so
-// results are bitwise repeatable run to run.
+// two (1..256) that covers the row's cases VB_CASES_PER_LANE per lane, so a
+// 256-thread block holds up to 256 short user rows or one popular item; longer
+// rows loop.  Each block reads a task {first row, rows, log2 G} built on the
+// host.  The row's natural-parameter sums are fixed-order group reductions.
+// A case's residual e and variance term t travel as one 16-byte {e, t}
+// record, kept in ONE copy in the batch's user-grouped order.  A user pass
+// reads its rows' records (consecutive lanes, consecutive records), keeps
+// them in registers between the row's two traversals (sums, then updates) and
+// writes them back in place.  An item pass gathers e through the case's
+// user-grouped position (i2u) and the partner user's fresh {mean, variance}
+// (VS, one 16-byte record), and writes nothing per case: its e / t updates
+// depend on the case only through the user's values, so they are left per
+// item (D) and applied by the next user pass -- the same operations in the
+// same order as applying them at once.  No pass scatters 16-byte records
+// over a batch-sized array (the r03 PMC passes: that scatter and the split
+// {mean}/{variance} gathers cost 3-5x the algorithmic bytes in HBM traffic).
+// Item factors of column f for the user pass stay in L2.  Every reduction
+// has a fixed order, so results are bitwise repeatable run to run.
 //
 // With x = 1 for every feature the reference's cached sums collapse:
 // q - x mu = partner mean, t.q - x^2 sigma = partner variance, t.z - ... =
@@ -186,88 +187,97 @@ constexpr int MC = VB_CASES_PER_LANE;  // cases a lane keeps in registers betwee
 #define SBMF_VB_OCC 6  // waves per SIMD the update kernels are compiled for
 #endif
 
-// update_w (:635-710) for the rows of one orientation.  apply_w0: first add
-// update_w0's deltas to the row's cases (the user pass touches every case once).
-// MODE (several ranks, item rows; VRow.pad = the item's index g in the batch's
-// global item list): VB_FUSED sums and updates in one pass (one rank);
-// VB_PART writes the row's local sums {e1, e2} to sums[g]; VB_FWD applies the
-// deltas k_item_w left in delta[g] to the local cases.
-enum { VB_FUSED = 0, VB_PART = 1, VB_FWD = 2 };
-template <int MODE>
-__global__ __launch_bounds__(256, SBMF_VB_OCC) void k_update_w(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
-                                                   const uint32_t* __restrict__ xperm, int apply_w0, VBTables tb,
-                                                   const double2* __restrict__ ETin, double2* __restrict__ ETout,
-                                                   double2* __restrict__ sums, const double4* __restrict__ delta) {
-    __shared__ double red[256];
+enum { VB_FUSED = 0, VB_PART = 1 };  // item passes: update here | local sums (several ranks)
+
+// The item pass's e / t updates, applied by the user pass after it: D[item] =
+// {dmu, dsg, dm2, ok} (k_item_wp / k_item_vp / vbo_item_update).  Bias pass
+// (update_w :700-708): e += dmu, t += dsg; factor pass fp (update_v :790-798):
+// e += h dmu, t += (h1 + h^2) dsg, t += h1 dm2, h and h1 the user's mean and
+// variance of factor fp (final since that factor's user pass).  The same
+// operations in the same order as applying them in the item pass.
+template <int PEND>
+__device__ __forceinline__ void vb_pending(double2& o, const double4& d, double hp, double sp) {
+    if (PEND == VB_PEND_NONE || d.w == 0.0) return;
+    if (PEND == VB_PEND_W) {
+        o.x += d.x;
+        o.y += d.y;
+    } else {
+        o.x += hp * d.x;
+        o.y += (sp + hp * hp) * d.y;
+        o.y += sp * d.z;
+    }
+}
+
+// the block's task: rows [row0, row0 + nrows), 2^lg lanes per row
+struct VLane {
+    VRow rw;
+    uint32_t n;
+    int G, ci;
+    bool live;
+};
+__device__ __forceinline__ VLane vb_lane(const VTask* __restrict__ tasks, const VRow* __restrict__ rows) {
     const VTask tk = tasks[blockIdx.x];
-    const int G = 1 << tk.lg;
+    VLane L;
+    L.G = 1 << tk.lg;
     const uint32_t g = threadIdx.x >> tk.lg;
-    const int ci = threadIdx.x & (G - 1);
-    const bool live = g < tk.nrows;  // G >= 128 blocks hold one row: always live
-    const VRow rw = rows[tk.row0 + (live ? g : 0)];
-    const uint32_t a = rw.attr, n = live ? rw.len : 0;
+    L.ci = threadIdx.x & (L.G - 1);
+    L.live = g < tk.nrows;  // G >= 128 blocks hold one row: always live
+    L.rw = rows[tk.row0 + (L.live ? g : 0)];
+    L.n = L.live ? L.rw.len : 0;
+    return L;
+}
+
+// update_w (:635-710) of the batch's users, update_w0's deltas applied first
+// (the user pass touches every case once); e / t updated in place.
+__global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_w(const VTask* __restrict__ tasks,
+                                                             const VRow* __restrict__ rows, VBTables tb,
+                                                             double2* __restrict__ ET) {
+    __shared__ double red[256];
+    const VLane L = vb_lane(tasks, rows);
+    const int G = L.G, ci = L.ci;
+    const uint32_t a = L.rw.attr, n = L.n, q0 = L.rw.start;
     const double alpha = tb.scal->alpha, sigma_w = tb.scal->sigma_w;
-    const double dm = apply_w0 ? tb.scal->d_mu0 : 0.0, ds = apply_w0 ? tb.scal->d_sg0 : 0.0;
+    const double dm = tb.scal->d_mu0, ds = tb.scal->d_sg0;
     const double md = tb.mu_w[a], sd = tb.sg_w[a], mo = tb.nm_w[a], so = tb.ns_w[a], rho = tb.rho_w[a];
     const double cc = (double)tb.cc[a];
     const double cs = ((1 - rho) * so) + rho * (sigma_w + alpha * cc * 1.0);
     double2 et[MC];
-    uint32_t xp[MC];
     double e1 = 0.0, e2 = 0.0;
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
-            et[j] = ETin[rw.start + x];
-            xp[j] = xperm[rw.start + x];
-            if (apply_w0) {
-                et[j].x = et[j].x + dm;
-                et[j].y = et[j].y + ds;
-            }
+            et[j] = ET[q0 + x];
+            et[j].x = et[j].x + dm;
+            et[j].y = et[j].y + ds;
             e1 += ((1 - rho) * mo) + rho * cc * alpha * (et[j].x + md);
             e2 += cs;
         }
     }
     for (uint32_t x = ci + MC * G; x < n; x += G) {  // rows longer than MC * G
-        double e = ETin[rw.start + x].x;
-        if (apply_w0) e = e + dm;
+        const double e = ET[q0 + x].x + dm;
         e1 += ((1 - rho) * mo) + rho * cc * alpha * (e + md);
         e2 += cs;
     }
-    bool ok;
-    double dmu, dsg;
-    if (MODE != VB_FWD) {
-        e1 = gsum(e1, G, red);
-        e2 = gsum(e2, G, red);
+    e1 = gsum(e1, G, red);
+    e2 = gsum(e2, G, red);
+    if (!L.live) return;  // after the last block-wide reduction
+    const uint32_t tw = tb.t_w[a] + n;
+    const double nm = e1 / n, ns = e2 / n;
+    const double mu = nm / ns;
+    double sigma = 1 / ns;
+    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+    const bool ok = !(std::isnan(mu) || std::isinf(mu));
+    if (ci == 0) {
+        tb.t_w[a] = tw;
+        tb.rho_w[a] = pow((double)(1 + tw), -0.5);
+        tb.nm_w[a] = nm;
+        tb.ns_w[a] = ns;
+        tb.sg_w[a] = sigma;
+        tb.mu_w[a] = ok ? mu : md;
     }
-    if (!live) return;  // after the last block-wide reduction
-    if (MODE == VB_PART) {
-        if (ci == 0) sums[rw.pad] = make_double2(e1, e2);
-        return;
-    } else if (MODE == VB_FWD) {
-        const double4 d = delta[rw.pad];
-        ok = d.w != 0.0;
-        dmu = d.x;
-        dsg = d.y;
-    } else {
-        const uint32_t tw = tb.t_w[a] + n;
-        const double nm = e1 / n, ns = e2 / n;
-        const double mu = nm / ns;
-        double sigma = 1 / ns;
-        if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
-        ok = !(std::isnan(mu) || std::isinf(mu));
-        if (ci == 0) {
-            tb.t_w[a] = tw;
-            tb.rho_w[a] = pow((double)(1 + tw), -0.5);
-            tb.nm_w[a] = nm;
-            tb.ns_w[a] = ns;
-            tb.sg_w[a] = sigma;
-            tb.mu_w[a] = ok ? mu : md;
-        }
-        // the reference reverts a non-finite mean and leaves e, t alone (the w0 deltas stay)
-        dmu = ok ? md - mu : 0.0;
-        dsg = ok ? sigma - sd : 0.0;
-    }
+    // the reference reverts a non-finite mean and leaves e, t alone (the w0 deltas stay)
+    const double dmu = ok ? md - mu : 0.0, dsg = ok ? sigma - sd : 0.0;
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
@@ -277,137 +287,272 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_update_w(const VTask* __re
                 o.x += dmu;
                 o.y += dsg;
             }
-            ETout[xp[j]] = o;
+            ET[q0 + x] = o;
         }
     }
     for (uint32_t x = ci + MC * G; x < n; x += G) {
-        double2 o = ETin[rw.start + x];
-        if (apply_w0) {
-            o.x = o.x + dm;
-            o.y = o.y + ds;
-        }
+        double2 o = ET[q0 + x];
+        o.x = o.x + dm;
+        o.y = o.y + ds;
         if (ok) {
             o.x += dmu;
             o.y += dsg;
         }
-        ETout[xperm[rw.start + x]] = o;
+        ET[q0 + x] = o;
     }
 }
 
-// update_v (:712-800) of factor f for the rows of one orientation (MODE as k_update_w)
-template <int MODE>
-__global__ __launch_bounds__(256, SBMF_VB_OCC) void k_update_v(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
-                                                   const uint32_t* __restrict__ xperm, const uint32_t* __restrict__ part,
-                                                   uint32_t f, VBTables tb, const double2* __restrict__ ETin,
-                                                   double2* __restrict__ ETout, double2* __restrict__ sums,
-                                                   const double4* __restrict__ delta) {
+// update_v (:712-800) of factor f for the batch's users: the previous item
+// pass's updates first (PEND), then the sums over the cases with the item
+// factors of column f (L2-resident), the update, and the user's own e / t
+// updates, in place.  VS[user] = the user's new {mean, variance} of f, the
+// record the item pass gathers.
+template <int PEND>
+__global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_v(const VTask* __restrict__ tasks,
+                                                             const VRow* __restrict__ rows,
+                                                             const uint32_t* __restrict__ part, uint32_t f,
+                                                             uint32_t fp, VBTables tb, const double4* __restrict__ D,
+                                                             double2* __restrict__ ET, double2* __restrict__ VS) {
     __shared__ double red[256];
-    const VTask tk = tasks[blockIdx.x];
-    const int G = 1 << tk.lg;
-    const uint32_t g = threadIdx.x >> tk.lg;
-    const int ci = threadIdx.x & (G - 1);
-    const bool live = g < tk.nrows;
-    const VRow rw = rows[tk.row0 + (live ? g : 0)];
-    const uint32_t a = rw.attr, n = live ? rw.len : 0;
+    const VLane L = vb_lane(tasks, rows);
+    const int G = L.G, ci = L.ci;
+    const uint32_t a = L.rw.attr, n = L.n, q0 = L.rw.start, I = tb.I;
     const size_t off = (size_t)f * tb.p;
     double* __restrict__ v = tb.mu_v + off;
     double* __restrict__ s = tb.sg_v + off;
     const double alpha = tb.scal->alpha, svg = tb.sigma_v[f];
     const double md = v[a], sd = s[a], mo = tb.nm_v[off + a], so = tb.ns_v[off + a], rho = tb.rho_v[a];
     const double cc = (double)tb.cc[a];
-    double hh[MC], hs[MC];
+    double hp = 0.0, sp = 0.0;  // the pending factor's user values
+    if (PEND == VB_PEND_V) {
+        hp = tb.mu_v[(size_t)fp * tb.p + a];
+        sp = tb.sg_v[(size_t)fp * tb.p + a];
+    }
+    uint32_t pj[MC];  // partner items (their column-f values re-read from L2 for the updates)
     double2 et[MC];
-    uint32_t xp[MC];  // the other order's positions, fetched with the partners (off the store's critical path)
     double e1 = 0.0, e2 = 0.0;
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
-            const uint32_t pa = part[rw.start + x];
-            xp[j] = xperm[rw.start + x];
-            hh[j] = v[pa];
-            hs[j] = s[pa];
-            et[j] = ETin[rw.start + x];
-            const double h = hh[j];
-            e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + hs[j]));
+            const uint32_t pa = part[q0 + x];
+            pj[j] = pa;
+            const double h = v[pa], h1 = s[pa];
+            et[j] = ET[q0 + x];
+            if (PEND != VB_PEND_NONE) vb_pending<PEND>(et[j], D[pa - I], hp, sp);
+            e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + h1));
             e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (et[j].x + md * h));
         }
     }
     for (uint32_t x = ci + MC * G; x < n; x += G) {
-        const uint32_t q = rw.start + x, pa = part[q];
-        const double h = v[pa], h1 = s[pa], e = ETin[q].x;
+        const uint32_t q = q0 + x, pa = part[q];
+        const double h = v[pa], h1 = s[pa];
+        double2 o = ET[q];
+        if (PEND != VB_PEND_NONE) vb_pending<PEND>(o, D[pa - I], hp, sp);
         e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + h1));
-        e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (e + md * h));
+        e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (o.x + md * h));
     }
-    bool ok;
-    double dmu, dsg, dm2;
-    if (MODE != VB_FWD) {
-        e1 = gsum(e1, G, red);
-        e2 = gsum(e2, G, red);
+    e1 = gsum(e1, G, red);
+    e2 = gsum(e2, G, red);
+    if (!L.live) return;
+    const double nm = e1 / n, ns = e2 / n;
+    const double mu = nm / ns;
+    double sigma = 1 / ns;
+    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+    const bool ok = !(std::isnan(mu) || std::isinf(mu));
+    if (ci == 0) {
+        tb.nm_v[off + a] = nm;
+        tb.ns_v[off + a] = ns;
+        s[a] = sigma;
+        v[a] = ok ? mu : md;
+        VS[a] = make_double2(ok ? mu : md, sigma);
+        if (f == 0) tb.t_v[a] += n;  // the caller's count (:447-450)
     }
-    if (!live) return;
-    if (MODE == VB_PART) {
-        if (ci == 0) sums[rw.pad] = make_double2(e1, e2);
-        return;
-    } else if (MODE == VB_FWD) {
-        const double4 d = delta[rw.pad];
-        ok = d.w != 0.0;
-        dmu = d.x;
-        dsg = d.y;
-        dm2 = d.z;
-    } else {
-        const double nm = e1 / n, ns = e2 / n;
-        const double mu = nm / ns;
-        double sigma = 1 / ns;
-        if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
-        ok = !(std::isnan(mu) || std::isinf(mu));
-        if (ci == 0) {
-            tb.nm_v[off + a] = nm;
-            tb.ns_v[off + a] = ns;
-            s[a] = sigma;
-            v[a] = ok ? mu : md;
-            if (f == 0) tb.t_v[a] += n;  // the caller's count (:447-450)
-        }
-        // a non-finite mean: the reference returns before touching e, t -- forwarded unchanged
-        dmu = ok ? md - mu : 0.0;
-        dsg = ok ? sigma - sd : 0.0;
-        dm2 = ok ? mu * mu - md * md : 0.0;
-    }
+    // a non-finite mean: the reference returns before touching e, t
+    const double dmu = ok ? md - mu : 0.0, dsg = ok ? sigma - sd : 0.0, dm2 = ok ? mu * mu - md * md : 0.0;
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
             double2 o = et[j];
             if (ok) {
-                const double h = hh[j], h1 = hs[j];
+                const double h = v[pj[j]], h1 = s[pj[j]];
                 o.x += h * dmu;
                 o.y += (h1 + h * h) * dsg;
                 o.y += h1 * dm2;
             }
-            ETout[xp[j]] = o;
+            ET[q0 + x] = o;
         }
     }
     for (uint32_t x = ci + MC * G; x < n; x += G) {
-        const uint32_t q = rw.start + x;
-        double2 o = ETin[q];
+        const uint32_t q = q0 + x, pa = part[q];
+        double2 o = ET[q];
+        if (PEND != VB_PEND_NONE) vb_pending<PEND>(o, D[pa - I], hp, sp);
         if (ok) {
-            const uint32_t pa = part[q];
             const double h = v[pa], h1 = s[pa];
             o.x += h * dmu;
             o.y += (h1 + h * h) * dsg;
             o.y += h1 * dm2;
         }
-        ETout[xperm[q]] = o;
+        ET[q] = o;
     }
+}
+
+// the last item pass's updates of a batch, applied before the hyperparameter sums
+template <int PEND>
+__global__ __launch_bounds__(256) void k_user_flush(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
+                                                    const uint32_t* __restrict__ part, uint32_t fp, VBTables tb,
+                                                    const double4* __restrict__ D, double2* __restrict__ ET) {
+    const VLane L = vb_lane(tasks, rows);
+    const uint32_t a = L.rw.attr;
+    double hp = 0.0, sp = 0.0;
+    if (PEND == VB_PEND_V && L.live) {
+        hp = tb.mu_v[(size_t)fp * tb.p + a];
+        sp = tb.sg_v[(size_t)fp * tb.p + a];
+    }
+    for (uint32_t x = L.ci; x < L.n; x += L.G) {
+        const uint32_t q = L.rw.start + x;
+        double2 o = ET[q];
+        vb_pending<PEND>(o, D[part[q] - tb.I], hp, sp);
+        ET[q] = o;
+    }
+}
+
+// update_w (:635-710) of the batch's items: e gathered from the user-grouped
+// records (i2u: a case's position there), read only.  MODE VB_FUSED: the
+// update, its deltas to D[item]; VB_PART (several ranks): the row's local
+// sums {e1, e2} to sums[VRow.pad].
+template <int MODE>
+__global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_wp(const VTask* __restrict__ tasks,
+                                                              const VRow* __restrict__ rows,
+                                                              const uint32_t* __restrict__ i2u, VBTables tb,
+                                                              const double2* __restrict__ ET,
+                                                              double4* __restrict__ D, double2* __restrict__ sums) {
+    __shared__ double red[256];
+    const VLane L = vb_lane(tasks, rows);
+    const int G = L.G, ci = L.ci;
+    const uint32_t a = L.rw.attr, n = L.n, q0 = L.rw.start;
+    const double alpha = tb.scal->alpha, sigma_w = tb.scal->sigma_w;
+    const double md = tb.mu_w[a], sd = tb.sg_w[a], mo = tb.nm_w[a], so = tb.ns_w[a], rho = tb.rho_w[a];
+    const double cc = (double)tb.cc[a];
+    const double cs = ((1 - rho) * so) + rho * (sigma_w + alpha * cc * 1.0);
+    double ev[MC];
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const uint32_t x = ci + j * G;
+        if (x < n) ev[j] = ET[i2u[q0 + x]].x;
+    }
+    double e1 = 0.0, e2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const uint32_t x = ci + j * G;
+        if (x < n) {
+            e1 += ((1 - rho) * mo) + rho * cc * alpha * (ev[j] + md);
+            e2 += cs;
+        }
+    }
+    for (uint32_t x = ci + MC * G; x < n; x += G) {
+        const double e = ET[i2u[q0 + x]].x;
+        e1 += ((1 - rho) * mo) + rho * cc * alpha * (e + md);
+        e2 += cs;
+    }
+    e1 = gsum(e1, G, red);
+    e2 = gsum(e2, G, red);
+    if (!L.live || ci != 0) return;
+    if (MODE == VB_PART) {
+        sums[L.rw.pad] = make_double2(e1, e2);
+        return;
+    }
+    const uint32_t tw = tb.t_w[a] + n;
+    const double nm = e1 / n, ns = e2 / n;
+    const double mu = nm / ns;
+    double sigma = 1 / ns;
+    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+    const bool ok = !(std::isnan(mu) || std::isinf(mu));
+    tb.t_w[a] = tw;
+    tb.rho_w[a] = pow((double)(1 + tw), -0.5);
+    tb.nm_w[a] = nm;
+    tb.ns_w[a] = ns;
+    tb.sg_w[a] = sigma;
+    tb.mu_w[a] = ok ? mu : md;
+    D[a - tb.I] = ok ? make_double4(md - mu, sigma - sd, 0.0, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+}
+
+// update_v (:712-800) of factor f for the batch's items: per case e (gathered
+// through i2u) and the user's fresh {mean, variance} of f (VS, one 16-byte
+// gather); nothing per case is written.  MODE as k_item_wp.
+template <int MODE>
+__global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_vp(const VTask* __restrict__ tasks,
+                                                              const VRow* __restrict__ rows,
+                                                              const uint32_t* __restrict__ i2u,
+                                                              const uint32_t* __restrict__ part, uint32_t f,
+                                                              VBTables tb, const double2* __restrict__ ET,
+                                                              const double2* __restrict__ VS,
+                                                              double4* __restrict__ D, double2* __restrict__ sums) {
+    __shared__ double red[256];
+    const VLane L = vb_lane(tasks, rows);
+    const int G = L.G, ci = L.ci;
+    const uint32_t a = L.rw.attr, n = L.n, q0 = L.rw.start;
+    const size_t off = (size_t)f * tb.p;
+    double* __restrict__ v = tb.mu_v + off;
+    double* __restrict__ s = tb.sg_v + off;
+    const double alpha = tb.scal->alpha, svg = tb.sigma_v[f];
+    const double md = v[a], sd = s[a], mo = tb.nm_v[off + a], so = tb.ns_v[off + a], rho = tb.rho_v[a];
+    const double cc = (double)tb.cc[a];
+    double ev[MC];
+    double2 hv[MC];
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const uint32_t x = ci + j * G;
+        if (x < n) {
+            ev[j] = ET[i2u[q0 + x]].x;
+            hv[j] = VS[part[q0 + x]];
+        }
+    }
+    double e1 = 0.0, e2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const uint32_t x = ci + j * G;
+        if (x < n) {
+            const double h = hv[j].x;
+            e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + hv[j].y));
+            e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (ev[j] + md * h));
+        }
+    }
+    for (uint32_t x = ci + MC * G; x < n; x += G) {
+        const double e = ET[i2u[q0 + x]].x;
+        const double2 hw = VS[part[q0 + x]];
+        const double h = hw.x;
+        e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + hw.y));
+        e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (e + md * h));
+    }
+    e1 = gsum(e1, G, red);
+    e2 = gsum(e2, G, red);
+    if (!L.live || ci != 0) return;
+    if (MODE == VB_PART) {
+        sums[L.rw.pad] = make_double2(e1, e2);
+        return;
+    }
+    const double nm = e1 / n, ns = e2 / n;
+    const double mu = nm / ns;
+    double sigma = 1 / ns;
+    if (std::isnan(sigma) || std::isinf(sigma)) sigma = sd;
+    const bool ok = !(std::isnan(mu) || std::isinf(mu));
+    tb.nm_v[off + a] = nm;
+    tb.ns_v[off + a] = ns;
+    s[a] = sigma;
+    v[a] = ok ? mu : md;
+    if (f == 0) tb.t_v[a] += n;
+    D[a - tb.I] = ok ? make_double4(md - mu, sigma - sd, mu * mu - md * md, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
 }
 
 // Several ranks: one thread per item g of the batch's global item list; its
 // local sums from every rank (recv[r][g], rank order), its global case count,
-// then exactly k_update_v / k_update_w's update; the deltas go to delta[g] for
-// the VB_FWD pass.  Identical inputs on every rank, so identical results.
+// then exactly k_item_vp / k_item_wp's update; the deltas go to D[item] for
+// the next user pass.  Identical inputs on every rank, so identical results.
 __global__ __launch_bounds__(256) void k_item_v(const VGItem* __restrict__ gi, uint32_t nG,
                                                  const double2* __restrict__ recv, int R, uint32_t f, VBTables tb,
-                                                 double4* __restrict__ delta) {
+                                                 double4* __restrict__ D) {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
     if (g >= nG) return;
     const uint32_t a = gi[g].attr, n = gi[g].n;
@@ -430,11 +575,11 @@ __global__ __launch_bounds__(256) void k_item_v(const VGItem* __restrict__ gi, u
     s[a] = sigma;
     v[a] = ok ? mu : md;
     if (f == 0) tb.t_v[a] += n;
-    delta[g] = ok ? make_double4(md - mu, sigma - sd, mu * mu - md * md, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+    D[a - tb.I] = ok ? make_double4(md - mu, sigma - sd, mu * mu - md * md, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
 }
 __global__ __launch_bounds__(256) void k_item_w(const VGItem* __restrict__ gi, uint32_t nG,
                                                  const double2* __restrict__ recv, int R, VBTables tb,
-                                                 double4* __restrict__ delta) {
+                                                 double4* __restrict__ D) {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
     if (g >= nG) return;
     const uint32_t a = gi[g].attr, n = gi[g].n;
@@ -456,7 +601,7 @@ __global__ __launch_bounds__(256) void k_item_w(const VGItem* __restrict__ gi, u
     tb.ns_w[a] = ns;
     tb.sg_w[a] = sigma;
     tb.mu_w[a] = ok ? mu : md;
-    delta[g] = ok ? make_double4(md - mu, sigma - sd, 0.0, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+    D[a - tb.I] = ok ? make_double4(md - mu, sigma - sd, 0.0, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
 }
 
 // fixed-order sum of n doubles into out[0] (one block)
@@ -617,39 +762,63 @@ hipError_t vbo_update_w0(const double2* ET, uint32_t B, const VBTables& tb, doub
     return hipGetLastError();
 }
 
-hipError_t vbo_update_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm, int apply_w0,
-                        const VBTables& tb, const double2* ETin, double2* ETout, hipStream_t st, int mode,
-                        double2* sums, const double4* delta) {
+hipError_t vbo_user_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const VBTables& tb, double2* ET,
+                      hipStream_t st) {
     if (ntask == 0) return hipSuccess;
-    if (mode == VB_PART)
-        k_update_w<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, xperm, apply_w0, tb, ETin, ETout, sums, delta);
-    else if (mode == VB_FWD)
-        k_update_w<VB_FWD><<<ntask, 256, 0, st>>>(tasks, rows, xperm, apply_w0, tb, ETin, ETout, sums, delta);
-    else
-        k_update_w<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, xperm, apply_w0, tb, ETin, ETout, sums, delta);
+    k_user_w<<<ntask, 256, 0, st>>>(tasks, rows, tb, ET);
     return hipGetLastError();
 }
 
-hipError_t vbo_update_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* xperm,
-                        const uint32_t* part, uint32_t f, const VBTables& tb, const double2* ETin, double2* ETout,
-                        hipStream_t st, int mode, double2* sums, const double4* delta) {
+hipError_t vbo_user_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, uint32_t f, int pend,
+                      uint32_t fp, const VBTables& tb, const double4* D, double2* ET, double2* VS, hipStream_t st) {
     if (ntask == 0) return hipSuccess;
-    if (mode == VB_PART)
-        k_update_v<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, xperm, part, f, tb, ETin, ETout, sums, delta);
-    else if (mode == VB_FWD)
-        k_update_v<VB_FWD><<<ntask, 256, 0, st>>>(tasks, rows, xperm, part, f, tb, ETin, ETout, sums, delta);
+    if (pend == VB_PEND_V)
+        k_user_v<VB_PEND_V><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, tb, D, ET, VS);
+    else if (pend == VB_PEND_W)
+        k_user_v<VB_PEND_W><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, tb, D, ET, VS);
     else
-        k_update_v<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, xperm, part, f, tb, ETin, ETout, sums, delta);
+        k_user_v<VB_PEND_NONE><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, tb, D, ET, VS);
+    return hipGetLastError();
+}
+
+hipError_t vbo_user_flush(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, int pend,
+                          uint32_t fp, const VBTables& tb, const double4* D, double2* ET, hipStream_t st) {
+    if (ntask == 0 || pend == VB_PEND_NONE) return hipSuccess;
+    if (pend == VB_PEND_V)
+        k_user_flush<VB_PEND_V><<<ntask, 256, 0, st>>>(tasks, rows, part, fp, tb, D, ET);
+    else
+        k_user_flush<VB_PEND_W><<<ntask, 256, 0, st>>>(tasks, rows, part, fp, tb, D, ET);
+    return hipGetLastError();
+}
+
+hipError_t vbo_item_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const VBTables& tb,
+                      const double2* ET, double4* D, double2* sums, hipStream_t st) {
+    if (ntask == 0) return hipSuccess;
+    if (sums)
+        k_item_wp<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, i2u, tb, ET, D, sums);
+    else
+        k_item_wp<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, i2u, tb, ET, D, sums);
+    return hipGetLastError();
+}
+
+hipError_t vbo_item_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const uint32_t* part,
+                      uint32_t f, const VBTables& tb, const double2* ET, const double2* VS, double4* D, double2* sums,
+                      hipStream_t st) {
+    if (ntask == 0) return hipSuccess;
+    if (sums)
+        k_item_vp<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, i2u, part, f, tb, ET, VS, D, sums);
+    else
+        k_item_vp<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, i2u, part, f, tb, ET, VS, D, sums);
     return hipGetLastError();
 }
 
 hipError_t vbo_item_update(const VGItem* gi, uint32_t nG, const double2* recv, int R, int factor, uint32_t f,
-                           const VBTables& tb, double4* delta, hipStream_t st) {
+                           const VBTables& tb, double4* D, hipStream_t st) {
     if (nG == 0) return hipSuccess;
     if (factor)
-        k_item_v<<<(nG + 255) / 256, 256, 0, st>>>(gi, nG, recv, R, f, tb, delta);
+        k_item_v<<<(nG + 255) / 256, 256, 0, st>>>(gi, nG, recv, R, f, tb, D);
     else
-        k_item_w<<<(nG + 255) / 256, 256, 0, st>>>(gi, nG, recv, R, tb, delta);
+        k_item_w<<<(nG + 255) / 256, 256, 0, st>>>(gi, nG, recv, R, tb, D);
     return hipGetLastError();
 }
 

@@ -72,6 +72,7 @@ SIGNATURES = {
     "sbmf_last_error": (C.c_char_p, [C.c_void_p]),
     "sbmf_last_global_error": (C.c_char_p, []),
     "sbmf_abi_version": (C.c_int, []),
+    "sbmf_exit_guard": (C.c_int, [C.c_int]),
     "sbmf_set_train": (C.c_int, [C.c_void_p, C.c_uint64, _P_U32, _P_U32, _P_F64]),
     "sbmf_set_test": (C.c_int, [C.c_void_p, C.c_uint64, _P_U32, _P_U32, _P_F64]),
     "sbmf_set_dims": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
@@ -114,13 +115,27 @@ def load(path=LIB_PATH):
 lib = load()
 
 
+_guarded = False
+
+
+def exit_guard(rc):
+    """sbmf_exit_guard (include/sbmf.h): the first call, before anything starts
+    the HIP runtime, makes the process leave with exit status rc once the exit
+    handlers registered after it (rocprofv3 writes its output in one) have
+    run, skipping the shared-library finalizers (the HIP runtime's faults under
+    rocprofv3, ROCm 7.2: profiles/r03_rocprof_teardown.txt); later calls set
+    rc.  For programs (bench.py), not for a library user's process."""
+    global _guarded
+    if lib.sbmf_exit_guard(int(rc)) != 0:
+        raise RuntimeError(lib.sbmf_last_global_error().decode())
+    _guarded = True
+
+
 def unload():
-    """dlclose libsbmf so its HIP module destructor (fat-binary unregistration)
-    runs now, while the HIP runtime is fully alive, instead of from exit()
-    handlers after tools such as rocprofv3 have finalised (which segfaults in
-    ROCm 7.2).  Every learner must be closed first; the module is unusable after."""
+    """dlclose libsbmf (every learner closed first; the module is unusable
+    after).  A no-op once exit_guard is installed: the handler lives in libsbmf."""
     global lib
     import _ctypes
-    if lib is not None:
+    if lib is not None and not _guarded:
         _ctypes.dlclose(lib._handle)
         lib = None
