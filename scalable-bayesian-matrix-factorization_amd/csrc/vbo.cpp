@@ -72,7 +72,7 @@ struct VBLearner {
     uint32_t built = 0;              // epochs whose layout exists (ready or being built)
     // device
     DBuf d_mu_v, d_sg_v, d_nm_v, d_ns_v, d_mu_w, d_sg_w, d_nm_w, d_ns_w, d_rho_w, d_rho_v, d_t_w, d_t_v, d_cc;
-    DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_ETu, d_part;
+    DBuf d_sigma_v, d_scal, d_muT, d_sgT, d_E, d_T, d_part;
     DBuf d_D, d_VS;  // per item: the last item pass's pending deltas; per user: fresh {mean, variance} of f
     size_t part_cap = 0;  // doubles in d_part
     DBuf d_tu, d_ti, d_tr, d_pred, d_tpart;
@@ -84,6 +84,11 @@ struct VBLearner {
     std::vector<uint64_t> ubounds;     // [R + 1] user ranges of every rank
     std::vector<uint8_t> mine;         // [N] case belongs to an owned user
     uint32_t gmax = 0;                 // largest per-batch item count
+    // one rank: item rows cut into XS slices by the partner user's batch row (slice x
+    // = user rows [x nu / XS, (x+1) nu / XS)); slice x's tasks take blocks x, x + XS, ...,
+    // i.e. XCD x under the round-robin block dispatch, so its gathers (e and the users'
+    // {mean, variance}) stay inside 1/XS of the batch -- resident in that XCD's L2
+    uint32_t XS = 1;
     DBuf d_send, d_recv, d_sums, d_recvg;
     double last_rmse = NAN, last_alpha = NAN;
     double ms_layout = 0.0;
@@ -101,7 +106,7 @@ struct VBLearner {
     void build_layout(VBLayout& L, uint32_t ep);
     void run(uint32_t epochs, sbmf_sweep_cb cb, void* user);
     void item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_, const uint32_t* i2u_,
-                   int factor, uint32_t f, const double2* ETu);
+                   int factor, uint32_t f, VBCases ETu);
     void sync_users();
 };
 
@@ -170,6 +175,10 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
         if (sbmf_partition_rows(uptr.data(), I, R, ubounds.data()) != SBMF_OK)
             fail(SBMF_E_ARG, "online VB: user partition failed");
     }
+    if (R == 1) {
+        const char* xs = std::getenv("SBMF_VB_SLICES");
+        XS = xs ? (uint32_t)std::min(32, std::max(1, std::atoi(xs))) : 1u;
+    }
     u0 = (uint32_t)ubounds[rank];
     u1 = (uint32_t)ubounds[rank + 1];
     mine.assign(N, 1);
@@ -210,9 +219,10 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     d_sgT.alloc((size_t)p * Kp * sizeof(double));
     HIPCHK(hipMemsetAsync(d_muT.p, 0, d_muT.bytes, st));
     HIPCHK(hipMemsetAsync(d_sgT.p, 0, d_sgT.bytes, st));
-    d_ETu.alloc((size_t)std::max(NL, 1u) * sizeof(double2));  // {e, t} per (own) case, user-grouped epoch order
-    d_D.alloc((size_t)std::max(J, 1u) * sizeof(double4));
-    d_VS.alloc((size_t)std::max(I, 1u) * sizeof(double2));
+    d_E.alloc((size_t)std::max(NL, 1u) * sizeof(double));  // e, t per (own) case, user-grouped epoch order
+    d_T.alloc((size_t)std::max(NL, 1u) * sizeof(double));
+    d_D.alloc((size_t)std::max(J, 1u) * sizeof(VBItemRec));
+    d_VS.alloc((size_t)std::max(I, 1u) * sizeof(double2));  // a batch has at most I user rows
     HIPCHK(hipMemsetAsync(d_D.p, 0, d_D.bytes, st));
     if (R > 1) {
         d_send.alloc((size_t)(K + 2) * sizeof(double));
@@ -328,7 +338,7 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
     }
     // several ranks: every batch's items over all ranks, and each item's index there
     std::vector<uint32_t> gidx;
-    if (R > 1) {
+    if (R > 1 || XS > 1) {
         std::vector<uint32_t> cnt((size_t)NB * J, 0);
         for (uint32_t l = 0; l < N; ++l) cnt[(size_t)bid[l] * J + ti[l]]++;
         L.gitems.clear();
@@ -339,7 +349,7 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
             for (uint32_t a = 0; a < J; ++a)
                 if (cnt[(size_t)b * J + a]) {
                     gidx[(size_t)b * J + a] = (uint32_t)L.gitems.size() - L.gitem0[b];
-                    L.gitems.push_back(VGItem{I + a, cnt[(size_t)b * J + a]});
+                    L.gitems.push_back(VGItem{I + a, cnt[(size_t)b * J + a], XS > 1 ? 0u : R >= 32 ? ~0u : (1u << R) - 1});
                 }
             gmax = std::max(gmax, (uint32_t)L.gitems.size() - L.gitem0[b]);
         }
@@ -360,54 +370,105 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
     // cases at VB_CASES_PER_LANE per lane in registers -- a user row of a batch (a few
     // cases) takes one lane, so a task covers up to 256 rows and every lane has several
     // independent loads in flight
-    auto lg_of = [](uint32_t n) {
+    auto lg_of = [](uint32_t n, uint32_t cpl) {
         uint32_t lg = 0;
-        while (lg < 8 && (VB_CASES_PER_LANE << lg) < n) ++lg;
+        while (lg < 8 && (cpl << lg) < n) ++lg;
         return lg;
     };
-    auto group = [&](uint32_t b, bool users, std::vector<uint32_t>& off, Part& P) {
-        const uint32_t nattr = users ? I : J;
-        const uint32_t c0 = L.bbase[b], c1 = L.bbase[b + 1];
-        std::fill(off.begin(), off.end(), 0u);
-        for (uint32_t x = c0; x < c1; ++x) off[users ? tu[bcase[x]] : ti[bcase[x]]]++;
-        std::vector<VRow> rows;  // attribute order; positions assigned after the sort
-        for (uint32_t a = 0; a < nattr; ++a)
-            if (off[a]) rows.push_back(VRow{users ? a : I + a, 0u, off[a], (!users && R > 1) ? gidx[(size_t)b * J + a] : 0u});
-        // counting sort by lane-group size, largest first (stable: attribute order within
-        // a size); the rows' records follow the sorted order, so a task's rows are one
-        // contiguous run of records (coalesced reads, whole-line writes from one block)
+    // rows of one orientation (and slice) in attribute order -> stably sorted by lane-group
+    // size, records in that order from position run (a task's rows are one contiguous run
+    // of records: coalesced reads, whole-line writes from one block), and its tasks
+    auto place = [&](std::vector<VRow>& rows, uint32_t& run, std::vector<VRow>& out, std::vector<VTask>& tasks,
+                     uint32_t cpl) {
         std::vector<uint32_t> cls(10, 0);
-        for (const VRow& r : rows) cls[lg_of(r.len)]++;
+        for (const VRow& r : rows) cls[lg_of(r.len, cpl)]++;
         uint32_t at = 0;
         std::vector<uint32_t> first(10, 0);
         for (int lg = 8; lg >= 0; --lg) {
             first[lg] = at;
             at += cls[lg];
         }
-        P.rows.resize(rows.size());
-        for (const VRow& r : rows) P.rows[first[lg_of(r.len)]++] = r;
-        uint32_t run = c0;
-        for (VRow& r : P.rows) {
-            r.start = run;
-            off[users ? r.attr : r.attr - I] = run;  // becomes the fill position
-            run += r.len;
+        const uint32_t r0 = (uint32_t)out.size();
+        out.resize(r0 + rows.size());
+        for (const VRow& r : rows) out[r0 + first[lg_of(r.len, cpl)]++] = r;
+        for (uint32_t r = r0; r < out.size(); ++r) {
+            out[r].start = run;
+            run += out[r].len;
         }
-        std::vector<uint32_t>& pos = users ? upos : ipos;
-        std::vector<uint32_t>& part = users ? L.upart : L.ipart;
+        for (uint32_t r = r0; r < out.size();) {
+            const uint32_t lg = lg_of(out[r].len, cpl);
+            uint32_t m = 0;
+            while (r + m < out.size() && m < (256u >> lg) && lg_of(out[r + m].len, cpl) == lg) ++m;
+            tasks.push_back(VTask{r, m, lg, 0});
+            r += m;
+        }
+    };
+    // users of batch b: urow[user] = its row in the batch (the item side's partner index)
+    auto group_users = [&](uint32_t b, std::vector<uint32_t>& off, std::vector<uint32_t>& urow, Part& P) {
+        const uint32_t c0 = L.bbase[b], c1 = L.bbase[b + 1];
+        std::fill(off.begin(), off.end(), 0u);
+        for (uint32_t x = c0; x < c1; ++x) off[tu[bcase[x]]]++;
+        std::vector<VRow> rows;
+        for (uint32_t a = 0; a < I; ++a)
+            if (off[a]) rows.push_back(VRow{a, 0u, off[a], 0u});
+        P.rows.clear();
+        P.tasks.clear();
+        uint32_t run = c0;
+        place(rows, run, P.rows, P.tasks, VB_CASES_PER_LANE);
+        for (uint32_t r = 0; r < P.rows.size(); ++r) {
+            off[P.rows[r].attr] = P.rows[r].start;  // becomes the fill position
+            urow[P.rows[r].attr] = r;
+        }
         for (uint32_t x = c0; x < c1; ++x) {
             const uint32_t l = bcase[x];
-            const uint32_t q = off[users ? tu[l] : ti[l]]++;
-            pos[l] = q;
-            part[q] = users ? I + ti[l] : tu[l];
-            if (users) L.ur[q] = (float)tr[l];
+            const uint32_t q = off[tu[l]]++;
+            upos[l] = q;
+            L.upart[q] = I + ti[l];
+            L.ur[q] = (float)tr[l];
         }
+    };
+    // items of batch b, cut into XS slices by the partner's user row (XS = 1: whole rows);
+    // a (sub-)row's pad: several ranks -> the item's index in the batch's global list,
+    // slices -> x * nG + that index (its slot among the partial sums)
+    auto group_items = [&](uint32_t b, std::vector<uint32_t>& off, const std::vector<uint32_t>& urow, uint32_t nu,
+                           Part& P) {
+        const uint32_t c0 = L.bbase[b], c1 = L.bbase[b + 1];
+        const uint32_t nG = (R > 1 || XS > 1) ? L.gitem0[b + 1] - L.gitem0[b] : 0;
+        auto slice = [&](uint32_t l) { return XS > 1 ? (uint32_t)((uint64_t)urow[tu[l]] * XS / nu) : 0u; };
+        std::fill(off.begin(), off.end(), 0u);  // [XS][J]
+        for (uint32_t x = c0; x < c1; ++x) {
+            const uint32_t l = bcase[x];
+            off[(size_t)slice(l) * J + ti[l]]++;
+        }
+        P.rows.clear();
         P.tasks.clear();
-        for (uint32_t r = 0; r < P.rows.size();) {
-            const uint32_t lg = lg_of(P.rows[r].len);
-            uint32_t m = 0;
-            while (r + m < P.rows.size() && m < (256u >> lg) && lg_of(P.rows[r + m].len) == lg) ++m;
-            P.tasks.push_back(VTask{r, m, lg, 0});
-            r += m;
+        std::vector<std::vector<VTask>> st(XS);
+        uint32_t run = c0;
+        for (uint32_t xs = 0; xs < XS; ++xs) {
+            std::vector<VRow> rows;
+            for (uint32_t a = 0; a < J; ++a) {
+                const uint32_t n = off[(size_t)xs * J + a];
+                if (!n) continue;
+                const uint32_t g = (R > 1 || XS > 1) ? gidx[(size_t)b * J + a] : 0u;
+                rows.push_back(VRow{I + a, 0u, n, XS > 1 ? xs * nG + g : g});
+                if (XS > 1) L.gitems[L.gitem0[b] + g].mask |= 1u << xs;
+            }
+            const uint32_t r0 = (uint32_t)P.rows.size();
+            place(rows, run, P.rows, st[xs], VB_ITEM_CASES_PER_LANE);
+            for (uint32_t r = r0; r < P.rows.size(); ++r)
+                off[(size_t)xs * J + (P.rows[r].attr - I)] = P.rows[r].start;
+        }
+        // slice x's tasks at x, x + XS, x + 2 XS, ...; empty tasks fill the gaps
+        size_t most = 0;
+        for (auto& t : st) most = std::max(most, t.size());
+        for (size_t t = 0; t < most; ++t)
+            for (uint32_t xs = 0; xs < XS; ++xs)
+                P.tasks.push_back(t < st[xs].size() ? st[xs][t] : VTask{0u, 0u, 0u, 0u});
+        for (uint32_t x = c0; x < c1; ++x) {
+            const uint32_t l = bcase[x];
+            const uint32_t q = off[(size_t)slice(l) * J + ti[l]]++;
+            ipos[l] = q;
+            L.ipart[q] = urow[tu[l]];
         }
     };
     const unsigned nth = host_threads();
@@ -415,10 +476,10 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         std::vector<std::thread> th;
         for (unsigned t = 0; t < nth; ++t)
             th.emplace_back([&, t] {
-                std::vector<uint32_t> offu(I), offi(J);
+                std::vector<uint32_t> offu(I), urow(I), offi((size_t)XS * J);
                 for (uint32_t b = t; b < NB; b += nth) {
-                    group(b, true, offu, pu[b]);
-                    group(b, false, offi, pi[b]);
+                    group_users(b, offu, urow, pu[b]);
+                    group_items(b, offi, urow, (uint32_t)pu[b].rows.size(), pi[b]);
                 }
             });
         for (auto& x : th) x.join();
@@ -454,19 +515,19 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
 // or update_v of factor f): local sums -> all-gather -> the same update on
 // every rank, its deltas to D for the next user pass.
 void VBLearner::item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_,
-                          const uint32_t* i2u_, int factor, uint32_t f, const double2* ETu) {
+                          const uint32_t* i2u_, int factor, uint32_t f, VBCases ETu) {
     const uint32_t nG = L.gitem0[b + 1] - L.gitem0[b];
     if (nG == 0) return;  // every rank sees the same global list
     double2* sums = d_sums.as<double2>();
     HIPCHK(hipMemsetAsync(sums, 0, (size_t)nG * sizeof(double2), st));
     if (factor)
         HIPCHK(vbo_item_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETu, d_VS.as<double2>(),
-                          d_D.as<double4>(), sums, st));
+                          d_D.as<VBItemRec>(), sums, st));
     else
-        HIPCHK(vbo_item_w(it_, nit, ir_, i2u_, tb, ETu, d_D.as<double4>(), sums, st));
+        HIPCHK(vbo_item_w(it_, nit, ir_, i2u_, tb, ETu, d_D.as<VBItemRec>(), sums, st));
     comm->allgather(sums, (size_t)nG * sizeof(double2), d_recvg.p, st);
     HIPCHK(vbo_item_update(L.d_gitems.as<VGItem>() + L.gitem0[b], nG, d_recvg.as<double2>(), R, factor, f, tb,
-                           d_D.as<double4>(), st));
+                           d_D.as<VBItemRec>(), st));
     n_launch += 1;  // vbo_item_update (the item pass itself is counted by run)
 }
 
@@ -503,11 +564,11 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         grow(L.d_ipart, L.ipart.size() * sizeof(L.ipart[0]));
         grow(L.d_utasks, L.utasks.size() * sizeof(L.utasks[0]));
         grow(L.d_itasks, L.itasks.size() * sizeof(L.itasks[0]));
-        if (R > 1) {
+        if (R > 1 || XS > 1) {
             grow(L.d_gitems, L.gitems.size() * sizeof(L.gitems[0]));
-            d_sums.ensure((size_t)std::max(gmax, 1u) * sizeof(double2));
-            d_recvg.ensure((size_t)R * std::max(gmax, 1u) * sizeof(double2));
+            d_sums.ensure((size_t)XS * std::max(gmax, 1u) * sizeof(double2));
         }
+        if (R > 1) d_recvg.ensure((size_t)R * std::max(gmax, 1u) * sizeof(double2));
         const auto h2 = std::chrono::steady_clock::now();
         upload_grow(L.d_urows, L.urows, st);
         upload_grow(L.d_irows, L.irows, st);
@@ -517,7 +578,7 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         upload_grow(L.d_ipart, L.ipart, st);
         upload_grow(L.d_utasks, L.utasks, st);
         upload_grow(L.d_itasks, L.itasks, st);
-        if (R > 1) upload_grow(L.d_gitems, L.gitems, st);
+        if (R > 1 || XS > 1) upload_grow(L.d_gitems, L.gitems, st);
         if (trace) {
             HIPCHK(hipStreamSynchronize(st));
             const auto h3 = std::chrono::steady_clock::now();
@@ -530,8 +591,8 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         ms_layout = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
         n_launch = 0;
         HIPCHK(hipEventRecord(ev[0], st));
-        double2* ETu = d_ETu.as<double2>();
-        double4* D = d_D.as<double4>();
+        const VBCases ETu{d_E.as<double>(), d_T.as<double>()};
+        VBItemRec* D = d_D.as<VBItemRec>();
         double2* VS = d_VS.as<double2>();
         double* part = d_part.as<double>();
         const VRow* ur_ = L.d_urows.as<VRow>();
@@ -544,11 +605,11 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             HIPCHK(vbo_predict(ur_ + L.urow0[b], nu, L.d_upart.as<uint32_t>(), L.d_ur.as<float>(), d_muT.as<double>(),
                                d_sgT.as<double>(), tb, Kp, ETu, st));
             if (R > 1) {  // update_w0 from every rank's local sum
-                HIPCHK(vbo_w0_local(ETu + L.bbase[b], B, tb, part, d_send.as<double>(), st));
+                HIPCHK(vbo_w0_local(ETu.at(L.bbase[b]), B, tb, part, d_send.as<double>(), st));
                 comm->allgather(d_send.p, sizeof(double), d_recv.p, st);
                 HIPCHK(vbo_w0_final(d_recv.as<double>(), R, L.gbsize[b], tb, st));
             } else {
-                HIPCHK(vbo_update_w0(ETu + L.bbase[b], B, tb, part, st));
+                HIPCHK(vbo_update_w0(ETu.at(L.bbase[b]), B, tb, part, st));
             }
             const VTask* ut = L.d_utasks.as<VTask>() + L.utask0[b];
             const VTask* it_ = L.d_itasks.as<VTask>() + L.itask0[b];
@@ -558,29 +619,37 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             const uint32_t* i2u_ = L.d_i2u.as<uint32_t>();
             // users update their records in place; items read them (through i2u) and leave
             // their updates in D, which the next user pass (or the flush) applies
+            // one rank, XS > 1: the slices' partial sums, then the items' updates
+            const VGItem* gi_ = XS > 1 ? L.d_gitems.as<VGItem>() + L.gitem0[b] : nullptr;
+            const uint32_t nG = XS > 1 ? L.gitem0[b + 1] - L.gitem0[b] : 0;
+            double2* sums = XS > 1 ? d_sums.as<double2>() : nullptr;
             HIPCHK(vbo_user_w(ut, nut, ur_, tb, ETu, st));
-            if (R > 1)
+            if (R > 1) {
                 item_pass(L, b, it_, nit, ir_, i2u_, 0, 0, ETu);
-            else
-                HIPCHK(vbo_item_w(it_, nit, ir_, i2u_, tb, ETu, D, nullptr, st));
+            } else {
+                HIPCHK(vbo_item_w(it_, nit, ir_, i2u_, tb, ETu, D, sums, st));
+                if (XS > 1) HIPCHK(vbo_item_update(gi_, nG, sums, (int)XS, 0, 0, tb, D, st));
+            }
             int pend = VB_PEND_W;
             for (uint32_t f = 0; f < K; ++f) {
-                HIPCHK(vbo_user_v(ut, nut, ur_, upart_, f, pend, f - 1, tb, D, ETu, VS, st));
-                if (R > 1)
+                HIPCHK(vbo_user_v(ut, nut, ur_, upart_, f, pend, f - 1, L.urow0[b], tb, D, ETu, VS, st));
+                if (R > 1) {
                     item_pass(L, b, it_, nit, ir_, i2u_, 1, f, ETu);
-                else
-                    HIPCHK(vbo_item_v(it_, nit, ir_, i2u_, ipart_, f, tb, ETu, VS, D, nullptr, st));
+                } else {
+                    HIPCHK(vbo_item_v(it_, nit, ir_, i2u_, ipart_, f, tb, ETu, VS, D, sums, st));
+                    if (XS > 1) HIPCHK(vbo_item_update(gi_, nG, sums, (int)XS, 1, f, tb, D, st));
+                }
                 pend = VB_PEND_V;
             }
             HIPCHK(vbo_user_flush(ut, nut, ur_, upart_, pend, K - 1, tb, D, ETu, st));
             if (R > 1) {  // the blends from every rank's alpha sum and user-range sig sums
-                HIPCHK(vbo_hyper_local(ETu + L.bbase[b], B, tb, u0, u1, part, part_cap, d_send.as<double>(), st));
+                HIPCHK(vbo_hyper_local(ETu.at(L.bbase[b]), B, tb, u0, u1, part, part_cap, d_send.as<double>(), st));
                 comm->allgather(d_send.p, (K + 2) * sizeof(double), d_recv.p, st);
                 HIPCHK(vbo_hyper_final(d_recv.as<double>(), R, L.gbsize[b], tb, I, part, part_cap, st));
             } else {
-                HIPCHK(vbo_hyper(ETu + L.bbase[b], B, tb, part, st));
+                HIPCHK(vbo_hyper(ETu.at(L.bbase[b]), B, tb, part, st));
             }
-            n_launch += 2 * K + 12;  // transposes 2, predict, w0 2, bias passes 2, factor passes 2K, flush, hyper 4
+            n_launch += 2 * K + 12 + (XS > 1 ? K + 1 : 0);  // transposes 2, predict, w0 2, bias passes 2, factor passes 2K, flush, hyper 4
         }
         // the next epoch's shuffle and layout, on the host while this epoch runs
         // (the reference stream after this epoch's shuffle is exactly the next one's)

@@ -47,24 +47,36 @@ struct VBTables {
     uint32_t I;                         // users (attributes [0, I)); items are [I, p)
 };
 
+// A batch's per-case terms in its user-grouped order: E = e (the residual),
+// T = t (its variance term), two arrays so an item pass's gathers of e touch
+// half the bytes.
+struct VBCases {
+    double *E, *T;
+    VBCases at(size_t o) const { return VBCases{E + o, T + o}; }
+};
 // [K][p] -> [p][Kp] (attribute-major rows for the prediction gathers)
 hipError_t vbo_transpose(const double* src, double* dst, uint32_t K, uint32_t Kp, uint32_t p, hipStream_t st);
 // e = r - prediction and t = its variance for every case of a batch, driven
 // by the batch's user rows (fm_learn_vb_online.h:80-310)
 hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* part, const float* r, const double* muT,
-                       const double* sgT, const VBTables& tb, uint32_t Kp, double2* ET, hipStream_t st);
+                       const double* sgT, const VBTables& tb, uint32_t Kp, VBCases ET, hipStream_t st);
 // update_w0 (:586-633): the global bias blend; its deltas are applied to e / t
 // by vbo_user_w
-hipError_t vbo_update_w0(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
+hipError_t vbo_update_w0(VBCases ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
 // Several ranks: an item present in a batch (any rank's cases) and its global
 // case count there; a rank's item rows carry their index in this list in VRow.pad.
 struct VGItem {
-    uint32_t attr, n;
+    uint32_t attr, n, mask;  // mask: the parts (ranks or XCD slices) holding its cases
 };
 // One 256-thread block of an update pass: rows [row0, row0 + nrows) of the
 // orientation's row list, each owned by 2^lg lanes (256 >> lg rows at most);
 // a lane keeps up to VB_CASES_PER_LANE of its row's cases in registers.
 constexpr uint32_t VB_CASES_PER_LANE = 4;
+// item rows (long, read-only passes: only e and the partner record per case in flight)
+#ifndef SBMF_VB_ITEM_CPL
+#define SBMF_VB_ITEM_CPL 8
+#endif
+constexpr uint32_t VB_ITEM_CASES_PER_LANE = SBMF_VB_ITEM_CPL;
 struct VTask {
     uint32_t row0, nrows, lg, pad;
 };
@@ -72,40 +84,47 @@ struct VTask {
 // user-grouped order (ET).  A user pass reads and writes its rows' records in
 // place; an item pass gathers e through i2u (a case's user-grouped position)
 // and writes nothing per case: its e / t updates are left per item in D
-// (double4 {dmu, dsg, dm2, ok}, indexed by item) and applied by the next user
-// pass (pend) or by vbo_user_flush before the hyperparameter sums.
-enum { VB_PEND_NONE = 0, VB_PEND_W = 1, VB_PEND_V = 2 };  // pending: none | bias pass | factor pass
+// (VBItemRec, indexed by item - I) and applied by the next user pass (pend)
+// or by vbo_user_flush before the hyperparameter sums.
+enum { VB_PEND_NONE = 0, VB_PEND_W = 1, VB_PEND_V = 2 };
+// per item, from the item pass for the user pass after it: the item's mean and
+// variance of that user pass's factor, and the item pass's e / t updates
+struct VBItemRec {
+    double v, s, dmu, dsg, dm2, ok;
+};  // pending: none | bias pass | factor pass
 // update_w (:635-710) of the users (update_w0's deltas applied first)
-hipError_t vbo_user_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const VBTables& tb, double2* ET,
+hipError_t vbo_user_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const VBTables& tb, VBCases ET,
                       hipStream_t st);
 // update_v (:712-800) of factor f for the users, after the pending item updates
-// (pend; factor fp for VB_PEND_V); VS[user] = its new {mean, variance} of f
+// (pend; factor fp for VB_PEND_V); VS[row - rbase] = the user's new {mean,
+// variance} of f, by its row in the batch (rbase: the batch's first user row)
 hipError_t vbo_user_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, uint32_t f, int pend,
-                      uint32_t fp, const VBTables& tb, const double4* D, double2* ET, double2* VS, hipStream_t st);
+                      uint32_t fp, uint32_t rbase, const VBTables& tb, const VBItemRec* D, VBCases ET, double2* VS,
+                      hipStream_t st);
 hipError_t vbo_user_flush(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, int pend,
-                          uint32_t fp, const VBTables& tb, const double4* D, double2* ET, hipStream_t st);
+                          uint32_t fp, const VBTables& tb, const VBItemRec* D, VBCases ET, hipStream_t st);
 // update_w / update_v of factor f for the items (D[item] = the deltas); several
 // ranks: sums != null -> each row's local sums to sums[VRow.pad] only
 hipError_t vbo_item_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const VBTables& tb,
-                      const double2* ET, double4* D, double2* sums, hipStream_t st);
+                      VBCases ET, VBItemRec* D, double2* sums, hipStream_t st);
 hipError_t vbo_item_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const uint32_t* part,
-                      uint32_t f, const VBTables& tb, const double2* ET, const double2* VS, double4* D, double2* sums,
+                      uint32_t f, const VBTables& tb, VBCases ET, const double2* VS, VBItemRec* D, double2* sums,
                       hipStream_t st);
 // several ranks: the items of a batch updated from every rank's local sums
 // (recv [R][nG], rank order; factor f, or the biases when factor == 0)
 hipError_t vbo_item_update(const VGItem* gi, uint32_t nG, const double2* recv, int R, int factor, uint32_t f,
-                           const VBTables& tb, double4* D, hipStream_t st);
+                           const VBTables& tb, VBItemRec* D, hipStream_t st);
 // several ranks: update_w0's local sum (out[0]) and the update from every rank's (recv[R])
-hipError_t vbo_w0_local(const double2* ET, uint32_t B, const VBTables& tb, double* part, double* out, hipStream_t st);
+hipError_t vbo_w0_local(VBCases ET, uint32_t B, const VBTables& tb, double* part, double* out, hipStream_t st);
 hipError_t vbo_w0_final(const double* recv, int R, uint32_t B, const VBTables& tb, hipStream_t st);
 // several ranks: out = [alpha's local sum | K + 1 sig sums over the users [u0, u1)],
 // then the blends from every rank's (recv [R][K + 2]) plus the item range [I, p)
-hipError_t vbo_hyper_local(const double2* ET, uint32_t B, const VBTables& tb, uint32_t u0, uint32_t u1, double* part,
+hipError_t vbo_hyper_local(VBCases ET, uint32_t B, const VBTables& tb, uint32_t u0, uint32_t u1, double* part,
                            size_t part_cap, double* out, hipStream_t st);
 hipError_t vbo_hyper_final(const double* recv, int R, uint32_t B, const VBTables& tb, uint32_t I, double* part,
                            size_t part_cap, hipStream_t st);
 // step sizes of update_v (:447-453) and the hyperparameter blends (:523-580)
-hipError_t vbo_hyper(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
+hipError_t vbo_hyper(VBCases ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st);
 // test predictions clamped to [lo, hi] and their squared errors per 256-case block
 hipError_t vbo_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t n, uint32_t I,
                     const double* muT, const VBTables& tb, uint32_t Kp, double lo, double hi, double* pred,

@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void k_predict(const VRow* __restrict__ rows, 
                                                   const uint32_t* __restrict__ part,
                                                   const float* __restrict__ r, const double* __restrict__ muT,
                                                   const double* __restrict__ sgT, VBTables tb, uint32_t Kp,
-                                                  double2* __restrict__ ET) {
+                                                  VBCases ET) {
     const uint32_t ri = blockIdx.x * 16 + (threadIdx.x >> 4);
     const int ci = threadIdx.x & 15;
     if (ri >= nrows) return;  // whole 16-lane groups
@@ -119,14 +119,15 @@ __global__ __launch_bounds__(256) void k_predict(const VRow* __restrict__ rows, 
             double2 o;
             o.x = (double)r[q] - (((d + wu) + tb.mu_w[pa]) + mu0);
             o.y = ((tv + swu) + tb.sg_w[pa]) + sg0;
-            ET[q] = o;
+            ET.E[q] = o.x;
+            ET.T[q] = o.y;
         }
     }
 }
 
 // update_w0 (:586-633): partial sums of the per-case natural mean
 // (1 - rho0) nm0 + rho0 N alpha (e + mu0'), 1024 cases per block
-__global__ __launch_bounds__(256) void k_w0_partial(const double2* __restrict__ ET, uint32_t B, VBTables tb,
+__global__ __launch_bounds__(256) void k_w0_partial(VBCases ET, uint32_t B, VBTables tb,
                                                      double* __restrict__ part) {
     __shared__ double red[256];
     const VBScal s = *tb.scal;
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(256) void k_w0_partial(const double2* __restrict__ 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const uint32_t c = blockIdx.x * 1024 + threadIdx.x * 4 + u;
-        if (c < B) acc += cmu + kmu * (ET[c].x + s.mu0);
+        if (c < B) acc += cmu + kmu * (ET.E[c] + s.mu0);
     }
     acc = block_sum256(acc, red);
     if (threadIdx.x == 0) part[blockIdx.x] = acc;
@@ -182,36 +183,59 @@ __device__ __forceinline__ double gsum(double x, int G, double* red) {
     return t;
 }
 
-constexpr int MC = VB_CASES_PER_LANE;  // cases a lane keeps in registers between the two passes of a row
+constexpr int MC = VB_CASES_PER_LANE;        // user rows: cases a lane keeps in registers between the two passes
+constexpr int MI = VB_ITEM_CASES_PER_LANE;   // item rows: cases a lane has in flight
 #ifndef SBMF_VB_OCC
-#define SBMF_VB_OCC 6  // waves per SIMD the update kernels are compiled for
+#define SBMF_VB_OCC 5  // waves per SIMD the update kernels are compiled for (r03: 6 or 8 slower)
 #endif
+
 
 enum { VB_FUSED = 0, VB_PART = 1 };  // item passes: update here | local sums (several ranks)
 
-// The item pass's e / t updates, applied by the user pass after it: D[item] =
-// {dmu, dsg, dm2, ok} (k_item_wp / k_item_vp / vbo_item_update).  Bias pass
+// The record an item pass leaves per item for the next user pass (VBItemRec,
+// three 16-byte loads): the item's mean and variance of the factor that user
+// pass updates (v, s), and the item pass's own e / t updates (dmu, dsg, dm2,
+// ok), which the user pass applies to its cases before its sums.  Bias pass
 // (update_w :700-708): e += dmu, t += dsg; factor pass fp (update_v :790-798):
 // e += h dmu, t += (h1 + h^2) dsg, t += h1 dm2, h and h1 the user's mean and
 // variance of factor fp (final since that factor's user pass).  The same
 // operations in the same order as applying them in the item pass.
+struct IRec {
+    double v, s, dmu, dsg, dm2, ok;
+};
+__device__ __forceinline__ IRec get_rec(const VBItemRec* __restrict__ D, uint32_t i) {
+    const double2* p = reinterpret_cast<const double2*>(D + i);
+    const double2 a = p[0], b = p[1], c = p[2];
+    return IRec{a.x, a.y, b.x, b.y, c.x, c.y};
+}
+__device__ __forceinline__ void put_rec(VBItemRec* __restrict__ D, uint32_t i, double v, double s, bool ok, double dmu,
+                                        double dsg, double dm2) {
+    double2* p = reinterpret_cast<double2*>(D + i);
+    p[0] = make_double2(v, s);
+    p[1] = ok ? make_double2(dmu, dsg) : make_double2(0.0, 0.0);
+    p[2] = ok ? make_double2(dm2, 1.0) : make_double2(0.0, 0.0);
+}
+// the item's mean and variance of factor f (0, 0 past the last factor)
+__device__ __forceinline__ double2 item_vs(const VBTables& tb, uint32_t f, uint32_t a) {
+    return f < tb.K ? make_double2(tb.mu_v[(size_t)f * tb.p + a], tb.sg_v[(size_t)f * tb.p + a]) : make_double2(0.0, 0.0);
+}
 template <int PEND>
-__device__ __forceinline__ void vb_pending(double2& o, const double4& d, double hp, double sp) {
-    if (PEND == VB_PEND_NONE || d.w == 0.0) return;
+__device__ __forceinline__ void vb_pending(double2& o, const IRec& d, double hp, double sp) {
+    if (d.ok == 0.0) return;
     if (PEND == VB_PEND_W) {
-        o.x += d.x;
-        o.y += d.y;
+        o.x += d.dmu;
+        o.y += d.dsg;
     } else {
-        o.x += hp * d.x;
-        o.y += (sp + hp * hp) * d.y;
-        o.y += sp * d.z;
+        o.x += hp * d.dmu;
+        o.y += (sp + hp * hp) * d.dsg;
+        o.y += sp * d.dm2;
     }
 }
 
 // the block's task: rows [row0, row0 + nrows), 2^lg lanes per row
 struct VLane {
     VRow rw;
-    uint32_t n;
+    uint32_t n, rid;  // rid: the row's index in the row list
     int G, ci;
     bool live;
 };
@@ -222,7 +246,8 @@ __device__ __forceinline__ VLane vb_lane(const VTask* __restrict__ tasks, const 
     const uint32_t g = threadIdx.x >> tk.lg;
     L.ci = threadIdx.x & (L.G - 1);
     L.live = g < tk.nrows;  // G >= 128 blocks hold one row: always live
-    L.rw = rows[tk.row0 + (L.live ? g : 0)];
+    L.rid = tk.row0 + (L.live ? g : 0);
+    L.rw = rows[L.rid];
     L.n = L.live ? L.rw.len : 0;
     return L;
 }
@@ -231,7 +256,7 @@ __device__ __forceinline__ VLane vb_lane(const VTask* __restrict__ tasks, const 
 // (the user pass touches every case once); e / t updated in place.
 __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_w(const VTask* __restrict__ tasks,
                                                              const VRow* __restrict__ rows, VBTables tb,
-                                                             double2* __restrict__ ET) {
+                                                             VBCases ET) {
     __shared__ double red[256];
     const VLane L = vb_lane(tasks, rows);
     const int G = L.G, ci = L.ci;
@@ -247,7 +272,7 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_w(const VTask* __rest
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
-            et[j] = ET[q0 + x];
+            et[j] = make_double2(ET.E[q0 + x], ET.T[q0 + x]);
             et[j].x = et[j].x + dm;
             et[j].y = et[j].y + ds;
             e1 += ((1 - rho) * mo) + rho * cc * alpha * (et[j].x + md);
@@ -255,7 +280,7 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_w(const VTask* __rest
         }
     }
     for (uint32_t x = ci + MC * G; x < n; x += G) {  // rows longer than MC * G
-        const double e = ET[q0 + x].x + dm;
+        const double e = ET.E[q0 + x] + dm;
         e1 += ((1 - rho) * mo) + rho * cc * alpha * (e + md);
         e2 += cs;
     }
@@ -287,32 +312,35 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_w(const VTask* __rest
                 o.x += dmu;
                 o.y += dsg;
             }
-            ET[q0 + x] = o;
+            ET.E[q0 + x] = o.x;
+            ET.T[q0 + x] = o.y;
         }
     }
     for (uint32_t x = ci + MC * G; x < n; x += G) {
-        double2 o = ET[q0 + x];
+        double2 o = make_double2(ET.E[q0 + x], ET.T[q0 + x]);
         o.x = o.x + dm;
         o.y = o.y + ds;
         if (ok) {
             o.x += dmu;
             o.y += dsg;
         }
-        ET[q0 + x] = o;
+        ET.E[q0 + x] = o.x;
+        ET.T[q0 + x] = o.y;
     }
 }
 
-// update_v (:712-800) of factor f for the batch's users: the previous item
-// pass's updates first (PEND), then the sums over the cases with the item
-// factors of column f (L2-resident), the update, and the user's own e / t
-// updates, in place.  VS[user] = the user's new {mean, variance} of f, the
-// record the item pass gathers.
+// update_v (:712-800) of factor f for the batch's users: per case the item's
+// record (its column-f mean and variance, and the previous item pass's
+// updates, applied first), then the sums, the update and the user's own
+// e / t updates, in place.  VS[row - rbase] = the user's new {mean, variance}
+// of f (by the user's row in the batch), the record the item pass gathers.
 template <int PEND>
 __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_v(const VTask* __restrict__ tasks,
                                                              const VRow* __restrict__ rows,
                                                              const uint32_t* __restrict__ part, uint32_t f,
-                                                             uint32_t fp, VBTables tb, const double4* __restrict__ D,
-                                                             double2* __restrict__ ET, double2* __restrict__ VS) {
+                                                             uint32_t fp, uint32_t rbase, VBTables tb,
+                                                             const VBItemRec* __restrict__ D, VBCases ET,
+                                                             double2* __restrict__ VS) {
     __shared__ double red[256];
     const VLane L = vb_lane(tasks, rows);
     const int G = L.G, ci = L.ci;
@@ -328,28 +356,30 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_v(const VTask* __rest
         hp = tb.mu_v[(size_t)fp * tb.p + a];
         sp = tb.sg_v[(size_t)fp * tb.p + a];
     }
-    uint32_t pj[MC];  // partner items (their column-f values re-read from L2 for the updates)
+    double hh[MC], hs[MC];  // the partners' column-f values, kept for the updates
     double2 et[MC];
     double e1 = 0.0, e2 = 0.0;
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
-            const uint32_t pa = part[q0 + x];
-            pj[j] = pa;
-            const double h = v[pa], h1 = s[pa];
-            et[j] = ET[q0 + x];
-            if (PEND != VB_PEND_NONE) vb_pending<PEND>(et[j], D[pa - I], hp, sp);
-            e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + h1));
+            const IRec r = get_rec(D, part[q0 + x] - I);
+            hh[j] = r.v;
+            hs[j] = r.s;
+            et[j] = make_double2(ET.E[q0 + x], ET.T[q0 + x]);
+            vb_pending<PEND>(et[j], r, hp, sp);
+            const double h = r.v;
+            e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + r.s));
             e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (et[j].x + md * h));
         }
     }
-    for (uint32_t x = ci + MC * G; x < n; x += G) {
-        const uint32_t q = q0 + x, pa = part[q];
-        const double h = v[pa], h1 = s[pa];
-        double2 o = ET[q];
-        if (PEND != VB_PEND_NONE) vb_pending<PEND>(o, D[pa - I], hp, sp);
-        e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + h1));
+    for (uint32_t x = ci + MC * G; x < n; x += G) {  // rows longer than MC * G
+        const uint32_t q = q0 + x;
+        const IRec r = get_rec(D, part[q] - I);
+        const double h = r.v;
+        double2 o = make_double2(ET.E[q], ET.T[q]);
+        vb_pending<PEND>(o, r, hp, sp);
+        e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + r.s));
         e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (o.x + md * h));
     }
     e1 = gsum(e1, G, red);
@@ -365,7 +395,7 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_v(const VTask* __rest
         tb.ns_v[off + a] = ns;
         s[a] = sigma;
         v[a] = ok ? mu : md;
-        VS[a] = make_double2(ok ? mu : md, sigma);
+        VS[L.rid - rbase] = make_double2(ok ? mu : md, sigma);
         if (f == 0) tb.t_v[a] += n;  // the caller's count (:447-450)
     }
     // a non-finite mean: the reference returns before touching e, t
@@ -376,25 +406,28 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_v(const VTask* __rest
         if (x < n) {
             double2 o = et[j];
             if (ok) {
-                const double h = v[pj[j]], h1 = s[pj[j]];
+                const double h = hh[j], h1 = hs[j];
                 o.x += h * dmu;
                 o.y += (h1 + h * h) * dsg;
                 o.y += h1 * dm2;
             }
-            ET[q0 + x] = o;
+            ET.E[q0 + x] = o.x;
+            ET.T[q0 + x] = o.y;
         }
     }
     for (uint32_t x = ci + MC * G; x < n; x += G) {
-        const uint32_t q = q0 + x, pa = part[q];
-        double2 o = ET[q];
-        if (PEND != VB_PEND_NONE) vb_pending<PEND>(o, D[pa - I], hp, sp);
+        const uint32_t q = q0 + x;
+        const IRec r = get_rec(D, part[q] - I);
+        double2 o = make_double2(ET.E[q], ET.T[q]);
+        vb_pending<PEND>(o, r, hp, sp);
         if (ok) {
-            const double h = v[pa], h1 = s[pa];
+            const double h = r.v, h1 = r.s;
             o.x += h * dmu;
             o.y += (h1 + h * h) * dsg;
             o.y += h1 * dm2;
         }
-        ET[q] = o;
+        ET.E[q] = o.x;
+        ET.T[q] = o.y;
     }
 }
 
@@ -402,7 +435,7 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_v(const VTask* __rest
 template <int PEND>
 __global__ __launch_bounds__(256) void k_user_flush(const VTask* __restrict__ tasks, const VRow* __restrict__ rows,
                                                     const uint32_t* __restrict__ part, uint32_t fp, VBTables tb,
-                                                    const double4* __restrict__ D, double2* __restrict__ ET) {
+                                                    const VBItemRec* __restrict__ D, VBCases ET) {
     const VLane L = vb_lane(tasks, rows);
     const uint32_t a = L.rw.attr;
     double hp = 0.0, sp = 0.0;
@@ -412,9 +445,10 @@ __global__ __launch_bounds__(256) void k_user_flush(const VTask* __restrict__ ta
     }
     for (uint32_t x = L.ci; x < L.n; x += L.G) {
         const uint32_t q = L.rw.start + x;
-        double2 o = ET[q];
-        vb_pending<PEND>(o, D[part[q] - tb.I], hp, sp);
-        ET[q] = o;
+        double2 o = make_double2(ET.E[q], ET.T[q]);
+        vb_pending<PEND>(o, get_rec(D, part[q] - tb.I), hp, sp);
+        ET.E[q] = o.x;
+        ET.T[q] = o.y;
     }
 }
 
@@ -426,8 +460,8 @@ template <int MODE>
 __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_wp(const VTask* __restrict__ tasks,
                                                               const VRow* __restrict__ rows,
                                                               const uint32_t* __restrict__ i2u, VBTables tb,
-                                                              const double2* __restrict__ ET,
-                                                              double4* __restrict__ D, double2* __restrict__ sums) {
+                                                              VBCases ET,
+                                                              VBItemRec* __restrict__ D, double2* __restrict__ sums) {
     __shared__ double red[256];
     const VLane L = vb_lane(tasks, rows);
     const int G = L.G, ci = L.ci;
@@ -436,23 +470,23 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_wp(const VTask* __res
     const double md = tb.mu_w[a], sd = tb.sg_w[a], mo = tb.nm_w[a], so = tb.ns_w[a], rho = tb.rho_w[a];
     const double cc = (double)tb.cc[a];
     const double cs = ((1 - rho) * so) + rho * (sigma_w + alpha * cc * 1.0);
-    double ev[MC];
+    double ev[MI];
 #pragma unroll
-    for (int j = 0; j < MC; ++j) {
+    for (int j = 0; j < MI; ++j) {
         const uint32_t x = ci + j * G;
-        if (x < n) ev[j] = ET[i2u[q0 + x]].x;
+        if (x < n) ev[j] = ET.E[i2u[q0 + x]];
     }
     double e1 = 0.0, e2 = 0.0;
 #pragma unroll
-    for (int j = 0; j < MC; ++j) {
+    for (int j = 0; j < MI; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
             e1 += ((1 - rho) * mo) + rho * cc * alpha * (ev[j] + md);
             e2 += cs;
         }
     }
-    for (uint32_t x = ci + MC * G; x < n; x += G) {
-        const double e = ET[i2u[q0 + x]].x;
+    for (uint32_t x = ci + MI * G; x < n; x += G) {
+        const double e = ET.E[i2u[q0 + x]];
         e1 += ((1 - rho) * mo) + rho * cc * alpha * (e + md);
         e2 += cs;
     }
@@ -475,20 +509,22 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_wp(const VTask* __res
     tb.ns_w[a] = ns;
     tb.sg_w[a] = sigma;
     tb.mu_w[a] = ok ? mu : md;
-    D[a - tb.I] = ok ? make_double4(md - mu, sigma - sd, 0.0, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+    const double2 nv = item_vs(tb, 0, a);  // factor 0: the next user pass's
+    put_rec(D, a - tb.I, nv.x, nv.y, ok, md - mu, sigma - sd, 0.0);
 }
 
 // update_v (:712-800) of factor f for the batch's items: per case e (gathered
-// through i2u) and the user's fresh {mean, variance} of f (VS, one 16-byte
-// gather); nothing per case is written.  MODE as k_item_wp.
+// through i2u) and the user's fresh {mean, variance} of f (VS by the user's
+// batch row: part; one 16-byte gather); nothing per case is written.  MODE as
+// k_item_wp.
 template <int MODE>
 __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_vp(const VTask* __restrict__ tasks,
                                                               const VRow* __restrict__ rows,
                                                               const uint32_t* __restrict__ i2u,
                                                               const uint32_t* __restrict__ part, uint32_t f,
-                                                              VBTables tb, const double2* __restrict__ ET,
+                                                              VBTables tb, VBCases ET,
                                                               const double2* __restrict__ VS,
-                                                              double4* __restrict__ D, double2* __restrict__ sums) {
+                                                              VBItemRec* __restrict__ D, double2* __restrict__ sums) {
     __shared__ double red[256];
     const VLane L = vb_lane(tasks, rows);
     const int G = L.G, ci = L.ci;
@@ -499,19 +535,19 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_vp(const VTask* __res
     const double alpha = tb.scal->alpha, svg = tb.sigma_v[f];
     const double md = v[a], sd = s[a], mo = tb.nm_v[off + a], so = tb.ns_v[off + a], rho = tb.rho_v[a];
     const double cc = (double)tb.cc[a];
-    double ev[MC];
-    double2 hv[MC];
+    double ev[MI];
+    double2 hv[MI];
 #pragma unroll
-    for (int j = 0; j < MC; ++j) {
+    for (int j = 0; j < MI; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
-            ev[j] = ET[i2u[q0 + x]].x;
+            ev[j] = ET.E[i2u[q0 + x]];
             hv[j] = VS[part[q0 + x]];
         }
     }
     double e1 = 0.0, e2 = 0.0;
 #pragma unroll
-    for (int j = 0; j < MC; ++j) {
+    for (int j = 0; j < MI; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
             const double h = hv[j].x;
@@ -519,8 +555,8 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_vp(const VTask* __res
             e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (ev[j] + md * h));
         }
     }
-    for (uint32_t x = ci + MC * G; x < n; x += G) {
-        const double e = ET[i2u[q0 + x]].x;
+    for (uint32_t x = ci + MI * G; x < n; x += G) {
+        const double e = ET.E[i2u[q0 + x]];
         const double2 hw = VS[part[q0 + x]];
         const double h = hw.x;
         e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + hw.y));
@@ -543,24 +579,27 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_vp(const VTask* __res
     s[a] = sigma;
     v[a] = ok ? mu : md;
     if (f == 0) tb.t_v[a] += n;
-    D[a - tb.I] = ok ? make_double4(md - mu, sigma - sd, mu * mu - md * md, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+    const double2 nv = item_vs(tb, f + 1, a);
+    put_rec(D, a - tb.I, nv.x, nv.y, ok, md - mu, sigma - sd, mu * mu - md * md);
 }
 
-// Several ranks: one thread per item g of the batch's global item list; its
-// local sums from every rank (recv[r][g], rank order), its global case count,
+// Several ranks (or one rank's XCD slices): one thread per item g of the
+// batch's item list; its partial sums (recv[r][g], r = rank or slice, in order,
+// the parts present in VGItem.mask), its case count,
 // then exactly k_item_vp / k_item_wp's update; the deltas go to D[item] for
 // the next user pass.  Identical inputs on every rank, so identical results.
 __global__ __launch_bounds__(256) void k_item_v(const VGItem* __restrict__ gi, uint32_t nG,
                                                  const double2* __restrict__ recv, int R, uint32_t f, VBTables tb,
-                                                 double4* __restrict__ D) {
+                                                 VBItemRec* __restrict__ D) {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
     if (g >= nG) return;
     const uint32_t a = gi[g].attr, n = gi[g].n;
     double e1 = 0.0, e2 = 0.0;
-    for (int r = 0; r < R; ++r) {
-        e1 += recv[(size_t)r * nG + g].x;
-        e2 += recv[(size_t)r * nG + g].y;
-    }
+    for (int r = 0; r < R; ++r)
+        if (gi[g].mask >> r & 1u) {
+            e1 += recv[(size_t)r * nG + g].x;
+            e2 += recv[(size_t)r * nG + g].y;
+        }
     const size_t off = (size_t)f * tb.p;
     double* __restrict__ v = tb.mu_v + off;
     double* __restrict__ s = tb.sg_v + off;
@@ -575,19 +614,21 @@ __global__ __launch_bounds__(256) void k_item_v(const VGItem* __restrict__ gi, u
     s[a] = sigma;
     v[a] = ok ? mu : md;
     if (f == 0) tb.t_v[a] += n;
-    D[a - tb.I] = ok ? make_double4(md - mu, sigma - sd, mu * mu - md * md, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+    const double2 nv = item_vs(tb, f + 1, a);
+    put_rec(D, a - tb.I, nv.x, nv.y, ok, md - mu, sigma - sd, mu * mu - md * md);
 }
 __global__ __launch_bounds__(256) void k_item_w(const VGItem* __restrict__ gi, uint32_t nG,
                                                  const double2* __restrict__ recv, int R, VBTables tb,
-                                                 double4* __restrict__ D) {
+                                                 VBItemRec* __restrict__ D) {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
     if (g >= nG) return;
     const uint32_t a = gi[g].attr, n = gi[g].n;
     double e1 = 0.0, e2 = 0.0;
-    for (int r = 0; r < R; ++r) {
-        e1 += recv[(size_t)r * nG + g].x;
-        e2 += recv[(size_t)r * nG + g].y;
-    }
+    for (int r = 0; r < R; ++r)
+        if (gi[g].mask >> r & 1u) {
+            e1 += recv[(size_t)r * nG + g].x;
+            e2 += recv[(size_t)r * nG + g].y;
+        }
     const double md = tb.mu_w[a], sd = tb.sg_w[a];
     const uint32_t tw = tb.t_w[a] + n;
     const double nm = e1 / n, ns = e2 / n;
@@ -601,7 +642,8 @@ __global__ __launch_bounds__(256) void k_item_w(const VGItem* __restrict__ gi, u
     tb.ns_w[a] = ns;
     tb.sg_w[a] = sigma;
     tb.mu_w[a] = ok ? mu : md;
-    D[a - tb.I] = ok ? make_double4(md - mu, sigma - sd, 0.0, 1.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+    const double2 nv = item_vs(tb, 0, a);
+    put_rec(D, a - tb.I, nv.x, nv.y, ok, md - mu, sigma - sd, 0.0);
 }
 
 // fixed-order sum of n doubles into out[0] (one block)
@@ -639,14 +681,14 @@ __global__ __launch_bounds__(256) void k_rho_v(VBTables tb) {
 }
 
 // alpha's sum of e^2 + t over the batch, 1024 cases per block
-__global__ __launch_bounds__(256) void k_alpha_partial(const double2* __restrict__ ET, uint32_t B,
+__global__ __launch_bounds__(256) void k_alpha_partial(VBCases ET, uint32_t B,
                                                         double* __restrict__ part) {
     __shared__ double red[256];
     double acc = 0.0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const uint32_t c = blockIdx.x * 1024 + threadIdx.x * 4 + u;
-        if (c < B) acc += ET[c].x * ET[c].x + ET[c].y;
+        if (c < B) acc += ET.E[c] * ET.E[c] + ET.T[c];
     }
     acc = block_sum256(acc, red);
     if (threadIdx.x == 0) part[blockIdx.x] = acc;
@@ -747,14 +789,14 @@ hipError_t vbo_transpose(const double* src, double* dst, uint32_t K, uint32_t Kp
 }
 
 hipError_t vbo_predict(const VRow* rows, uint32_t nrows, const uint32_t* part, const float* r, const double* muT,
-                       const double* sgT, const VBTables& tb, uint32_t Kp, double2* ET, hipStream_t st) {
+                       const double* sgT, const VBTables& tb, uint32_t Kp, VBCases ET, hipStream_t st) {
     if (nrows == 0) return hipSuccess;
     if (Kp > 16 * KBMAX) return hipErrorInvalidValue;
     k_predict<<<(nrows + 15) / 16, 256, 0, st>>>(rows, nrows, part, r, muT, sgT, tb, Kp, ET);
     return hipGetLastError();
 }
 
-hipError_t vbo_update_w0(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
+hipError_t vbo_update_w0(VBCases ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
     if (B == 0) return hipErrorInvalidValue;
     const uint32_t nblk = (B + 1023) / 1024;
     k_w0_partial<<<nblk, 256, 0, st>>>(ET, B, tb, part);
@@ -762,7 +804,7 @@ hipError_t vbo_update_w0(const double2* ET, uint32_t B, const VBTables& tb, doub
     return hipGetLastError();
 }
 
-hipError_t vbo_user_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const VBTables& tb, double2* ET,
+hipError_t vbo_user_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const VBTables& tb, VBCases ET,
                       hipStream_t st) {
     if (ntask == 0) return hipSuccess;
     k_user_w<<<ntask, 256, 0, st>>>(tasks, rows, tb, ET);
@@ -770,19 +812,21 @@ hipError_t vbo_user_w(const VTask* tasks, uint32_t ntask, const VRow* rows, cons
 }
 
 hipError_t vbo_user_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, uint32_t f, int pend,
-                      uint32_t fp, const VBTables& tb, const double4* D, double2* ET, double2* VS, hipStream_t st) {
+                      uint32_t fp, uint32_t rbase, const VBTables& tb, const VBItemRec* D, VBCases ET, double2* VS,
+                      hipStream_t st) {
     if (ntask == 0) return hipSuccess;
+    // every user pass follows an item pass, whose records carry the column-f values
     if (pend == VB_PEND_V)
-        k_user_v<VB_PEND_V><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, tb, D, ET, VS);
+        k_user_v<VB_PEND_V><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, rbase, tb, D, ET, VS);
     else if (pend == VB_PEND_W)
-        k_user_v<VB_PEND_W><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, tb, D, ET, VS);
+        k_user_v<VB_PEND_W><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, rbase, tb, D, ET, VS);
     else
-        k_user_v<VB_PEND_NONE><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, tb, D, ET, VS);
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
 hipError_t vbo_user_flush(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, int pend,
-                          uint32_t fp, const VBTables& tb, const double4* D, double2* ET, hipStream_t st) {
+                          uint32_t fp, const VBTables& tb, const VBItemRec* D, VBCases ET, hipStream_t st) {
     if (ntask == 0 || pend == VB_PEND_NONE) return hipSuccess;
     if (pend == VB_PEND_V)
         k_user_flush<VB_PEND_V><<<ntask, 256, 0, st>>>(tasks, rows, part, fp, tb, D, ET);
@@ -792,7 +836,7 @@ hipError_t vbo_user_flush(const VTask* tasks, uint32_t ntask, const VRow* rows, 
 }
 
 hipError_t vbo_item_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const VBTables& tb,
-                      const double2* ET, double4* D, double2* sums, hipStream_t st) {
+                      VBCases ET, VBItemRec* D, double2* sums, hipStream_t st) {
     if (ntask == 0) return hipSuccess;
     if (sums)
         k_item_wp<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, i2u, tb, ET, D, sums);
@@ -802,7 +846,7 @@ hipError_t vbo_item_w(const VTask* tasks, uint32_t ntask, const VRow* rows, cons
 }
 
 hipError_t vbo_item_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const uint32_t* part,
-                      uint32_t f, const VBTables& tb, const double2* ET, const double2* VS, double4* D, double2* sums,
+                      uint32_t f, const VBTables& tb, VBCases ET, const double2* VS, VBItemRec* D, double2* sums,
                       hipStream_t st) {
     if (ntask == 0) return hipSuccess;
     if (sums)
@@ -813,7 +857,7 @@ hipError_t vbo_item_v(const VTask* tasks, uint32_t ntask, const VRow* rows, cons
 }
 
 hipError_t vbo_item_update(const VGItem* gi, uint32_t nG, const double2* recv, int R, int factor, uint32_t f,
-                           const VBTables& tb, double4* D, hipStream_t st) {
+                           const VBTables& tb, VBItemRec* D, hipStream_t st) {
     if (nG == 0) return hipSuccess;
     if (factor)
         k_item_v<<<(nG + 255) / 256, 256, 0, st>>>(gi, nG, recv, R, f, tb, D);
@@ -822,7 +866,7 @@ hipError_t vbo_item_update(const VGItem* gi, uint32_t nG, const double2* recv, i
     return hipGetLastError();
 }
 
-hipError_t vbo_hyper(const double2* ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
+hipError_t vbo_hyper(VBCases ET, uint32_t B, const VBTables& tb, double* part, hipStream_t st) {
     k_rho_v<<<(tb.p + 255) / 256, 256, 0, st>>>(tb);
     const uint32_t nab = (B + 1023) / 1024, nchunk = (tb.p + 2047) / 2048;
     double* spart = part + nab + 8;
@@ -833,7 +877,7 @@ hipError_t vbo_hyper(const double2* ET, uint32_t B, const VBTables& tb, double* 
 }
 
 // ---- several ranks: local partial sums, then the final steps from every rank's sums
-hipError_t vbo_w0_local(const double2* ET, uint32_t B, const VBTables& tb, double* part, double* out, hipStream_t st) {
+hipError_t vbo_w0_local(VBCases ET, uint32_t B, const VBTables& tb, double* part, double* out, hipStream_t st) {
     if (B == 0) return hipMemsetAsync(out, 0, sizeof(double), st);
     const uint32_t nblk = (B + 1023) / 1024;
     k_w0_partial<<<nblk, 256, 0, st>>>(ET, B, tb, part);
@@ -844,7 +888,7 @@ hipError_t vbo_w0_final(const double* recv, int R, uint32_t B, const VBTables& t
     k_w0_final<<<1, 256, 0, st>>>(recv, (uint32_t)R, B, tb);
     return hipGetLastError();
 }
-hipError_t vbo_hyper_local(const double2* ET, uint32_t B, const VBTables& tb, uint32_t u0, uint32_t u1, double* part,
+hipError_t vbo_hyper_local(VBCases ET, uint32_t B, const VBTables& tb, uint32_t u0, uint32_t u1, double* part,
                            size_t part_cap, double* out, hipStream_t st) {
     const uint32_t nab = (B + 1023) / 1024;
     if ((size_t)nab + 8 + (size_t)(tb.K + 1) * std::max(1u, (u1 - u0 + 2047) / 2048) > part_cap)
