@@ -31,7 +31,9 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <exception>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "comm.h"
@@ -68,7 +70,11 @@ struct VBLearner {
     std::vector<double> tr, sr;
     std::vector<uint32_t> shuffle, bid, bcase, upos, ipos;
     VBLayout lay[2];                 // epoch e uses lay[e & 1]
-    std::thread worker;              // builds lay[(e + 1) & 1] during epoch e
+    std::thread worker;              // builds and uploads lay[(e + 1) & 1] during epoch e
+    std::exception_ptr worker_err;   // its failure, rethrown by run()
+    int dev = 0;
+    hipStream_t ust = nullptr;       // layout uploads (the worker's)
+    hipEvent_t uev[2] = {}, done[2] = {};  // layout e & 1: uploaded / free again
     uint32_t built = 0;              // epochs whose layout exists (ready or being built)
     // device
     DBuf d_mu_v, d_sg_v, d_nm_v, d_ns_v, d_mu_w, d_sg_w, d_nm_w, d_ns_w, d_rho_w, d_rho_v, d_t_w, d_t_v, d_cc;
@@ -84,10 +90,11 @@ struct VBLearner {
     std::vector<uint64_t> ubounds;     // [R + 1] user ranges of every rank
     std::vector<uint8_t> mine;         // [N] case belongs to an owned user
     uint32_t gmax = 0;                 // largest per-batch item count
-    // one rank: item rows cut into XS slices by the partner user's batch row (slice x
-    // = user rows [x nu / XS, (x+1) nu / XS)); slice x's tasks take blocks x, x + XS, ...,
+    // one rank: item rows cut into XS slices by the partner case's user-grouped position
+    // (equal case counts); slice x's tasks take blocks x, x + XS, ...,
     // i.e. XCD x under the round-robin block dispatch, so its gathers (e and the users'
-    // {mean, variance}) stay inside 1/XS of the batch -- resident in that XCD's L2
+    // {mean, variance}) stay inside 1/XS of the batch -- resident in that XCD's L2.
+    // SBMF_VB_SLICES (default 8): 838 ms per Netflix-shaped K=200 epoch vs 1061 unsliced (r03r)
     uint32_t XS = 1;
     DBuf d_send, d_recv, d_sums, d_recvg;
     double last_rmse = NAN, last_alpha = NAN;
@@ -98,12 +105,16 @@ struct VBLearner {
         if (worker.joinable()) worker.join();
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {uev[0], uev[1], done[0], done[1]})
+            if (e) (void)hipEventDestroy(e);
+        if (ust) (void)hipStreamDestroy(ust);
     }
 
     void init(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r, uint64_t nt,
               const uint32_t* tu_, const uint32_t* ti_, const double* tr_, uint32_t I_, uint32_t J_, hipStream_t s,
               Comm* cm);
     void build_layout(VBLayout& L, uint32_t ep);
+    void stage_layout(VBLayout& L, uint32_t e);
     void run(uint32_t epochs, sbmf_sweep_cb cb, void* user);
     void item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_, const uint32_t* i2u_,
                    int factor, uint32_t f, VBCases ETu);
@@ -177,7 +188,7 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     }
     if (R == 1) {
         const char* xs = std::getenv("SBMF_VB_SLICES");
-        XS = xs ? (uint32_t)std::min(32, std::max(1, std::atoi(xs))) : 1u;
+        XS = xs ? (uint32_t)std::min(32, std::max(1, std::atoi(xs))) : 8u;
     }
     u0 = (uint32_t)ubounds[rank];
     u1 = (uint32_t)ubounds[rank + 1];
@@ -257,6 +268,13 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     shuffle.resize(N);
     for (uint32_t x = 0; x < N; ++x) shuffle[x] = x + 1;
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipGetDevice(&dev));
+    HIPCHK(hipStreamCreateWithFlags(&ust, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+        HIPCHK(hipEventCreateWithFlags(&uev[k], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(done[k], st));
+    }
     HIPCHK(hipStreamSynchronize(st));
 }
 
@@ -322,25 +340,70 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
             for (uint32_t l = lo; l < hi; ++l) bid[l] = perm(l) / S;  // = ceil((perm + 1) / S) - 1
         });
     }
+    const bool trace = std::getenv("SBMF_VB_TRACE") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!trace) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[vbo] layout %u: %s %.1f ms\n", ep, what,
+                     std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+    };
+    lap("shuffle");
+    // per-thread counts of each batch (all cases / own cases), then the fill positions:
+    // thread t's own cases of batch b go after threads < t's, each chunk in file order
+    const unsigned nth = host_threads();
+    std::vector<uint32_t> tcnt((size_t)nth * NB * 2, 0);
+    parallel_chunks(N, [&](unsigned t, uint32_t lo, uint32_t hi) {
+        uint32_t* c = &tcnt[(size_t)t * NB * 2];
+        for (uint32_t l = lo; l < hi; ++l) {
+            c[2 * bid[l]]++;
+            c[2 * bid[l] + 1] += mine[l];
+        }
+    });
     L.bsize.assign(NB, 0);
     L.gbsize.assign(NB, 0);
-    for (uint32_t l = 0; l < N; ++l) {
-        L.gbsize[bid[l]]++;
-        L.bsize[bid[l]] += mine[l];
-    }
+    for (unsigned t = 0; t < nth; ++t)
+        for (uint32_t b = 0; b < NB; ++b) {
+            L.gbsize[b] += tcnt[((size_t)t * NB + b) * 2];
+            L.bsize[b] += tcnt[((size_t)t * NB + b) * 2 + 1];
+        }
     L.bbase.assign(NB + 1, 0);  // a batch's (own) cases are entries [bbase[b], bbase[b+1]) of either order
     for (uint32_t b = 0; b < NB; ++b) L.bbase[b + 1] = L.bbase[b] + L.bsize[b];
     bcase.resize(NL);  // the (own) cases of each batch, in file order
     {
-        std::vector<uint32_t> fill(L.bbase.begin(), L.bbase.end() - 1);
-        for (uint32_t l = 0; l < N; ++l)
-            if (mine[l]) bcase[fill[bid[l]]++] = l;
+        std::vector<uint32_t> fill((size_t)nth * NB);
+        for (uint32_t b = 0; b < NB; ++b) {
+            uint32_t at = L.bbase[b];
+            for (unsigned t = 0; t < nth; ++t) {
+                fill[(size_t)t * NB + b] = at;
+                at += tcnt[((size_t)t * NB + b) * 2 + 1];
+            }
+        }
+        parallel_chunks(N, [&](unsigned t, uint32_t lo, uint32_t hi) {
+            uint32_t* f = &fill[(size_t)t * NB];
+            for (uint32_t l = lo; l < hi; ++l)
+                if (mine[l]) bcase[f[bid[l]]++] = l;
+        });
     }
-    // several ranks: every batch's items over all ranks, and each item's index there
+    lap("batches");
+    // several ranks (every batch's items over all ranks) or XCD slices: each batch's item
+    // list, and each item's index there
     std::vector<uint32_t> gidx;
     if (R > 1 || XS > 1) {
         std::vector<uint32_t> cnt((size_t)NB * J, 0);
-        for (uint32_t l = 0; l < N; ++l) cnt[(size_t)bid[l] * J + ti[l]]++;
+        {
+            std::vector<std::vector<uint32_t>> tc(nth);
+            parallel_chunks(N, [&](unsigned t, uint32_t lo, uint32_t hi) {
+                tc[t].assign((size_t)NB * J, 0);
+                for (uint32_t l = lo; l < hi; ++l) tc[t][(size_t)bid[l] * J + ti[l]]++;
+            });
+            parallel_chunks(NB * J, [&](unsigned, uint32_t lo, uint32_t hi) {
+                for (auto& c : tc)
+                    if (!c.empty())
+                        for (uint32_t x = lo; x < hi; ++x) cnt[x] += c[x];
+            });
+        }
         L.gitems.clear();
         L.gitem0.assign(NB + 1, 0);
         gidx.assign((size_t)NB * J, 0);
@@ -355,6 +418,7 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         }
         L.gitem0[NB] = (uint32_t)L.gitems.size();
     }
+    lap("item lists");
     upos.resize(N);
     ipos.resize(N);
     L.upart.resize(NL);
@@ -434,7 +498,11 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
                            Part& P) {
         const uint32_t c0 = L.bbase[b], c1 = L.bbase[b + 1];
         const uint32_t nG = (R > 1 || XS > 1) ? L.gitem0[b + 1] - L.gitem0[b] : 0;
-        auto slice = [&](uint32_t l) { return XS > 1 ? (uint32_t)((uint64_t)urow[tu[l]] * XS / nu) : 0u; };
+        // slice x: the cases at user-grouped positions [c0 + x B / XS, c0 + (x+1) B / XS) --
+        // equal case counts, and whole users' rows but the boundary ones (positions follow rows)
+        const uint64_t B = c1 - c0;
+        auto slice = [&](uint32_t l) { return XS > 1 ? (uint32_t)((uint64_t)(upos[l] - c0) * XS / B) : 0u; };
+        (void)nu;
         std::fill(off.begin(), off.end(), 0u);  // [XS][J]
         for (uint32_t x = c0; x < c1; ++x) {
             const uint32_t l = bcase[x];
@@ -471,7 +539,6 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
             L.ipart[q] = urow[tu[l]];
         }
     };
-    const unsigned nth = host_threads();
     {
         std::vector<std::thread> th;
         for (unsigned t = 0; t < nth; ++t)
@@ -484,23 +551,28 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
             });
         for (auto& x : th) x.join();
     }
+    lap("grouping");
+    // every batch's rows and tasks, batch-major (copied in parallel, one batch per task)
     auto concat = [&](std::vector<Part>& P, std::vector<VRow>& rows, std::vector<uint32_t>& row0,
                       std::vector<VTask>& tasks, std::vector<uint32_t>& task0) {
-        rows.clear();
-        tasks.clear();
         row0.assign(NB + 1, 0);
         task0.assign(NB + 1, 0);
         for (uint32_t b = 0; b < NB; ++b) {
-            row0[b] = (uint32_t)rows.size();
-            task0[b] = (uint32_t)tasks.size();
-            for (VTask tk : P[b].tasks) {
-                tk.row0 += row0[b];
-                tasks.push_back(tk);
-            }
-            rows.insert(rows.end(), P[b].rows.begin(), P[b].rows.end());
+            row0[b + 1] = row0[b] + (uint32_t)P[b].rows.size();
+            task0[b + 1] = task0[b] + (uint32_t)P[b].tasks.size();
         }
-        row0[NB] = (uint32_t)rows.size();
-        task0[NB] = (uint32_t)tasks.size();
+        rows.resize(row0[NB]);
+        tasks.resize(task0[NB]);
+        parallel_chunks(NB, [&](unsigned, uint32_t lo, uint32_t hi) {
+            for (uint32_t b = lo; b < hi; ++b) {
+                std::copy(P[b].rows.begin(), P[b].rows.end(), rows.begin() + row0[b]);
+                for (size_t k = 0; k < P[b].tasks.size(); ++k) {
+                    VTask tk = P[b].tasks[k];
+                    tk.row0 += row0[b];
+                    tasks[task0[b] + k] = tk;
+                }
+            }
+        });
     };
     concat(pu, L.urows, L.urow0, L.utasks, L.utask0);
     concat(pi, L.irows, L.irow0, L.itasks, L.itask0);
@@ -509,6 +581,7 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         for (uint32_t l = lo; l < hi; ++l)
             if (mine[l]) L.i2u[ipos[l]] = upos[l];
     });
+    lap("concat + i2u");
 }
 
 // Several ranks: one item pass of a batch (the update_w biases, factor == 0,
@@ -538,56 +611,50 @@ void VBLearner::sync_users() {
     comm->bcast_ranges(tb.mu_w, sizeof(double), ubounds, st);
 }
 
+// Epoch e's layout to the device on the upload stream once the kernels of epoch
+// e - 2 (the last users of these buffers, which may be reallocated here) are
+// done; uev[e & 1] marks completion.  Pageable copies: the calling (worker)
+// thread blocks, the compute stream does not.
+void VBLearner::stage_layout(VBLayout& L, uint32_t e) {
+    const auto h0 = std::chrono::steady_clock::now();
+    HIPCHK(hipEventSynchronize(done[e & 1]));
+    upload_grow(L.d_urows, L.urows, ust);
+    upload_grow(L.d_irows, L.irows, ust);
+    upload_grow(L.d_upart, L.upart, ust);
+    upload_grow(L.d_ur, L.ur, ust);
+    upload_grow(L.d_i2u, L.i2u, ust);
+    upload_grow(L.d_ipart, L.ipart, ust);
+    upload_grow(L.d_utasks, L.utasks, ust);
+    upload_grow(L.d_itasks, L.itasks, ust);
+    if (R > 1 || XS > 1) upload_grow(L.d_gitems, L.gitems, ust);
+    HIPCHK(hipEventRecord(uev[e & 1], ust));
+    if (std::getenv("SBMF_VB_TRACE")) {
+        HIPCHK(hipEventSynchronize(uev[e & 1]));
+        std::fprintf(stderr, "[vbo] layout %u: upload %.1f ms (to completion)\n", e,
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count());
+    }
+}
+
 void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
     for (uint32_t it = 0; it < epochs; ++it) {
         const auto h0 = std::chrono::steady_clock::now();
-        // this epoch's layout: built by the worker during the previous epoch (or now)
+        // this epoch's layout: built and uploaded by the worker during the previous epoch
+        // (or now); the compute stream waits for its upload
         if (built == epoch) {
             build_layout(lay[epoch & 1], epoch);
+            stage_layout(lay[epoch & 1], epoch);
             built = epoch + 1;
         } else if (worker.joinable()) {
             worker.join();
+            if (worker_err) std::rethrow_exception(std::exchange(worker_err, nullptr));
         }
         VBLayout& L = lay[epoch & 1];
-        // SBMF_VB_TRACE=1: the host side of an epoch -- layout wait / build, device
-        // (re)allocation of the layout buffers (first epochs), and the uploads timed to
-        // their completion (the stream is drained before and after, trace runs only)
-        const bool trace = std::getenv("SBMF_VB_TRACE") != nullptr;
-        if (trace) HIPCHK(hipStreamSynchronize(st));
-        const auto h1 = std::chrono::steady_clock::now();
-        auto grow = [](DBuf& d, size_t bytes) { d.ensure(std::max<size_t>(bytes, 1)); };
-        grow(L.d_urows, L.urows.size() * sizeof(L.urows[0]));
-        grow(L.d_irows, L.irows.size() * sizeof(L.irows[0]));
-        grow(L.d_upart, L.upart.size() * sizeof(L.upart[0]));
-        grow(L.d_ur, L.ur.size() * sizeof(L.ur[0]));
-        grow(L.d_i2u, L.i2u.size() * sizeof(L.i2u[0]));
-        grow(L.d_ipart, L.ipart.size() * sizeof(L.ipart[0]));
-        grow(L.d_utasks, L.utasks.size() * sizeof(L.utasks[0]));
-        grow(L.d_itasks, L.itasks.size() * sizeof(L.itasks[0]));
-        if (R > 1 || XS > 1) {
-            grow(L.d_gitems, L.gitems.size() * sizeof(L.gitems[0]));
-            d_sums.ensure((size_t)XS * std::max(gmax, 1u) * sizeof(double2));
-        }
+        HIPCHK(hipStreamWaitEvent(st, uev[epoch & 1], 0));
+        if (R > 1 || XS > 1) d_sums.ensure((size_t)XS * std::max(gmax, 1u) * sizeof(double2));
         if (R > 1) d_recvg.ensure((size_t)R * std::max(gmax, 1u) * sizeof(double2));
-        const auto h2 = std::chrono::steady_clock::now();
-        upload_grow(L.d_urows, L.urows, st);
-        upload_grow(L.d_irows, L.irows, st);
-        upload_grow(L.d_upart, L.upart, st);
-        upload_grow(L.d_ur, L.ur, st);
-        upload_grow(L.d_i2u, L.i2u, st);
-        upload_grow(L.d_ipart, L.ipart, st);
-        upload_grow(L.d_utasks, L.utasks, st);
-        upload_grow(L.d_itasks, L.itasks, st);
-        if (R > 1 || XS > 1) upload_grow(L.d_gitems, L.gitems, st);
-        if (trace) {
-            HIPCHK(hipStreamSynchronize(st));
-            const auto h3 = std::chrono::steady_clock::now();
-            auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-                return std::chrono::duration<double, std::milli>(b - a).count();
-            };
-            std::fprintf(stderr, "[vbo] epoch %u host: layout %.1f ms, device alloc %.1f ms, upload %.1f ms (to completion)\n",
-                         epoch, ms(h0, h1), ms(h1, h2), ms(h2, h3));
-        }
+        if (std::getenv("SBMF_VB_TRACE"))
+            std::fprintf(stderr, "[vbo] epoch %u: waited %.1f ms for its layout\n", epoch,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count());
         ms_layout = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
         n_launch = 0;
         HIPCHK(hipEventRecord(ev[0], st));
@@ -653,10 +720,19 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         }
         // the next epoch's shuffle and layout, on the host while this epoch runs
         // (the reference stream after this epoch's shuffle is exactly the next one's)
+        HIPCHK(hipEventRecord(done[epoch & 1], st));  // this layout's device buffers are free after this
         if (built == epoch + 1) {
             built = epoch + 2;
             const uint32_t nx = epoch + 1;
-            worker = std::thread([this, nx] { build_layout(lay[nx & 1], nx); });
+            worker = std::thread([this, nx] {
+                try {
+                    HIPCHK(hipSetDevice(dev));
+                    build_layout(lay[nx & 1], nx);
+                    stage_layout(lay[nx & 1], nx);
+                } catch (...) {
+                    worker_err = std::current_exception();
+                }
+            });
         }
         sync_users();  // several ranks: owned user means to every rank (test RMSE, factors)
         HIPCHK(hipEventRecord(ev[1], st));
