@@ -45,16 +45,23 @@ namespace sbmf {
 // One epoch's batch layout (host side), built by a worker thread while the
 // GPU runs the previous epoch, and its device copy.
 struct VBLayout {
-    std::vector<VRow> urows, irows;    // every batch's rows, batch-major
-    std::vector<VTask> utasks, itasks; // 256-thread tasks over those rows
+    // per batch and orientation: rows stably sorted by lane-group size (records in row
+    // order) and the 256-thread tasks over them (row0 relative to the batch's first row);
+    // on the device every batch's rows and tasks at urow0[b] / utask0[b] (batch-major)
+    struct Part {
+        std::vector<VRow> rows;
+        std::vector<VTask> tasks;
+    };
+    std::vector<Part> pu, pi;
     std::vector<uint32_t> urow0, irow0, utask0, itask0, bsize, bbase;
-    std::vector<uint32_t> upart, i2u, ipart;  // [N] per entry of each order (i2u: the user-order position)
+    std::vector<uint32_t> upart;  // [N] user order: the case's item attribute
+    std::vector<uint2> iu;        // [N] item order: {user-grouped position, the user's batch row}
     std::vector<float> ur;                          // [N] target per user-order entry
     // several ranks: bsize / bbase count this rank's cases; gbsize the whole batch;
     // gitems the batch's items over all ranks (entries [gitem0[b], gitem0[b+1]))
     std::vector<uint32_t> gbsize, gitem0;
     std::vector<VGItem> gitems;
-    DBuf d_urows, d_irows, d_utasks, d_itasks, d_upart, d_i2u, d_ipart, d_ur, d_gitems;
+    DBuf d_urows, d_irows, d_utasks, d_itasks, d_upart, d_iu, d_ur, d_gitems;
 };
 
 struct VBLearner {
@@ -68,7 +75,9 @@ struct VBLearner {
     // host data
     std::vector<uint32_t> tu, ti, su, si;
     std::vector<double> tr, sr;
-    std::vector<uint32_t> shuffle, bid, bcase, upos, ipos;
+    std::vector<uint32_t> shuffle, bid;
+    std::vector<uint32_t> btu, bti, bupos;  // the (own) cases batch-major, file order inside a batch
+    std::vector<float> btr;
     VBLayout lay[2];                 // epoch e uses lay[e & 1]
     std::thread worker;              // builds and uploads lay[(e + 1) & 1] during epoch e
     std::exception_ptr worker_err;   // its failure, rethrown by run()
@@ -116,7 +125,7 @@ struct VBLearner {
     void build_layout(VBLayout& L, uint32_t ep);
     void stage_layout(VBLayout& L, uint32_t e);
     void run(uint32_t epochs, sbmf_sweep_cb cb, void* user);
-    void item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_, const uint32_t* i2u_,
+    void item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_, const uint2* iu_,
                    int factor, uint32_t f, VBCases ETu);
     void sync_users();
 };
@@ -291,28 +300,41 @@ void parallel_chunks(uint32_t n, F&& f) {
     }
     for (auto& x : th) x.join();
 }
-// Keyed pseudorandom permutation of [0, n) (throughput mode's shuffle):
-// a 4-round balanced Feistel network on 2h >= log2(n) bits with Philox round
-// keys, cycle-walking back into [0, n).  O(1) per case, no shared state, so
-// every case's batch is computed in parallel.
+// Keyed pseudorandom permutation of [0, n) (throughput mode's shuffle): a
+// 4-round unbalanced Feistel network on bits = ceil(log2 n) (halves of a and
+// c = bits - a bits, swapping sizes every round), cycle-walking back into
+// [0, n) (< 2 steps on average).  Round function: a murmur3 finaliser of the
+// half keyed per (seed, epoch, round) with Philox.  O(1) per case, no shared
+// state, so every case's batch is computed in parallel.
 struct FeistelPerm {
-    uint64_t seed;
-    uint32_t ep, n, h, mask;
-    FeistelPerm(uint64_t s, uint32_t e, uint32_t n_) : seed(s), ep(e), n(n_) {
-        h = 1;
-        while ((1ull << (2 * h)) < n) ++h;
-        mask = (1u << h) - 1;
+    uint32_t n, a, c, key[4];
+    FeistelPerm(uint64_t seed, uint32_t ep, uint32_t n_) : n(n_) {
+        uint32_t bits = 2;
+        while ((1ull << bits) < n) ++bits;
+        a = bits / 2;
+        c = bits - a;
+        const P4 o = philox4x32_10(ep, 0, 0x56424f00u, PHILOX_SALT, (uint32_t)seed, (uint32_t)(seed >> 32));
+        for (int r = 0; r < 4; ++r) key[r] = o.x[r];
+    }
+    static uint32_t mix(uint32_t h) {
+        h ^= h >> 16;
+        h *= 0x85ebca6bu;
+        h ^= h >> 13;
+        h *= 0xc2b2ae35u;
+        h ^= h >> 16;
+        return h;
     }
     uint32_t operator()(uint32_t x) const {
         do {
-            uint32_t L = x >> h, R = x & mask;
-            for (uint32_t r = 0; r < 4; ++r) {
-                const P4 o = philox4x32_10(R, ep, 0x56424f00u | r, PHILOX_SALT, (uint32_t)seed, (uint32_t)(seed >> 32));
-                const uint32_t nl = R;
-                R = (L ^ o.x[0]) & mask;
+            uint32_t hl = a, hr = c;  // bits of L and R
+            uint32_t L = x >> hr, R = x & ((1u << hr) - 1);
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t nl = R, nr = (L ^ mix(R ^ key[r])) & ((1u << hl) - 1);
                 L = nl;
+                R = nr;
+                std::swap(hl, hr);
             }
-            x = (L << h) | R;
+            x = (L << hr) | R;
         } while (x >= n);
         return x;
     }
@@ -370,7 +392,9 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         }
     L.bbase.assign(NB + 1, 0);  // a batch's (own) cases are entries [bbase[b], bbase[b+1]) of either order
     for (uint32_t b = 0; b < NB; ++b) L.bbase[b + 1] = L.bbase[b] + L.bsize[b];
-    bcase.resize(NL);  // the (own) cases of each batch, in file order
+    btu.resize(NL);  // the (own) cases of each batch, in file order: user, item, rating
+    bti.resize(NL);
+    btr.resize(NL);
     {
         std::vector<uint32_t> fill((size_t)nth * NB);
         for (uint32_t b = 0; b < NB; ++b) {
@@ -383,7 +407,12 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         parallel_chunks(N, [&](unsigned t, uint32_t lo, uint32_t hi) {
             uint32_t* f = &fill[(size_t)t * NB];
             for (uint32_t l = lo; l < hi; ++l)
-                if (mine[l]) bcase[f[bid[l]]++] = l;
+                if (mine[l]) {
+                    const uint32_t x = f[bid[l]]++;
+                    btu[x] = tu[l];
+                    bti[x] = ti[l];
+                    btr[x] = (float)tr[l];
+                }
         });
     }
     lap("batches");
@@ -419,17 +448,15 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         L.gitem0[NB] = (uint32_t)L.gitems.size();
     }
     lap("item lists");
-    upos.resize(N);
-    ipos.resize(N);
+    bupos.resize(NL);  // a batch case's user-grouped position
+    L.iu.resize(NL);
     L.upart.resize(NL);
-    L.ipart.resize(NL);
     L.ur.resize(NL);
-    // per batch and orientation: rows stably sorted by lane-group size, records in row order
-    struct Part {
-        std::vector<VRow> rows;
-        std::vector<VTask> tasks;  // row0 relative to the batch's first row
-    };
-    std::vector<Part> pu(NB), pi(NB);
+    using Part = VBLayout::Part;
+    L.pu.resize(NB);
+    L.pi.resize(NB);
+    std::vector<Part>& pu = L.pu;
+    std::vector<Part>& pi = L.pi;
     // lane-group size of a row: the fewest lanes (a power of two, 1..256) that hold its
     // cases at VB_CASES_PER_LANE per lane in registers -- a user row of a batch (a few
     // cases) takes one lane, so a task covers up to 256 rows and every lane has several
@@ -471,7 +498,7 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
     auto group_users = [&](uint32_t b, std::vector<uint32_t>& off, std::vector<uint32_t>& urow, Part& P) {
         const uint32_t c0 = L.bbase[b], c1 = L.bbase[b + 1];
         std::fill(off.begin(), off.end(), 0u);
-        for (uint32_t x = c0; x < c1; ++x) off[tu[bcase[x]]]++;
+        for (uint32_t x = c0; x < c1; ++x) off[btu[x]]++;
         std::vector<VRow> rows;
         for (uint32_t a = 0; a < I; ++a)
             if (off[a]) rows.push_back(VRow{a, 0u, off[a], 0u});
@@ -484,11 +511,10 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
             urow[P.rows[r].attr] = r;
         }
         for (uint32_t x = c0; x < c1; ++x) {
-            const uint32_t l = bcase[x];
-            const uint32_t q = off[tu[l]]++;
-            upos[l] = q;
-            L.upart[q] = I + ti[l];
-            L.ur[q] = (float)tr[l];
+            const uint32_t q = off[btu[x]]++;
+            bupos[x] = q;
+            L.upart[q] = I + bti[x];
+            L.ur[q] = btr[x];
         }
     };
     // items of batch b, cut into XS slices by the partner's user row (XS = 1: whole rows);
@@ -501,13 +527,10 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         // slice x: the cases at user-grouped positions [c0 + x B / XS, c0 + (x+1) B / XS) --
         // equal case counts, and whole users' rows but the boundary ones (positions follow rows)
         const uint64_t B = c1 - c0;
-        auto slice = [&](uint32_t l) { return XS > 1 ? (uint32_t)((uint64_t)(upos[l] - c0) * XS / B) : 0u; };
+        auto slice = [&](uint32_t x) { return XS > 1 ? (uint32_t)((uint64_t)(bupos[x] - c0) * XS / B) : 0u; };
         (void)nu;
         std::fill(off.begin(), off.end(), 0u);  // [XS][J]
-        for (uint32_t x = c0; x < c1; ++x) {
-            const uint32_t l = bcase[x];
-            off[(size_t)slice(l) * J + ti[l]]++;
-        }
+        for (uint32_t x = c0; x < c1; ++x) off[(size_t)slice(x) * J + bti[x]]++;
         P.rows.clear();
         P.tasks.clear();
         std::vector<std::vector<VTask>> st(XS);
@@ -533,10 +556,8 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
             for (uint32_t xs = 0; xs < XS; ++xs)
                 P.tasks.push_back(t < st[xs].size() ? st[xs][t] : VTask{0u, 0u, 0u, 0u});
         for (uint32_t x = c0; x < c1; ++x) {
-            const uint32_t l = bcase[x];
-            const uint32_t q = off[(size_t)slice(l) * J + ti[l]]++;
-            ipos[l] = q;
-            L.ipart[q] = urow[tu[l]];
+            const uint32_t q = off[(size_t)slice(x) * J + bti[x]]++;
+            L.iu[q] = make_uint2(bupos[x], urow[btu[x]]);
         }
     };
     {
@@ -552,52 +573,34 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
         for (auto& x : th) x.join();
     }
     lap("grouping");
-    // every batch's rows and tasks, batch-major (copied in parallel, one batch per task)
-    auto concat = [&](std::vector<Part>& P, std::vector<VRow>& rows, std::vector<uint32_t>& row0,
-                      std::vector<VTask>& tasks, std::vector<uint32_t>& task0) {
+    // every batch's rows and tasks, batch-major on the device (stage_layout copies them)
+    auto offsets = [&](const std::vector<Part>& P, std::vector<uint32_t>& row0, std::vector<uint32_t>& task0) {
         row0.assign(NB + 1, 0);
         task0.assign(NB + 1, 0);
         for (uint32_t b = 0; b < NB; ++b) {
             row0[b + 1] = row0[b] + (uint32_t)P[b].rows.size();
             task0[b + 1] = task0[b] + (uint32_t)P[b].tasks.size();
         }
-        rows.resize(row0[NB]);
-        tasks.resize(task0[NB]);
-        parallel_chunks(NB, [&](unsigned, uint32_t lo, uint32_t hi) {
-            for (uint32_t b = lo; b < hi; ++b) {
-                std::copy(P[b].rows.begin(), P[b].rows.end(), rows.begin() + row0[b]);
-                for (size_t k = 0; k < P[b].tasks.size(); ++k) {
-                    VTask tk = P[b].tasks[k];
-                    tk.row0 += row0[b];
-                    tasks[task0[b] + k] = tk;
-                }
-            }
-        });
     };
-    concat(pu, L.urows, L.urow0, L.utasks, L.utask0);
-    concat(pi, L.irows, L.irow0, L.itasks, L.itask0);
-    L.i2u.resize(NL);
-    parallel_chunks(N, [&](unsigned, uint32_t lo, uint32_t hi) {
-        for (uint32_t l = lo; l < hi; ++l)
-            if (mine[l]) L.i2u[ipos[l]] = upos[l];
-    });
-    lap("concat + i2u");
+    offsets(pu, L.urow0, L.utask0);
+    offsets(pi, L.irow0, L.itask0);
+    lap("offsets");
 }
 
 // Several ranks: one item pass of a batch (the update_w biases, factor == 0,
 // or update_v of factor f): local sums -> all-gather -> the same update on
 // every rank, its deltas to D for the next user pass.
 void VBLearner::item_pass(const VBLayout& L, uint32_t b, const VTask* it_, uint32_t nit, const VRow* ir_,
-                          const uint32_t* i2u_, int factor, uint32_t f, VBCases ETu) {
+                          const uint2* iu_, int factor, uint32_t f, VBCases ETu) {
     const uint32_t nG = L.gitem0[b + 1] - L.gitem0[b];
     if (nG == 0) return;  // every rank sees the same global list
     double2* sums = d_sums.as<double2>();
     HIPCHK(hipMemsetAsync(sums, 0, (size_t)nG * sizeof(double2), st));
     if (factor)
-        HIPCHK(vbo_item_v(it_, nit, ir_, i2u_, L.d_ipart.as<uint32_t>(), f, tb, ETu, d_VS.as<double2>(),
+        HIPCHK(vbo_item_v(it_, nit, ir_, iu_, f, tb, ETu, d_VS.as<double2>(),
                           d_D.as<VBItemRec>(), sums, st));
     else
-        HIPCHK(vbo_item_w(it_, nit, ir_, i2u_, tb, ETu, d_D.as<VBItemRec>(), sums, st));
+        HIPCHK(vbo_item_w(it_, nit, ir_, iu_, tb, ETu, d_D.as<VBItemRec>(), sums, st));
     comm->allgather(sums, (size_t)nG * sizeof(double2), d_recvg.p, st);
     HIPCHK(vbo_item_update(L.d_gitems.as<VGItem>() + L.gitem0[b], nG, d_recvg.as<double2>(), R, factor, f, tb,
                            d_D.as<VBItemRec>(), st));
@@ -618,14 +621,24 @@ void VBLearner::sync_users() {
 void VBLearner::stage_layout(VBLayout& L, uint32_t e) {
     const auto h0 = std::chrono::steady_clock::now();
     HIPCHK(hipEventSynchronize(done[e & 1]));
-    upload_grow(L.d_urows, L.urows, ust);
-    upload_grow(L.d_irows, L.irows, ust);
+    auto parts = [&](const std::vector<VBLayout::Part>& P, const std::vector<uint32_t>& row0,
+                     const std::vector<uint32_t>& task0, DBuf& drows, DBuf& dtasks) {
+        drows.ensure(std::max<size_t>(row0[NB], 1) * sizeof(VRow));
+        dtasks.ensure(std::max<size_t>(task0[NB], 1) * sizeof(VTask));
+        for (uint32_t b = 0; b < NB; ++b) {
+            if (!P[b].rows.empty())
+                HIPCHK(hipMemcpyAsync(drows.as<VRow>() + row0[b], P[b].rows.data(), P[b].rows.size() * sizeof(VRow),
+                                      hipMemcpyHostToDevice, ust));
+            if (!P[b].tasks.empty())
+                HIPCHK(hipMemcpyAsync(dtasks.as<VTask>() + task0[b], P[b].tasks.data(),
+                                      P[b].tasks.size() * sizeof(VTask), hipMemcpyHostToDevice, ust));
+        }
+    };
+    parts(L.pu, L.urow0, L.utask0, L.d_urows, L.d_utasks);
+    parts(L.pi, L.irow0, L.itask0, L.d_irows, L.d_itasks);
     upload_grow(L.d_upart, L.upart, ust);
     upload_grow(L.d_ur, L.ur, ust);
-    upload_grow(L.d_i2u, L.i2u, ust);
-    upload_grow(L.d_ipart, L.ipart, ust);
-    upload_grow(L.d_utasks, L.utasks, ust);
-    upload_grow(L.d_itasks, L.itasks, ust);
+    upload_grow(L.d_iu, L.iu, ust);
     if (R > 1 || XS > 1) upload_grow(L.d_gitems, L.gitems, ust);
     HIPCHK(hipEventRecord(uev[e & 1], ust));
     if (std::getenv("SBMF_VB_TRACE")) {
@@ -662,14 +675,15 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         VBItemRec* D = d_D.as<VBItemRec>();
         double2* VS = d_VS.as<double2>();
         double* part = d_part.as<double>();
-        const VRow* ur_ = L.d_urows.as<VRow>();
-        const VRow* ir_ = L.d_irows.as<VRow>();
+
         for (uint32_t b = 0; b < NB; ++b) {
             const uint32_t B = L.bsize[b];
             const uint32_t nu = L.urow0[b + 1] - L.urow0[b];
             HIPCHK(vbo_transpose(tb.mu_v, d_muT.as<double>(), K, Kp, p, st));
             HIPCHK(vbo_transpose(tb.sg_v, d_sgT.as<double>(), K, Kp, p, st));
-            HIPCHK(vbo_predict(ur_ + L.urow0[b], nu, L.d_upart.as<uint32_t>(), L.d_ur.as<float>(), d_muT.as<double>(),
+            const VRow* ur_ = L.d_urows.as<VRow>() + L.urow0[b];  // tasks index the batch's rows
+            const VRow* ir_ = L.d_irows.as<VRow>() + L.irow0[b];
+            HIPCHK(vbo_predict(ur_, nu, L.d_upart.as<uint32_t>(), L.d_ur.as<float>(), d_muT.as<double>(),
                                d_sgT.as<double>(), tb, Kp, ETu, st));
             if (R > 1) {  // update_w0 from every rank's local sum
                 HIPCHK(vbo_w0_local(ETu.at(L.bbase[b]), B, tb, part, d_send.as<double>(), st));
@@ -682,8 +696,7 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             const VTask* it_ = L.d_itasks.as<VTask>() + L.itask0[b];
             const uint32_t nut = L.utask0[b + 1] - L.utask0[b], nit = L.itask0[b + 1] - L.itask0[b];
             const uint32_t* upart_ = L.d_upart.as<uint32_t>();
-            const uint32_t* ipart_ = L.d_ipart.as<uint32_t>();
-            const uint32_t* i2u_ = L.d_i2u.as<uint32_t>();
+            const uint2* iu_ = L.d_iu.as<uint2>();
             // users update their records in place; items read them (through i2u) and leave
             // their updates in D, which the next user pass (or the flush) applies
             // one rank, XS > 1: the slices' partial sums, then the items' updates
@@ -692,18 +705,18 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
             double2* sums = XS > 1 ? d_sums.as<double2>() : nullptr;
             HIPCHK(vbo_user_w(ut, nut, ur_, tb, ETu, st));
             if (R > 1) {
-                item_pass(L, b, it_, nit, ir_, i2u_, 0, 0, ETu);
+                item_pass(L, b, it_, nit, ir_, iu_, 0, 0, ETu);
             } else {
-                HIPCHK(vbo_item_w(it_, nit, ir_, i2u_, tb, ETu, D, sums, st));
+                HIPCHK(vbo_item_w(it_, nit, ir_, iu_, tb, ETu, D, sums, st));
                 if (XS > 1) HIPCHK(vbo_item_update(gi_, nG, sums, (int)XS, 0, 0, tb, D, st));
             }
             int pend = VB_PEND_W;
             for (uint32_t f = 0; f < K; ++f) {
-                HIPCHK(vbo_user_v(ut, nut, ur_, upart_, f, pend, f - 1, L.urow0[b], tb, D, ETu, VS, st));
+                HIPCHK(vbo_user_v(ut, nut, ur_, upart_, f, pend, f - 1, tb, D, ETu, VS, st));
                 if (R > 1) {
-                    item_pass(L, b, it_, nit, ir_, i2u_, 1, f, ETu);
+                    item_pass(L, b, it_, nit, ir_, iu_, 1, f, ETu);
                 } else {
-                    HIPCHK(vbo_item_v(it_, nit, ir_, i2u_, ipart_, f, tb, ETu, VS, D, sums, st));
+                    HIPCHK(vbo_item_v(it_, nit, ir_, iu_, f, tb, ETu, VS, D, sums, st));
                     if (XS > 1) HIPCHK(vbo_item_update(gi_, nG, sums, (int)XS, 1, f, tb, D, st));
                 }
                 pend = VB_PEND_V;

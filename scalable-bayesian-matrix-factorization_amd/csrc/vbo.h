@@ -82,8 +82,8 @@ struct VTask {
 };
 // The passes of a batch keep one {e, t} record per case, in the batch's
 // user-grouped order (ET).  A user pass reads and writes its rows' records in
-// place; an item pass gathers e through i2u (a case's user-grouped position)
-// and writes nothing per case: its e / t updates are left per item in D
+// place; an item pass gathers e through its user-grouped position
+// (iu[q] = {that position, the user's batch row}) and writes nothing per case: its e / t updates are left per item in D
 // (VBItemRec, indexed by item - I) and applied by the next user pass (pend)
 // or by vbo_user_flush before the hyperparameter sums.
 enum { VB_PEND_NONE = 0, VB_PEND_W = 1, VB_PEND_V = 2 };
@@ -96,19 +96,17 @@ struct VBItemRec {
 hipError_t vbo_user_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const VBTables& tb, VBCases ET,
                       hipStream_t st);
 // update_v (:712-800) of factor f for the users, after the pending item updates
-// (pend; factor fp for VB_PEND_V); VS[row - rbase] = the user's new {mean,
-// variance} of f, by its row in the batch (rbase: the batch's first user row)
+// (pend; factor fp for VB_PEND_V); VS[row] = the user's new {mean, variance}
+// of f, by its row in the batch (rows: the batch's user rows, tasks index them)
 hipError_t vbo_user_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, uint32_t f, int pend,
-                      uint32_t fp, uint32_t rbase, const VBTables& tb, const VBItemRec* D, VBCases ET, double2* VS,
-                      hipStream_t st);
+                      uint32_t fp, const VBTables& tb, const VBItemRec* D, VBCases ET, double2* VS, hipStream_t st);
 hipError_t vbo_user_flush(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, int pend,
                           uint32_t fp, const VBTables& tb, const VBItemRec* D, VBCases ET, hipStream_t st);
 // update_w / update_v of factor f for the items (D[item] = the deltas); several
 // ranks: sums != null -> each row's local sums to sums[VRow.pad] only
-hipError_t vbo_item_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const VBTables& tb,
+hipError_t vbo_item_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint2* iu, const VBTables& tb,
                       VBCases ET, VBItemRec* D, double2* sums, hipStream_t st);
-hipError_t vbo_item_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const uint32_t* part,
-                      uint32_t f, const VBTables& tb, VBCases ET, const double2* VS, VBItemRec* D, double2* sums,
+hipError_t vbo_item_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint2* iu, uint32_t f, const VBTables& tb, VBCases ET, const double2* VS, VBItemRec* D, double2* sums,
                       hipStream_t st);
 // several ranks: the items of a batch updated from every rank's local sums
 // (recv [R][nG], rank order; factor f, or the biases when factor == 0)

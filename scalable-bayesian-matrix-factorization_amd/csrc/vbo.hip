@@ -12,7 +12,7 @@
 // reads its rows' records (consecutive lanes, consecutive records), keeps
 // them in registers between the row's two traversals (sums, then updates) and
 // writes them back in place.  An item pass gathers e through the case's
-// user-grouped position (i2u) and the partner user's fresh {mean, variance}
+// user-grouped position (iu[q].x) and the partner user's fresh {mean, variance}
 // (VS, one 16-byte record), and writes nothing per case: its e / t updates
 // depend on the case only through the user's values, so they are left per
 // item (D) and applied by the next user pass -- the same operations in the
@@ -332,13 +332,13 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_w(const VTask* __rest
 // update_v (:712-800) of factor f for the batch's users: per case the item's
 // record (its column-f mean and variance, and the previous item pass's
 // updates, applied first), then the sums, the update and the user's own
-// e / t updates, in place.  VS[row - rbase] = the user's new {mean, variance}
-// of f (by the user's row in the batch), the record the item pass gathers.
+// e / t updates, in place.  VS[row] = the user's new {mean, variance} of f
+// (by the user's row in the batch), the record the item pass gathers.
 template <int PEND>
 __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_v(const VTask* __restrict__ tasks,
                                                              const VRow* __restrict__ rows,
                                                              const uint32_t* __restrict__ part, uint32_t f,
-                                                             uint32_t fp, uint32_t rbase, VBTables tb,
+                                                             uint32_t fp, VBTables tb,
                                                              const VBItemRec* __restrict__ D, VBCases ET,
                                                              double2* __restrict__ VS) {
     __shared__ double red[256];
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_v(const VTask* __rest
         tb.ns_v[off + a] = ns;
         s[a] = sigma;
         v[a] = ok ? mu : md;
-        VS[L.rid - rbase] = make_double2(ok ? mu : md, sigma);
+        VS[L.rid] = make_double2(ok ? mu : md, sigma);
         if (f == 0) tb.t_v[a] += n;  // the caller's count (:447-450)
     }
     // a non-finite mean: the reference returns before touching e, t
@@ -453,13 +453,13 @@ __global__ __launch_bounds__(256) void k_user_flush(const VTask* __restrict__ ta
 }
 
 // update_w (:635-710) of the batch's items: e gathered from the user-grouped
-// records (i2u: a case's position there), read only.  MODE VB_FUSED: the
+// records (iu[q].x: a case's position there), read only.  MODE VB_FUSED: the
 // update, its deltas to D[item]; VB_PART (several ranks): the row's local
 // sums {e1, e2} to sums[VRow.pad].
 template <int MODE>
 __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_wp(const VTask* __restrict__ tasks,
                                                               const VRow* __restrict__ rows,
-                                                              const uint32_t* __restrict__ i2u, VBTables tb,
+                                                              const uint2* __restrict__ iu, VBTables tb,
                                                               VBCases ET,
                                                               VBItemRec* __restrict__ D, double2* __restrict__ sums) {
     __shared__ double red[256];
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_wp(const VTask* __res
 #pragma unroll
     for (int j = 0; j < MI; ++j) {
         const uint32_t x = ci + j * G;
-        if (x < n) ev[j] = ET.E[i2u[q0 + x]];
+        if (x < n) ev[j] = ET.E[iu[q0 + x].x];
     }
     double e1 = 0.0, e2 = 0.0;
 #pragma unroll
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_wp(const VTask* __res
         }
     }
     for (uint32_t x = ci + MI * G; x < n; x += G) {
-        const double e = ET.E[i2u[q0 + x]];
+        const double e = ET.E[iu[q0 + x].x];
         e1 += ((1 - rho) * mo) + rho * cc * alpha * (e + md);
         e2 += cs;
     }
@@ -514,14 +514,13 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_wp(const VTask* __res
 }
 
 // update_v (:712-800) of factor f for the batch's items: per case e (gathered
-// through i2u) and the user's fresh {mean, variance} of f (VS by the user's
-// batch row: part; one 16-byte gather); nothing per case is written.  MODE as
+// through iu[q].x) and the user's fresh {mean, variance} of f (VS by the user's
+// batch row iu[q].y; one 16-byte gather); nothing per case is written.  MODE as
 // k_item_wp.
 template <int MODE>
 __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_vp(const VTask* __restrict__ tasks,
                                                               const VRow* __restrict__ rows,
-                                                              const uint32_t* __restrict__ i2u,
-                                                              const uint32_t* __restrict__ part, uint32_t f,
+                                                              const uint2* __restrict__ iu, uint32_t f,
                                                               VBTables tb, VBCases ET,
                                                               const double2* __restrict__ VS,
                                                               VBItemRec* __restrict__ D, double2* __restrict__ sums) {
@@ -541,8 +540,9 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_vp(const VTask* __res
     for (int j = 0; j < MI; ++j) {
         const uint32_t x = ci + j * G;
         if (x < n) {
-            ev[j] = ET.E[i2u[q0 + x]];
-            hv[j] = VS[part[q0 + x]];
+            const uint2 c = iu[q0 + x];
+            ev[j] = ET.E[c.x];
+            hv[j] = VS[c.y];
         }
     }
     double e1 = 0.0, e2 = 0.0;
@@ -556,8 +556,9 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_vp(const VTask* __res
         }
     }
     for (uint32_t x = ci + MI * G; x < n; x += G) {
-        const double e = ET.E[i2u[q0 + x]];
-        const double2 hw = VS[part[q0 + x]];
+        const uint2 c = iu[q0 + x];
+        const double e = ET.E[c.x];
+        const double2 hw = VS[c.y];
         const double h = hw.x;
         e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + hw.y));
         e1 += ((1 - rho) * mo) + rho * cc * alpha * (h * (e + md * h));
@@ -812,14 +813,13 @@ hipError_t vbo_user_w(const VTask* tasks, uint32_t ntask, const VRow* rows, cons
 }
 
 hipError_t vbo_user_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* part, uint32_t f, int pend,
-                      uint32_t fp, uint32_t rbase, const VBTables& tb, const VBItemRec* D, VBCases ET, double2* VS,
-                      hipStream_t st) {
+                      uint32_t fp, const VBTables& tb, const VBItemRec* D, VBCases ET, double2* VS, hipStream_t st) {
     if (ntask == 0) return hipSuccess;
     // every user pass follows an item pass, whose records carry the column-f values
     if (pend == VB_PEND_V)
-        k_user_v<VB_PEND_V><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, rbase, tb, D, ET, VS);
+        k_user_v<VB_PEND_V><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, tb, D, ET, VS);
     else if (pend == VB_PEND_W)
-        k_user_v<VB_PEND_W><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, rbase, tb, D, ET, VS);
+        k_user_v<VB_PEND_W><<<ntask, 256, 0, st>>>(tasks, rows, part, f, fp, tb, D, ET, VS);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -835,24 +835,23 @@ hipError_t vbo_user_flush(const VTask* tasks, uint32_t ntask, const VRow* rows, 
     return hipGetLastError();
 }
 
-hipError_t vbo_item_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const VBTables& tb,
+hipError_t vbo_item_w(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint2* iu, const VBTables& tb,
                       VBCases ET, VBItemRec* D, double2* sums, hipStream_t st) {
     if (ntask == 0) return hipSuccess;
     if (sums)
-        k_item_wp<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, i2u, tb, ET, D, sums);
+        k_item_wp<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, iu, tb, ET, D, sums);
     else
-        k_item_wp<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, i2u, tb, ET, D, sums);
+        k_item_wp<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, iu, tb, ET, D, sums);
     return hipGetLastError();
 }
 
-hipError_t vbo_item_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint32_t* i2u, const uint32_t* part,
-                      uint32_t f, const VBTables& tb, VBCases ET, const double2* VS, VBItemRec* D, double2* sums,
+hipError_t vbo_item_v(const VTask* tasks, uint32_t ntask, const VRow* rows, const uint2* iu, uint32_t f, const VBTables& tb, VBCases ET, const double2* VS, VBItemRec* D, double2* sums,
                       hipStream_t st) {
     if (ntask == 0) return hipSuccess;
     if (sums)
-        k_item_vp<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, i2u, part, f, tb, ET, VS, D, sums);
+        k_item_vp<VB_PART><<<ntask, 256, 0, st>>>(tasks, rows, iu, f, tb, ET, VS, D, sums);
     else
-        k_item_vp<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, i2u, part, f, tb, ET, VS, D, sums);
+        k_item_vp<VB_FUSED><<<ntask, 256, 0, st>>>(tasks, rows, iu, f, tb, ET, VS, D, sums);
     return hipGetLastError();
 }
 
