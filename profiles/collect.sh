@@ -7,9 +7,9 @@
 #   bash profiles/collect.sh <tag> l2      --pmc TCC_HIT/MISS     tracing domains)
 #   bash profiles/collect.sh <tag> lds     --pmc SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS (bank-conflict share)
 #   bash profiles/collect.sh <tag> gather  --pmc FETCH_SIZE over tests/hip/gather_bench (known bytes: calibration)
-# Outputs land in gpurun_out/<tag>_<pass>*.  Under rocprofv3 (ROCm 7.2) the
-# HIP runtime's exit-time teardown segfaults after the profiler has written
-# its files, so each rocprofv3 pass is the last GPU step of its gpurun call.
+# Outputs land in gpurun_out/<tag>_<pass>*.  bench.py leaves through
+# sbmf_exit_guard, so a rocprofv3 pass exits 0 with its files written
+# (profiles/r03_rocprof_teardown.txt) and passes can be chained.
 set -euo pipefail
 TAG=${1:-r01}
 PASS=${2:-bench}
