@@ -450,26 +450,34 @@ __device__ __forceinline__ T gblock_solve(const T (&H)[GB], T gam) {
 
 // Same recurrence with the H row read from LDS (row `hrow`, scaled by Bq)
 // step by step, for kernels without the registers to hold it.
+#ifndef SBMF_SOLVE2
+#define SBMF_SOLVE2 0
+#endif
 template <typename T>
 __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, T gam) {
+    if constexpr (SBMF_SOLVE2) {
+        // two steps per serial lane read: with d_j = gamma_j, every lane forms
+        // d_{j+1} = gamma_{j+1} - H[j+1][j] d_j (the fma lane j+1 applies at step j,
+        // on the same operands: the same bits), then applies both updates in step
+        // order -- one readlane hop per pair instead of two
+        T H[GB];
+#pragma unroll
+        for (int j = 0; j < GB; ++j) H[j] = Bq * hrow[j];
+#pragma unroll
+        for (int j = 0; j < GB; j += 2) {
+            const T h10 = readlane(H[j], j + 1);
+            const T dj = readlane(gam, j);
+            const T g1 = readlane(gam, j + 1);
+            const T dj1 = g1 - h10 * dj;
+            gam -= H[j] * dj;
+            gam -= H[j + 1] * dj1;
+        }
+        return gam;
+    }
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
         const T dj = readlane(gam, j);
         gam -= (Bq * hrow[j]) * dj;
-    }
-    return gam;
-}
-
-// Same recurrence over a full 16x17 image of G (row `hrow`): only the strictly
-// lower entries j < c take part (the diagonal and the upper part hold other data);
-// a masked entry contributes (Bq * 0) * d_j, exactly as the zero-filled image did.
-template <typename T>
-__device__ __forceinline__ T gblock_solve_lds_lower(const T* __restrict__ hrow, T Bq, T gam, int c) {
-#pragma unroll
-    for (int j = 0; j < GB; ++j) {
-        const T dj = readlane(gam, j);
-        const T h = j < c ? hrow[j] : T(0);
-        gam -= (Bq * h) * dj;
     }
     return gam;
 }
@@ -679,7 +687,11 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         // (no barrier), or -- SW, multi-wave rows -- wave 0 alone, handing D
         // to the others through LDS (their issue slots go to other rows)
         T dlt = T(0);
+        // tune bit 28: the solving wave of a multi-wave row at raised priority (the
+        // row's other waves wait for it; other rows' waves share its SIMD)
+        const bool prio = SW && NW > 1 && (a.tune & 0x10000000u);
         if (!(SW && NW > 1) || wr == 0) {
+            if (prio) __builtin_amdgcn_s_setprio(3);
             const T P = Ps[ws][ci];
             const T old = oldc, sg = sgc, mu = muc;
             const T z = zS[ws][kk];
@@ -702,6 +714,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             } else {
                 if (lane < GB && kin) a.own[(size_t)row * Kp + kk] = nwv;  // one wave: program order
             }
+            if (prio) __builtin_amdgcn_s_setprio(0);
         }
         if constexpr (SW && NW > 1) {
             lds_barrier();
@@ -1205,11 +1218,12 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
     __shared__ T eL[CAP];              // residuals (bit-identical in the 16 lanes of a rating)
     __shared__ T rL[CAP];              // ratings (train error), when requested
     // per-wave block partials: the 16x17 image of G_B (row r, column c at r*GLD + c, all 256
-    // entries as the MFMA leaves them) followed by c_B; Rr: the reduced entries (lower triangle
-    // with the diagonal, and c_B) in the same layout
+    // entries as the MFMA leaves them) followed by c_B; Rr: the reduced entries in the same
+    // layout, except that the diagonal goes to Rr[PW + r]: the image's diagonal and upper part
+    // stay zero (cleared once), so the solve reads whole H rows unmasked
     constexpr int PW = GB * GLD + GB;
     __shared__ T Pw[NW][PW];
-    __shared__ T Rr[PW];
+    __shared__ T Rr[PW + GB];
     __shared__ T Dsh[GB];
     __shared__ T newS[256];
     __shared__ double red2[NW][2];
@@ -1219,16 +1233,19 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
     constexpr int XP = (64 * NW) / SLP;
     static_assert(XP >= 1 && SLP <= SL, "exchange geometry");
     __shared__ double xsum[XP][SLP];
-    // packed entry x -> its offset in a partial image (computed once: no per-block geometry)
-    __shared__ uint16_t xoff[SLP];
+    // packed entry x -> its offset in a partial image, and in Rr (computed once: no per-block geometry)
+    __shared__ uint16_t xoff[SLP], xdst[SLP];
     // the row's normals and old values, sigma and mu: read by the solving wave from LDS
     // (kept out of the VGPRs the held slices need)
     __shared__ T zL[256], oL[256], sgL[256], muL[256];
     for (int x = threadIdx.x; x < SLP; x += 64 * NW) {
         int r = 0;
         while ((r + 1) * (r + 2) / 2 <= x && r < GB) ++r;  // row of the packed triangle
-        xoff[x] = (uint16_t)(x < GB * (GB + 1) / 2 ? r * GLD + (x - r * (r + 1) / 2) : GB * GLD + (x - GB * (GB + 1) / 2));
+        const int c = x - r * (r + 1) / 2;  // column (packed triangle entries)
+        xoff[x] = (uint16_t)(x < GB * (GB + 1) / 2 ? r * GLD + c : GB * GLD + (x - GB * (GB + 1) / 2));
+        xdst[x] = (uint16_t)(x < GB * (GB + 1) / 2 && c == r ? PW + r : xoff[x]);
     }
+    for (int x = threadIdx.x; x < PW + GB; x += 64 * NW) Rr[x] = T(0);
     // this wave's index as a scalar, and the lane: the thread id is rebuilt from them in the
     // block loop (no VGPR held across it, no spill slot to reload)
     const int wr_s = __builtin_amdgcn_readfirstlane(wr);
@@ -1415,6 +1432,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 const int xe = tid % SLP, xpart = tid / SLP;
                 const bool xin = tid < SLP;
                 const int xo = xin ? (int)xoff[xe] : 0;  // the entry's offset in every partial image
+                const int xd = xin ? (int)xdst[xe] : 0;  // and in Rr
                 T val = T(0);
                 if (xin) {
 #pragma unroll
@@ -1482,7 +1500,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                         val = (T)sum;
                     }
                 }
-                if (xin) Rr[xo] = val;
+                if (xin) Rr[xd] = val;
                 lds_barrier();
                 stamp(4);  // cross-wave sum + split-row exchange
                 // the 16 draws: wave 0, D handed over in LDS (default), or -- tune bit 0 --
@@ -1494,7 +1512,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                     const bool kin = kk < K;
                     // the block's old values, hyperparameters and normals (zero padded)
                     const T old = oL[kk], sg = sgL[kk], mu = muL[kk], z = zL[kk];
-                    const T P = Rr[ci * GLD + ci];
+                    const T P = Rr[PW + ci];
                     const T Cc = Rr[GB * GLD + ci];
                     const T var = kin ? T(1) / (sg + tau * P) : T(0);
                     T sd = var;  // a uniform branch: no square root under the variance-as-stdev quirk
@@ -1506,7 +1524,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                         dlt = A - old + Bq * (Cc + P * old);
                     else
 #endif
-                    dlt = gblock_solve_lds_lower(&Rr[ci * GLD], Bq, A - old + Bq * (Cc + P * old), ci);
+                    dlt = gblock_solve_lds(&Rr[ci * GLD], Bq, A - old + Bq * (Cc + P * old));
                     if (wr == 0 && lane < GB) {
                         if (kin) newS[kk] = old + dlt;
                         Dsh[lane] = dlt;
