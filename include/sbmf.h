@@ -80,8 +80,11 @@ enum sbmf_quirks { SBMF_QUIRKS_FINAL = 0, SBMF_QUIRKS_SBPMF2 = 1, SBMF_QUIRKS_NO
  * posterior standard deviation; a sweep re-predicts train and test.  ALS =
  * the same learner without sampling or hyperparameter inference (bin/libFM
  * -method als, libfm.cpp:132-136): deterministic.  Both use libfm_dim and
- * reg0 / regw / regv, f64 only, one GPU; rmse_train / rmse_avg are libFM's
- * "Train=" / "Test=", tau is alpha. */
+ * reg0 / regw / regv, f64 only; rmse_train / rmse_avg are libFM's "Train=" /
+ * "Test=", tau is alpha.  On several GPUs (sbmf_comm_init) each rank owns a
+ * sbmf_partition_rows user range and every case of those users; the item sums
+ * are all-gathered and added in rank order, so every rank draws the same items
+ * and the chain equals one rank's up to the rounding of that sum. */
 enum sbmf_method { SBMF_METHOD_MCMC = 0, SBMF_METHOD_VB = 1, SBMF_METHOD_LIBFM_MCMC = 2, SBMF_METHOD_ALS = 3 };
 
 /* Arithmetic type of factors, residuals and reductions on the GPU.  F64 is
@@ -133,14 +136,17 @@ typedef struct sbmf_config {
                                           waves (default: rows of 5-8 8-vector waves),
                                  bit 21 = no multi-wave f64 Gram-block row on 16-vector waves,
                                  bit 24 = k_gres (queue order) as an ordinary launch instead of
-                                          a cooperative one (measured neutral, 8.93 vs 8.95 ms),
+                                          a cooperative one (measured neutral, 8.93 vs 8.95 ms;
+                                          split rows then rely on the claiming workgroups being
+                                          resident: a hand-off that times out fails sbmf_run),
                                  bit 25 = k_gres with double-buffered slices (slice t+1 in flight
                                           through block t's exchange; one workgroup per CU),
                                  bit 26 = no overlap of the next sweep's prologue (sums, column
                                           statistics, host draws) with the test evaluation
                                           (Philox mode; the chain is the same either way),
                                  bit 27 = f64 item rows on 8-wave k_gres workgroups (default:
-                                          16-wave, as bit 17 does for both sides)              */
+                                          16-wave, as bit 17 does for both sides),
+                                 bit 28 = k_gres block epilogue at raised wave priority    */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

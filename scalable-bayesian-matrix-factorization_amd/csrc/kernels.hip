@@ -450,30 +450,8 @@ __device__ __forceinline__ T gblock_solve(const T (&H)[GB], T gam) {
 
 // Same recurrence with the H row read from LDS (row `hrow`, scaled by Bq)
 // step by step, for kernels without the registers to hold it.
-#ifndef SBMF_SOLVE2
-#define SBMF_SOLVE2 0
-#endif
 template <typename T>
 __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, T gam) {
-    if constexpr (SBMF_SOLVE2) {
-        // two steps per serial lane read: with d_j = gamma_j, every lane forms
-        // d_{j+1} = gamma_{j+1} - H[j+1][j] d_j (the fma lane j+1 applies at step j,
-        // on the same operands: the same bits), then applies both updates in step
-        // order -- one readlane hop per pair instead of two
-        T H[GB];
-#pragma unroll
-        for (int j = 0; j < GB; ++j) H[j] = Bq * hrow[j];
-#pragma unroll
-        for (int j = 0; j < GB; j += 2) {
-            const T h10 = readlane(H[j], j + 1);
-            const T dj = readlane(gam, j);
-            const T g1 = readlane(gam, j + 1);
-            const T dj1 = g1 - h10 * dj;
-            gam -= H[j] * dj;
-            gam -= H[j + 1] * dj1;
-        }
-        return gam;
-    }
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
         const T dj = readlane(gam, j);
@@ -565,6 +543,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     asm volatile("" ::: "memory");  // read back by the other lanes of the wave (LDS keeps its order)
     const T* __restrict__ pbase = a.partner + ci;
 #define PROW(v) (pbase + pjR[4 * (v)])
+    auto gat = [&](int v, uint32_t k0) -> T { return PROW(v)[k0]; };  // vector v's slice at column k0
     if (a.e_from_dot) {
         T dot[V];
 #pragma unroll
@@ -601,7 +580,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     // the last block stays inside the tables (slack row / padding).
     T s[V], sn[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) s[v] = PROW(v)[0];
+    for (int v = 0; v < V; ++v) s[v] = gat(v, 0);
     // ratings for the train error, parked in LDS (read back by the same lanes
     // in the epilogue) so the epilogue waits on no global load
     __shared__ T Rs[NWAVE * V * 4];
@@ -630,7 +609,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         const T sgn = a.sig[kn + ci];
         const T mun = a.mu[kn + ci];
 #pragma unroll
-        for (int v = 0; v < V; ++v) sn[v] = PROW(v)[kn];
+        for (int v = 0; v < V; ++v) sn[v] = gat(v, kn);
         acc_t g = {T(0), T(0), T(0), T(0)};
         T cc = T(0);
 #pragma unroll
@@ -687,11 +666,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         // (no barrier), or -- SW, multi-wave rows -- wave 0 alone, handing D
         // to the others through LDS (their issue slots go to other rows)
         T dlt = T(0);
-        // tune bit 28: the solving wave of a multi-wave row at raised priority (the
-        // row's other waves wait for it; other rows' waves share its SIMD)
-        const bool prio = SW && NW > 1 && (a.tune & 0x10000000u);
         if (!(SW && NW > 1) || wr == 0) {
-            if (prio) __builtin_amdgcn_s_setprio(3);
             const T P = Ps[ws][ci];
             const T old = oldc, sg = sgc, mu = muc;
             const T z = zS[ws][kk];
@@ -714,7 +689,6 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             } else {
                 if (lane < GB && kin) a.own[(size_t)row * Kp + kk] = nwv;  // one wave: program order
             }
-            if (prio) __builtin_amdgcn_s_setprio(0);
         }
         if constexpr (SW && NW > 1) {
             lds_barrier();
@@ -1195,6 +1169,34 @@ template <int NW>
 __device__ __forceinline__ uint32_t gres_slot(uint32_t q) {
     return q ^ gres_swz<NW>(q / (4 * NW));
 }
+// The order in which k_gres' residual update issues the next block's gathers:
+// the butterfly frees vectors [VP/2, VC) first, then [VP/4, VP/2), ..., and the
+// vectors whose residuals the lane updates ([0, RV)) last.
+#ifndef SBMF_GRES_ORD
+#define SBMF_GRES_ORD 1  // measured: item streaming 3.56 -> 3.49 ms, user 1.515 -> 1.49 (r03s3)
+#endif
+template <int VC>
+struct GresOrder {
+    static constexpr int VP = VC <= 8 ? 8 : VC <= 16 ? 16 : VC <= 32 ? 32 : VC <= 64 ? 64 : 128;
+    static constexpr int RV = VP >= 16 ? VP / 16 : 1;
+    struct Arr {
+        int a[VC];
+    };
+    static constexpr Arr make() {
+        Arr o{};
+        int n = 0;
+        const int lo[4] = {VP / 2, VP / 4, VP / 8, VP / 16};
+        const int hi[4] = {VC, VP / 2, VP / 4, VP / 8};
+        for (int l = 0; l < 4; ++l) {
+            if (l == 3 && VP < 16) break;
+            for (int j = lo[l]; j < hi[l] && j < VC; ++j) o.a[n++] = j;
+        }
+        for (int j = 0; j < RV && j < VC; ++j) o.a[n++] = j;
+        return o;
+    }
+    static constexpr Arr arr = make();
+    static constexpr const int* v = arr.a;
+};
 template <typename T>
 struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of slices
     static constexpr int VW = sizeof(T) == 8 ? 32 : 64;
@@ -1338,6 +1340,8 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
             }
             stamp(0);  // staging
             const T* __restrict__ pbase = a.partner + ci;
+            // the gather of vector j's slice of block t
+            auto gat = [&](int j, uint32_t t) -> T { return pbase[(size_t)pjW[j * JS] + t * GB]; };
             // Residual update e_v -= S_v D (vector v: 4 ratings x 16 columns, lane ci
             // holding column ci): s_v *= D in place, then a butterfly reduce-scatter
             // over the 16 lanes of each rating (row_ror:8, row_half_mirror, quad_perm
@@ -1347,7 +1351,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
             // frees take their next slices at once (next(j) = the gather of vector j).
             auto apply = [&](auto& s, T D, auto&& next) {
                 // VC rounded up to a power of two (VP); vectors VC..VP-1 are zero
-                constexpr int VP = VC <= 8 ? 8 : VC <= 16 ? 16 : VC <= 32 ? 32 : 64;
+                constexpr int VP = VC <= 8 ? 8 : VC <= 16 ? 16 : VC <= 32 ? 32 : VC <= 64 ? 64 : 128;
 #pragma unroll
                 for (int j = 0; j < VC; ++j) s[j] = s[j] * D;
                 bfly_level<0x128, VP>(s, ci & 8);
@@ -1394,7 +1398,10 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 } else
 #endif
 #pragma unroll
-                for (int j = 0; j < VC; ++j) {
+                for (int i = 0; i < VC; ++i) {
+                    // vectors in the order their gathers were issued (GresOrder): the first
+                    // MFMAs wait only for the oldest loads, not for all of them
+                    const int j = SBMF_GRES_ORD ? GresOrder<VC>::v[i] : i;
                     g = MfmaT<T>::mfma(s[j], g);
                     cc += s[j] * eS(j);
                 }
@@ -1543,7 +1550,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
             if constexpr (!DB) {
                 T s[VC];
 #pragma unroll
-                for (int j = 0; j < VC; ++j) s[j] = pbase[pjW[j * JS]];
+                for (int j = 0; j < VC; ++j) s[j] = gat(j, 0);
                 for (uint32_t t = 0; t < nblk; ++t) {
                     // keep the per-vector partner offsets in LDS: hoisting them out of
                     // the block loop would hold VC 64-bit addresses in VGPRs
@@ -1553,10 +1560,10 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
 #ifdef SBMF_ABLATIONS
                         if (a.tune & 0x40000u) {  // ablation (wrong results): no residual update
 #pragma unroll
-                            for (int j = 0; j < VC; ++j) s[j] = pbase[(size_t)pjW[j * JS] + t * GB];
+                            for (int j = 0; j < VC; ++j) s[j] = gat(j, t);
                         } else
 #endif
-                        apply(s, Dl, [&](int j) { s[j] = pbase[(size_t)pjW[j * JS] + t * GB]; });
+                        apply(s, Dl, [&](int j) { s[j] = gat(j, t); });
                     }
                     stamp(1);  // apply + gather issue
                     acc_t g = {T(0), T(0), T(0), T(0)};
@@ -1574,7 +1581,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 // 8-wave workgroup per CU)
                 T sA[VC], sB[VC];
 #pragma unroll
-                for (int j = 0; j < VC; ++j) sA[j] = pbase[pjW[j * JS]];
+                for (int j = 0; j < VC; ++j) sA[j] = gat(j, 0);
                 auto dstep = [&](auto& cur, auto& prv, uint32_t t) {
                     asm volatile("" ::: "memory");
                     if (t > 0) apply(prv, Dl, [](int) {});  // e -= S_{t-1} D_{t-1}
@@ -1589,7 +1596,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                     Dl = finish_block(g, cc, t, [&] {
                         if (t + 1 < nblk) {
 #pragma unroll
-                            for (int j = 0; j < VC; ++j) prv[j] = pbase[(size_t)pjW[j * JS] + (t + 1) * GB];
+                            for (int j = 0; j < VC; ++j) prv[j] = gat(j, t + 1);
                         }
                     }, std::integral_constant<int, VC>{});
                 };
