@@ -528,23 +528,43 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     T e[V];  // the starting residuals (then kept in LDS)
     T* const eR = &eS[wv][rr];
     const uint32_t* const pjR = &pjS[wv][rr];
+    // the row's ids, scatter targets and residuals by unconditional loads, issued a group
+    // of (at most) 8 vectors at a time before their first use (a slot past the row's end
+    // reads case 0 and then takes the zero row and a zero residual): per-slot conditional
+    // loads were one dependent round trip each
+    constexpr int SG = V < 8 ? V : V >= 16 ? 4 : 8;
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-        const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-        uint32_t pj = q < n ? a.part[beg + q] : a.zrow;
+    for (int g0 = 0; g0 < V; g0 += SG) {
+        uint32_t pjv[SG], pmv[SG];
+        T ev[SG];
+#pragma unroll
+        for (int u = 0; u < SG; ++u) {
+            const uint32_t q = (uint32_t)((wr * V + g0 + u) * 4 + rr);
+            const uint32_t qi = q < n ? beg + q : 0u;
+            pjv[u] = a.part[qi];
+            pmv[u] = a.perm[qi];
+            ev[u] = a.e_from_dot ? T(0) : a.E_this[qi];
+        }
+#pragma unroll
+        for (int u = 0; u < SG; ++u) {
+            const int v = g0 + u;
+            const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
+            uint32_t pj = q < n ? pjv[u] : a.zrow;
 #ifdef SBMF_ABLATIONS
-        if (a.tune & 0x100u) pj = 0;  // ablation (wrong results): every gather hits one cached row
+            if (a.tune & 0x100u) pj = 0;  // ablation (wrong results): every gather hits one cached row
 #endif
-        if (ci == 0) {
-            pjS[wv][4 * v + rr] = pj * Kp;
-            pmS[wv][4 * v + rr] = q < n ? a.perm[beg + q] : 0u;
+            if (ci == 0) {
+                pjS[wv][4 * v + rr] = pj * Kp;
+                pmS[wv][4 * v + rr] = q < n ? pmv[u] : 0u;
+                eR[4 * v] = q < n ? ev[u] : T(0);
+            }
         }
     }
     asm volatile("" ::: "memory");  // read back by the other lanes of the wave (LDS keeps its order)
     const T* __restrict__ pbase = a.partner + ci;
 #define PROW(v) (pbase + pjR[4 * (v)])
     auto gat = [&](int v, uint32_t k0) -> T { return PROW(v)[k0]; };  // vector v's slice at column k0
-    if (a.e_from_dot) {
+    if (a.e_from_dot) {  // validation mode (tune bit 1): e0 = r - own.partner
         T dot[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) dot[v] = T(0);
@@ -557,19 +577,9 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         for (int v = 0; v < V; ++v) {
             const T d = row16_sum(dot[v]);
             const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-            e[v] = q < n ? a.r_this[beg + q] - d : T(0);
+            const T e0 = q < n ? a.r_this[beg + q] - d : T(0);
+            if (ci == 0) eR[4 * v] = e0;
         }
-    } else {
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-            const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-            e[v] = q < n ? a.E_this[beg + q] : T(0);
-        }
-    }
-
-    if (ci == 0) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) eR[4 * v] = e[v];
     }
     asm volatile("" ::: "memory");  // read back by the other lanes of the wave (LDS keeps its order)
     const T tau = a.tau;
@@ -578,20 +588,31 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     // software pipeline: block b+1's slices and own/sigma/mu values are in
     // flight while block b is reduced, solved and applied.  The prefetch past
     // the last block stays inside the tables (slack row / padding).
-    T s[V], sn[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) s[v] = gat(v, 0);
     // ratings for the train error, parked in LDS (read back by the same lanes
     // in the epilogue) so the epilogue waits on no global load
     __shared__ T Rs[NWAVE * V * 4];
     const bool want_r = a.row_tr != nullptr;
-    if (want_r && ci == 0) {
+    if (want_r) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) {
-            const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-            Rs[(wv * V + v) * 4 + rr] = q < n ? a.r_this[beg + q] : T(0);
+        for (int g0 = 0; g0 < V; g0 += SG) {
+            T rv[SG];
+#pragma unroll
+            for (int u = 0; u < SG; ++u) {
+                const uint32_t q = (uint32_t)((wr * V + g0 + u) * 4 + rr);
+                rv[u] = a.r_this[q < n ? beg + q : 0u];
+            }
+            if (ci == 0) {
+#pragma unroll
+                for (int u = 0; u < SG; ++u) {
+                    const uint32_t q = (uint32_t)((wr * V + g0 + u) * 4 + rr);
+                    Rs[(wv * V + g0 + u) * 4 + rr] = q < n ? rv[u] : T(0);
+                }
+            }
         }
     }
+    T s[V], sn[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) s[v] = gat(v, 0);
     T oldc = orow[0], sgc = a.sig[ci], muc = a.mu[ci];
 #ifdef SBMF_ABLATIONS
     // ablation (wrong results): tune 0x800 runs the block loop twice (block index wraps)
