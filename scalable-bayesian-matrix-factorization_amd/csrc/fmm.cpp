@@ -72,6 +72,10 @@ struct FMLearner {
     // several ranks
     Comm* comm = nullptr;
     int R = 1;
+    // one rank: residuals in both orders updated in place (FMPassArgs::e_io), the
+    // attributes' last draws in d_rec; the pass each side must apply on read
+    DBuf d_rec;
+    int pend_u = 0, pend_i = 0;
     std::vector<uint64_t> ubounds;
     DBuf d_sums, d_recvg, d_delta, d_recv;
 
@@ -184,7 +188,20 @@ struct FMLearner {
         a.alpha = alpha;
         a.do_sample = do_sample;
         a.item_side = items ? 1 : 0;
+        if (R == 1) {
+            a.e_io = (items ? d_ei : d_eu).as<double>();
+            a.rec = d_rec.as<double4>();
+            a.pend = items ? pend_i : pend_u;
+        }
         return a;
+    }
+    // one rank: the item-order copy of the residuals from the user-order one (after the
+    // train re-prediction and the w0 shift); nothing is pending on either side
+    void start_passes() {
+        if (R != 1) return;
+        if (NL) HIPCHK(launch_unpack<double>(d_eu.as<double>(), d_uperm.as<uint32_t>(), NL, d_ei.as<double>(), st));
+        ++n_launch;
+        pend_u = pend_i = 0;
     }
     void run_bins(FMPassArgs a, bool items, bool vpass) {
         auto launch = [&](int xmode) {
@@ -199,6 +216,11 @@ struct FMLearner {
         };
         if (!(items && R > 1)) {
             launch(0);
+            // one rank: the other side applies this pass on read
+            if (items)
+                pend_u = vpass ? 2 : 1;
+            else
+                pend_i = vpass ? 2 : 1;
             return;
         }
         // several ranks: local sums of every item row -> all-gather -> the same draw everywhere
@@ -275,6 +297,7 @@ struct FMLearner {
                 ++n_launch;
             }
         }
+        start_passes();
         // ---- w (:422-455): group hyperparameters, then users and items
         if (k1) {
             draw_hyper_w(g);
@@ -315,7 +338,8 @@ struct FMLearner {
             }
             for (uint32_t f = 0; f < K; ++f) {
                 double* col = d_v.as<double>() + (size_t)f * p;
-                HIPCHK(hipMemcpyAsync(d_vold.p, col, (size_t)I * sizeof(double), hipMemcpyDeviceToDevice, st));
+                if (R > 1)  // one rank: the item pass reads the users' old values from d_rec
+                    HIPCHK(hipMemcpyAsync(d_vold.p, col, (size_t)I * sizeof(double), hipMemcpyDeviceToDevice, st));
                 for (int side = 0; side < 2; ++side) {
                     FMPassArgs a = pass_args(side == 1);
                     a.own = col;
@@ -516,6 +540,7 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
     L->d_vT.alloc(std::max<size_t>((size_t)p * L->Kp, 1) * sizeof(double));
     HIPCHK(hipMemsetAsync(L->d_vT.p, 0, L->d_vT.bytes, st));
     L->d_vold.alloc((size_t)std::max(I, 1u) * sizeof(double));
+    L->d_rec.alloc((size_t)p * sizeof(double4));
     L->d_zw.alloc((size_t)p * sizeof(double));
     L->d_zv.alloc(std::max<size_t>((size_t)K * p, 1) * sizeof(double));
     L->d_pthis.alloc(std::max<uint64_t>(nt, 1) * sizeof(double));

@@ -49,6 +49,13 @@ struct FMPassArgs {
     int xmode;
     double2* sums;
     const double4* delta;
+    // one rank (e_io non-null): the residuals are kept in BOTH orders, each read and
+    // written in place by its own side's passes (sequential, no scatter); the other
+    // side's last pass is applied to a case on read, from that side's per-attribute
+    // records -- the same operations the scatter form applied, in the same order
+    double* e_io;
+    double4* rec;   // [p] by attribute: {old, value kept, keep, 0} of the attribute's last draw
+    int pend;       // the other side's last pass: 0 none, 1 a w pass, 2 a v pass
 };
 // several ranks: every item row's draw from every rank's local sums (recv
 // [R][nrows], rank order), the same on every rank; a.own / a.z / a.mu ... as for

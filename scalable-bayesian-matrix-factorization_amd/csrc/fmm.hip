@@ -46,7 +46,7 @@ __device__ __forceinline__ double fmm_draw(const FMPassArgs& a, uint32_t at, dou
 // MODE 0: draw_w (fm_learn_mcmc.h:670-719); MODE 1: draw_v (:780-835).
 // NT threads per row; a 256-thread block holds 256 / NT rows (NT <= 256) or
 // one row (NT = 1024).
-template <int MODE, int NT>
+template <int MODE, int NT, bool IP>
 __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) {
     constexpr int RPB = NT >= 256 ? 1 : 256 / NT;
     constexpr int NWR = NT >= 64 ? NT / 64 : 1;  // waves per row
@@ -60,19 +60,59 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
     const double4 dl = xm == 2 ? a.delta[row] : make_double4(0.0, 0.0, 0.0, 0.0);
     const double old = xm == 2 ? dl.x : a.own[at];
     const float x = 1.0f;  // one-hot value (DATA_FLOAT)
+    // IP: this user's values of the factor of the item pass to be applied on read
+    double qo = 0.0, qn = 0.0;
+    if constexpr (IP) {
+        if (a.pend == 2 && !a.item_side) {
+            const double4 r = a.rec[at];
+            qo = r.x;
+            qn = r.y;
+        }
+    }
+    // IP: the other side's last pass applied to case q's residual e (its record:
+    // old, value kept, keep), with the h that pass used -- the scatter form's update
+    auto pend = [&](uint32_t q, double e) -> double {
+        if constexpr (!IP) {
+            return e;
+        } else {
+            if (a.pend == 0) return e;
+            const double4 r = a.rec[a.pa0 + a.part[q]];
+            if (r.z != 0.0) return e;  // that draw was kept: nothing changed
+            double h;
+            if (a.pend == 1) {
+                h = (double)x;  // a w pass
+            } else if (a.item_side) {  // the user pass of this factor: h of its hval
+                const double qc = (0.0 + r.x * x) + old * x;
+                h = x * (qc - x * r.x);
+            } else {  // the item pass of the previous factor: h of its hval
+                const double qc = ((0.0 + qo * x) + r.x * x) - x * (qo - qn);
+                h = x * (qc - x * r.x);
+            }
+            return e - h * (r.x - r.y);
+        }
+    };
     // h of the case at position q (factor pass): x * (q_c - x * v) with the
     // case's q rebuilt from the factor column (see the file header)
     auto hval = [&](uint32_t q) {
         const uint32_t pr = a.part[q];
         double qc;
         if (a.item_side) {
-            const double vo = a.vold_u[pr], vn = a.partner_col[pr];
+            double vo, vn;
+            if constexpr (IP) {  // the user's record of this factor's user pass
+                const double4 r = a.rec[pr];
+                vo = r.x;
+                vn = r.y;
+            } else {
+                vo = a.vold_u[pr];
+                vn = a.partner_col[pr];
+            }
             qc = ((0.0 + vo * x) + old * x) - x * (vo - vn);
         } else {
             qc = (0.0 + old * x) + a.partner_col[a.pa0 + pr] * x;
         }
         return x * (qc - x * old);
     };
+    const double* __restrict__ ein = IP ? a.e_io : a.e_in;
     // a lane's first MCF cases stay in registers (residual, h, scatter target) from
     // the sums to the residual update; the rest are reloaded (same values: the pass
     // changes neither h nor e before the update)
@@ -89,9 +129,9 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
         cp[j] = 0;
         if (k < nsum) {
             const uint32_t q = beg + k;
-            const double e = a.e_in[q];
+            const double e = pend(q, ein[q]);
             ce[j] = e;
-            cp[j] = a.perm[q];
+            cp[j] = IP ? 0u : a.perm[q];
             if constexpr (MODE == 0) {
                 m += x * (e - old * x);
                 s2 += x * x;
@@ -104,7 +144,7 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
         }
     }
     for (uint32_t k = lt + MCF * NT; k < nsum; k += NT) {
-        const double e = a.e_in[beg + k];
+        const double e = pend(beg + k, ein[beg + k]);
         if constexpr (MODE == 0) {
             m += x * (e - old * x);
             s2 += x * x;
@@ -143,7 +183,10 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
         keep = dl.z != 0.0;
     } else {
         nv = fmm_draw<MODE>(a, at, old, m, s2, keep);
-        if (lt == 0) a.own[at] = nv;
+        if (lt == 0) {
+            a.own[at] = nv;
+            if constexpr (IP) a.rec[at] = make_double4(old, nv, keep ? 1.0 : 0.0, 0.0);
+        }
     }
 #pragma unroll
     for (int j = 0; j < MCF; ++j) {
@@ -157,12 +200,15 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
                 const double h = MODE == 0 ? (double)x : (cached ? ch[j] : hval(q));
                 eo = e - h * (old - nv);
             }
-            a.e_out[cached ? cp[j] : a.perm[q]] = eo;
+            if constexpr (IP)
+                a.e_io[q] = eo;
+            else
+                a.e_out[cached ? cp[j] : a.perm[q]] = eo;
         }
     }
     for (uint32_t k = lt + MCF * NT; k < n; k += NT) {
         const uint32_t q = beg + k;
-        const double e = a.e_in[q];
+        const double e = IP ? pend(q, ein[q]) : a.e_in[q];
         double eo = e;
         if (!keep) {
             if constexpr (MODE == 0) {
@@ -172,7 +218,10 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
                 eo = e - hval(q) * (old - nv);
             }
         }
-        a.e_out[a.perm[q]] = eo;
+        if constexpr (IP)
+            a.e_io[q] = eo;
+        else
+            a.e_out[a.perm[q]] = eo;
     }
 }
 
@@ -321,23 +370,31 @@ __global__ __launch_bounds__(256) void k_fmm_item(FMPassArgs a, const double2* _
     delta[row] = make_double4(old, nv, keep ? 1.0 : 0.0, 0.0);
 }
 
-template <int MODE>
-hipError_t launch_pass(const FMPassArgs& a, int tpr, hipStream_t st) {
-    if (a.nrows == 0) return hipSuccess;
+template <int MODE, bool IP>
+hipError_t launch_pass_ip(const FMPassArgs& a, int tpr, hipStream_t st) {
     switch (tpr) {
         case 64:
-            k_fmm_pass<MODE, 64><<<(a.nrows + 3) / 4, 256, 0, st>>>(a);
+            k_fmm_pass<MODE, 64, IP><<<(a.nrows + 3) / 4, 256, 0, st>>>(a);
             break;
         case 256:
-            k_fmm_pass<MODE, 256><<<a.nrows, 256, 0, st>>>(a);
+            k_fmm_pass<MODE, 256, IP><<<a.nrows, 256, 0, st>>>(a);
             break;
         case 1024:
-            k_fmm_pass<MODE, 1024><<<a.nrows, 1024, 0, st>>>(a);
+            k_fmm_pass<MODE, 1024, IP><<<a.nrows, 1024, 0, st>>>(a);
             break;
         default:
             return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+template <int MODE>
+hipError_t launch_pass(const FMPassArgs& a, int tpr, hipStream_t st) {
+    if (a.nrows == 0) return hipSuccess;
+    if (a.e_io) {
+        if (a.xmode != 0 || !a.rec) return hipErrorInvalidValue;  // in place: one rank only
+        return launch_pass_ip<MODE, true>(a, tpr, st);
+    }
+    return launch_pass_ip<MODE, false>(a, tpr, st);
 }
 
 }  // namespace

@@ -2055,31 +2055,62 @@ __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, c
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ci = lane & 15, rr = lane >> 4;
     const uint64_t base = t0 + (uint64_t)blockIdx.x * 256 + (uint64_t)w * 64;
+    const uint32_t nb = Kp / 16;  // k-blocks; the padding columns are zero in both tables
     double a2 = 0.0, t2 = 0.0;
-    for (int it = 0; it < 16; ++it) {
-        const uint64_t t = base + it * 4 + rr;
-        const bool ok = t < t1;
-        const T* u = U + (size_t)(ok ? tu[t] : 0u) * Kp;
-        const T* v = V + (size_t)(ok ? ti[t] : 0u) * Kp;
-        T p = T(0);
-        for (uint32_t k0 = 0; k0 < K; k0 += 16) {
-            const uint32_t kk = k0 + ci;
-            if (ok && kk < K) p += u[kk] * v[kk];
+    // two ratings per 16-lane group at a time, their ids and every row slice of a chunk of up
+    // to CB k-blocks loaded before the first product (the per-block masked loads of one rating
+    // at a time were a dependent round trip each); products summed in k order, the zero
+    // padding columns adding +0 (the clamped prediction is the same)
+    constexpr int PR = 2, CB = 8;
+    for (int it = 0; it < 16; it += PR) {
+        uint32_t uu[PR], ii[PR];
+        uint64_t tt[PR];
+        bool ok[PR];
+#pragma unroll
+        for (int j = 0; j < PR; ++j) {
+            tt[j] = base + (it + j) * 4 + rr;
+            ok[j] = tt[j] < t1;
+            const uint64_t tc = ok[j] ? tt[j] : t0;
+            uu[j] = tu[tc];
+            ii[j] = ti[tc];
         }
-        p = row16_sum(p);
-        if (ok && ci == 0) {
-            if (bu) p = (T)((b0 + bu[tu[t]]) + bv[ti[t]]) + p;  // biased sampler (gibbs_sbpmf2.cpp:614-618)
-            p = (p < hi) ? p : hi;
-            p = (lo < p) ? p : lo;
-            double s = sum[t];
-            if (collect) {
-                s += (double)p;
-                sum[t] = s;
+        T p[PR];
+#pragma unroll
+        for (int j = 0; j < PR; ++j) p[j] = T(0);
+        for (uint32_t c0 = 0; c0 < nb; c0 += CB) {
+            T ub[PR][CB], vb[PR][CB];
+#pragma unroll
+            for (int j = 0; j < PR; ++j)
+#pragma unroll
+                for (int b = 0; b < CB; ++b)
+                    if (c0 + b < nb) {
+                        ub[j][b] = U[(size_t)uu[j] * Kp + (c0 + b) * 16 + ci];
+                        vb[j][b] = V[(size_t)ii[j] * Kp + (c0 + b) * 16 + ci];
+                    }
+#pragma unroll
+            for (int j = 0; j < PR; ++j)
+#pragma unroll
+                for (int b = 0; b < CB; ++b)
+                    if (c0 + b < nb) p[j] += ub[j][b] * vb[j][b];
+        }
+#pragma unroll
+        for (int j = 0; j < PR; ++j) {
+            T pj = row16_sum(p[j]);
+            const uint64_t t = tt[j];
+            if (ok[j] && ci == 0) {
+                if (bu) pj = (T)((b0 + bu[uu[j]]) + bv[ii[j]]) + pj;  // biased sampler (gibbs_sbpmf2.cpp:614-618)
+                pj = (pj < hi) ? pj : hi;
+                pj = (lo < pj) ? pj : lo;
+                double s = sum[t];
+                if (collect) {
+                    s += (double)pj;
+                    sum[t] = s;
+                }
+                const double d = tr[t] - s / div;
+                a2 += d * d;
+                const double dt = tr[t] - (double)pj;
+                t2 += dt * dt;
             }
-            const double d = tr[t] - s / div;
-            a2 += d * d;
-            const double dt = tr[t] - (double)p;
-            t2 += dt * dt;
         }
     }
     __shared__ double red[4][2];
