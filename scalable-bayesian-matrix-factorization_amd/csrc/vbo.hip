@@ -359,14 +359,24 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_user_v(const VTask* __rest
     double hh[MC], hs[MC];  // the partners' column-f values, kept for the updates
     double2 et[MC];
     double e1 = 0.0, e2 = 0.0;
+    // a lane's cases by unconditional loads, all issued before the sums (a slot past the
+    // row reads case 0 and is not summed): per-slot conditional loads were two dependent
+    // round trips each
+    uint32_t pr[MC];
 #pragma unroll
     for (int j = 0; j < MC; ++j) {
         const uint32_t x = ci + j * G;
+        const uint32_t xi = x < n ? q0 + x : 0u;
+        pr[j] = part[xi];
+        et[j] = make_double2(ET.E[xi], ET.T[xi]);
+    }
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const uint32_t x = ci + j * G;
+        const IRec r = get_rec(D, pr[j] - I);
         if (x < n) {
-            const IRec r = get_rec(D, part[q0 + x] - I);
             hh[j] = r.v;
             hs[j] = r.s;
-            et[j] = make_double2(ET.E[q0 + x], ET.T[q0 + x]);
             vb_pending<PEND>(et[j], r, hp, sp);
             const double h = r.v;
             e2 += (1 - rho) * so + rho * (svg + alpha * cc * (h * h + r.s));
@@ -536,14 +546,17 @@ __global__ __launch_bounds__(256, SBMF_VB_OCC) void k_item_vp(const VTask* __res
     const double cc = (double)tb.cc[a];
     double ev[MI];
     double2 hv[MI];
+    // unconditional loads, all issued before the sums (a slot past the row reads case 0)
+    uint2 cv[MI];
 #pragma unroll
     for (int j = 0; j < MI; ++j) {
         const uint32_t x = ci + j * G;
-        if (x < n) {
-            const uint2 c = iu[q0 + x];
-            ev[j] = ET.E[c.x];
-            hv[j] = VS[c.y];
-        }
+        cv[j] = iu[x < n ? q0 + x : 0u];
+    }
+#pragma unroll
+    for (int j = 0; j < MI; ++j) {
+        ev[j] = ET.E[cv[j].x];
+        hv[j] = VS[cv[j].y];
     }
     double e1 = 0.0, e2 = 0.0;
 #pragma unroll
