@@ -2230,14 +2230,32 @@ __global__ __launch_bounds__(256) void k_bias_rows(const uint32_t* __restrict__ 
     const double mu = s4 * ((p.sg * p.mg) + bo * sig) + (p.sd_is_var ? s4 : sqrt(s4)) * zm;  // zm = 0: draw skipped
     const uint32_t beg = ptr[row], end = ptr[row + 1];
     const T d0 = (T)p.d0;
+    // each lane's cases in order, eight loads in flight (a long item row is one wave's
+    // serial walk: one load round trip per 64 ratings without them)
     double acc = 0.0;
-    for (uint32_t q = beg + lane; q < end; q += 64) acc += (double)(E[q] + d0) + bo;
+    uint32_t q = beg + lane;
+    for (; q + 7 * 64 < end; q += 8 * 64) {
+        T ev[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ev[u] = E[q + u * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += (double)(ev[u] + d0) + bo;
+    }
+    for (; q < end; q += 64) acc += (double)(E[q] + d0) + bo;
     acc = wave_sum(acc);
     const double sb = 1.0 / (sig + (p.alpha * (double)(end - beg)));
     const double mb = sb * ((sig * mu) + p.alpha * acc);
     const double bn = mb + (p.sd_is_var ? sb : sqrt(sb)) * zb;
     const T db = (T)(bo - bn);
-    for (uint32_t q = beg + lane; q < end; q += 64) E[q] = (E[q] + d0) + db;
+    q = beg + lane;
+    for (; q + 7 * 64 < end; q += 8 * 64) {
+        T ev[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ev[u] = E[q + u * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) E[q + u * 64] = (ev[u] + d0) + db;
+    }
+    for (; q < end; q += 64) E[q] = (E[q] + d0) + db;
     if (lane == 0) {
         b[row] = bn;
         mu_b[row] = mu;
@@ -2283,7 +2301,20 @@ __global__ __launch_bounds__(256) void k_rowsum2(const uint32_t* __restrict__ pt
     if (r >= r1) return;
     const int lane = threadIdx.x & 63;
     double s = 0.0, s2 = 0.0;
-    for (uint32_t q = ptr[r] + lane; q < ptr[r + 1]; q += 64) {
+    const uint32_t end = ptr[r + 1];
+    uint32_t q = ptr[r] + lane;
+    for (; q + 7 * 64 < end; q += 8 * 64) {  // eight loads in flight, each lane's cases in order
+        T ev[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ev[u] = E[q + u * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const double e = (double)ev[u];
+            s += e;
+            s2 += e * e;
+        }
+    }
+    for (; q < end; q += 64) {
         const double e = (double)E[q];
         s += e;
         s2 += e * e;
