@@ -132,6 +132,8 @@ typedef struct sbmf_config {
                                  bits 8-10 = hybrid k_gres / k_gstream stream sets by row length,
                                  bit 16 = k_gres tasks in static rounds (default: a queue),
                                  bit 17 = k_gres on 16-wave workgroups (both sides),
+                                 bit 23 = f64 user streaming rows on 8-wave k_gres workgroups
+                                          (default: 4-wave, 512-rating tasks),
                                  bit 20 = every multi-wave f64 Gram-block row on 16-vector
                                           waves (default: rows of 5-8 8-vector waves),
                                  bit 21 = no multi-wave f64 Gram-block row on 16-vector waves,

@@ -495,7 +495,12 @@ static void prepare_T(sbmf_ctx* c) {
             const bool item16 = sd == &c->items && sizeof(T) == 8 && !hyb &&
                                 !(cf.tune & (64u | 128u | 0x20000u | 0x2000000u | 0x8000000u));
             const uint32_t shyb = item16 ? 1024u : hyb;
-            const uint32_t stunes[2] = {tunes[0], item16 ? cf.tune | 0x20000u : tunes[1]};
+            // f64 user rows on 4-wave k_gres workgroups (512-rating tasks, four workgroups per
+            // CU): measured user streaming 1.49 -> 1.40 ms against 8-wave (r03s10); tune bit 23,
+            // or an explicit workgroup-shape bit, keeps them on 8-wave workgroups
+            const bool user4 = sd == &c->users && sizeof(T) == 8 && !hyb &&
+                               !(cf.tune & (64u | 128u | 0x20000u | 0x2000000u | 0x800000u));
+            const uint32_t stunes[2] = {user4 ? tunes[0] | 128u : tunes[0], item16 ? cf.tune | 0x20000u : tunes[1]};
             for (auto& gp : sd->stg) {
             std::vector<uint32_t> rows[2];
             for (uint32_t r : gp->bin_rows[KIND_STREAM])  // degree-descending
