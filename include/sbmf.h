@@ -148,7 +148,10 @@ typedef struct sbmf_config {
                                           (Philox mode; the chain is the same either way),
                                  bit 27 = f64 item rows on 8-wave k_gres workgroups (default:
                                           16-wave, as bit 17 does for both sides),
-                                 bit 28 = k_gres block epilogue at raised wave priority    */
+                                 bit 28 = k_gres block epilogue at raised wave priority,
+                                 bit 29 = a half's Gram-block launches after its streaming launch
+                                          on one stream (default: on a second stream beside it,
+                                          the streaming launch then an ordinary one as bit 24) */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

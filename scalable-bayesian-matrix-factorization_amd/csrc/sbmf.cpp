@@ -313,6 +313,8 @@ struct sbmf_ctx {
     hipStream_t stc = nullptr;     // multi-GPU: the exchange of stage p runs here while stage p+1 computes
     std::vector<hipEvent_t> sev;   // [side][stage]: stage computed (compute stream)
     hipEvent_t cev[2] = {};        // [side]: the half's exchange done (comm stream)
+    hipStream_t sto = nullptr;     // a half's Gram-block launches, beside its streaming launch
+    hipEvent_t oev[2] = {};        // [fork, join] of those launches
     DBuf d_uptr, d_upart, d_uperm, d_ur, d_vptr, d_vpart, d_vperm, d_vr;
     DBuf d_U, d_V, d_Eu, d_Ev, d_zU, d_zV, d_hyper;
     DBuf d_rowsq_u, d_rowtr_u, d_rowsq_v, d_rowtr_v;
@@ -963,8 +965,24 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         HIPCHK(hipEventRecord(c->kev(stage, sd, KIND_GRAM, 1), st));
         c->timing.n_launch += 4;
     }
+    // Overlap (default; tune bit 29 off): the streaming launch (persistent, queue
+    // order) on `st`, every other bin on `sto` beside it, so the short Gram-block
+    // launches fill the CU time the streaming launch's serial phases (solve,
+    // split-row hand-offs) and its tail leave idle.  Rows of different bins are
+    // disjoint and no launch reads another's outputs, so the results do not
+    // depend on the interleaving.  The streaming launch is then an ordinary one
+    // (tune bit 24): its claiming workgroups are resident by construction, while a
+    // cooperative launch would wait for the whole device.
+    bool others = false;
+    for (int k = 0; k < NBIN; ++k) others |= k != KIND_STREAM && !g.bin_rows[k].empty();
+    const bool ovl = !(c->cfg.tune & 0x20000000u) && others && !g.bin_rows[KIND_STREAM].empty();
+    if (ovl) {
+        HIPCHK(hipEventRecord(c->oev[0], st));
+        HIPCHK(hipStreamWaitEvent(c->sto, c->oev[0], 0));
+    }
     for (int k = NBIN - 1; k >= 0; --k) {
         if (g.bin_rows[k].empty()) continue;
+        if (ovl && k != KIND_STREAM) st = c->sto;
         HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
         if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
             for (const auto& gs : g.gsub[k])
@@ -988,7 +1006,9 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 sy.cmax = S.cmax;
                 sy.prof = c->kprof && set == c->kprof_set ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
                 HalfArgs<T> as = a;
-                as.tune = S.tune;
+                // (k_gres in static rounds and k_gstream stay cooperative: their
+                // workgroups wait for the Gram-block ones to drain before they all fit)
+                as.tune = ovl && !(S.tune & (64u | 0x10000u)) ? S.tune | 0x1000000u : S.tune;
                 HIPCHK(launch_gstream<T>(g.d_stasks[set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
                                          g.d_xrows[set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, st));
             }
@@ -997,6 +1017,10 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
             HIPCHK(launch_rows<T>(k - KIND_RK0, g.d_bins[k].as<uint32_t>(), (uint32_t)g.bin_rows[k].size(), a, st));
         HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
         c->timing.n_launch++;
+    }
+    if (ovl) {
+        HIPCHK(hipEventRecord(c->oev[1], c->sto));
+        HIPCHK(hipStreamWaitEvent(c->st, c->oev[1], 0));
     }
 }
 
@@ -1424,6 +1448,9 @@ sbmf_ctx::~sbmf_ctx() {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : cev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : oev)
+        if (e) (void)hipEventDestroy(e);
+    if (sto) (void)hipStreamDestroy(sto);
     if (stc) (void)hipStreamDestroy(stc);
     if (st) (void)hipStreamDestroy(st);
 }
@@ -1544,6 +1571,8 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&c->stc, hipStreamNonBlocking));
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
     for (auto& e : c->cev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipStreamCreateWithFlags(&c->sto, hipStreamNonBlocking));
+    for (auto& e : c->oev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     *out = c.release();
     API_END(ctx)
 }
