@@ -498,7 +498,11 @@ def main():
                      "rows_per_launch": int(main_res["kern_rows"][s, k]),
                      "ms_per_launch": float(km[s, k]),
                      "sweep_alg_GBs": main_res["bytes_alg"] / (main_res["seconds"] / args.steps) / 1e9,
-                     "bins": bins},
+                     "bins": bins,
+                     "bins_overlap": None if args.tune & (1 << 29) else
+                     "a half's Gram-block launches run on a second stream beside its streaming launch "
+                     "(and the item half's two streaming sets side by side unless tune bit 30): a bin's ms is "
+                     "its start-to-end time while it shares the device, so the bins of a half overlap"},
     }
     if f32 is not None:
         out["f32_value"] = n_train * args.steps / f32["seconds"]

@@ -151,7 +151,9 @@ typedef struct sbmf_config {
                                  bit 28 = k_gres block epilogue at raised wave priority,
                                  bit 29 = a half's Gram-block launches after its streaming launch
                                           on one stream (default: on a second stream beside it,
-                                          the streaming launch then an ordinary one as bit 24) */
+                                          the streaming launch then an ordinary one as bit 24),
+                                 bit 30 = a half's two streaming sets (items: rows > 1024 and the
+                                          rest) one after the other (default: side by side)  */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

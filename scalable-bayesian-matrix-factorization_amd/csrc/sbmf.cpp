@@ -314,7 +314,7 @@ struct sbmf_ctx {
     std::vector<hipEvent_t> sev;   // [side][stage]: stage computed (compute stream)
     hipEvent_t cev[2] = {};        // [side]: the half's exchange done (comm stream)
     hipStream_t sto = nullptr;     // a half's Gram-block launches, beside its streaming launch
-    hipEvent_t oev[2] = {};        // [fork, join] of those launches
+    hipEvent_t oev[3] = {};        // [fork, join] of those launches, [2]: stream set 0 done
     DBuf d_uptr, d_upart, d_uperm, d_ur, d_vptr, d_vpart, d_vperm, d_vr;
     DBuf d_U, d_V, d_Eu, d_Ev, d_zU, d_zV, d_hyper;
     DBuf d_rowsq_u, d_rowtr_u, d_rowsq_v, d_rowtr_v;
@@ -326,6 +326,7 @@ struct sbmf_ctx {
     DBuf d_kprof;
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
     DBuf d_xslabs, d_xtotals, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
+    size_t xset_nx = 1, xset_nr = 1;  // set 0's split chunks / rows: set 1's areas follow them
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
     DBuf d_uperm2, d_vperm2, d_uunpack, d_vunpack, d_xrecv;  // multi-GPU residual exchange
     DBuf d_bu, d_bv, d_mbu, d_mbv, d_sbu, d_sbv;  // biases b_i / b_j and their per-row (mu, sigma)
@@ -557,24 +558,29 @@ static void prepare_T(sbmf_ctx* c) {
         upload(c->d_rtptr, s.rtptr, st);
         c->d_rtsq.alloc(std::max<size_t>(s.rtasks.size(), 1) * sizeof(double));
     }
-    size_t nx = 0, nr = 0;  // split-row slots of the largest stream set (the sets run one after another)
+    // split-row slots of stream set k: the largest over the stages and sides (set 0 and
+    // set 1 of a half may run at the same time, so each set has an area of its own)
+    size_t nxk[2] = {0, 0}, nrk[2] = {0, 0};
     for (Side* sd : {&c->users, &c->items})
         for (auto& g : sd->stg)
             for (int k = 0; k < 2; ++k) {
                 const Side::StreamSet& S = g->ss[k];
                 upload(g->d_stasks[k], S.stasks, st);
                 upload(g->d_xrows[k], S.xrows, st);
-                nx = std::max<size_t>(nx, S.nxchunk);
-                nr = std::max<size_t>(nr, S.xrows.size());
+                nxk[k] = std::max<size_t>(nxk[k], S.nxchunk);
+                nrk[k] = std::max<size_t>(nrk[k], S.xrows.size());
             }
+    c->xset_nx = std::max<size_t>(nxk[0], 1);
+    c->xset_nr = std::max<size_t>(nrk[0], 1);
     {
-        c->d_xslabs.alloc(std::max<size_t>(nx, 1) * nblk * (16 * 16 + 16) * sizeof(double));
-        c->d_xcnt.alloc((nr * nblk + 1) * sizeof(uint32_t));  // + the task-queue head
-        c->d_xtotals.alloc(std::max<size_t>(nr, 1) * nblk * (16 * 16 + 16) * sizeof(double));
-        c->d_xchunk_sq.alloc(std::max<size_t>(nx, 1) * sizeof(double));
-        c->d_xchunk_tr.alloc(std::max<size_t>(nx, 1) * sizeof(double));
+        const size_t nx = c->xset_nx + std::max<size_t>(nxk[1], 1), nr = c->xset_nr + std::max<size_t>(nrk[1], 1);
+        c->d_xslabs.alloc(nx * nblk * (16 * 16 + 16) * sizeof(double));
+        c->d_xcnt.alloc((nr * nblk + 2) * sizeof(uint32_t));  // + each set's task-queue head
+        c->d_xtotals.alloc(nr * nblk * (16 * 16 + 16) * sizeof(double));
+        c->d_xchunk_sq.alloc(nx * sizeof(double));
+        c->d_xchunk_tr.alloc(nx * sizeof(double));
         HIPCHK(hipMemsetAsync(c->d_xchunk_tr.p, 0, c->d_xchunk_tr.bytes, st));
-        c->d_xnewown.alloc(std::max<size_t>(nx, 1) * c->Kp * sizeof(T));
+        c->d_xnewown.alloc(nx * c->Kp * sizeof(T));
         c->d_xtimeout.alloc(sizeof(uint32_t));
         HIPCHK(hipMemsetAsync(c->d_xtimeout.p, 0, sizeof(uint32_t), st));
     }
@@ -980,9 +986,14 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         HIPCHK(hipEventRecord(c->oev[0], st));
         HIPCHK(hipStreamWaitEvent(c->sto, c->oev[0], 0));
     }
+    // With two stream sets (items: rows > 1024 on 16-wave workgroups, set 1, and the
+    // rest on 8-wave ones, set 0), set 1 runs on `st` and set 0 on `sto` beside it
+    // (tune bit 30: one after the other), each with split-row areas of its own.
+    auto gres_q = [](const Side::StreamSet& S) { return !S.stasks.empty() && !(S.tune & (64u | 0x10000u)); };
+    const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && gres_q(g.ss[0]) && gres_q(g.ss[1]);
     for (int k = NBIN - 1; k >= 0; --k) {
         if (g.bin_rows[k].empty()) continue;
-        if (ovl && k != KIND_STREAM) st = c->sto;
+        st = ovl && k != KIND_STREAM ? c->sto : c->st;
         HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
         if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
             for (const auto& gs : g.gsub[k])
@@ -990,18 +1001,21 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         } else if (k < GK_NUM)
             HIPCHK(launch_gblock<T>(k, g.d_bins[k].as<uint32_t>(), (uint32_t)g.bin_rows[k].size(), a, st));
         else if (k == KIND_STREAM) {
-            for (int set = 0; set < 2; ++set) {
+            for (int q = 0; q < 2; ++q) {
+                const int set = sov ? 1 - q : q;
                 const Side::StreamSet& S = g.ss[set];
                 if (S.stasks.empty()) continue;
+                const hipStream_t ss = sov && set == 0 ? c->sto : st;
+                const size_t ox = set ? c->xset_nx : 0, orow = set ? c->xset_nr : 0;
                 SplitSync sy{};
-                sy.slabs = c->d_xslabs.as<double>();
-                sy.totals = c->d_xtotals.as<double>();
-                sy.counters = c->d_xcnt.as<uint32_t>();
                 sy.nblk = (c->K + 15) / 16;
+                sy.slabs = c->d_xslabs.as<double>() + ox * sy.nblk * (16 * 16 + 16);
+                sy.totals = c->d_xtotals.as<double>() + orow * sy.nblk * (16 * 16 + 16);
+                sy.counters = c->d_xcnt.as<uint32_t>() + (set ? orow * sy.nblk + 1 : 0);
                 sy.ncounters = (uint32_t)S.xrows.size() * sy.nblk;
-                sy.chunk_sq = c->d_xchunk_sq.as<double>();
-                sy.chunk_tr = c->d_xchunk_tr.as<double>();
-                sy.newown = c->d_xnewown.p;
+                sy.chunk_sq = c->d_xchunk_sq.as<double>() + ox;
+                sy.chunk_tr = c->d_xchunk_tr.as<double>() + ox;
+                sy.newown = c->d_xnewown.as<T>() + ox * c->Kp;
                 sy.timeout = c->d_xtimeout.as<uint32_t>();
                 sy.cmax = S.cmax;
                 sy.prof = c->kprof && set == c->kprof_set ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
@@ -1010,7 +1024,11 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 // workgroups wait for the Gram-block ones to drain before they all fit)
                 as.tune = ovl && !(S.tune & (64u | 0x10000u)) ? S.tune | 0x1000000u : S.tune;
                 HIPCHK(launch_gstream<T>(g.d_stasks[set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
-                                         g.d_xrows[set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, st));
+                                         g.d_xrows[set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, ss));
+            }
+            if (sov) {  // the streaming stage ends with both sets
+                HIPCHK(hipEventRecord(c->oev[2], c->sto));
+                HIPCHK(hipStreamWaitEvent(st, c->oev[2], 0));
             }
         }
         else
