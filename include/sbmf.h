@@ -153,7 +153,9 @@ typedef struct sbmf_config {
                                           on one stream (default: on a second stream beside it,
                                           the streaming launch then an ordinary one as bit 24),
                                  bit 30 = a half's two streaming sets (items: rows > 1024 and the
-                                          rest) one after the other (default: side by side)  */
+                                          rest) one after the other (default: side by side),
+                                 bit 31 = with the overlap, the Gram-block launches enqueued before
+                                          the streaming launch (default: after it)            */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

@@ -991,8 +991,11 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     // (tune bit 30: one after the other), each with split-row areas of its own.
     auto gres_q = [](const Side::StreamSet& S) { return !S.stasks.empty() && !(S.tune & (64u | 0x10000u)); };
     const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && gres_q(g.ss[0]) && gres_q(g.ss[1]);
-    for (int k = NBIN - 1; k >= 0; --k) {
-        if (g.bin_rows[k].empty()) continue;
+    // tune bit 31 (with the overlap): the Gram-block launches enqueued before the streaming one
+    const bool gfirst = ovl && (c->cfg.tune & 0x80000000u);
+    for (int it = 0; it < NBIN + (gfirst ? 1 : 0); ++it) {
+        const int k = !gfirst ? NBIN - 1 - it : it < NBIN ? NBIN - 1 - it : KIND_STREAM;
+        if (g.bin_rows[k].empty() || (gfirst && (k == KIND_STREAM) != (it == NBIN))) continue;
         st = ovl && k != KIND_STREAM ? c->sto : c->st;
         HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
         if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
