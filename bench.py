@@ -56,9 +56,8 @@ def parse():
     ap.add_argument("--no-f32", action="store_true", help="skip the extra f32 measurement")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
-    ap.add_argument("--gram-threshold", type=int, default=0)
-    ap.add_argument("--row-kernel", type=int, default=0)
     ap.add_argument("--no-ttr", action="store_true", help="skip the time-to-RMSE runs")
+    ap.add_argument("--no-load", action="store_true", help="skip the text / binary load timing")
     ap.add_argument("--tune", type=int, default=0, help="kernel-variant bits (sbmf_config.tune)")
     ap.add_argument("--split-chunk", type=int, default=0, help="streaming task size (0 = LDS capacity)")
     ap.add_argument("--stream-threshold", type=int, default=0, help="rows above this use the streaming kernel")
@@ -125,9 +124,8 @@ def device_sync():
 def make_learner(args, world, rank, local, precision, uid):
     from sbmf import Data, FMLearnSBPMF
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=precision, device=local,
-                     quirks=args.quirks, recompute_every=0, eval_train=False, gram_threshold=args.gram_threshold,
-                     row_kernel=args.row_kernel, tune=args.tune, split_chunk=args.split_chunk,
-                     stream_threshold=args.stream_threshold)
+                     quirks=args.quirks, recompute_every=0, eval_train=False, tune=args.tune,
+                     split_chunk=args.split_chunk, stream_threshold=args.stream_threshold)
     L.init(comm=(world, rank, uid) if world > 1 else None)
     return L, Data
 
@@ -165,20 +163,26 @@ def measure(args, world, rank, local, precision, train, test, uid):
     return res
 
 
-def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85, max_sweeps=200):
+def time_to_rmse(args, world, rank, local, train, test, uid, burnin, quirks="final", target=0.85, max_sweeps=200):
     """Wall-clock from the end of data load to the first sweep whose running-mean
-    test RMSE <= target, with the reference's averaging rule."""
+    test RMSE <= target, with the reference's averaging rule.
+    Two clocks: `seconds` starts after set_data (host CSR/CSC build, task lists,
+    uploads, factor init: `prepare_s`), `seconds_from_load` before it."""
     from sbmf import Data, FMLearnSBPMF
-    # The reference sampler in both runs (quirks "final": variance used as the
-    # stdev).  Burn-in 0: the reference default and its averaging rule
-    # (sum / (sweep+1)); burn-in 50 (paper protocol): the running mean is taken
-    # over the collected sweeps only -- the one change from the reference, whose
-    # divisor also counts the burn-in sweeps (gibbs_sbpmf_final.cpp:559).
+    # quirks "final": the reference sampler gibbs_sbpmf_final.cpp (no biases);
+    # "bias2": the paper's SBMF-P model with biases, top-level gibbs_sbpmf2.cpp:335-637
+    # (init N(0, 0.1), clamp [0.5, 5]).  Both use the variance as the stdev.
+    # Burn-in 0: the reference default and its averaging rule (sum / (sweep+1));
+    # burn-in 50 (paper protocol): the running mean is taken over the collected
+    # sweeps only -- the one change from the reference, whose divisor also counts
+    # the burn-in sweeps (gibbs_sbpmf_final.cpp:559).
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=args.precision, device=local,
-                     recompute_every=0, burnin=burnin, row_kernel=args.row_kernel, tune=args.tune,
+                     recompute_every=0, burnin=burnin, tune=args.tune,
                      split_chunk=args.split_chunk, stream_threshold=args.stream_threshold,
-                     quirks="final", average="collected" if burnin else "reference")
+                     quirks=quirks, average="collected" if burnin else "reference")
     L.init(comm=(world, rank, uid) if world > 1 else None)
+    barrier(world)
+    tl = time.perf_counter()
     L.set_data(Data(*train), Data(*test))
     barrier(world)
     t0 = time.perf_counter()
@@ -195,7 +199,8 @@ def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85
     this = np.array([h["rmse_this"] for h in L.history])
     tau = np.array([h["tau"] for h in L.history])
     L.close()
-    out = {"seconds": hit, "sweeps": n, "rmse": last, "burnin": burnin, "quirks": "final",
+    out = {"seconds": hit, "seconds_from_load": None if hit is None else hit + (t0 - tl), "prepare_s": t0 - tl,
+           "sweeps": n, "rmse": last, "burnin": burnin, "quirks": quirks,
            "average": "collected sweeps" if burnin else "sum / (sweep + 1) (reference)",
            "target": "synthetic proxy: RMSE %.2f on the planted rank-10 set (noise floor ~0.58), not MovieLens" % target,
            "clock": "end of data load -> first sweep with running-mean test RMSE <= %.2f" % target,
@@ -203,14 +208,62 @@ def time_to_rmse(args, world, rank, local, train, test, uid, burnin, target=0.85
            "rmse_this_last": float(this[-1]), "tau_last": float(tau[-1])}
     if hit is None:
         bad = np.flatnonzero(~np.isfinite(tau) | (tau < 1e-3))
-        out["note"] = ("not reached: the reference sampler's chain (posterior variance used as the stdev) leaves its "
+        out["note"] = ("not reached: the %s sampler's chain (posterior variance used as the stdev) leaves its "
                        "best per-sweep test RMSE %.3f at sweep %d%s; the CPU oracle, bit-exact to "
                        "gibbs_sbpmf_final.cpp, collapses the same way on an ML-1M-shaped set (DESIGN.md §6), so the "
                        "mean of the sweeps collected after burn-in %d stays above the target"
-                       % (out["min_rmse_this"], out["min_rmse_this_sweep"],
+                       % ("reference" if quirks == "final" else quirks + " (biased)", out["min_rmse_this"],
+                          out["min_rmse_this_sweep"],
                           " and collapses from sweep %d (tau -> 0 -> NaN, predictions clamp)" % bad[0] if len(bad)
                           else "", burnin))
     return out
+
+
+def load_times(train, world, rank):
+    """the input formats at this workload's size, from the page
+    cache on the bench host -- the SBPMF triple text (gibbs_sbpmf_final.cpp:26-215's
+    format) and libFM's binary .x/.y (tools/convert.cpp:55-205), each written once
+    by the library's writers and read back through the boundary loaders
+    (sbmf_load_triples / sbmf_load_libfm_binary: one read or mapping, line-aligned
+    chunks on threads).  The read-back is checked against the generated arrays."""
+    import shutil
+    import tempfile
+    import sbmf
+    if world > 1 and rank != 0:
+        return None
+    d = tempfile.mkdtemp(prefix="sbmf_load_")
+    try:
+        data = sbmf.Data(*train)
+        txt, stem = os.path.join(d, "train.tsv"), os.path.join(d, "train")
+        t = time.perf_counter()
+        sbmf.save_triples(txt, data)
+        w_txt = time.perf_counter() - t
+        t = time.perf_counter()
+        sbmf.save_libfm_binary(stem, data)
+        w_bin = time.perf_counter() - t
+        out = {"n": len(train[0]), "threads": int(os.environ.get("SBMF_LOAD_THREADS") or
+                                                  min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS") or 64))),
+               "text_bytes": os.path.getsize(txt),
+               "binary_bytes": os.path.getsize(stem + ".x") + os.path.getsize(stem + ".y"),
+               "write_text_s": w_txt, "write_binary_s": w_bin}
+        for key, fn in (("load_text_s", lambda: sbmf.load_triples(txt)),
+                        ("load_binary_s", lambda: sbmf.load_libfm_binary(stem))):
+            best = None
+            for _ in range(2):  # first read (cold process memory) and a second one
+                t = time.perf_counter()
+                got = fn()
+                dt = time.perf_counter() - t
+                best = dt if best is None else min(best, dt)
+                out.setdefault(key + "_first", dt)
+            out[key] = best
+            ok = np.array_equal(got.user, train[0]) and np.array_equal(got.item, train[1])
+            # the text round trip is bit-exact; the binary format stores f32 targets (ratings 1..5: exact)
+            ok = ok and np.array_equal(got.rating, train[2])
+            if not ok:
+                raise RuntimeError("%s read back different ratings" % key)
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def cpu_baseline(train, test, dims, K, seconds):
@@ -417,13 +470,16 @@ def main():
     from sbmf._lib import KIND_NAMES, NKIND
     train, test, dims = synth.generate(args.shape)
     main_res = measure(args, world, rank, local, args.precision, train, test, mk_uid(world, rank))
-    if args.quirks != "final":  # the extra legs (f32, time-to-RMSE) belong to the headline sampler
-        args.no_f32 = args.no_ttr = True
+    if args.quirks != "final":  # the extra legs (f32, time-to-RMSE, loads) belong to the headline sampler
+        args.no_f32 = args.no_ttr = args.no_load = True
     f32 = None
     if not args.no_f32 and args.precision != "f32":
         f32 = measure(args, world, rank, local, "f32", train, test, mk_uid(world, rank))
-    ttr = [time_to_rmse(args, world, rank, local, train, test, mk_uid(world, rank), b) for b in (0, 50)] \
-        if not args.no_ttr else []
+    # time to 0.85: the reference sampler (final) and the paper's biased SBMF-P model (bias2),
+    # burn-in 0 and 50 each
+    ttr = [time_to_rmse(args, world, rank, local, train, test, mk_uid(world, rank), b, q)
+           for q in ("final", "bias2") for b in (0, 50)] if not args.no_ttr else []
+    loads = None if args.no_load else load_times(train, world, rank)
     n_train = len(train[0])
     value = n_train * args.steps / main_res["seconds"]
     ms = 1e3 * main_res["seconds"] / args.steps
@@ -480,13 +536,16 @@ def main():
         "scaling": "not a scaling number (%d ranks on one GPU)" % world if one_device else "strong",
         "vs_baseline": None if one_device else value / BASELINE_RPS,
         "dtype": args.precision,
-        "data": "synthetic ML-20M-shaped (sbmf/synth.py: planted rank-10, Pareto users, log-normal items)",
+        "data": "synthetic %s-shaped (sbmf/synth.py: planted rank-10, Pareto users, log-normal items)"
+                % {"ml-20m": "ML-20M", "ml-10m": "ML-10M", "ml-1m": "ML-1M", "ml-100k": "ML-100k",
+                   "netflix": "Netflix"}[args.shape],
         "config": {"workload": "%s K=%d SBPMF Gibbs sweep (%suser+item half-sweeps, hyperparameters, test RMSE)"
                                % (args.shape, args.K, "bias draws + " if args.quirks.startswith("bias") else ""),
                    "num_users": dims[0], "num_items": dims[1], "n_train": n_train, "n_test": len(test[0]),
                    "K": args.K, "rng": "philox", "quirks": args.quirks,
                    "parallelism": "rows x%d (%s)" % (world, "host-shm exchange, testing only" if os.environ.get("SBMF_COMM") == "host" else "RCCL block broadcast + p2p residual exchange"),
                    "test_rmse_after": main_res["rmse"], "sweeps_run": main_res["sweeps_run"],
+                   "prepare_s": main_res["prep_s"], "load": loads,
                    "time_to_test_rmse_0.85": ttr,
                    "ms_user_half": main_res["ms_user"], "ms_item_half": main_res["ms_item"],
                    "ms_hyper": main_res["ms_hyper"], "ms_eval": main_res["ms_eval"], "ms_comm": main_res["ms_comm"],
@@ -526,8 +585,15 @@ if __name__ == "__main__":
         # after rocprofv3's (if any) has written its output -- the HIP runtime's library
         # finalizer faults under rocprofv3 (ROCm 7.2, profiles/r03_rocprof_teardown.txt)
         _sbmf_lib.exit_guard(1)
-    main()
+    rc = 0
+    try:
+        main()
+    except SystemExit as e:  # argparse --help / errors, sys.exit(n): keep their status
+        rc = e.code if isinstance(e.code, int) else (0 if e.code is None else 1)
+        if e.code is not None and not isinstance(e.code, int):
+            print(e.code, file=sys.stderr)
     sys.stdout.flush()
     sys.stderr.flush()
     if os.environ.get("SBMF_EXIT") != "normal":
-        _sbmf_lib.exit_guard(0)
+        _sbmf_lib.exit_guard(rc)
+    sys.exit(rc)

@@ -109,53 +109,39 @@ typedef struct sbmf_config {
                                  sweep, :317-334); 0 = only at start                            */
     uint32_t eval_train;      /* 1: compute train RMSE of the current sample each sweep          */
     uint32_t eval_test;       /* 1: test prediction + running-mean RMSE each sweep (:539-563)    */
-    uint32_t gram_threshold;  /* rows with more ratings use the Gram route (0 = default)         */
-    uint32_t row_kernel;      /* 0: MFMA Gram-block kernels (default); 1: per-coordinate
-                                 wave-reduction kernels + Gram route                             */
-    uint32_t stream_threshold;/* row_kernel 0: rows with more ratings use the streaming
-                                 Gram-block kernel (0 = default: 256 f64 / 512 f32)              */
+    uint32_t gram_threshold;  /* reserved, must be 0 (the full-Gram row route was removed)       */
+    uint32_t row_kernel;      /* reserved, must be 0 (the per-coordinate row kernels were removed:
+                                 the MFMA Gram-block kernels are the only row kernels)          */
+    uint32_t stream_threshold;/* rows with more ratings use the streaming Gram-block kernel
+                                 k_gres (0 = default: 256 f64 / 512 f32)                        */
     uint32_t split_chunk;     /* streaming-kernel task size: rows longer than this are split
-                                 into chunks on co-resident workgroups (0 = the LDS capacity,
-                                 4096 f64 / ~8K f32, sized to LDS; larger values are capped to it)            */
+                                 into chunks on co-resident workgroups (0 = the register
+                                 capacity of the workgroup shape; larger values are capped to it) */
     uint32_t tune;            /* kernel-variant bits for experiments (0 = tuned defaults):
-                                 bit 0 = block solve replicated in every wave of a row
-                                 (default: one wave solves, D shared through LDS),
                                  bit 1 = residuals from r - own.partner as on several GPUs,
                                  bit 2 = power-of-two waves per Gram-block row (2/4/8) instead
                                          of ceil(ratings / ratings-per-wave),
                                  bit 3 = f64 rows of 33..64 ratings on two 8-vector waves instead
                                          of one 16-vector wave,
-                                 bit 5 = LDS-staged streaming kernel on 16-wave workgroups,
-                                 bit 6 = LDS-staged streaming kernel (k_gstream) instead of the
-                                         register-resident one (k_gres),
-                                 bit 7 = k_gres on 4-wave workgroups (default 8),
-                                 bits 8-10 = hybrid k_gres / k_gstream stream sets by row length,
-                                 bit 16 = k_gres tasks in static rounds (default: a queue),
+                                 bit 7 = k_gres on 4-wave workgroups (both sides),
                                  bit 17 = k_gres on 16-wave workgroups (both sides),
                                  bit 23 = f64 user streaming rows on 8-wave k_gres workgroups
                                           (default: 4-wave, 512-rating tasks),
-                                 bit 20 = every multi-wave f64 Gram-block row on 16-vector
-                                          waves (default: rows of 5-8 8-vector waves),
-                                 bit 21 = no multi-wave f64 Gram-block row on 16-vector waves,
-                                 bit 24 = k_gres (queue order) as an ordinary launch instead of
-                                          a cooperative one (measured neutral, 8.93 vs 8.95 ms;
-                                          split rows then rely on the claiming workgroups being
-                                          resident: a hand-off that times out fails sbmf_run),
-                                 bit 25 = k_gres with double-buffered slices (slice t+1 in flight
-                                          through block t's exchange; one workgroup per CU),
+                                 bit 24 = k_gres as an ordinary launch instead of a cooperative one
+                                          (set internally under the launch overlap),
                                  bit 26 = no overlap of the next sweep's prologue (sums, column
                                           statistics, host draws) with the test evaluation
                                           (Philox mode; the chain is the same either way),
                                  bit 27 = f64 item rows on 8-wave k_gres workgroups (default:
-                                          16-wave, as bit 17 does for both sides),
-                                 bit 28 = k_gres block epilogue at raised wave priority,
+                                          rows > 1024 ratings on 16-wave ones, the rest 8-wave),
                                  bit 29 = a half's Gram-block launches after its streaming launch
                                           on one stream (default: on a second stream beside it,
                                           the streaming launch then an ordinary one as bit 24),
                                  bit 30 = a half's two streaming sets (items: rows > 1024 and the
-                                          rest) one after the other (default: side by side),
-                                 bit 31 = with the overlap, the Gram-block launches enqueued before
-                                          the streaming launch (default: after it)            */
+                                          rest) one after the other (default: side by side).
+                                 Removed in round 4 with the variants they selected (measured
+                                 slower, kept in git history): bits 0, 5, 6, 8-10, 16, 20-22, 25,
+                                 28, 31; they are now ignored.                                   */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */
@@ -237,13 +223,12 @@ int sbmf_get_biases(sbmf_ctx* ctx, double* bu, double* bv, double* b0);
  *   0..4  MFMA Gram-block row kernels: 1 wave/row (two sizes), then 2..8
  *         waves/row (ceil(ratings/32) f64, /64 f32) timed in three groups; up to
  *         8/64/64/128/256 ratings (f64), 16/64/128/256/512 (f32),
- *   5     streaming MFMA Gram-block kernel: one persistent cooperative launch
- *         over tasks of <= 4096 (f64) / ~8K (f32) ratings (LDS capacity) -- whole rows, or
- *         chunks of longer rows on co-resident workgroups -- plus the publish
- *         of split rows,
- *   6..9  per-coordinate wave-reduction row kernels (1 wave/row <=128 and
- *         <=512, 4 / 8 waves/row <=2048 / 4096),
- *   10    Gram route (all its launches).  kern_bytes is the
+ *   5     streaming MFMA Gram-block kernel k_gres: one persistent launch per
+ *         stream set over tasks of <= 512 / 1024 / 2048 (f64, 4- / 8- / 16-wave
+ *         workgroups) ratings held in VGPRs -- whole rows, or chunks of longer
+ *         rows on co-resident workgroups -- plus the publish of split rows,
+ *   6..10 reserved (the removed per-coordinate and full-Gram row kernels: 0).
+ * kern_bytes is the
  * algorithmic traffic of that launch per SURVEY.md §8(d): per rating
  * s*K (partner row) + 4 (partner id) + s (residual), per row 2*s*K (own row
  * read + write), s = 4 (f32) or 8 (f64). */
@@ -272,7 +257,10 @@ typedef struct sbmf_ratings {
     double* rating;
 } sbmf_ratings;
 /* SBPMF triple format "u<sep>i<sep>r" per line, lines accepted iff
- * sscanf("%u%c%u%c%lf") >= 5 (gibbs_sbpmf_final.cpp:43). */
+ * sscanf("%u%c%u%c%lf") >= 5 (gibbs_sbpmf_final.cpp:43).  Replaces the three
+ * serial text passes of gibbs_sbpmf_final.cpp:26-215: one read, line-aligned
+ * chunks parsed on threads (SBMF_LOAD_THREADS, default min(cores,
+ * OMP_NUM_THREADS)), concatenated in file order. */
 int sbmf_load_triples(const char* path, sbmf_ratings* out);
 /* libFM text "r f1:v f2:v" (Data.h:192-217) with exactly one user and one
  * item feature per line: the first feature is the user id, the second the
@@ -288,6 +276,11 @@ int sbmf_load_libfm_binary(const char* stem, uint32_t item_offset, sbmf_ratings*
  * rating data): row q = {user[q]:1, item_offset + item[q]:1}, f32 targets;
  * num_cols = max(num_cols, largest feature id + 1). */
 int sbmf_save_libfm_binary(const char* stem, const sbmf_ratings* in, uint32_t item_offset, uint32_t num_cols);
+/* Writes the SBPMF triple format "u\tv\tr\n" (0-based ids) that the reference's
+ * data scripts produce (data/m100k/create_file_scalable_bpmf.py:6-12) and
+ * sbmf_load_triples reads back bit for bit: integer ratings as integers, others
+ * with %.17g. */
+int sbmf_save_triples(const char* path, const sbmf_ratings* in);
 void sbmf_free_ratings(sbmf_ratings* r);
 
 /* --- multi-GPU layout (host only) ---------------------------------------------------------- */

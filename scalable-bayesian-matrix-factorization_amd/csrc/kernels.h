@@ -15,7 +15,7 @@ struct HalfArgs {
     const uint32_t* perm;  // [N] position of the rating in the other orientation's order
     const T* E_this;       // [N] residuals in this orientation's order (read sequentially)
     T* E_other;            // [N] residuals in the other orientation's order: E_other[perm[q]] (scatter)
-    const T* r_this;       // [N] ratings in this order (E_FROM_DOT, train RMSE, Gram update)
+    const T* r_this;       // [N] ratings in this order (e_from_dot, train RMSE)
     T* own;                // [R][Kp]
     const T* partner;      // [P+2][Kp]: row P is all zeros (sentinel), row P+1 slack
     const T* sig;          // [Kp] precision hyperparameter of this side (zero padded)
@@ -31,39 +31,18 @@ struct HalfArgs {
     double* row_tr;        // [R] per-row train squared error of the clamped sample (or null)
     T lo, hi;
     int e_from_dot;        // 1: e0 = r - own.partner (no gather; multi-GPU)
-    uint32_t tune;         // kernel variant bits (sbmf_config.tune): bit 0 = replicated block solve
+    uint32_t tune;         // kernel variant bits (sbmf_config.tune)
     unsigned long long* prof;  // [8] phase cycles of wave 0 (SBMF_KPROF diagnostics) or null
 };
-
-// Heavy-row (Gram route) work description.
-struct GramItem {
-    uint32_t row;     // global row id
-    uint32_t beg;     // first rating (absolute index into the orientation arrays)
-    uint32_t len;     // ratings in this chunk
-    uint32_t slab;    // chunk slab index
-};
-struct GramRow {
-    uint32_t row;
-    uint32_t slab0;   // first slab of the row
-    uint32_t nslab;   // number of chunk slabs
-};
-
-// Bin launch descriptor for the light / medium row kernels.
-// W2/W8: one wave per row, 2/8 rating slots per lane; B4/B8: 4/8 waves per
-// row, 8 slots per lane.  Heavier rows take the Gram route.
-enum RowKernelKind { RK_W2 = 0, RK_W8 = 1, RK_B4 = 2, RK_B8 = 3, RK_NUM = 4 };
-static const uint32_t RK_MAXDEG[RK_NUM] = {128, 512, 2048, 4096};
 
 // Gram-block (MFMA) row kernels.  Max ratings per row for each kind: f64
 // holds 8 vectors (32 ratings) per wave, f32 16 (64 ratings).
 enum GblockKind { GK_W4 = 0, GK_W16 = 1, GK_B2 = 2, GK_B4 = 3, GK_B8 = 4, GK_NUM = 5 };
-inline uint32_t gk_maxdeg(int kind, bool f64, bool wide = false, bool big = false) {
+inline uint32_t gk_maxdeg(int kind, bool f64, bool wide = false) {
     static const uint32_t waves4[GK_NUM] = {1, 4, 8, 16, 32};  // (waves x vectors) / V*4 ratings
     const uint32_t per_wave = f64 ? 32 : 64;
     // wide (f64 default; tune bit 3 turns it off): the 1-wave kind holds 16 vectors (64 ratings)
     if (wide && f64 && (kind == GK_W16 || kind == GK_B2)) return 64;
-    // big (f64): the last kind takes rows up to 512 ratings, as up to 8 sixteen-vector waves
-    if (big && f64 && kind == GK_B8) return 512;
     return kind == GK_W4 ? per_wave / 4 : per_wave * waves4[kind] / 4;
 }
 
@@ -73,8 +52,6 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
 template <typename T>
 hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
 
-// Streaming Gram-block kernel: one 512-thread workgroup per task (a whole
-// row, or one chunk of a row split over several co-resident workgroups).
 // Streaming-kernel task: at most `cmax` ratings of one row (the whole row,
 // or one chunk of a row split over `nch` co-resident workgroups).  A task
 // with len == 0 is an empty slot (round padding).
@@ -93,7 +70,6 @@ struct SplitRow {
 };
 struct SplitSync {
     double* slabs;       // [nchunk_total][nblk][16*16+16]
-    double* totals;      // k_gres: [nsplit_rows * nblk][16*16+16] the chunk-ordered sum (rows > GRES_ALLREAD chunks)
     uint32_t* counters;  // [nsplit_rows * nblk], zeroed per launch; then the task-queue head (dynamic order)
     uint32_t ncounters;
     uint32_t nblk;       // ceil(K/16)
@@ -101,38 +77,26 @@ struct SplitSync {
     double* chunk_tr;    // [nchunk_total]
     void* newown;        // [nchunk_total][Kp] (T), slot slab0 of each split row
     uint32_t* timeout;   // set to 1 if a spin gave up
-    uint32_t cmax;       // ratings per task (LDS-resident partner ids and residuals)
+    uint32_t cmax;       // ratings per task
     unsigned long long* prof;  // [8] phase cycles of wave 0 (SBMF_KPROF diagnostics) or null
 };
-// Largest task (ratings) the streaming kernel keeps in LDS with two
-// workgroups per CU, for the kernel variant `tune`.
+// Task capacity (ratings) of the streaming kernel k_gres for the variant `tune`:
+// 4 * waves * vectors-per-wave, the partner slices held in VGPRs.
 template <typename T>
 uint32_t gstream_cmax(uint32_t tune);
 // Workgroups per CU the streaming kernel variant `tune` is sized for.
 int gstream_wg_target(uint32_t tune);
-// Co-resident k_gstream workgroups per CU at the given task capacity (occupancy API).
+// Co-resident k_gres workgroups per CU (occupancy API).
 template <typename T>
 int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune);
-// All streaming tasks of a half-sweep in one cooperative persistent launch of
-// `grid` (<= residency) workgroups; workgroup w runs tasks w, w+grid, ...
-// Tasks are laid out in rounds of `grid` slots and every split row's chunks
-// share a round, so chunk hand-offs only wait on co-resident peers (k_gstream,
-// and k_gres with tune bit 16); k_gres by default takes one list, claimed in
-// order from a queue head by whichever workgroup is free (a split row's chunks
-// are consecutive, so a chunk only waits for peers that the next free
-// workgroups claim).  Split rows are then
-// published by k_split_finish.
+// All streaming tasks of a half-sweep in one persistent launch of `grid`
+// (<= residency) workgroups.  Tasks are one list, claimed in order from a queue
+// head by whichever workgroup is free; a split row's chunks are consecutive, so
+// a chunk only waits for peers that the next free workgroups claim.  Split rows
+// are then published by k_split_finish.
 template <typename T>
 hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid, const SplitRow* srows, uint32_t nsrow,
                           const HalfArgs<T>& a, const SplitSync& sy, hipStream_t st);
-
-template <typename T>
-hipError_t launch_rows(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
-
-template <typename T>
-hipError_t launch_gram(const GramItem* items, uint32_t nitems, const GramRow* grows, uint32_t ngrows,
-                       double* slabs, T* delta, double* chunk_sq, double* chunk_tr, const HalfArgs<T>& a,
-                       hipStream_t st);
 
 // Full residual recompute over rows [r0, r1) of one orientation, split into
 // tasks of <= RESID_CHUNK ratings (one wave each): e = r - own.partner is

@@ -9,18 +9,15 @@
 //     E_n += v_nk (old - new).
 // Rows are independent given the partner table, so a half-sweep is one
 // launch per degree bin:
-//   * k_rows<..., NW=1>  one 64-lane wave per row (deg <= 512): lanes own
-//     ratings, the row's residuals live in VGPRs, partner slices of 32 B are
-//     gathered per k-block, the two k-reductions per coordinate are DPP
-//     wave sums (row_shr / row_bcast, no LDS);
-//   * k_rows<..., NW>1>  NW waves cooperate on one row (deg <= 4096); wave
-//     sums meet in LDS once per coordinate (double-buffered, one barrier);
-//   * Gram route (deg > gram threshold): G = S^T S and b = S^T e0 per chunk
-//     (k_gram_partial), fixed-order chunk reduction + the exact K-step
-//     recurrence Q_k = b_k - sum_{l<k} G_kl D_l + G_kk u_k (k_gram_solve),
-//     and e = r - S u_new (k_gram_update).  Algebraically identical to the
-//     sequential coordinate loop.
-// Layout: factor tables row-major [rows][Kp] (Kp = K padded to 32 B), so a
+//   * k_gblock<T, V, NW, RPW>  rows of <= 256 ratings (f64): 1 wave per row (RPW
+//     rows per block) or NW waves per row; per 16-wide k-block the row's
+//     partner slices sit in VGPRs, G_B = S^T S by MFMA, the 16 draws as the
+//     exact recurrence over G_B, e -= S_B D_B by DPP;
+//   * k_gres<T, NW, SIDE>  longer rows and the chunks of split rows: one
+//     persistent launch, the same per-block steps with a task's slices held in
+//     the VGPRs of NW waves and split rows' (G_B, c_B) partials summed across
+//     workgroups in chunk order.
+// Layout: factor tables row-major [rows][Kp] (Kp = K padded to 16), so a
 // partner row is one contiguous 4K/8K-byte record; ratings in CSR (users)
 // and CSC (items) order; residuals kept per orientation and gathered through
 // a fixed permutation (no atomics, deterministic).
@@ -113,199 +110,6 @@ __device__ __forceinline__ T draw_coord(T P, T Q, T sg, T mu, T tau, T z, int sd
     return mean + sd * z;
 }
 
-// ------------------------------------------------------------ light / medium rows
-// NW waves per row, RPB rows per block (NW==1) ; KS = ceil(K/64) <= 4.
-template <typename T, int MMAX, int NW, int RPB, int KS>
-__global__ __launch_bounds__(64 * NW * RPB) void k_rows(const uint32_t* __restrict__ rows, uint32_t nrows,
-                                                          HalfArgs<T> a) {
-    constexpr int B = 32 / sizeof(T);  // slice width (k values per 32-byte gather)
-    constexpr int ZS = (KS + 1) / 2;
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    const int wr = wv % NW;
-    const int rib = wv / NW;
-    const uint32_t ri = blockIdx.x * RPB + rib;
-    if (ri >= nrows) return;  // uniform per row group (NW>1 => RPB==1: whole block)
-    const uint32_t row = rows[ri];
-    const uint32_t beg = a.ptr[row];
-    const uint32_t n = a.ptr[row + 1] - beg;
-    constexpr uint32_t G = 64 * NW;
-    const uint32_t g = wr * 64 + lane;
-    const int m = (int)((n + G - 1) / G);
-    const uint32_t K = a.K, Kp = a.Kp;
-
-    T own_r[KS], sig_r[KS], mu_r[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const uint32_t k = 64 * s + lane;
-        own_r[s] = k < K ? a.own[(size_t)row * Kp + k] : T(0);
-        sig_r[s] = k < K ? a.sig[k] : T(0);
-        mu_r[s] = k < K ? a.mu[k] : T(0);
-    }
-    T z_r[ZS][2];
-#pragma unroll
-    for (int zs = 0; zs < ZS; ++zs) {
-        const uint32_t i0 = 128 * zs + 2 * lane;
-        {  // per-half normals (host reference stream or launch_philox_fill)
-            z_r[zs][0] = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
-            z_r[zs][1] = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
-
-        }
-    }
-
-    T e[MMAX];
-    uint32_t pj[MMAX];
-    bool ok[MMAX];
-#pragma unroll
-    for (int t = 0; t < MMAX; ++t) {
-        const uint32_t nl = g + t * G;
-        ok[t] = (t < m) && (nl < n);
-        pj[t] = ok[t] ? a.part[beg + nl] : 0u;
-        e[t] = T(0);
-    }
-    if (a.e_from_dot) {
-        // e0 = r - own . partner  (pre-pass over the partner rows)
-        T dot[MMAX];
-#pragma unroll
-        for (int t = 0; t < MMAX; ++t) dot[t] = T(0);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            if (64 * s >= (int)K) break;
-            for (int kb = 0; kb < 64; kb += B) {
-                const int k0 = 64 * s + kb;
-                if (k0 >= (int)K) break;
-#pragma unroll
-                for (int t = 0; t < MMAX; ++t) {
-                    if (t < m) {
-                        T sl[B];
-                        if (ok[t]) load_slice(a.partner + (size_t)pj[t] * Kp + k0, sl);
-                        else
-#pragma unroll
-                            for (int b = 0; b < B; ++b) sl[b] = T(0);
-#pragma unroll
-                        for (int b = 0; b < B; ++b) dot[t] += sl[b] * readlane(own_r[s], kb + b);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < MMAX; ++t)
-            if (ok[t]) e[t] = a.r_this[beg + g + t * G] - dot[t];
-    } else {
-#pragma unroll
-        for (int t = 0; t < MMAX; ++t)
-            if (ok[t]) e[t] = a.E_this[beg + g + t * G];
-    }
-
-    __shared__ T red[NW > 1 ? 2 : 1][NW][2];
-    int par = 0;
-    const T tau = a.tau;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        if (64 * s >= (int)K) break;
-        for (int kb = 0; kb < 64; kb += B) {
-            const int k0 = 64 * s + kb;
-            if (k0 >= (int)K) break;
-            T sl[MMAX][B];
-#pragma unroll
-            for (int t = 0; t < MMAX; ++t) {
-                if (t < m) {
-                    if (ok[t]) load_slice(a.partner + (size_t)pj[t] * Kp + k0, sl[t]);
-                    else
-#pragma unroll
-                        for (int b = 0; b < B; ++b) sl[t][b] = T(0);
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const int kl = kb + b;
-                if (k0 + b >= (int)K) break;
-                T p = T(0), q = T(0);
-#pragma unroll
-                for (int t = 0; t < MMAX; ++t) {
-                    if (t < m) {
-                        p += sl[t][b] * sl[t][b];
-                        q += sl[t][b] * e[t];
-                    }
-                }
-                T P = wave_sum(p);
-                T Qe = wave_sum(q);
-                if constexpr (NW > 1) {
-                    if (lane == 0) {
-                        red[par][wr][0] = P;
-                        red[par][wr][1] = Qe;
-                    }
-                    __syncthreads();
-                    P = T(0);
-                    Qe = T(0);
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) {
-                        P += red[par][w][0];
-                        Qe += red[par][w][1];
-                    }
-                    par ^= 1;
-                }
-                const T old = readlane(own_r[s], kl);
-                const T sg = readlane(sig_r[s], kl);
-                const T mu = readlane(mu_r[s], kl);
-                const T z = readlane(z_r[s >> 1][b & 1], ((s & 1) << 5) + (kl >> 1));
-                const T nw = draw_coord(P, Qe + P * old, sg, mu, tau, z, a.sd_is_var);
-                const T d = old - nw;
-#pragma unroll
-                for (int t = 0; t < MMAX; ++t)
-                    if (t < m) e[t] += sl[t][b] * d;
-                own_r[s] = (lane == kl) ? nw : own_r[s];
-            }
-        }
-    }
-
-    // epilogue: own row, residuals, per-row partial sums
-    if (wr == 0) {
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const uint32_t k = 64 * s + lane;
-            if (k < K) a.own[(size_t)row * Kp + k] = own_r[s];
-        }
-    }
-    T sq = T(0), tr = T(0);
-#pragma unroll
-    for (int t = 0; t < MMAX; ++t) {
-        if (ok[t]) {
-            const uint32_t idx = beg + g + t * G;
-            a.E_other[a.perm[idx]] = e[t];
-            sq += e[t] * e[t];
-            if (a.row_tr) {
-                const T r = a.r_this[idx];
-                T pr = r - e[t];
-                pr = (pr < a.hi) ? pr : a.hi;
-                pr = (a.lo < pr) ? pr : a.lo;
-                tr += (pr - r) * (pr - r);
-            }
-        }
-    }
-    if (a.row_sq || a.row_tr) {
-        double dsq = wave_sum((double)sq);
-        double dtr = wave_sum((double)tr);
-        if constexpr (NW > 1) {
-            __shared__ double red2[NW][2];
-            if (lane == 0) {
-                red2[wr][0] = dsq;
-                red2[wr][1] = dtr;
-            }
-            __syncthreads();
-            dsq = 0.0;
-            dtr = 0.0;
-            for (int w = 0; w < NW; ++w) {
-                dsq += red2[w][0];
-                dtr += red2[w][1];
-            }
-        }
-        if (wr == 0 && lane == 0) {
-            if (a.row_sq) a.row_sq[row] = dsq;
-            if (a.row_tr) a.row_tr[row] = dtr;
-        }
-    }
-}
 
 // ------------------------------------------------------------ Gram-block rows (MFMA)
 // Layout: 16 lanes per rating, 4 ratings per 64-lane vector; lane (r = l>>4,
@@ -472,7 +276,7 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
 #define SBMF_GBLOCK_OCC_WIDE 4
 #endif
 #define GBLOCK_OCC(T, V) ((V) * sizeof(T) > 64 ? SBMF_GBLOCK_OCC_WIDE : (sizeof(T) == 8 ? SBMF_GBLOCK_OCC64 : 3))
-template <typename T, int V, int NW, int RPW, bool SW>
+template <typename T, int V, int NW, int RPW>
 __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_gblock(const uint32_t* __restrict__ rows,
                                                                      uint32_t nrows, HalfArgs<T> a) {
     typedef typename MfmaT<T>::acc_t acc_t;
@@ -507,7 +311,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     __shared__ T Ps[NWAVE][GB];               // diagonal of G_B
     __shared__ T Cs[NWAVE][GB];               // c_B
     __shared__ T newS[NW > 1 ? 256 : 1];
-    __shared__ T Dsh[GB];                     // SW: the block's D from the solving wave
+    __shared__ T Dsh[GB];                     // multi-wave rows: the block's D from the solving wave
     const int ws = NW > 1 ? 0 : wv;           // LDS slot holding this row's reduced G / c
 
     // Per-rating and per-row values live in LDS, not VGPRs (occupancy): the row's
@@ -683,11 +487,11 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own LDS writes visible to own reads
             __builtin_amdgcn_wave_barrier();
         }
-        // ---- 3. the 16 sequential draws: every wave of the row redundantly
-        // (no barrier), or -- SW, multi-wave rows -- wave 0 alone, handing D
-        // to the others through LDS (their issue slots go to other rows)
+        // ---- 3. the 16 sequential draws: the row's one wave, or -- multi-wave
+        // rows -- wave 0 alone, handing D to the others through LDS (their issue
+        // slots go to other rows)
         T dlt = T(0);
-        if (!(SW && NW > 1) || wr == 0) {
+        if (NW == 1 || wr == 0) {
             const T P = Ps[ws][ci];
             const T old = oldc, sg = sgc, mu = muc;
             const T z = zS[ws][kk];
@@ -706,12 +510,12 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
                 // staged in LDS, written after the last barrier: no wave of this
                 // row can still have a load of the same own value in flight
                 if (wr == 0 && lane < GB && kin) newS[kk] = nwv;
-                if (SW && lane < GB) Dsh[lane] = dlt;
+                if (lane < GB) Dsh[lane] = dlt;
             } else {
                 if (lane < GB && kin) a.own[(size_t)row * Kp + kk] = nwv;  // one wave: program order
             }
         }
-        if constexpr (SW && NW > 1) {
+        if constexpr (NW > 1) {
             lds_barrier();
             dlt = Dsh[ci];
         }
@@ -784,359 +588,6 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
 #undef PROW
 }
 
-// ------------------------------------------------------------ streaming Gram-block rows
-// Long rows (and their chunks): one 8-wave workgroup per task of at most
-// cmax ratings, in one persistent cooperative launch per half-sweep.  The
-// task's partner ids and residuals are staged in LDS once, so every later
-// traversal issues its partner-slice loads straight from LDS addresses (no
-// dependent global id load) and updates residuals on-chip.  Traversal t
-// applies block t-1 (e -= S_{t-1} D_{t-1}) and accumulates block t
-// (G_t = S^T S by MFMA, c_t = S^T e) in one pass over the task's ratings.
-// Split rows exchange their (G_B, c_B) partials through global slabs (plain
-// stores -> agent release -> counter; poll -> agent acquire -> loads, the
-// CDNA guide's G16 hand-off); every chunk sums them in chunk order, so all
-// chunks draw identical coordinates.  Wave w owns vectors w, w+NW, ...
-// LDS geometry of a task, derived from the workgroup shape (NW waves, UNR
-// vectors of 4 ratings per wave per group):
-//   STRIDE  ratings one traversal group covers across the workgroup;
-//   PAD     slots past the task's end: the task rounded up to a stride, plus
-//           the group a prefetching traversal reads past its end (the padded
-//           slots hold the zero partner row and zero residuals);
-//   SINK    one private slot per lane of every wave, the target of the
-//           masked-off residual stores (eDummy below).
-template <int NW, int UNR>
-struct GsGeom {
-    static constexpr uint32_t STRIDE = 4 * NW * UNR;
-    static constexpr uint32_t PAD = 2 * STRIDE;
-    static constexpr uint32_t SINK = 64 * NW;
-    // dynamic LDS: [cmax+PAD] partner ids, then (16-byte aligned) [cmax+PAD+SINK] residuals
-    static __host__ __device__ constexpr size_t ids_bytes(uint32_t cmax) {
-        return ((size_t)(cmax + PAD) * sizeof(uint32_t) + 15) / 16 * 16;
-    }
-    template <typename T>
-    static __host__ __device__ constexpr size_t dyn_bytes(uint32_t cmax) {
-        return ids_bytes(cmax) + (size_t)(cmax + PAD + SINK) * sizeof(T);
-    }
-};
-// SIDE (0 users, 1 items) only names the instantiation, so profiles tell the
-// two half-sweeps apart.
-template <typename T, int NW, int UNR, bool SW, int SIDE>
-__global__ __launch_bounds__(64 * NW, 4) void k_gstream(const SplitTask* __restrict__ tasks, uint32_t ntask,
-                                                     HalfArgs<T> a, SplitSync sy) {
-    typedef typename MfmaT<T>::acc_t acc_t;
-    const int lane = threadIdx.x & 63;
-    const int wr = threadIdx.x >> 6;
-    const uint32_t K = a.K, Kp = a.Kp;
-    const int ci = lane & 15;
-    const int rr = lane >> 4;
-    constexpr int SL = GB * GB + GB;  // slab doubles per (chunk, block)
-    __shared__ T Ls[NW][GB][GLD];     // strictly lower part of G_B
-    __shared__ T Ps[NW][GB];          // diagonal of G_B
-    __shared__ T Cs[NW][GB];
-    __shared__ double red2[NW][2];
-    __shared__ T newS[256];           // new own values of the row, written once at the end
-    __shared__ T Dsh[GB];             // SW: the block's D from the solving wave
-    extern __shared__ unsigned char dyn_lds[];
-    uint32_t* pjL = reinterpret_cast<uint32_t*>(dyn_lds);  // [cmax+pad] partner ids
-    typedef GsGeom<NW, UNR> Geo;
-    T* eL = reinterpret_cast<T*>(dyn_lds + Geo::ids_bytes(sy.cmax));  // [cmax+PAD] residuals
-    const T tau = a.tau;
-    const uint32_t nblk = (K + GB - 1) / GB;
-
-    for (uint32_t ti = blockIdx.x; ti < ntask; ti += gridDim.x) {
-        const SplitTask tk = tasks[ti];
-        const uint32_t n = tk.len;
-        if (n == 0) continue;  // empty round slot (uniform)
-        const uint32_t row = tk.row;
-        const uint32_t beg = tk.beg;
-        const uint32_t nch = tk.nch;
-        const uint32_t nvec = (n + 3) / 4;
-
-        T zA0, zA1, zB0 = T(0), zB1 = T(0);
-        {  // per-half normals (host reference stream or launch_philox_fill)
-            const uint32_t i0 = 2 * lane;
-            zA0 = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
-            zA1 = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
-            if (K > 128) {
-                zB0 = 128 + i0 < K ? a.zbuf[(size_t)row * K + 128 + i0] : T(0);
-                zB1 = 129 + i0 < K ? a.zbuf[(size_t)row * K + 129 + i0] : T(0);
-            }
-        }
-
-        // optional phase profile (build with KPROF=1, run with SBMF_KPROF=1): wave 0's cycles per phase
-#ifdef SBMF_KPROF_BUILD
-        unsigned long long tp = (sy.prof && threadIdx.x == 0) ? clock64() : 0ull;
-        auto stamp = [&](int ph) {
-            if (sy.prof && threadIdx.x == 0) {
-                const unsigned long long now = clock64();
-                atomicAdd(&sy.prof[ph], now - tp);
-                tp = now;
-            }
-        };
-#else
-        auto stamp = [](int) {};
-#endif
-        // ---- stage the task's partner ids and initial residuals in LDS; the
-        // slots up to the traversal stride (4*NW*UNR ratings) hold the zero
-        // row and zero residuals, so the traversal needs no per-rating masks
-        // npad <= cmax + PAD: n rounded up to a stride, plus one stride
-        const uint32_t npad = (n + Geo::STRIDE - 1) / Geo::STRIDE * Geo::STRIDE + Geo::STRIDE;
-        for (uint32_t x = threadIdx.x; x < npad; x += 64 * NW) pjL[x] = x < n ? a.part[beg + x] : a.zrow;
-        for (uint32_t x = n + threadIdx.x; x < npad; x += 64 * NW) eL[x] = T(0);
-        if (a.e_from_dot) {
-            __syncthreads();
-            for (uint32_t v = wr; v < nvec; v += NW) {
-                const uint32_t q = 4 * v + rr;
-                const uint32_t pj = q < n ? pjL[q] : a.zrow;
-                T d = T(0);
-                for (uint32_t k0 = 0; k0 < K; k0 += GB)  // padding columns are zero
-                    d += a.partner[(size_t)pj * Kp + k0 + ci] * a.own[(size_t)row * Kp + k0 + ci];
-                d = row16_sum(d);
-                if (q < n && ci == 0) eL[q] = a.r_this[beg + q] - d;
-            }
-        } else {
-            for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) eL[x] = a.E_this[beg + x];
-        }
-        __syncthreads();
-        stamp(0);  // staging
-
-        double sq = 0.0, trs = 0.0;
-        T Dl = T(0);  // D of the previous block, lane (r,i) holds D_i
-        T oldn = a.own[(size_t)row * Kp + ci];  // block 0's old values (padding columns are zero)
-        // Traversal over the task's padded vectors, specialised by phase so
-        // the group body is straight-line code (a branch around a load makes
-        // the compiler drain every outstanding load at the join):
-        //   PH 0: t = 0     accumulate block 0 only
-        //   PH 1: 0<t<nblk  apply block t-1, accumulate block t
-        //   PH 2: t = nblk  apply the last block, emit residuals
-        // All loads are unconditional: the unused slice of phases 0 / 2 reads
-        // a valid column (padding / slack row) and is ignored.
-        static_assert(Geo::SINK >= 64 * NW, "every lane of every wave needs its own sink slot");
-        T* const eDummy = eL + (size_t)(sy.cmax + Geo::PAD) + 64 * wr;  // per-lane sink of masked stores
-        for (uint32_t t = 0; t <= nblk; ++t) {
-            const bool app = t > 0, acc = t < nblk;
-            const uint32_t kc = t * GB + ci;
-            const uint32_t kp = app ? kc - GB : kc;
-            acc_t g = {T(0), T(0), T(0), T(0)};
-            T cc = T(0);
-            auto traverse = [&](auto phase) {
-                constexpr int PH = decltype(phase)::value;
-                uint32_t pm[UNR];  // PH 2: residual scatter targets, in flight with the slices
-                auto load = [&](uint32_t v0, T (&sp)[UNR], T (&sc)[UNR], T (&e)[UNR]) {
-                    uint32_t pj[UNR];
-#pragma unroll
-                    for (int u = 0; u < UNR; ++u) {
-                        const uint32_t q = 4 * (v0 + u * NW) + rr;  // < npad: padded slots
-                        pj[u] = pjL[q];
-                        e[u] = eL[q];
-                        if constexpr (PH == 2) pm[u] = q < n ? a.perm[beg + q] : 0u;
-                    }
-#pragma unroll
-                    for (int u = 0; u < UNR; ++u) {
-                        const T* src = a.partner + (size_t)pj[u] * Kp;
-                        if constexpr (PH != 0) sp[u] = src[kp];
-                        if constexpr (PH != 2) sc[u] = src[kc];
-                    }
-                };
-                auto proc = [&](uint32_t v0, const T (&sp)[UNR], const T (&sc)[UNR], T (&e)[UNR]) {
-                    if constexpr (PH != 0) {
-#pragma unroll
-                        for (int u = 0; u < UNR; ++u) e[u] -= row16_sum(sp[u] * Dl);
-                    }
-                    if constexpr (PH == 1) {
-                        // lane ci == 0 of each rating writes its residual back (the
-                        // same lanes of the same wave read it next traversal); the
-                        // other lanes write a private dummy slot: no branch
-#pragma unroll
-                        for (int u = 0; u < UNR; ++u) {
-                            T* dst = ci == 0 ? &eL[4 * (v0 + u * NW) + rr] : &eDummy[lane];
-                            *dst = e[u];
-                        }
-                    }
-                    if constexpr (PH == 2) {
-#pragma unroll
-                        for (int u = 0; u < UNR; ++u) {
-                            const uint32_t q = 4 * (v0 + u * NW) + rr;
-                            if (q < n && ci == 0) {
-                                a.E_other[pm[u]] = e[u];
-                                sq += (double)(e[u] * e[u]);
-                                if (a.row_tr) {
-                                    const T r = a.r_this[beg + q];
-                                    T pr = r - e[u];
-                                    pr = (pr < a.hi) ? pr : a.hi;
-                                    pr = (a.lo < pr) ? pr : a.lo;
-                                    trs += (double)((pr - r) * (pr - r));
-                                }
-                            }
-                        }
-                    }
-                    if constexpr (PH != 2) {
-#pragma unroll
-                        for (int u = 0; u < UNR; ++u) {
-                            g = MfmaT<T>::mfma(sc[u], g);
-                            cc += sc[u] * e[u];
-                        }
-                    }
-                };
-                for (uint32_t v0 = wr; v0 < nvec; v0 += NW * UNR) {
-                    T sp[UNR], sc[UNR], e[UNR];
-                    load(v0, sp, sc, e);
-                    proc(v0, sp, sc, e);
-                }
-            };
-            if (t == 0)
-                traverse(std::integral_constant<int, 0>{});
-            else if (t < nblk)
-                traverse(std::integral_constant<int, 1>{});
-            else
-                traverse(std::integral_constant<int, 2>{});
-            stamp(1);  // traversal
-            if (!acc) break;
-            const T old = oldn;  // loaded before this block's barriers: never sees the new value
-            const uint32_t kk = kc;
-            const bool kin = kk < K;
-            if (t + 1 < nblk) oldn = a.own[(size_t)row * Kp + kk + GB];  // padding columns are zero
-            cc += shfl_xor_t(cc, 16);
-            cc += shfl_xor_t(cc, 32);
-            __syncthreads();  // previous block's solve reads of Ls/Ps/Cs[0] are done
-            stamp(2);  // wait for the workgroup's other waves
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int r = MfmaT<T>::row(lane, j);
-                Ls[wr][r][ci] = ci < r ? g[j] : T(0);
-                if (r == ci) Ps[wr][ci] = g[j];
-            }
-            if (lane < GB) Cs[wr][lane] = cc;
-            __syncthreads();
-            for (int x = threadIdx.x; x < GB * GB; x += 64 * NW) {
-                const int r0 = x >> 4, c0 = x & 15;
-                if (c0 < r0) {
-                    T sum = Ls[0][r0][c0];
-#pragma unroll
-                    for (int w = 1; w < NW; ++w) sum += Ls[w][r0][c0];
-                    Ls[0][r0][c0] = sum;
-                }
-                if (x < GB) {
-                    T cs = Cs[0][x], ps = Ps[0][x];
-#pragma unroll
-                    for (int w = 1; w < NW; ++w) {
-                        cs += Cs[w][x];
-                        ps += Ps[w][x];
-                    }
-                    Cs[0][x] = cs;
-                    Ps[0][x] = ps;
-                }
-            }
-            __syncthreads();
-            stamp(3);  // G / c partials and their cross-wave reduction
-            if (nch > 1) {
-                // ---- cross-workgroup reduction of (G_B, c_B) over the row's chunks
-                // slab: [lower part + diagonal as a 16x16 image | c]
-                double* myslab = sy.slabs + ((size_t)(tk.slab0 + tk.chunk) * sy.nblk + t) * SL;
-                for (int x = threadIdx.x; x < SL; x += 64 * NW) {
-                    const int r0 = (x >> 4) & 15, c0 = x & 15;
-                    myslab[x] = x < GB * GB ? (double)(r0 == c0 ? Ps[0][r0] : Ls[0][r0][c0]) : (double)Cs[0][x - GB * GB];
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                uint32_t* cnt = sy.counters + (size_t)tk.cnt0 + t;
-                if (threadIdx.x == 0) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    uint32_t spins = 0;
-                    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
-                        __builtin_amdgcn_s_sleep(2);
-                        if (++spins > (1u << 26)) {  // give up: flag, never hang the device
-                            __hip_atomic_store(sy.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            break;
-                        }
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                __syncthreads();
-                const double* slab0 = sy.slabs + ((size_t)tk.slab0 * sy.nblk + t) * SL;
-                for (int x = threadIdx.x; x < SL; x += 64 * NW) {
-                    double sum = 0.0;
-                    for (uint32_t c = 0; c < nch; ++c) sum += slab0[(size_t)c * sy.nblk * SL + x];
-                    if (x < GB * GB) {
-                        const int r0 = x >> 4, c0 = x & 15;
-                        if (r0 == c0)
-                            Ps[0][r0] = (T)sum;
-                        else
-                            Ls[0][r0][c0] = (T)sum;  // upper entries stay 0 in every chunk
-                    } else {
-                        Cs[0][x - GB * GB] = (T)sum;
-                    }
-                }
-                __syncthreads();
-            }
-            stamp(4);  // split-row exchange
-            // ---- the 16 draws: every wave of every chunk (identical inputs ->
-            // identical results), or -- SW -- wave 0 alone, D handed over in LDS
-            T dlt = T(0);
-            if (!SW || wr == 0) {
-                const T P = Ps[0][ci];
-                const T sg = a.sig[kk];  // zero padded
-                const T mu = a.mu[kk];
-                const int zl = (int)((kk >> 1) & 63);
-                const T za0 = shfl_t(zA0, zl), za1 = shfl_t(zA1, zl);
-                T z = (kk & 1) ? za1 : za0;
-                if (K > 128) {
-                    const T zb0 = shfl_t(zB0, zl), zb1 = shfl_t(zB1, zl);
-                    z = kk < 128 ? z : ((kk & 1) ? zb1 : zb0);
-                }
-                const T var = kin ? T(1) / (sg + tau * P) : T(0);
-                const T sd = a.sd_is_var ? var : tsqrt(var);
-                const T A = var * sg * mu + sd * z;
-                const T Bq = var * tau;
-                dlt = gblock_solve_lds(&Ls[0][ci][0], Bq, A - old + Bq * (Cs[0][ci] + P * old));
-                if (wr == 0 && lane < GB && kin) newS[kk] = old + dlt;
-                if (SW && lane < GB) Dsh[lane] = dlt;
-            }
-            if constexpr (SW) {
-                __syncthreads();
-                dlt = Dsh[ci];
-            }
-            Dl = dlt;  // lane (r,i) holds D_i
-            stamp(5);  // solve
-        }
-        __syncthreads();
-        // ---- new own row: whole rows write it, split rows stage it (k_split_finish publishes)
-        if (tk.chunk == 0)
-            for (uint32_t k = threadIdx.x; k < K; k += 64 * NW) {
-                if (nch > 1)
-                    static_cast<T*>(sy.newown)[(size_t)tk.slab0 * Kp + k] = newS[k];
-                else
-                    a.own[(size_t)row * Kp + k] = newS[k];
-            }
-        double dsq = wave_sum(sq);
-        double dtr = wave_sum(trs);
-        if (lane == 0) {
-            red2[wr][0] = dsq;
-            red2[wr][1] = dtr;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            dsq = 0.0;
-            dtr = 0.0;
-            for (int w = 0; w < NW; ++w) {
-                dsq += red2[w][0];
-                dtr += red2[w][1];
-            }
-            if (nch > 1) {
-                sy.chunk_sq[tk.slab0 + tk.chunk] = dsq;
-                sy.chunk_tr[tk.slab0 + tk.chunk] = dtr;
-            } else {
-                if (a.row_sq) a.row_sq[row] = dsq;
-                if (a.row_tr) a.row_tr[row] = dtr;
-            }
-        }
-        __syncthreads();  // LDS (ids, residuals, newS, red2) is reused by the next task
-        stamp(6);  // task epilogue
-    }
-}
 
 // ------------------------------------------------- register-resident streaming rows
 // The default kernel for rows above the Gram-block bins: one 8-wave workgroup
@@ -1222,8 +673,14 @@ template <typename T>
 struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of slices
     static constexpr int VW = sizeof(T) == 8 ? 32 : 64;
 };
-template <typename T, int NW, int SIDE, bool DB = false>
-__global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* __restrict__ tasks, uint32_t ntask,
+// PFV > 0 (f64): LDS-DMA prefetch.  Right after block t's accumulate, each wave
+// issues global_load_lds_dwordx4 copies of the first PFV vectors (in gather-issue
+// order, GresOrder) of slice t+1 into an LDS buffer of its own; the requests stay
+// in flight through block t's cross-wave sum, split-row exchange and draws (LDS-
+// only barriers do not drain them) and the apply of block t then takes those
+// vectors from LDS instead of issuing their gathers after D_t is known.
+template <typename T, int NW, int SIDE, int PFV = 0>
+__global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict__ tasks, uint32_t ntask,
                                                            HalfArgs<T> a, SplitSync sy) {
     typedef typename MfmaT<T>::acc_t acc_t;
     constexpr int VW = GresW<T>::VW;
@@ -1239,7 +696,10 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
     __shared__ uint32_t pjL[CAP];      // partner row offset (row * Kp) per rating slot (zero row past the end)
     __shared__ uint32_t pmL[CAP];      // residual scatter target per rating
     __shared__ T eL[CAP];              // residuals (bit-identical in the 16 lanes of a rating)
-    __shared__ T rL[CAP];              // ratings (train error), when requested
+    static_assert(PFV == 0 || sizeof(T) == 8, "LDS-DMA prefetch geometry is for f64 slices");
+    static_assert(PFV % 2 == 0, "prefetched vectors go in pairs (one 1 KB LDS-DMA per pair)");
+    // [wave][vector][4 ratings x 16 columns]: a pair of vectors = one wave's 1 KB LDS-DMA
+    __shared__ T pfL[PFV > 0 ? NW : 1][PFV > 0 ? PFV : 1][4 * GB];
     // per-wave block partials: the 16x17 image of G_B (row r, column c at r*GLD + c, all 256
     // entries as the MFMA leaves them) followed by c_B; Rr: the reduced entries in the same
     // layout, except that the diagonal goes to Rr[PW + r]: the image's diagonal and upper part
@@ -1293,20 +753,15 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
             return eL[gres_slot<NW>(j * JS + lbo)];
     };
 
-    // task order (default): a queue claimed in list order, one returning atomic
-    // per task, so a split row's chunks start as soon as enough workgroups are
-    // free; tune bit 16: static rounds (workgroup w runs w, w + grid, ...)
-    const bool dyn = !(a.tune & 0x10000u);
+    // task order: a queue claimed in list order, one returning atomic per task,
+    // so a split row's chunks start as soon as enough workgroups are free
     __shared__ uint32_t qti;
-    for (uint32_t it = 0;; ++it) {
-        uint32_t ti = blockIdx.x + it * gridDim.x;
-        if (dyn) {
-            if (threadIdx.x == 0)
-                qti = __hip_atomic_fetch_add(sy.counters + sy.ncounters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            ti = qti;
-            __syncthreads();  // every thread has its ticket before thread 0 claims the next
-        }
+    for (;;) {
+        if (threadIdx.x == 0)
+            qti = __hip_atomic_fetch_add(sy.counters + sy.ncounters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t ti = qti;
+        __syncthreads();  // every thread has its ticket before thread 0 claims the next
         if (ti >= ntask) break;
         const SplitTask tk = tasks[ti];
         const uint32_t n = tk.len;
@@ -1340,7 +795,6 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 pjL[x] = (in ? a.part[beg + x] : a.zrow) * Kp;  // host checks (P+2)*Kp < 2^32
                 pmL[x] = in ? a.perm[beg + x] : 0u;
                 if (!a.e_from_dot) eL[gres_slot<NW>(x)] = in ? a.E_this[beg + x] : T(0);
-                if (a.row_tr) rL[x] = in ? a.r_this[beg + x] : T(0);
             }
             for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {  // per-half normals and old values of the row
                 zL[k] = k < K ? a.zbuf[(size_t)row * K + k] : T(0);
@@ -1431,17 +885,13 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
             };
             // the block's partials into LDS, the cross-wave sum, the split-row
             // exchange and the 16 draws: returns D_t (every lane: its column's)
-            // pf: the double-buffered kernel's gather of the next block's slices (NPF loads per
-            // wave), issued here so that it stays in flight through the block's exchange and
-            // draws.  Every barrier below is an LDS-only barrier (lds_barrier: __syncthreads()
-            // would wait vmcnt(0) and drain the prefetch); a split row's partial stores are
-            // issued before the prefetch and waited for with vmcnt(NPF).
+            // pf: a prefetch of the next block's slices (NPF vector-memory loads per wave),
+            // issued here so that it stays in flight through the block's exchange and draws.
+            // Every barrier below is an LDS-only barrier (lds_barrier: __syncthreads() would
+            // wait vmcnt(0) and drain the prefetch); a split row's partial stores are issued
+            // before the prefetch and waited for with vmcnt(NPF).
             auto finish_block = [&](const acc_t& g, T cc, uint32_t t, auto&& pf, auto npf) -> T {
                 constexpr int NPF = decltype(npf)::value;
-                // tune bit 28: the block's critical path (partials, cross-wave sum, split-row
-                // exchange, draws) at raised wave priority over a co-resident workgroup's stream
-                const bool prio = a.tune & 0x10000000u;
-                if (prio) __builtin_amdgcn_s_setprio(2);
                 T Dl;
                 if (nch == 1) pf();
                 {
@@ -1531,11 +981,9 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 if (xin) Rr[xd] = val;
                 lds_barrier();
                 stamp(4);  // cross-wave sum + split-row exchange
-                // the 16 draws: wave 0, D handed over in LDS (default), or -- tune bit 0 --
-                // every wave redundantly (identical inputs, identical results; one barrier less)
-                const bool rep = a.tune & 1u;
+                // the 16 draws: wave 0, D handed over in LDS
                 T dlt = T(0);
-                if (rep || wr == 0) {
+                if (wr == 0) {
                     const uint32_t kk = t * GB + ci;
                     const bool kin = kk < K;
                     // the block's old values, hyperparameters and normals (zero padded)
@@ -1553,22 +1001,17 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                     else
 #endif
                     dlt = gblock_solve_lds(&Rr[ci * GLD], Bq, A - old + Bq * (Cc + P * old));
-                    if (wr == 0 && lane < GB) {
+                    if (lane < GB) {
                         if (kin) newS[kk] = old + dlt;
                         Dsh[lane] = dlt;
                     }
                 }
-                if (rep) {
-                    Dl = dlt;  // the next block's barrier keeps Rr until every wave has solved
-                } else {
-                    lds_barrier();
-                    Dl = Dsh[ci];
-                }
+                lds_barrier();
+                Dl = Dsh[ci];
                 stamp(5);  // solve
-                if (prio) __builtin_amdgcn_s_setprio(0);
                 return Dl;
             };
-            if constexpr (!DB) {
+            {
                 T s[VC];
 #pragma unroll
                 for (int j = 0; j < VC; ++j) s[j] = gat(j, 0);
@@ -1595,40 +1038,6 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 }
                 // apply the last block
                 apply(s, Dl, [](int) {});
-            } else {
-                // double-buffered slices: slice t+1 is gathered into the second
-                // buffer right after block t's accumulate, so its loads are in flight
-                // through block t's exchange and draws (128 VGPRs of slices, one
-                // 8-wave workgroup per CU)
-                T sA[VC], sB[VC];
-#pragma unroll
-                for (int j = 0; j < VC; ++j) sA[j] = gat(j, 0);
-                auto dstep = [&](auto& cur, auto& prv, uint32_t t) {
-                    asm volatile("" ::: "memory");
-                    if (t > 0) apply(prv, Dl, [](int) {});  // e -= S_{t-1} D_{t-1}
-                    stamp(1);
-                    acc_t g = {T(0), T(0), T(0), T(0)};
-                    T cc = T(0);
-                    accumulate(cur, g, cc);
-                    stamp(2);
-                    // slice t+1 into the registers slice t-1 held, in flight through this block's
-                    // exchange and draws (a block without a successor issues nothing: NPF stays
-                    // an upper bound of the loads in flight)
-                    Dl = finish_block(g, cc, t, [&] {
-                        if (t + 1 < nblk) {
-#pragma unroll
-                            for (int j = 0; j < VC; ++j) prv[j] = gat(j, t + 1);
-                        }
-                    }, std::integral_constant<int, VC>{});
-                };
-                for (uint32_t t = 0; t < nblk; t += 2) {
-                    dstep(sA, sB, t);
-                    if (t + 1 < nblk) dstep(sB, sA, t + 1);
-                }
-                if (nblk & 1u)
-                    apply(sA, Dl, [](int) {});
-                else
-                    apply(sB, Dl, [](int) {});
             }
             // residuals out and the per-row sums, one rating per thread in rating
             // order (no per-vector branches)
@@ -1639,7 +1048,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 2 : 4) void k_gres(const SplitTask* _
                 a.E_other[pmL[x]] = e;
                 sq += (double)(e * e);
                 if (a.row_tr) {
-                    const T r = rL[x];
+                    const T r = a.r_this[beg + x];
                     T pr = r - e;
                     pr = (pr < a.hi) ? pr : a.hi;
                     pr = (a.lo < pr) ? pr : a.lo;
@@ -1710,239 +1119,6 @@ __global__ __launch_bounds__(64) void k_split_finish(const SplitRow* __restrict_
     }
 }
 
-// ------------------------------------------------------------------ Gram route
-constexpr int GT = 128;  // Gram tile edge (K padded to 16 inside)
-constexpr int GSUB = 32; // ratings staged per LDS sub-chunk
-
-// One block per (chunk, tile_i, tile_j) with tile_i >= tile_j.  256 threads as
-// 16x16, each owning an 8x8 sub-grid of the 128x128 tile.  slab layout per
-// chunk: [Kt*Kt G (row-major) | Kt b].
-template <typename T>
-__global__ __launch_bounds__(256) void k_gram_partial(const GramItem* __restrict__ items, HalfArgs<T> a,
-                                                       double* __restrict__ slabs, uint32_t Kt, uint32_t ntile) {
-    const uint32_t npair = ntile * (ntile + 1) / 2;
-    const uint32_t it = blockIdx.x / npair;
-    uint32_t pr = blockIdx.x % npair, ti = 0;
-    while (pr > ti) { pr -= ti + 1; ++ti; }
-    const uint32_t tj = pr;
-    const GramItem w = items[it];
-    const uint32_t K = a.K, Kp = a.Kp;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    __shared__ T As[GSUB][GT];
-    __shared__ T Bs[GSUB][GT];
-    __shared__ T es[GSUB];
-    __shared__ T ownS[256];
-    for (uint32_t k = threadIdx.x; k < 256; k += 256) ownS[k] = (k < K) ? a.own[(size_t)w.row * Kp + k] : T(0);
-    double acc[8][8];
-    double bacc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        bacc[i] = 0.0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
-    }
-    const uint32_t ci = ti * GT, cj = tj * GT;
-    for (uint32_t s0 = 0; s0 < w.len; s0 += GSUB) {
-        __syncthreads();
-        const uint32_t ns = min((uint32_t)GSUB, w.len - s0);
-        // stage: thread -> (rating r = tid / 8, 16-col segment c = tid % 8) for both tiles
-        for (uint32_t x = threadIdx.x; x < GSUB * (GT / 16); x += 256) {
-            const uint32_t r = x / (GT / 16), c = (x % (GT / 16)) * 16;
-            const bool v = r < ns;
-            const uint32_t pj = v ? a.part[w.beg + s0 + r] : 0u;
-            const T* src = a.partner + (size_t)pj * Kp;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const uint32_t ka = ci + c + q, kb = cj + c + q;
-                As[r][c + q] = (v && ka < K) ? src[ka] : T(0);
-                Bs[r][c + q] = (v && kb < K) ? src[kb] : T(0);
-            }
-        }
-        if (threadIdx.x < GSUB) {
-            const uint32_t r = threadIdx.x;
-            T ev = T(0);
-            if (r < ns) {
-                const uint32_t idx = w.beg + s0 + r;
-                if (a.e_from_dot) {
-                    const T* src = a.partner + (size_t)a.part[idx] * Kp;
-                    T d = T(0);
-                    for (uint32_t k = 0; k < K; ++k) d += src[k] * ownS[k];
-                    ev = a.r_this[idx] - d;
-                } else {
-                    ev = a.E_this[idx];
-                }
-            }
-            es[r] = ev;
-        }
-        __syncthreads();
-        for (uint32_t r = 0; r < ns; ++r) {
-            T av[8], bv[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) av[i] = As[r][ty + 16 * i];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) bv[j] = Bs[r][tx + 16 * j];
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[i][j] += (double)(av[i] * bv[j]);
-            if (tj == 0 && tx == 0) {
-                const T ev = es[r];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) bacc[i] += (double)(av[i] * ev);
-            }
-        }
-    }
-    double* slab = slabs + (size_t)w.slab * ((size_t)Kt * Kt + Kt);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t gi = ci + ty + 16 * i;
-        if (gi >= Kt) continue;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t gj = cj + tx + 16 * j;
-            if (gj < Kt) slab[(size_t)gi * Kt + gj] = acc[i][j];
-        }
-        if (tj == 0 && tx == 0) slab[(size_t)Kt * Kt + gi] = bacc[i];
-    }
-}
-
-// One block (256 threads) per heavy row: fixed-order slab reduction into
-// gsum (global, [Kt*Kt + Kt] per row), then one wave runs the recurrence.
-template <typename T, int KS>
-__global__ __launch_bounds__(256) void k_gram_solve(const GramRow* __restrict__ grows, const double* __restrict__ slabs,
-                                                     double* __restrict__ gsum, T* __restrict__ delta, HalfArgs<T> a,
-                                                     uint32_t Kt) {
-    const GramRow gr = grows[blockIdx.x];
-    const size_t SL = (size_t)Kt * Kt + Kt;
-    double* Gs = gsum + (size_t)blockIdx.x * SL;
-    const uint32_t K = a.K, Kp = a.Kp;
-    // lower triangle + diagonal + b only
-    for (size_t x = threadIdx.x; x < SL; x += 256) {
-        const uint32_t gi = (uint32_t)(x / Kt), gj = (uint32_t)(x % Kt);
-        if (x < (size_t)Kt * Kt && (gj > gi || gi >= K)) continue;
-        double s = 0.0;
-        for (uint32_t c = 0; c < gr.nslab; ++c) s += slabs[(size_t)(gr.slab0 + c) * SL + x];
-        Gs[x] = s;
-    }
-    __syncthreads();
-    __threadfence_block();
-    if (threadIdx.x >= 64) return;
-    const int lane = threadIdx.x;
-    const uint32_t row = gr.row;
-    constexpr int ZS = (KS + 1) / 2;
-    T own_r[KS], sig_r[KS], mu_r[KS], dl[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const uint32_t k = 64 * s + lane;
-        own_r[s] = k < K ? a.own[(size_t)row * Kp + k] : T(0);
-        sig_r[s] = k < K ? a.sig[k] : T(0);
-        mu_r[s] = k < K ? a.mu[k] : T(0);
-        dl[s] = T(0);
-    }
-    T z_r[ZS][2];
-#pragma unroll
-    for (int zs = 0; zs < ZS; ++zs) {
-        const uint32_t i0 = 128 * zs + 2 * lane;
-        {  // per-half normals (host reference stream or launch_philox_fill)
-            z_r[zs][0] = i0 < K ? a.zbuf[(size_t)row * K + i0] : T(0);
-            z_r[zs][1] = i0 + 1 < K ? a.zbuf[(size_t)row * K + i0 + 1] : T(0);
-
-        }
-    }
-    const double* bvec = Gs + (size_t)Kt * Kt;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        for (int kl = 0; kl < 64; ++kl) {
-            const uint32_t k = 64 * s + kl;
-            if (k >= K) break;
-            // dot = sum_{l<k} G_kl D_l
-            double part = 0.0;
-#pragma unroll
-            for (int s2 = 0; s2 < KS; ++s2) {
-                const uint32_t l = 64 * s2 + lane;
-                if (l < k) part += Gs[(size_t)k * Kt + l] * (double)dl[s2];
-            }
-            const double dot = wave_sum(part);
-            const T P = (T)Gs[(size_t)k * Kt + k];
-            const T old = readlane(own_r[s], kl);
-            const T Q = (T)(bvec[k] - dot) + P * old;
-            const T sg = readlane(sig_r[s], kl), mu = readlane(mu_r[s], kl);
-            const T z = readlane(z_r[s >> 1][kl & 1], ((s & 1) << 5) + (kl >> 1));
-            const T nw = draw_coord(P, Q, sg, mu, a.tau, z, a.sd_is_var);
-            own_r[s] = (lane == kl) ? nw : own_r[s];
-            dl[s] = (lane == kl) ? (nw - old) : dl[s];
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const uint32_t k = 64 * s + lane;
-        if (k < K) {
-            a.own[(size_t)row * Kp + k] = own_r[s];
-            delta[(size_t)blockIdx.x * Kp + k] = dl[s];
-        }
-    }
-    if (lane == 0) {
-        if (a.row_sq) a.row_sq[row] = 0.0;  // heavy rows report through chunk_sq
-        if (a.row_tr) a.row_tr[row] = 0.0;
-    }
-}
-
-// e = r - S u_new  (or e0 - S delta when no ratings array), one thread per rating.
-template <typename T>
-__global__ __launch_bounds__(256) void k_gram_update(const GramItem* __restrict__ items, HalfArgs<T> a,
-                                                      double* __restrict__ chunk_sq, double* __restrict__ chunk_tr) {
-    const GramItem w = items[blockIdx.x];
-    const uint32_t K = a.K, Kp = a.Kp;
-    __shared__ T ownS[256];
-    for (uint32_t k = threadIdx.x; k < 256; k += 256) ownS[k] = (k < K) ? a.own[(size_t)w.row * Kp + k] : T(0);
-    __syncthreads();
-    double sq = 0.0, trs = 0.0;
-    for (uint32_t x = threadIdx.x; x < w.len; x += 256) {
-        const uint32_t idx = w.beg + x;
-        const T* src = a.partner + (size_t)a.part[idx] * Kp;
-        T d = T(0);
-        for (uint32_t k = 0; k < K; ++k) d += src[k] * ownS[k];
-        const T r = a.r_this[idx];
-        const T e = r - d;
-        a.E_other[a.perm[idx]] = e;
-        sq += (double)(e * e);
-        if (chunk_tr) {
-            T pr = d;
-            pr = (pr < a.hi) ? pr : a.hi;
-            pr = (a.lo < pr) ? pr : a.lo;
-            trs += (double)((pr - r) * (pr - r));
-        }
-    }
-    __shared__ double red[4][2];
-    sq = wave_sum(sq);
-    trs = wave_sum(trs);
-    if ((threadIdx.x & 63) == 0) {
-        red[threadIdx.x >> 6][0] = sq;
-        red[threadIdx.x >> 6][1] = trs;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        chunk_sq[w.slab] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        if (chunk_tr) chunk_tr[w.slab] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-    }
-}
-
-// Heavy rows: fold chunk partial sums into the per-row arrays (chunk order).
-__global__ __launch_bounds__(64) void k_gram_rowsum(const GramRow* __restrict__ grows, uint32_t ngrows,
-                                                     const double* __restrict__ chunk_sq,
-                                                     const double* __restrict__ chunk_tr, double* __restrict__ row_sq,
-                                                     double* __restrict__ row_tr) {
-    const uint32_t h = blockIdx.x * 64 + threadIdx.x;
-    if (h >= ngrows) return;
-    const GramRow gr = grows[h];
-    double s = 0.0, t = 0.0;
-    for (uint32_t c = 0; c < gr.nslab; ++c) {
-        s += chunk_sq[gr.slab0 + c];
-        if (chunk_tr) t += chunk_tr[gr.slab0 + c];
-    }
-    if (row_sq) row_sq[gr.row] = s;
-    if (row_tr) row_tr[gr.row] = t;
-}
 
 // ------------------------------------------------------------------ residual recompute
 // One wave per row; 16 lanes per rating (lane (r = l>>4, i = l&15) covers
@@ -2339,140 +1515,72 @@ __global__ __launch_bounds__(256) void k_unpack(const T* __restrict__ recv, cons
 }  // namespace
 
 // ===================================================================== launchers
-template <typename T, int KS>
-static hipError_t launch_rows_ks(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a,
-                                 hipStream_t st) {
-    if (nrows == 0) return hipSuccess;
-    switch (kind) {
-        case RK_W2:
-            k_rows<T, 2, 1, 4, KS><<<(nrows + 3) / 4, 256, 0, st>>>(rows, nrows, a);
-            break;
-        case RK_W8:
-            k_rows<T, 8, 1, 4, KS><<<(nrows + 3) / 4, 256, 0, st>>>(rows, nrows, a);
-            break;
-        case RK_B4:
-            k_rows<T, 8, 4, 1, KS><<<nrows, 256, 0, st>>>(rows, nrows, a);
-            break;
-        case RK_B8:
-            k_rows<T, 8, 8, 1, KS><<<nrows, 512, 0, st>>>(rows, nrows, a);
-            break;
-        default:
-            return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-template <typename T>
-hipError_t launch_rows(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st) {
-    if (a.K <= 64) return launch_rows_ks<T, 1>(kind, rows, nrows, a, st);
-    if (a.K <= 128) return launch_rows_ks<T, 2>(kind, rows, nrows, a, st);
-    if (a.K <= 256) return launch_rows_ks<T, 4>(kind, rows, nrows, a, st);
-    return hipErrorInvalidValue;
-}
-
 template <typename T>
 hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st) {
     if (nrows == 0) return hipSuccess;
     if (a.K > 256) return hipErrorInvalidValue;
     // f64: 8 vectors (32 ratings) per wave; f32: 16 vectors (64 ratings) per wave
     constexpr int V = sizeof(T) == 8 ? 8 : 16;
-    const bool sw = !(a.tune & 1u);
-#define SBMF_GBLOCK(V_, NW_, RPW_, GRID_, THR_)                                                  \
-    if (sw)                                                                                      \
-        k_gblock<T, V_, NW_, RPW_, true><<<GRID_, THR_, 0, st>>>(rows, nrows, a);                \
-    else                                                                                         \
-        k_gblock<T, V_, NW_, RPW_, false><<<GRID_, THR_, 0, st>>>(rows, nrows, a);
     switch (kind) {
         case GK_W4:  // 1 wave / row, V/4 vectors, 4 rows / block
-            SBMF_GBLOCK(V / 4, 1, 4, (nrows + 3) / 4, 256);
+            k_gblock<T, V / 4, 1, 4><<<(nrows + 3) / 4, 256, 0, st>>>(rows, nrows, a);
             break;
         case GK_W16:  // 1 wave / row
-            if (sizeof(T) == 8 && !(a.tune & 8u)) {  // wide (default): 16 vectors (64 ratings), 2 waves/SIMD
-                SBMF_GBLOCK(16, 1, 2, (nrows + 1) / 2, 128);
-            } else {
-                SBMF_GBLOCK(V, 1, 4, (nrows + 3) / 4, 256);
-            }
+            if (sizeof(T) == 8 && !(a.tune & 8u))  // wide (default): 16 vectors (64 ratings), 2 waves/SIMD
+                k_gblock<T, 16, 1, 2><<<(nrows + 1) / 2, 128, 0, st>>>(rows, nrows, a);
+            else
+                k_gblock<T, V, 1, 4><<<(nrows + 3) / 4, 256, 0, st>>>(rows, nrows, a);
             break;
         case GK_B2:  // 2 waves / row
-            SBMF_GBLOCK(V, 2, 1, nrows, 128);
+            k_gblock<T, V, 2, 1><<<nrows, 128, 0, st>>>(rows, nrows, a);
             break;
         case GK_B4:  // 4 waves / row
-            SBMF_GBLOCK(V, 4, 1, nrows, 256);
+            k_gblock<T, V, 4, 1><<<nrows, 256, 0, st>>>(rows, nrows, a);
             break;
         case GK_B8:  // 8 waves / row
-            SBMF_GBLOCK(V, 8, 1, nrows, 512);
+            k_gblock<T, V, 8, 1><<<nrows, 512, 0, st>>>(rows, nrows, a);
             break;
         default:
             return hipErrorInvalidValue;
     }
-#undef SBMF_GBLOCK
     return hipGetLastError();
 }
 
-// Streaming rows: k_gres (register-resident slices, default) or, with tune
-// bit 6, the LDS-staged k_gstream.  k_gstream variants: tune bit 0 = every
-// wave solves redundantly (no extra barrier); tune bit 5 = 16-wave
-// workgroups (UNR 4), one per CU, instead of two 8-wave ones.
-// k_gres variant: tune bit 7 = 4-wave workgroups (4 per CU, 512-rating f64 tasks)
-static bool use_gres(uint32_t tune) { return !(tune & 64u); }
+// Streaming rows: k_gres.  Tune bit 7 = 4-wave workgroups (4 per CU, 512-rating
+// f64 tasks), bit 17 = 16-wave workgroups (one per CU, 2048-rating tasks),
+// default 8-wave (two per CU); sbmf.cpp picks the shape per side and row length.
 static int gres_nw(uint32_t tune) { return (tune & 128u) ? 4 : (tune & 0x20000u) ? 16 : 8; }
-static int gstream_nw(uint32_t tune) { return use_gres(tune) ? gres_nw(tune) : (tune & 32u) ? 16 : 8; }
-// k_gres variant: tune bit 25 = double-buffered slices (8 waves, one workgroup per CU)
-int gstream_wg_target(uint32_t tune) {
-    if (use_gres(tune)) return (tune & 0x2000000u) && gres_nw(tune) == 8 ? 1 : 16 / gres_nw(tune);
-    return (tune & 32u) ? 1 : 2;
-}
-template <typename T>
-static size_t gstream_dyn(uint32_t tune, uint32_t cmax) {
-    if (use_gres(tune)) return 0;
-    return (tune & 32u) ? GsGeom<16, 4>::dyn_bytes<T>(cmax) : GsGeom<8, 8>::dyn_bytes<T>(cmax);
-}
+int gstream_wg_target(uint32_t tune) { return 16 / gres_nw(tune); }
 
+// Multi-wave Gram-block rows of nw 8-vector waves (f64) / 16-vector waves (f32);
+// f64 rows of 5-8 waves run as 3-4 waves of 16 vectors (measured faster: fewer
+// waves meet at each block's barriers).
 template <typename T>
 hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st) {
     if (nrows == 0) return hipSuccess;
     constexpr int V = sizeof(T) == 8 ? 8 : 16;
-    const bool sw = !(a.tune & 1u);
-    // f64 rows of 5-8 waves of 8 vectors run as 3-4 waves of 16 vectors (measured faster:
-    // fewer waves meet at each block's barriers); tune bit 20: every multi-wave row so,
-    // bit 21: none
-    const bool wide = sizeof(T) == 8 && !(a.tune & 0x200000u) && (nw >= 5 || (a.tune & 0x100000u));
-    if (wide) {
-        const int nw2 = (nw + 1) / 2;
-#define SBMF_GB_NW16(NW_)                                                                        \
+    const bool wide = sizeof(T) == 8 && nw >= 5;
+#define SBMF_GB_NW(V_, NW_)                                                                      \
     case NW_:                                                                                    \
-        k_gblock<T, 16, NW_, 1, true><<<nrows, 64 * NW_, 0, st>>>(rows, nrows, a);               \
+        k_gblock<T, V_, NW_, 1><<<nrows, 64 * NW_, 0, st>>>(rows, nrows, a);                     \
         break;
-        switch (nw2) {
-            SBMF_GB_NW16(1)
-            SBMF_GB_NW16(2)
-            SBMF_GB_NW16(3)
-            SBMF_GB_NW16(4)
-            SBMF_GB_NW16(5)
-            SBMF_GB_NW16(6)
-            SBMF_GB_NW16(7)
-            SBMF_GB_NW16(8)
+    if (wide) {
+        switch ((nw + 1) / 2) {
+            SBMF_GB_NW(16, 3)
+            SBMF_GB_NW(16, 4)
             default:
                 return hipErrorInvalidValue;
         }
-#undef SBMF_GB_NW16
         return hipGetLastError();
     }
-#define SBMF_GB_NW(NW_)                                                                          \
-    case NW_:                                                                                    \
-        if (sw)                                                                                  \
-            k_gblock<T, V, NW_, 1, true><<<nrows, 64 * NW_, 0, st>>>(rows, nrows, a);            \
-        else                                                                                     \
-            k_gblock<T, V, NW_, 1, false><<<nrows, 64 * NW_, 0, st>>>(rows, nrows, a);           \
-        break;
     switch (nw) {
-        SBMF_GB_NW(2)
-        SBMF_GB_NW(3)
-        SBMF_GB_NW(4)
-        SBMF_GB_NW(5)
-        SBMF_GB_NW(6)
-        SBMF_GB_NW(7)
-        SBMF_GB_NW(8)
+        SBMF_GB_NW(V, 2)
+        SBMF_GB_NW(V, 3)
+        SBMF_GB_NW(V, 4)
+        SBMF_GB_NW(V, 5)
+        SBMF_GB_NW(V, 6)
+        SBMF_GB_NW(V, 7)
+        SBMF_GB_NW(V, 8)
         default:
             return hipErrorInvalidValue;
     }
@@ -2482,42 +1590,21 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
 
 template <typename T>
 static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
-    if (use_gres(tune)) {
-        if (gres_nw(tune) == 4) return side ? (const void*)k_gres<T, 4, 1> : (const void*)k_gres<T, 4, 0>;
-        if (gres_nw(tune) == 16) return side ? (const void*)k_gres<T, 16, 1> : (const void*)k_gres<T, 16, 0>;
-        if (tune & 0x2000000u) return side ? (const void*)k_gres<T, 8, 1, true> : (const void*)k_gres<T, 8, 0, true>;
-        return side ? (const void*)k_gres<T, 8, 1> : (const void*)k_gres<T, 8, 0>;
-    }
-    const bool sw = !(tune & 1u);
-    if (tune & 32u) {
-        if (side) return sw ? (const void*)k_gstream<T, 16, 4, true, 1> : (const void*)k_gstream<T, 16, 4, false, 1>;
-        return sw ? (const void*)k_gstream<T, 16, 4, true, 0> : (const void*)k_gstream<T, 16, 4, false, 0>;
-    }
-    if (side) return sw ? (const void*)k_gstream<T, 8, 8, true, 1> : (const void*)k_gstream<T, 8, 8, false, 1>;
-    return sw ? (const void*)k_gstream<T, 8, 8, true, 0> : (const void*)k_gstream<T, 8, 8, false, 0>;
+    if (gres_nw(tune) == 4) return side ? (const void*)k_gres<T, 4, 1> : (const void*)k_gres<T, 4, 0>;
+    if (gres_nw(tune) == 16) return side ? (const void*)k_gres<T, 16, 1> : (const void*)k_gres<T, 16, 0>;
+    return side ? (const void*)k_gres<T, 8, 1> : (const void*)k_gres<T, 8, 0>;
 }
 
 template <typename T>
 uint32_t gstream_cmax(uint32_t tune) {
-    hipFuncAttributes fa{};
-    int dev = 0, lds_cu = 65536;
-    if (use_gres(tune)) return 4 * gres_nw(tune) * GresW<T>::VW;  // the VGPR-resident task
-    if (hipFuncGetAttributes(&fa, gstream_fn<T>(tune)) != hipSuccess) return 1024;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
-    // gstream_wg_target workgroups per CU: static + [ids | residuals] each
-    const long per_wg = lds_cu / gstream_wg_target(tune) - (long)fa.sharedSizeBytes - 16;
-    const long fixed = (long)gstream_dyn<T>(tune, 0);  // PAD ids + PAD and SINK residuals (+ alignment)
-    const long c = (per_wg - fixed) / (long)(sizeof(uint32_t) + sizeof(T));
-    const long cap = sizeof(T) == 8 ? 4096 : 8192;
-    return (uint32_t)std::max(256L, std::min(cap, c) / 64 * 64);
+    return 4 * gres_nw(tune) * GresW<T>::VW;  // the VGPR-resident task
 }
 
 template <typename T>
 int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune) {
+    (void)cmax;
     int n = 0;
-    const size_t dyn = gstream_dyn<T>(tune, cmax);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gstream_fn<T>(tune), 64 * gstream_nw(tune), dyn) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gstream_fn<T>(tune), 64 * gres_nw(tune), 0) != hipSuccess)
         return 1;
     return n;
 }
@@ -2530,59 +1617,28 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     hipError_t err;
     err = hipMemsetAsync(sy.counters, 0, ((size_t)sy.ncounters + 1) * sizeof(uint32_t), st);  // + queue head
     if (err != hipSuccess) return err;
-    // all chunks of a split row must be resident together: the cooperative
-    // launch checks that the whole grid fits (the host sizes it to residency)
+    // Tasks are claimed from a queue in list order by running workgroups, so only
+    // the most recently claimed split row can have chunks still unclaimed, and its
+    // waiting chunks (fewer than its chunk count, far below the resident
+    // workgroups) never block the claims that complete it: an ordinary launch.
+    // Tune bit 29 (no launch overlap) keeps the cooperative launch, which checks
+    // that the whole grid fits (the host sizes it to residency).
     const SplitTask* tp = tasks;
     HalfArgs<T> ap = a;
     SplitSync syp = sy;
     void* args[] = {(void*)&tp, (void*)&ntask, (void*)&ap, (void*)&syp};
-    const size_t dyn = gstream_dyn<T>(a.tune, sy.cmax);
-    // tune bit 24 (k_gres in queue order only): an ordinary launch. A workgroup
-    // claims a task only while it runs, so only the most recently claimed row can
-    // have chunks still unclaimed, and its waiting chunks (< its chunk count,
-    // far below the resident workgroups) never block the claims that complete it.
-    const bool plain = (a.tune & 0x1000000u) && use_gres(a.tune) && !(a.tune & 0x10000u);
-    if (plain)
-        err = hipLaunchKernel(gstream_fn<T>(a.tune, a.tag == TAG_ITEMS ? 1u : 0u), dim3(std::min(grid, ntask)),
-                              dim3(64 * gstream_nw(a.tune)), args, (unsigned)dyn, st);
+    const void* fn = gstream_fn<T>(a.tune, a.tag == TAG_ITEMS ? 1u : 0u);
+    const dim3 g(std::min(grid, ntask)), b(64 * gres_nw(a.tune));
+    if (a.tune & 0x1000000u)
+        err = hipLaunchKernel(fn, g, b, args, 0, st);
     else
-        err = hipLaunchCooperativeKernel(gstream_fn<T>(a.tune, a.tag == TAG_ITEMS ? 1u : 0u), dim3(std::min(grid, ntask)),
-                                         dim3(64 * gstream_nw(a.tune)),
-                                         args, (unsigned)dyn, st);
+        err = hipLaunchCooperativeKernel(fn, g, b, args, 0, st);
     if (err != hipSuccess) return err;
     if (nsrow) {
         k_split_finish<T><<<nsrow, 64, 0, st>>>(srows, nsrow, a, sy);
         return hipGetLastError();
     }
     return hipSuccess;
-}
-
-template <typename T>
-hipError_t launch_gram(const GramItem* items, uint32_t nitems, const GramRow* grows, uint32_t ngrows, double* slabs,
-                       T* delta, double* chunk_sq, double* chunk_tr, const HalfArgs<T>& a, hipStream_t st) {
-    if (nitems == 0) return hipSuccess;
-    const uint32_t Kt = (a.K + 15) / 16 * 16;
-    const uint32_t ntile = (Kt + GT - 1) / GT;
-    const uint32_t npair = ntile * (ntile + 1) / 2;
-    k_gram_partial<T><<<nitems * npair, 256, 0, st>>>(items, a, slabs, Kt, ntile);
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return err;
-    double* gsum = slabs + (size_t)nitems * ((size_t)Kt * Kt + Kt);
-    if (a.K <= 64)
-        k_gram_solve<T, 1><<<ngrows, 256, 0, st>>>(grows, slabs, gsum, delta, a, Kt);
-    else if (a.K <= 128)
-        k_gram_solve<T, 2><<<ngrows, 256, 0, st>>>(grows, slabs, gsum, delta, a, Kt);
-    else
-        k_gram_solve<T, 4><<<ngrows, 256, 0, st>>>(grows, slabs, gsum, delta, a, Kt);
-    err = hipGetLastError();
-    if (err != hipSuccess) return err;
-    k_gram_update<T><<<nitems, 256, 0, st>>>(items, a, chunk_sq, chunk_tr);
-    err = hipGetLastError();
-    if (err != hipSuccess) return err;
-    if (a.row_sq || a.row_tr)
-        k_gram_rowsum<<<(ngrows + 63) / 64, 64, 0, st>>>(grows, ngrows, chunk_sq, a.row_tr ? chunk_tr : nullptr,
-                                                           a.row_sq, a.row_tr);
-    return hipGetLastError();
 }
 
 template <typename T>
@@ -2692,15 +1748,12 @@ hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, h
 }
 
 #define SBMF_INST(T)                                                                                                 \
-    template hipError_t launch_rows<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);            \
     template hipError_t launch_gblock<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);          \
     template hipError_t launch_gblock_nw<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);       \
     template hipError_t launch_gstream<T>(const SplitTask*, uint32_t, uint32_t, const SplitRow*, uint32_t,           \
                                           const HalfArgs<T>&, const SplitSync&, hipStream_t);                        \
     template int gstream_blocks_per_cu<T>(uint32_t, uint32_t);                                                      \
     template uint32_t gstream_cmax<T>(uint32_t);                                                                    \
-    template hipError_t launch_gram<T>(const GramItem*, uint32_t, const GramRow*, uint32_t, double*, T*, double*,   \
-                                       double*, const HalfArgs<T>&, hipStream_t);                                    \
     template hipError_t launch_resid<T>(const ResidTask*, uint32_t, const uint32_t*, uint32_t, uint32_t,              \
                                         const uint32_t*, const uint32_t*, const T*, const T*, const T*, uint32_t,     \
                                         uint32_t, T*, double*, double*, const double*, const double*, double,         \

@@ -49,7 +49,7 @@ namespace sbmf {
 
 // ------------------------------------------------------------------ host layout
 // One orientation: users (CSR by user, partner = item) or items (CSC).
-static const int NBIN = 10;  // row bins (kinds 0..9)
+static const int NBIN = GK_NUM + 1;  // row bins: Gram-block kinds GK_* (0..4), streaming rows (5)
 
 struct Side {
     uint32_t R = 0;                     // rows
@@ -59,8 +59,8 @@ struct Side {
     std::vector<double> r;              // [N] ratings
     uint32_t r0 = 0, r1 = 0;            // owned row range (multi-GPU)
     std::vector<uint64_t> bounds;       // [nranks+1] row ranges of every rank
-    // streaming rows: set 0 (k_gres, or k_gstream with tune bit 6) and, in the
-    // hybrid schedule, set 1 = the rows above the hybrid threshold (k_gstream)
+    // streaming rows (k_gres): set 0 and set 1 (f64 items: rows above 1024 ratings,
+    // on 16-wave workgroups) -- see prepare_T
     struct StreamSet {
         std::vector<SplitTask> stasks;  // tasks, in rounds of `sgrid` slots
         std::vector<SplitRow> xrows;    // rows split over several tasks
@@ -76,12 +76,10 @@ struct Side {
     // draws are the same in any launch.
     struct Stage {
         uint32_t r0 = 0, r1 = 0;
-        std::vector<uint32_t> bin_rows[NBIN];  // kinds: GK_* (0..4), KIND_STREAM (5), KIND_RK0 + RK_* (6..9)
-        std::vector<GramItem> gitems;
-        std::vector<GramRow> grows;
+        std::vector<uint32_t> bin_rows[NBIN];  // kinds: GK_* (0..4), KIND_STREAM (5)
         StreamSet ss[2];
         std::vector<std::array<uint32_t, 3>> gsub[GK_NUM];  // multi-wave bins: (waves, offset, count) sub-ranges
-        DBuf d_bins[NBIN], d_stasks[2], d_xrows[2], d_gitems, d_grows;
+        DBuf d_bins[NBIN], d_stasks[2], d_xrows[2];
         // multi-GPU residual exchange of this stage: [peer] segments of the send / receive areas
         std::vector<size_t> soff, scnt, roff, rcnt;
         size_t rbeg = 0, rend = 0;  // this stage's receive elements [rbeg, rend)
@@ -223,46 +221,25 @@ static void partition(Side& s, int nranks, int rank, uint32_t nstages) {
     }
 }
 
-static const int KIND_STREAM = GK_NUM;  // 5: streaming kernel, whole rows (row bin: every streaming row)
-static const int KIND_RK0 = GK_NUM + 1;  // 6..9
-static const int KIND_GRAM = 10;         // Gram route
+static const int KIND_STREAM = GK_NUM;  // 5: streaming kernel (row bin: every streaming row)
 
-static void build_bins(const Side& s, Side::Stage& g, uint32_t gram_thr, int row_kernel, uint32_t stream_thr,
-                       bool f64, bool wide, bool big = false) {
+static void build_bins(const Side& s, Side::Stage& g, uint32_t stream_thr, bool f64, bool wide) {
     for (auto& b : g.bin_rows) b.clear();
-    g.gitems.clear();
-    g.grows.clear();
     std::vector<uint32_t> order(g.r1 - g.r0);
     std::iota(order.begin(), order.end(), g.r0);
     auto deg = [&](uint32_t r) { return s.ptr[r + 1] - s.ptr[r]; };
     // heaviest first: blocks are dispatched roughly in index order, so the
     // longest rows start earliest (LPT)
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return deg(a) > deg(b); });
-    const uint32_t chunk = 2048;
     for (uint32_t r : order) {
         const uint32_t d = deg(r);
-        if (row_kernel == 0 && d > stream_thr && d <= gram_thr) {
+        if (d > stream_thr) {
             g.bin_rows[KIND_STREAM].push_back(r);
             continue;
         }
-        if (d > gram_thr || d > RK_MAXDEG[RK_NUM - 1]) {
-            GramRow gr{r, (uint32_t)g.gitems.size(), 0};
-            for (uint32_t o = 0; o < d; o += chunk) {
-                g.gitems.push_back(GramItem{r, s.ptr[r] + o, std::min(chunk, d - o), (uint32_t)g.gitems.size()});
-                gr.nslab++;
-            }
-            g.grows.push_back(gr);
-            continue;
-        }
-        if (row_kernel == 0) {
-            int kind = GK_W4;
-            while (d > gk_maxdeg(kind, f64, wide, big)) ++kind;
-            g.bin_rows[kind].push_back(r);
-            continue;
-        }
-        int kind = RK_W2;
-        while (d > RK_MAXDEG[kind]) ++kind;
-        g.bin_rows[KIND_RK0 + kind].push_back(r);
+        int kind = GK_W4;
+        while (d > gk_maxdeg(kind, f64, wide)) ++kind;
+        g.bin_rows[kind].push_back(r);
     }
 }
 
@@ -318,14 +295,13 @@ struct sbmf_ctx {
     DBuf d_uptr, d_upart, d_uperm, d_ur, d_vptr, d_vpart, d_vperm, d_vr;
     DBuf d_U, d_V, d_Eu, d_Ev, d_zU, d_zV, d_hyper;
     DBuf d_rowsq_u, d_rowtr_u, d_rowsq_v, d_rowtr_v;
-    DBuf d_slabs, d_delta, d_chunk_sq, d_chunk_tr;
     DBuf d_colpart, d_res, d_scratch;
 
     bool kprof = false; // SBMF_KPROF=1: streaming-kernel phase cycles printed per sweep
     int kprof_set = 0;  // SBMF_KPROF_SET: which streaming launch of a half is stamped (0: the 8-wave one)
     DBuf d_kprof;
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
-    DBuf d_xslabs, d_xtotals, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
+    DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
     size_t xset_nx = 1, xset_nr = 1;  // set 0's split chunks / rows: set 1's areas follow them
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
     DBuf d_uperm2, d_vperm2, d_uunpack, d_vunpack, d_xrecv;  // multi-GPU residual exchange
@@ -438,22 +414,13 @@ static void prepare_T(sbmf_ctx* c) {
         build_exchange(c->users, c->items, c->nranks, c->rank);  // user half -> item order
         build_exchange(c->items, c->users, c->nranks, c->rank);  // item half -> user order
     }
-    // row_kernel 0: Gram-block kernels for rows <= stream threshold, the
-    // streaming kernel above it, the Gram route only if a threshold is set.
-    // row_kernel 1: per-coordinate kernels up to 4096 ratings, Gram route above.
+    // Gram-block kernels for rows <= the stream threshold, the streaming kernel above it
     const bool f64 = sizeof(T) == 8;
-    // tune bit 22: f64 Gram-block rows up to 512 ratings (16-vector waves; not with bit 21)
-    const bool gbig = (cf.tune & 0x400000u) && !(cf.tune & 0x200000u);
-    const uint32_t gkmax = gk_maxdeg(GK_NUM - 1, f64, !(cf.tune & 8u), gbig);
-    const uint32_t sthr = std::min<uint32_t>(cf.stream_threshold ? cf.stream_threshold : gkmax, gkmax);
-    uint32_t thr;
-    if (cf.row_kernel == 0)
-        thr = cf.gram_threshold ? cf.gram_threshold : 0xffffffffu;
-    else
-        thr = cf.gram_threshold ? std::min(cf.gram_threshold, RK_MAXDEG[RK_NUM - 1]) : RK_MAXDEG[RK_NUM - 1];
     const bool wide = !(cf.tune & 8u);  // f64 rows <= 64 ratings on one wave (default)
+    const uint32_t gkmax = gk_maxdeg(GK_NUM - 1, f64, wide);
+    const uint32_t sthr = std::min<uint32_t>(cf.stream_threshold ? cf.stream_threshold : gkmax, gkmax);
     for (Side* sd : {&c->users, &c->items})
-        for (auto& g : sd->stg) build_bins(*sd, *g, thr, (int)cf.row_kernel, sthr, f64, wide, gbig);
+        for (auto& g : sd->stg) build_bins(*sd, *g, sthr, f64, wide);
     // multi-wave Gram-block bins: ceil(deg / ratings-per-wave) waves per row,
     // contiguous sub-ranges since each bin is degree-descending
     for (Side* sd : {&c->users, &c->items})
@@ -478,14 +445,6 @@ static void prepare_T(sbmf_ctx* c) {
     {
         int dev_cus = 0;
         HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, cf.device));
-        // hybrid schedule (tune bits 8/9/10): rows up to 1024 / 4096 / 128 (tests)
-        // ratings in k_gres, longer ones in k_gstream's LDS-staged tasks
-        // tune bits 29/30: rows above 2048 / 1024 ratings on 16-wave k_gres workgroups,
-        // the rest on 8-wave ones (both sides), as two launches
-        const uint32_t hyb16 = (cf.tune & 0x20000000u) ? 2048u : (cf.tune & 0x40000000u) ? 1024u : 0u;
-        const uint32_t hyb = hyb16 ? hyb16
-                                   : (cf.tune & 256u) ? 1024u : (cf.tune & 512u) ? 4096u : (cf.tune & 1024u) ? 128u : 0u;
-        const uint32_t tunes[2] = {hyb16 ? cf.tune & ~0x20000u : cf.tune, hyb16 ? cf.tune | 0x20000u : cf.tune | 64u};
         for (Side* sd : {&c->users, &c->items}) {
             // f64 item rows above 1024 ratings (75 % of the item ratings sit in rows
             // split over several tasks) on 16-wave k_gres workgroups, 2048-rating
@@ -495,19 +454,16 @@ static void prepare_T(sbmf_ctx* c) {
             // 8-wave) / 3.88 (all 16-wave) / 3.70 (this split); the user side is
             // slower with any 16-wave share (1.59 / 2.23 / 1.66 ms).  Tune bit 27,
             // or an explicit workgroup-shape or hybrid bit, keeps 8-wave items.
-            const bool item16 = sd == &c->items && sizeof(T) == 8 && !hyb &&
-                                !(cf.tune & (64u | 128u | 0x20000u | 0x2000000u | 0x8000000u));
-            const uint32_t shyb = item16 ? 1024u : hyb;
+            const bool item16 = sd == &c->items && sizeof(T) == 8 && !(cf.tune & (128u | 0x20000u | 0x8000000u));
             // f64 user rows on 4-wave k_gres workgroups (512-rating tasks, four workgroups per
             // CU): measured user streaming 1.49 -> 1.40 ms against 8-wave (r03s10); tune bit 23,
             // or an explicit workgroup-shape bit, keeps them on 8-wave workgroups
-            const bool user4 = sd == &c->users && sizeof(T) == 8 && !hyb &&
-                               !(cf.tune & (64u | 128u | 0x20000u | 0x2000000u | 0x800000u));
-            const uint32_t stunes[2] = {user4 ? tunes[0] | 128u : tunes[0], item16 ? cf.tune | 0x20000u : tunes[1]};
+            const bool user4 = sd == &c->users && sizeof(T) == 8 && !(cf.tune & (128u | 0x20000u | 0x800000u));
+            const uint32_t stunes[2] = {user4 ? cf.tune | 128u : cf.tune, cf.tune | 0x20000u};
             for (auto& gp : sd->stg) {
             std::vector<uint32_t> rows[2];
             for (uint32_t r : gp->bin_rows[KIND_STREAM])  // degree-descending
-                rows[shyb && sd->ptr[r + 1] - sd->ptr[r] > shyb ? 1 : 0].push_back(r);
+                rows[item16 && sd->ptr[r + 1] - sd->ptr[r] > 1024u ? 1 : 0].push_back(r);
             for (int k = 0; k < 2; ++k) {
                 Side::StreamSet& S = gp->ss[k];
                 S.tune = stunes[k];
@@ -576,7 +532,6 @@ static void prepare_T(sbmf_ctx* c) {
         const size_t nx = c->xset_nx + std::max<size_t>(nxk[1], 1), nr = c->xset_nr + std::max<size_t>(nrk[1], 1);
         c->d_xslabs.alloc(nx * nblk * (16 * 16 + 16) * sizeof(double));
         c->d_xcnt.alloc((nr * nblk + 2) * sizeof(uint32_t));  // + each set's task-queue head
-        c->d_xtotals.alloc(nr * nblk * (16 * 16 + 16) * sizeof(double));
         c->d_xchunk_sq.alloc(nx * sizeof(double));
         c->d_xchunk_tr.alloc(nx * sizeof(double));
         HIPCHK(hipMemsetAsync(c->d_xchunk_tr.p, 0, c->d_xchunk_tr.bytes, st));
@@ -584,21 +539,6 @@ static void prepare_T(sbmf_ctx* c) {
         c->d_xtimeout.alloc(sizeof(uint32_t));
         HIPCHK(hipMemsetAsync(c->d_xtimeout.p, 0, sizeof(uint32_t), st));
     }
-    size_t nslab = 0, ngrow = 0;  // Gram-route slabs of the largest stage (the stages run one after another)
-    for (Side* sd : {&c->users, &c->items})
-        for (auto& g : sd->stg) {
-            upload(g->d_gitems, g->gitems, st);
-            upload(g->d_grows, g->grows, st);
-            nslab = std::max(nslab, g->gitems.size());
-            ngrow = std::max(ngrow, g->grows.size());
-        }
-    const uint32_t Kt = (c->K + 15) / 16 * 16;
-    const size_t SL = (size_t)Kt * Kt + Kt;
-    c->d_slabs.alloc((nslab + ngrow) * SL * sizeof(double));
-    c->d_delta.alloc(std::max<size_t>(ngrow, 1) * c->Kp * sizeof(T));
-    c->d_chunk_sq.alloc(std::max<size_t>(nslab, 1) * sizeof(double));
-    c->d_chunk_tr.alloc(std::max<size_t>(nslab, 1) * sizeof(double));
-
     // factor tables [rows + 2][Kp]: row `rows` stays zero (the sentinel partner of
     // padded rating slots), row `rows + 1` is slack for the next-block prefetch
     // past the last column block; padding columns K..Kp-1 stay zero.
@@ -635,7 +575,7 @@ static void prepare_T(sbmf_ctx* c) {
     c->h_pre = nullptr;
     HIPCHK(hipHostMalloc((void**)&c->h_pre, c->h_res.size() * sizeof(double), hipHostMallocDefault));
     c->pre.valid = false;
-    const uint64_t big = std::max<uint64_t>({(uint64_t)c->I, (uint64_t)c->J, (uint64_t)nslab, c->su.size() / 128 + 2});
+    const uint64_t big = std::max<uint64_t>({(uint64_t)c->I, (uint64_t)c->J, c->su.size() / 128 + 2});
     c->d_scratch.alloc((big / 1024 + 16) * 2 * sizeof(double));
     // test set
     const uint64_t T_ = c->su.size();
@@ -715,10 +655,9 @@ static void prepare_T(sbmf_ctx* c) {
 }
 
 // Streaming-kernel tasks (at most `cmax` ratings each: a whole row, or the
-// equal chunks of a longer row) laid out in rounds of `gres` slots, largest
-// rows first; a split row's chunks always share a round, so its workgroups
-// are co-resident (workgroup w runs slot w of every round).  Rounds alternate
-// direction so no slot always gets the largest task.
+// equal chunks of a longer row) in one list, largest rows first, claimed in
+// order by the running workgroups of a launch of `gres` workgroups (k_gres'
+// queue); a split row's chunks are consecutive.
 static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vector<uint32_t>& rows, uint32_t gres,
                                uint32_t nblk) {
     const uint32_t cmax = S.cmax;
@@ -726,42 +665,26 @@ static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vec
     S.xrows.clear();
     S.nxchunk = 0;
     S.sgrid = 0;
-    if (rows.empty()) return;  // rows: degree-descending
-    std::vector<std::vector<SplitTask>> rounds;
-    uint32_t fill = gres;
-    // k_gres' dynamic order (default; tune bit 16: rounds): one list, heaviest rows first, no padding
-    const bool dyn = !(S.tune & 0x10000u) && !(S.tune & 64u);
-    for (uint32_t r : rows) {
+    for (uint32_t r : rows) {  // rows: degree-descending
         const uint32_t n = s.ptr[r + 1] - s.ptr[r];
         const uint32_t nch = (n + cmax - 1) / cmax;
         if (nch > gres)
             fail(SBMF_E_ARG, "row %u has %u ratings: more than %u co-resident chunks of %u", r, n, gres, cmax);
-        if (rounds.empty() || (!dyn && fill + nch > gres)) {
-            rounds.emplace_back();
-            fill = 0;
-        }
         if (nch == 1) {
-            rounds.back().push_back(SplitTask{r, s.ptr[r], n, 1, 0, 0, 0, 0});
+            S.stasks.push_back(SplitTask{r, s.ptr[r], n, 1, 0, 0, 0, 0});
         } else {
             const uint32_t slab0 = S.nxchunk;
             const uint32_t cnt0 = (uint32_t)S.xrows.size() * nblk;
             const uint32_t per = (n + nch - 1) / nch;
             for (uint32_t c = 0; c < nch; ++c) {
                 const uint32_t b = c * per, e = std::min(n, b + per);
-                rounds.back().push_back(SplitTask{r, s.ptr[r] + b, e - b, nch, c, slab0, cnt0, 0});
+                S.stasks.push_back(SplitTask{r, s.ptr[r] + b, e - b, nch, c, slab0, cnt0, 0});
             }
             S.xrows.push_back(SplitRow{r, slab0, nch, 0});
             S.nxchunk += nch;
         }
-        fill += nch;
     }
-    S.sgrid = rounds.size() > 1 ? gres : std::min<uint32_t>(gres, (uint32_t)rounds[0].size());
-    for (size_t k = 0; k < rounds.size(); ++k) {
-        std::vector<SplitTask>& rd = rounds[k];
-        if (k + 1 < rounds.size()) rd.resize(gres, SplitTask{0, 0, 0, 1, 0, 0, 0, 0});  // empty slots
-        if (k & 1) std::reverse(rd.begin(), rd.end());
-        S.stasks.insert(S.stasks.end(), rd.begin(), rd.end());
-    }
+    S.sgrid = std::min<uint32_t>(gres, (uint32_t)S.stasks.size());
 }
 
 // ------------------------------------------------------------------ one sweep
@@ -963,14 +886,6 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     HalfArgs<T> a = half_args<T>(c, users);
     hipStream_t st = c->st;
     const int sd = users ? 0 : 1;
-    if (!g.gitems.empty()) {
-        HIPCHK(hipEventRecord(c->kev(stage, sd, KIND_GRAM, 0), st));
-        HIPCHK(launch_gram<T>(g.d_gitems.as<GramItem>(), (uint32_t)g.gitems.size(), g.d_grows.as<GramRow>(),
-                              (uint32_t)g.grows.size(), c->d_slabs.as<double>(), c->d_delta.as<T>(),
-                              c->d_chunk_sq.as<double>(), a.row_tr ? c->d_chunk_tr.as<double>() : nullptr, a, st));
-        HIPCHK(hipEventRecord(c->kev(stage, sd, KIND_GRAM, 1), st));
-        c->timing.n_launch += 4;
-    }
     // Overlap (default; tune bit 29 off): the streaming launch (persistent, queue
     // order) on `st`, every other bin on `sto` beside it, so the short Gram-block
     // launches fill the CU time the streaming launch's serial phases (solve,
@@ -989,13 +904,9 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     // With two stream sets (items: rows > 1024 on 16-wave workgroups, set 1, and the
     // rest on 8-wave ones, set 0), set 1 runs on `st` and set 0 on `sto` beside it
     // (tune bit 30: one after the other), each with split-row areas of its own.
-    auto gres_q = [](const Side::StreamSet& S) { return !S.stasks.empty() && !(S.tune & (64u | 0x10000u)); };
-    const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && gres_q(g.ss[0]) && gres_q(g.ss[1]);
-    // tune bit 31 (with the overlap): the Gram-block launches enqueued before the streaming one
-    const bool gfirst = ovl && (c->cfg.tune & 0x80000000u);
-    for (int it = 0; it < NBIN + (gfirst ? 1 : 0); ++it) {
-        const int k = !gfirst ? NBIN - 1 - it : it < NBIN ? NBIN - 1 - it : KIND_STREAM;
-        if (g.bin_rows[k].empty() || (gfirst && (k == KIND_STREAM) != (it == NBIN))) continue;
+    const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && !g.ss[0].stasks.empty() && !g.ss[1].stasks.empty();
+    for (int k = NBIN - 1; k >= 0; --k) {
+        if (g.bin_rows[k].empty()) continue;
         st = ovl && k != KIND_STREAM ? c->sto : c->st;
         HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
         if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
@@ -1003,7 +914,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 HIPCHK(launch_gblock_nw<T>((int)gs[0], g.d_bins[k].as<uint32_t>() + gs[1], gs[2], a, st));
         } else if (k < GK_NUM)
             HIPCHK(launch_gblock<T>(k, g.d_bins[k].as<uint32_t>(), (uint32_t)g.bin_rows[k].size(), a, st));
-        else if (k == KIND_STREAM) {
+        else {
             for (int q = 0; q < 2; ++q) {
                 const int set = sov ? 1 - q : q;
                 const Side::StreamSet& S = g.ss[set];
@@ -1013,7 +924,6 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 SplitSync sy{};
                 sy.nblk = (c->K + 15) / 16;
                 sy.slabs = c->d_xslabs.as<double>() + ox * sy.nblk * (16 * 16 + 16);
-                sy.totals = c->d_xtotals.as<double>() + orow * sy.nblk * (16 * 16 + 16);
                 sy.counters = c->d_xcnt.as<uint32_t>() + (set ? orow * sy.nblk + 1 : 0);
                 sy.ncounters = (uint32_t)S.xrows.size() * sy.nblk;
                 sy.chunk_sq = c->d_xchunk_sq.as<double>() + ox;
@@ -1023,9 +933,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 sy.cmax = S.cmax;
                 sy.prof = c->kprof && set == c->kprof_set ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
                 HalfArgs<T> as = a;
-                // (k_gres in static rounds and k_gstream stay cooperative: their
-                // workgroups wait for the Gram-block ones to drain before they all fit)
-                as.tune = ovl && !(S.tune & (64u | 0x10000u)) ? S.tune | 0x1000000u : S.tune;
+                as.tune = ovl ? S.tune | 0x1000000u : S.tune;
                 HIPCHK(launch_gstream<T>(g.d_stasks[set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
                                          g.d_xrows[set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, ss));
             }
@@ -1034,8 +942,6 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 HIPCHK(hipStreamWaitEvent(st, c->oev[2], 0));
             }
         }
-        else
-            HIPCHK(launch_rows<T>(k - KIND_RK0, g.d_bins[k].as<uint32_t>(), (uint32_t)g.bin_rows[k].size(), a, st));
         HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
         c->timing.n_launch++;
     }
@@ -1064,10 +970,6 @@ static void fill_kernel_bytes(sbmf_ctx* c) {
                 c->timing.kern_bytes[sd][k] += alg_bytes(s, g->bin_rows[k], c->K, tsz);
                 c->timing.kern_rows[sd][k] += (uint32_t)g->bin_rows[k].size();
             }
-            std::vector<uint32_t> gr;
-            for (const GramRow& x : g->grows) gr.push_back(x.row);
-            c->timing.kern_bytes[sd][KIND_GRAM] += alg_bytes(s, gr, c->K, tsz);
-            c->timing.kern_rows[sd][KIND_GRAM] += (uint32_t)gr.size();
         }
     }
 }
@@ -1392,22 +1294,19 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                                  100.0 * (double)h[16 + 8 * sd + k] / tot);
                 std::fprintf(stderr, "\n");
             }
-            static const char* nm_gs[7] = {"stage", "traverse", "wg-wait", "reduce", "split-xchg", "solve", "epilogue"};
-            static const char* nm_gr[7] = {"stage", "apply+issue", "gather+acc", "wg-wait", "xwave+xchg", "solve", "epilogue"};
-            const char* const* nm = (cf.tune & 64u) ? nm_gs : nm_gr;
+            static const char* nm[7] = {"stage", "apply+issue", "gather+acc", "wg-wait", "xwave+xchg", "solve", "epilogue"};
             for (int sd = 0; sd < 2; ++sd) {
                 const Side& S = sd ? c->items : c->users;
                 double tot = 0;
                 for (int k = 0; k < 7; ++k) tot += (double)h[8 * sd + k];
                 if (tot == 0) continue;
-                std::fprintf(stderr, "[kprof] sweep %u %s %s (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep,
-                             (cf.tune & 64u) ? "gstream" : "gres", sd ? "items" : "users", S.stg[0]->ss[c->kprof_set].sgrid,
+                std::fprintf(stderr, "[kprof] sweep %u gres %s (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep,
+                             sd ? "items" : "users", S.stg[0]->ss[c->kprof_set].sgrid,
                              S.stg[0]->ss[c->kprof_set].stasks.size());
                 for (int k = 0; k < 7; ++k)
                     std::fprintf(stderr, " %s %.3f (%.0f%%)", nm[k], (double)h[8 * sd + k] / S.stg[0]->ss[c->kprof_set].sgrid / 1e6,
                                  100.0 * (double)h[8 * sd + k] / tot);
                 std::fprintf(stderr, "\n");
-                if (cf.tune & 64u) continue;
                 static const char* cn[3] = {"whole rows", "2-16 chunks", ">16 chunks"};
                 for (int cl = 0; cl < 3; ++cl) {
                     const unsigned long long* hc = h + 32 + 24 * sd + 8 * cl;
@@ -1418,7 +1317,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 }
             }
         }
-        if (split_timeout)  // a bounded spin in k_gstream gave up: the sweep's results are not valid
+        if (split_timeout)  // a bounded spin in k_gres gave up: the sweep's results are not valid
             fail(SBMF_E_STATE, "sweep %u: split-row hand-off timed out (workgroups not co-resident)", c->sweep);
 
         sbmf_sweep_info info{};
@@ -1440,7 +1339,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 double ms = 0.0;
                 for (uint32_t p = 0; p < c->nstages; ++p) {
                     const Side::Stage& g = *sdd.stg[p];
-                    const bool ran = k == KIND_GRAM ? !g.gitems.empty() : !g.bin_rows[k].empty();
+                    const bool ran = k < NBIN && !g.bin_rows[k].empty();
                     if (ran) ms += ev_ms(c->kev(p, sd, k, 0), c->kev(p, sd, k, 1));
                 }
                 c->timing.kern_ms[sd][k] = ms;
@@ -1542,7 +1441,6 @@ int sbmf_config_default(sbmf_config* c) {
     c->recompute_every = 1;
     c->eval_train = 0;
     c->eval_test = 1;
-    c->gram_threshold = 0;
     c->libfm_dim = 3;  // libfm.cpp:130 default -dim 1,1,8
     return SBMF_OK;
 }
@@ -1566,6 +1464,9 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     if ((cfg->method == SBMF_METHOD_LIBFM_MCMC || cfg->method == SBMF_METHOD_ALS) && cfg->precision != SBMF_F64)
         sbmf::fail(SBMF_E_ARG, "the libFM MCMC / ALS learner computes in f64 (the reference's double) only");
     if (cfg->libfm_dim > 3) sbmf::fail(SBMF_E_ARG, "bad libfm_dim (bit 0 = w0, bit 1 = w)");
+    if (cfg->gram_threshold || cfg->row_kernel)
+        sbmf::fail(SBMF_E_ARG, "gram_threshold / row_kernel are reserved (must be 0): the per-coordinate and "
+                               "full-Gram row kernels were removed (measured slower than the Gram-block kernels)");
     int ndev = 0;
     const hipError_t derr = hipGetDeviceCount(&ndev);
     if (derr != hipSuccess || ndev <= 0)

@@ -322,10 +322,8 @@ int main(int argc, char** argv) {
         cl.reg("item_offset", "libFM input: item feature id offset; default=0");
         cl.reg("device", "HIP device ordinal; default=0");
         cl.reg("recompute_every", "recompute residuals from scratch every n sweeps; default=1");
-        cl.reg("gram_threshold", "rows with more ratings take the Gram route; default: never (row_kernel 0)");
         cl.reg("stream_threshold", "rows with more ratings take the streaming kernel; default=256 (f64) / 512 (f32)");
         cl.reg("split_chunk", "streaming task size; longer rows are split over co-resident workgroups; default: LDS capacity (4096 f64 / ~8K f32)");
-        cl.reg("row_kernel", "0: MFMA Gram-block kernels (default) | 1: per-coordinate wave-reduction kernels");
         if (cl.has("help") || argc == 1) {
             cl.print_help();
             return leave(0);
@@ -399,9 +397,7 @@ int main(int argc, char** argv) {
         cfg.device = (int32_t)cl.getl("device", 0);
         if (cl.has("init_stdev")) cfg.init_stdev = cl.getd("init_stdev", 1.0);
         cfg.recompute_every = (uint32_t)cl.getl("recompute_every", 1);
-        cfg.gram_threshold = (uint32_t)cl.getl("gram_threshold", 0);
         cfg.stream_threshold = (uint32_t)cl.getl("stream_threshold", 0);
-        cfg.row_kernel = (uint32_t)cl.getl("row_kernel", 0);
         cfg.split_chunk = (uint32_t)cl.getl("split_chunk", 0);
         cfg.eval_train = vb ? 0 : 1;
         cfg.method = vb ? SBMF_METHOD_VB : als ? SBMF_METHOD_ALS : lfm ? SBMF_METHOD_LIBFM_MCMC : SBMF_METHOD_MCMC;

@@ -23,7 +23,7 @@ from . import _lib
 from ._lib import (F32, F64, METHOD_ALS, METHOD_LIBFM_MCMC, METHOD_MCMC, METHOD_VB, QUIRKS_BIAS2, QUIRKS_BIAS22, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
                    SBMF_E_COMM, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_NOMEM, SBMF_E_STATE, SBMF_OK)
 
-__all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "load_libfm_binary", "save_libfm_binary", "config_default",
+__all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "load_libfm_binary", "save_libfm_binary", "save_triples", "config_default",
            "RNG_REFERENCE", "RNG_PHILOX", "QUIRKS_FINAL", "QUIRKS_SBPMF2", "QUIRKS_NONE",
            "QUIRKS_BIAS2", "QUIRKS_BIAS22", "F64", "F32"]
 
@@ -124,6 +124,20 @@ def save_libfm_binary(stem, data, item_offset=0, num_cols=0):
         raise SBMFError(rc, lib.sbmf_loader_error().decode())
 
 
+def save_triples(path, data):
+    """Write the SBPMF triple format (u\ti\tr per line) that load_triples reads back bit for bit."""
+    u, i = _u32(data.user), _u32(data.item)
+    v = np.ascontiguousarray(data.rating, dtype=np.float64)
+    r = _lib.Ratings()
+    r.n = len(u)
+    r.user = u.ctypes.data_as(C.POINTER(C.c_uint32))
+    r.item = i.ctypes.data_as(C.POINTER(C.c_uint32))
+    r.rating = v.ctypes.data_as(C.POINTER(C.c_double))
+    rc = lib.sbmf_save_triples(str(path).encode(), C.byref(r))
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_loader_error().decode())
+
+
 def load_libfm(path, item_offset=0):
     """libFM text with one user and one item feature per line (Data.h:192-217)."""
     r = _lib.Ratings()
@@ -157,7 +171,7 @@ class FMLearnSBPMF:
                "bias22": QUIRKS_BIAS22}
 
     def __init__(self, num_factor=20, num_iter=100, seed=1, rng="ref", quirks="final", precision="f64", burnin=0,
-                 device=0, init_stdev=None, recompute_every=1, eval_train=False, gram_threshold=0, row_kernel=0,
+                 device=0, init_stdev=None, recompute_every=1, eval_train=False,
                  stream_threshold=0, split_chunk=0, tune=0, method="mcmc", vb_batches=0, average="default",
                  order="sbpmf", k0=1, k1=1, regular=(0.0, 0.0, 0.0), **hyper):
         """method "mcmc" with order "sbpmf" (default): the SBPMF Gibbs sampler;
@@ -188,8 +202,6 @@ class FMLearnSBPMF:
             self.cfg.init_stdev = init_stdev
         self.cfg.recompute_every = recompute_every
         self.cfg.eval_train = 1 if eval_train else 0
-        self.cfg.gram_threshold = gram_threshold
-        self.cfg.row_kernel = row_kernel
         self.cfg.stream_threshold = stream_threshold
         self.cfg.split_chunk = split_chunk
         self.cfg.tune = tune

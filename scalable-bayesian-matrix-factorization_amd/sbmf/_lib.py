@@ -91,6 +91,7 @@ SIGNATURES = {
     "sbmf_load_libfm": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(Ratings)]),
     "sbmf_load_libfm_binary": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(Ratings)]),
     "sbmf_save_libfm_binary": (C.c_int, [C.c_char_p, C.POINTER(Ratings), C.c_uint32, C.c_uint32]),
+    "sbmf_save_triples": (C.c_int, [C.c_char_p, C.POINTER(Ratings)]),
     "sbmf_free_ratings": (None, [C.POINTER(Ratings)]),
     "sbmf_partition_rows": (C.c_int, [_P_U32, C.c_uint32, C.c_int, C.POINTER(C.c_uint64)]),
     "sbmf_ref_stream": (C.c_int, [C.c_uint32, C.c_int, C.c_double, C.c_uint64, _P_F64]),

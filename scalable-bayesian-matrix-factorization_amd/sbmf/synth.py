@@ -109,6 +109,24 @@ def _generate(shape, seed, rank, noise, test_frac):
     return train, test, (I, J)
 
 
+def relabel_by_degree(train, test, dims):
+    """The same ratings with user and item ids renumbered by train degree,
+    heaviest first (ties by old id).  Contiguous nnz-balanced row blocks then
+    hold a few very long rows at the front and thousands of short ones at the
+    back: at 8 ranks the first item block is empty (its 256-aligned cut falls
+    at row 0), the last user block holds only Gram-block rows -- the partition
+    edge cases a shuffled id order never produces."""
+    out_tr, out_te = list(train), list(test)
+    for a, n in ((0, dims[0]), (1, dims[1])):
+        deg = np.bincount(train[a], minlength=n)
+        order = np.argsort(-deg, kind="stable")
+        new = np.empty(n, np.uint32)
+        new[order] = np.arange(n, dtype=np.uint32)
+        out_tr[a] = new[train[a]]
+        out_te[a] = new[test[a]]
+    return tuple(out_tr), tuple(out_te), dims
+
+
 def describe(train, dims):
     u, i, _ = train
     du = np.bincount(u, minlength=dims[0])

@@ -99,3 +99,15 @@ def test_bad_config_rejected_before_device():
     cfg.method = sbmf._lib.METHOD_ALS
     cfg.libfm_dim = 4
     assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG
+
+
+def test_removed_row_kernels_are_refused():
+    """row_kernel / gram_threshold are reserved since the per-coordinate and
+    full-Gram row kernels were removed (round 4): a non-zero value fails with
+    SBMF_E_ARG before any device is touched (so on CPU too)."""
+    import sbmf
+    for kw in ({"row_kernel": 1}, {"gram_threshold": 64}):
+        L = sbmf.FMLearnSBPMF(num_factor=8, **kw)
+        with pytest.raises(sbmf.SBMFError) as e:
+            L.init()
+        assert e.value.code == sbmf.SBMF_E_ARG and "reserved" in str(e.value)

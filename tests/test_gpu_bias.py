@@ -39,7 +39,7 @@ def test_biased_sampler_tracks_reference_100_sweeps(ml100k, ragged, variant, dat
     L.close()
 
 
-@pytest.mark.parametrize("kw", [{}, {"split_chunk": 64}, {"row_kernel": 1}, {"stream_threshold": 16}])
+@pytest.mark.parametrize("kw", [{}, {"split_chunk": 64}, {"stream_threshold": 16}, {"stream_threshold": 40, "split_chunk": 16}])
 def test_biases_and_factors_match_oracle_after_5_sweeps(ml100k, kw):
     """Every row path (Gram-block bins, streaming kernel, split rows,
     per-coordinate kernels) sees the bias-shifted residuals."""

@@ -154,21 +154,19 @@ def test_libfm_ranks_on_one_gpu(ml100k, ragged, tmp_path, nranks, run):
     assert _within_printed(z0["rmse"], [float(l.split("Test=")[1]) for l in lines])
 
 
-@pytest.mark.timeout(900)
-def test_config4_ml20m_k200_two_ranks_match_single_rank(tmp_path):
-    """BASELINE config 4's split (ML-20M K=200, user and item row blocks over ranks)
-    at its own shape, reference stream, one sweep: two ranks on one GPU (host comm
-    backend) end with the single-rank U, V, tau and RMSE bit for bit.  The
-    single-rank run is pinned to the oracle by test_gpu_production.py::
-    test_ml20m_k200_reference_stream_one_sweep.  At this shape both ranks own
-    split item rows (over 1024 ratings: several co-resident chunks per row) and
-    the residual exchange carries tens of MB across the cut."""
+_C4 = {}  # (relabel) -> (cache dir, data, single-rank digests): one single-rank run per id order
+
+
+def _config4(tmp_path_factory, relabel):
+    """ML-20M K=200 synthetic (ids shuffled, or renumbered heaviest-first) and the
+    single-rank chain's U / V digests, RMSE and tau after one reference-stream sweep."""
     import hashlib
-    from sbmf import partition_rows, synth
-    K, sweeps, seed = 200, 1, 1
-    cache = str(tmp_path / "synth")  # generated once here, read back by the ranks
+    from sbmf import synth
+    if relabel in _C4:
+        return _C4[relabel]
+    cache = os.environ.get("SBMF_SYNTH_CACHE") or str(tmp_path_factory.mktemp("synth"))
     old = os.environ.get("SBMF_SYNTH_CACHE")
-    os.environ["SBMF_SYNTH_CACHE"] = cache
+    os.environ["SBMF_SYNTH_CACHE"] = cache  # generated once here, read back by the ranks
     try:
         tr, te, dims = synth.generate("ml-20m")
     finally:
@@ -176,37 +174,66 @@ def test_config4_ml20m_k200_two_ranks_match_single_rank(tmp_path):
             del os.environ["SBMF_SYNTH_CACHE"]
         else:
             os.environ["SBMF_SYNTH_CACHE"] = old
+    if relabel == "degree":
+        tr, te, dims = synth.relabel_by_degree(tr, te, dims)
+    L = FMLearnSBPMF(num_factor=200, seed=1, rng="ref")
+    L.set_data(Data(*tr), Data(*te), num_users=dims[0], num_items=dims[1])
+    L.learn(sweeps=1)
+    U1, V1 = L.factors()
+    ref = {"rmse": L.rmse_trajectory, "tau": np.array([h["tau"] for h in L.history]),
+           "U": np.frombuffer(hashlib.sha256(np.ascontiguousarray(U1).tobytes()).digest(), np.uint8),
+           "V": np.frombuffer(hashlib.sha256(np.ascontiguousarray(V1).tobytes()).digest(), np.uint8)}
+    L.close()
+    del U1, V1
+    _C4[relabel] = (cache, tr, dims, ref)
+    return _C4[relabel]
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("nranks,relabel", [(2, "none"), (4, "none"), (8, "none"), (8, "degree")])
+def test_config4_ml20m_k200_ranks_match_single_rank(tmp_path, tmp_path_factory, nranks, relabel):
+    """BASELINE config 4's split (ML-20M K=200, user and item row blocks over ranks,
+    /root/reference/src/libfm/gibbs_sbpmf_final.cpp:453-535 sharded) at its own shape
+    and at 2, 4 and its own 8 ranks, reference stream, one sweep, default 4 stages per
+    half: every rank (host comm backend, all on one GPU) ends with the single-rank U, V,
+    tau and RMSE bit for bit.  The single-rank run is pinned to the oracle by
+    test_gpu_production.py::test_ml20m_k200_reference_stream_one_sweep.  With shuffled
+    ids every rank owns split item rows (over 2048 ratings: co-resident chunks) and
+    residuals of over a million ratings cross the cuts.  With ids renumbered
+    heaviest-first (relabel "degree") the 8-way cut has the edge cases a shuffled order
+    never produces: an empty item block (rank 0), item blocks of only split rows and
+    of no split row, a user block of only Gram-block rows (every row <= 256 ratings)."""
+    from sbmf import partition_rows
+    cache, tr, dims, ref = _config4(tmp_path_factory, relabel)
     I, J = dims
-    # the item row blocks of the 2-rank cut: split rows on both sides, ratings crossing it
     iptr = np.concatenate([[0], np.cumsum(np.bincount(tr[1], minlength=J))]).astype(np.uint64)
     uptr = np.concatenate([[0], np.cumsum(np.bincount(tr[0], minlength=I))]).astype(np.uint64)
-    ib, ub = partition_rows(iptr, 2), partition_rows(uptr, 2)
-    deg = np.diff(iptr)
-    for r in range(2):
-        assert deg[ib[r]:ib[r + 1]].max() > 1024, (r, ib)
-    user_rank = (tr[0] >= ub[1]).astype(np.int8)
-    item_rank = (tr[1] >= ib[1]).astype(np.int8)
+    ib, ub = partition_rows(iptr, nranks), partition_rows(uptr, nranks)
+    ideg, udeg = np.diff(iptr), np.diff(uptr)
+    imax = [int(ideg[ib[r]:ib[r + 1]].max()) if ib[r + 1] > ib[r] else 0 for r in range(nranks)]
+    umax = [int(udeg[ub[r]:ub[r + 1]].max()) if ub[r + 1] > ub[r] else 0 for r in range(nranks)]
+    user_rank = np.searchsorted(np.asarray(ub[1:-1], np.int64), tr[0].astype(np.int64), side="right")
+    item_rank = np.searchsorted(np.asarray(ib[1:-1], np.int64), tr[1].astype(np.int64), side="right")
     cross = int((user_rank != item_rank).sum())
-    assert cross > 1_000_000  # residuals of > 1 M ratings cross the cut each half (8 B each)
-    L = FMLearnSBPMF(num_factor=K, seed=seed, rng="ref")
-    L.set_data(Data(*tr), Data(*te), num_users=I, num_items=J)
-    L.learn(sweeps=sweeps)
-    U1, V1 = L.factors()
-    rmse1 = L.rmse_trajectory
-    tau1 = np.array([h["tau"] for h in L.history])
-    L.close()
-    hU = np.frombuffer(hashlib.sha256(np.ascontiguousarray(U1).tobytes()).digest(), np.uint8)
-    hV = np.frombuffer(hashlib.sha256(np.ascontiguousarray(V1).tobytes()).digest(), np.uint8)
-    del U1, V1
-    outs = _run_ranks(tmp_path, 2, [str(K), str(sweeps), str(seed), "ref", "0", "final"],
-                      env={"SBMF_WORKER_DATA": "synth:ml-20m", "SBMF_WORKER_DIGEST": "1", "SBMF_SYNTH_CACHE": cache},
-                      timeout=600)
-    for r in range(2):
+    if relabel == "none":
+        assert min(imax) > 2048, imax  # every rank owns split item rows
+        assert cross > 1_000_000
+    else:
+        assert nranks == 8
+        assert ib[1] == ib[0], list(ib)  # rank 0 owns no item row
+        assert any(m <= 2048 for m in imax[1:]), imax  # an item block without a split row
+        assert udeg[ub[-2]:ub[-1]].max() <= 256, umax  # a user block of Gram-block rows only
+        assert ideg[ib[1]:ib[2]].min() > 2048, imax  # an item block of split rows only
+    env = {"SBMF_WORKER_DATA": "synth:ml-20m", "SBMF_WORKER_DIGEST": "1", "SBMF_SYNTH_CACHE": cache}
+    if relabel == "degree":
+        env["SBMF_WORKER_RELABEL"] = "degree"
+    outs = _run_ranks(tmp_path, nranks, ["200", "1", "1", "ref", "0", "final"], env=env, timeout=900)
+    for r in range(nranks):
         z = np.load(outs[r])
-        assert np.array_equal(z["U"], hU) and np.array_equal(z["V"], hV), r
-        assert np.array_equal(z["rmse"], rmse1) and np.array_equal(z["tau"], tau1), r
-    print("config 4 split: item blocks %s, user blocks %s, %d ratings cross the cut, rmse %s" % (
-        list(ib), list(ub), cross, rmse1))
+        assert np.array_equal(z["U"], ref["U"]) and np.array_equal(z["V"], ref["V"]), r
+        assert np.array_equal(z["rmse"], ref["rmse"]) and np.array_equal(z["tau"], ref["tau"]), r
+    print("config 4 split, %d ranks (%s ids): item blocks %s (max degree %s), user blocks %s (max degree %s), "
+          "%d ratings cross the cuts, rmse %s" % (nranks, relabel, list(ib), imax, list(ub), umax, cross, ref["rmse"]))
 
 
 @pytest.mark.parametrize("stages", [2, 3])

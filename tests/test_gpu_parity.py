@@ -38,12 +38,11 @@ def test_f64_ref_stream_tracks_reference_100_sweeps(ml100k, seed):
     assert err.max() < 1e-6
 
 
-@pytest.mark.parametrize("row_kernel", [0, 1])
-def test_f64_factors_match_oracle_after_5_sweeps(ml100k, row_kernel):
-    """row_kernel 0: MFMA Gram-block kernels; 1: per-coordinate wave-reduction kernels."""
+def test_f64_factors_match_oracle_after_5_sweeps(ml100k):
+    """The MFMA Gram-block kernels (every row of ML-100k at K=20 is in a Gram-block bin or k_gres)."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=20, iters=5, seed=1)
-    L = _run(tr, te, 5, num_factor=20, seed=1, row_kernel=row_kernel)
+    L = _run(tr, te, 5, num_factor=20, seed=1)
     U, V = L.factors()
     h = L.hyper()
     assert np.abs(U - o["U"]).max() < 1e-7
@@ -70,28 +69,13 @@ def test_ragged_edge_cases_track_reference(ragged, name, quirks, seed):
     assert np.abs(L.rmse_trajectory - gold).max() < 1e-6
 
 
-@pytest.mark.parametrize("row_kernel", [0, 1])
-def test_f32_ref_stream_within_north_star_tolerance(ml100k, row_kernel):
+def test_f32_ref_stream_within_north_star_tolerance(ml100k):
     tr, te = ml100k
     gold = golden_rmse("ref_final_ml100k_k20_s1.txt")
-    L = _run(tr, te, 100, num_factor=20, seed=1, precision="f32", row_kernel=row_kernel)
+    L = _run(tr, te, 100, num_factor=20, seed=1, precision="f32")
     err = np.abs(L.rmse_trajectory - gold)
     print("f32 max |dRMSE| = %.3e" % err.max())
     assert err.max() < 1e-3
-
-
-@pytest.mark.parametrize("row_kernel", [0, 1])
-@pytest.mark.parametrize("thr", [16, 64, 300])
-def test_gram_route_matches_oracle(ml100k, thr, row_kernel):
-    """Force rows above `thr` ratings onto the Gram route (G = S^T S, exact
-    K-step recurrence) and compare with the sequential oracle."""
-    tr, te = ml100k
-    o = oracle.run(tr, te, K=20, iters=5, seed=1)
-    L = _run(tr, te, 5, num_factor=20, seed=1, gram_threshold=thr, row_kernel=row_kernel)
-    U, V = L.factors()
-    assert np.abs(U - o["U"]).max() < 1e-7
-    assert np.abs(V - o["V"]).max() < 1e-7
-    np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
 
 
 @pytest.mark.parametrize("thr", [1, 40, 200])
@@ -121,20 +105,20 @@ def test_split_rows_match_oracle(ml100k, chunk, K):
     np.testing.assert_allclose(L.rmse_trajectory, o["rmse"], rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("tune", [0, 1, 4, 8, 13, 64, 65, 96, 97, 128, 1024, 1024 + 128, 65536, 65536 + 128, 65536 + 1024, 131072,
-                                  1 << 20, 1 << 21, (1 << 20) + 4, 1 << 24, 1 << 25, 1 << 29])
+@pytest.mark.parametrize("tune", [0, 4, 8, 12, 128, 131072, 1 << 23, 1 << 24, 1 << 27, 1 << 29, 1 << 30,
+                                  (1 << 30) | (1 << 27), (1 << 29) | 128, (1 << 30) | 131072])
 def test_kernel_variants_match_oracle(ml100k, tune):
-    """Kernel variants (sbmf_config.tune): block solve by one wave that hands D
-    over in LDS (default, bit 0 clear) or by every wave of a row (bit 0 set);
-    bit 6: the LDS-staged streaming kernel k_gstream instead of k_gres, with
-    bit 5 on 16-wave workgroups (LDS geometry GsGeom<16, 4>); bit 7: k_gres on
-    4-wave workgroups (bit 17: 16-wave, 2048-rating tasks); bit 10: the hybrid schedule (k_gres up to 128 ratings,
-    k_gstream above); bit 16: k_gres tasks in static rounds instead of
-    claimed from a queue in list order; bit 20: every multi-wave f64 Gram-block
-    row on 16-vector waves (default: rows of 5-8 eight-vector waves), bit 21:
-    none; bit 24: k_gres as an ordinary (not cooperative) launch.  split_chunk 16 splits the longest rows into more than 16 chunks, 64
-    into fewer (the one-hop exchange splits each entry's chunk sum over 3
-    threads either way)."""
+    """Kernel variants (sbmf_config.tune, include/sbmf.h): bit 2 power-of-two
+    waves per Gram-block row, bit 3 two 8-vector waves for 33..64-rating f64
+    rows; k_gres workgroup shapes (bit 7: 4-wave everywhere, 17: 16-wave
+    everywhere, 23: 8-wave user rows, 27: 8-wave item rows); bit 24: k_gres as an
+    ordinary launch without the overlap; bit 29: no launch overlap (Gram-block
+    launches after the streaming one, cooperative); bit 30: the item half's two
+    streaming sets one after the other instead of side by side.  Under the
+    default overlap the two item streaming sets run concurrently on two streams
+    beside the Gram-block launches, their split rows handing partials over while
+    the other launches hold CUs: split_chunk 16 splits the longest rows into
+    more than 30 chunks (co-residency of both sets under load), 64 into fewer."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=50, iters=3, seed=4)
     for kw in ({}, {"stream_threshold": 40, "split_chunk": 64}, {"stream_threshold": 40, "split_chunk": 16}):
@@ -144,8 +128,7 @@ def test_kernel_variants_match_oracle(ml100k, tune):
         assert np.abs(V - o["V"]).max() < 1e-7
 
 
-@pytest.mark.parametrize("kw", [{}, {"stream_threshold": 40, "split_chunk": 64}, {"row_kernel": 1},
-                                {"gram_threshold": 64}])
+@pytest.mark.parametrize("kw", [{}, {"stream_threshold": 40, "split_chunk": 64}, {"stream_threshold": 16}])
 def test_multigpu_residual_mode_matches_oracle(ml100k, kw):
     """The residual form every rank uses with several GPUs (e0 = r - own.partner
     recomputed per row instead of carried), forced on one GPU (tune bit 1)."""
@@ -166,13 +149,12 @@ def test_split_rows_deterministic(ml100k):
         assert np.array_equal(x, y)
 
 
-@pytest.mark.parametrize("row_kernel", [0, 1])
-@pytest.mark.parametrize("K", [8, 50, 100, 130, 200])
-def test_factor_counts_match_oracle(ml100k, K, row_kernel):
+@pytest.mark.parametrize("K", [8, 50, 100, 130, 200, 256])
+def test_factor_counts_match_oracle(ml100k, K):
     """K spanning 1..4 register slots of 64, partial 16-wide k-blocks and padded tails."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=K, iters=3, seed=3)
-    L = _run(tr, te, 3, num_factor=K, seed=3, row_kernel=row_kernel)
+    L = _run(tr, te, 3, num_factor=K, seed=3)
     U, V = L.factors()
     assert np.abs(U - o["U"]).max() < 1e-7
     assert np.abs(V - o["V"]).max() < 1e-7

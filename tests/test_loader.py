@@ -72,3 +72,82 @@ def test_missing_file():
     with pytest.raises(sbmf.SBMFError) as e:
         sbmf.load_triples("/nonexistent/file")
     assert "unable to open" in str(e.value)
+
+
+def _oracle_triples(path):
+    import ctypes as C
+    L = oracle.lib()
+    n = C.c_uint64()
+    u, i, r = C.POINTER(C.c_uint32)(), C.POINTER(C.c_uint32)(), C.POINTER(C.c_double)()
+    assert L.oracle_load_triples(str(path).encode(), C.byref(n), C.byref(u), C.byref(i), C.byref(r)) == 0
+    m = n.value
+    return (np.ctypeslib.as_array(u, (m,)).copy(), np.ctypeslib.as_array(i, (m,)).copy(),
+            np.ctypeslib.as_array(r, (m,)).copy())
+
+
+@pytest.fixture
+def chunked(monkeypatch):
+    """Small line-aligned chunks on several threads (the ML-20M path's shape, at test size)."""
+    def set_(threads, chunk):
+        monkeypatch.setenv("SBMF_LOAD_THREADS", str(threads))
+        monkeypatch.setenv("SBMF_LOAD_CHUNK", str(chunk))
+    return set_
+
+
+def test_triples_chunked_parse_matches_sscanf(tmp_path, chunked):
+    """The threaded loader (line-aligned chunks, per-chunk arrays joined in file
+    order, m / 10^k fast path for short decimals) against the oracle's plain
+    sscanf("%u%c%u%c%lf") loop (gibbs_sbpmf_final.cpp:43), bit for bit, on lines
+    that take every path: integers, half stars, long and exponent decimals, hex,
+    signs, blanks, CRLF, garbage and a final line without newline."""
+    rng = np.random.default_rng(3)
+    forms = ["{u}\t{i}\t{r}\n", "{u} {i} {r}\n", "{u},{i},{r}\r\n", "{u}\t{i}\t{r} trailing\n", "{u}\t{i}\n",
+             "# note\n", "\n", "{u}\t {i}\t{r}\n"]
+    vals = ["4", "3.5", "0.1", "2.675", "1e0", "4.", ".5", "-3", "+2", "0x1A", "3.14159265358979323846",
+            "1.7976931348623157e308", "5e-324", "0.30000000000000004", "nan", "007", "12345678901234567890",
+            "9007199254740993", "0.1234567890123456789012345"]
+    lines = []
+    for _ in range(30000):
+        f = forms[rng.integers(len(forms))]
+        lines.append(f.format(u=int(rng.integers(0, 2 ** 32)), i=int(rng.integers(0, 30000)),
+                              r=vals[rng.integers(len(vals))]))
+    p = tmp_path / "mixed.txt"
+    p.write_text("".join(lines) + "7\t8\t2.5")
+    ou, oi, orr = _oracle_triples(p)
+    for threads, chunk in ((1, 1 << 30), (7, 1000), (16, 1)):
+        chunked(threads, chunk)
+        d = sbmf.load_triples(p)
+        assert np.array_equal(d.user, ou) and np.array_equal(d.item, oi)
+        assert np.array_equal(d.rating.view(np.uint64), orr.view(np.uint64)), threads
+
+
+def test_save_triples_round_trip(tmp_path, chunked):
+    rng = np.random.default_rng(5)
+    n = 50000
+    u = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    i = rng.integers(0, 70000, n).astype(np.uint32)
+    r = np.where(rng.random(n) < 0.5, rng.integers(1, 6, n).astype(np.float64), rng.normal(3, 2, n))
+    r[:4] = [0.5, -0.0, 1e300, 4.9e-324]
+    p = tmp_path / "out.tsv"
+    sbmf.save_triples(p, sbmf.Data(u, i, r))
+    chunked(5, 4096)
+    d = sbmf.load_triples(p)
+    assert np.array_equal(d.user, u) and np.array_equal(d.item, i)
+    assert np.array_equal(d.rating.view(np.uint64), r.view(np.uint64))
+
+
+def test_libfm_chunked_error_line(tmp_path, chunked):
+    """A bad line far into a multi-chunk file is reported with its file line number."""
+    good = "".join("%d %d:1 %d:1\n" % (1 + k % 5, k % 900, 1000 + k % 700) for k in range(5000))
+    p = tmp_path / "big.libfm"
+    p.write_text(good + "4 17:1\n" + good)
+    chunked(8, 512)
+    with pytest.raises(sbmf.SBMFError) as e:
+        sbmf.load_libfm(p)
+    assert "line 5001 of" in str(e.value)
+    q = tmp_path / "ok.libfm"
+    q.write_text(good * 3)
+    d = sbmf.load_libfm(q)
+    chunked(1, 1 << 30)
+    d1 = sbmf.load_libfm(q)
+    assert d.num_cases == 15000 and np.array_equal(d.item, d1.item) and np.array_equal(d.rating, d1.rating)

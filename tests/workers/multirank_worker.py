@@ -42,6 +42,8 @@ def main():
     if data.startswith("synth:"):  # a full-size synthetic shape (sbmf/synth.py), identical in every rank
         from sbmf import synth
         tr, te, dims = synth.generate(data[6:])
+        if os.environ.get("SBMF_WORKER_RELABEL") == "degree":
+            tr, te, dims = synth.relabel_by_degree(tr, te, dims)
     else:
         tr, te = read(os.path.join(g, data + "_train.tsv.gz")), read(os.path.join(g, data + "_test.tsv.gz"))
     if method == "vb":
