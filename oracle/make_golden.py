@@ -29,6 +29,8 @@ Fixtures written (all data, no reference source):
   ref_libfm_<...>_pred.txt.gz                 its -out file (averaged clamped test predictions)
   ref_final_ml1msynth_k20_s1.txt              gibbs_sbpmf_final on the ML-1M-shaped synthetic set
                                               (sbmf/synth.py), through its long-chain collapse
+  ref_bias2_ml1msynth_k20_s1.txt              the top-level biased gibbs_sbpmf2.cpp on that set:
+                                              stalls at the bias-only fit
 `make_golden.py vbo` / `make_golden.py libfm` / `make_golden.py collapse` regenerate only those fixtures.
 Only runnable in the build container (needs /root/reference).
 """
@@ -205,11 +207,19 @@ def collapse_golden():
         write_tsv(pth, zip(u.tolist(), i.tolist(), r.tolist()))
         paths.append(pth)
     vals = run_ref(os.path.join(HERE, "_ref", "gibbs_sbpmf_final"), paths[0], paths[1], 1)
-    shutil.rmtree(root)
     assert len(vals) == 100
     with open(os.path.join(GOLD, "ref_final_ml1msynth_k20_s1.txt"), "w") as f:
         f.write("\n".join(vals) + "\n")
     print("golden collapse", vals[0], min(vals, key=float), vals[-1])
+    # the biased sampler (top-level gibbs_sbpmf2.cpp, the paper's SBMF-P model, K=20)
+    # on the same set: it never leaves the bias-only fit (factor precisions drawn with
+    # shape alpha0 + I and the variance passed as the stdev shrink every factor to ~0)
+    vals = run_ref(os.path.join(HERE, "_ref", "gibbs_sbpmf2_bias"), paths[0], paths[1], 1)
+    shutil.rmtree(root)
+    assert len(vals) == 100
+    with open(os.path.join(GOLD, "ref_bias2_ml1msynth_k20_s1.txt"), "w") as f:
+        f.write("\n".join(vals) + "\n")
+    print("golden bias2 stall", vals[0], min(vals, key=float), vals[-1])
 
 
 def main():

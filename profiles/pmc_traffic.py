@@ -32,10 +32,7 @@ def per_dispatch(path, counter):
 
 
 def key_of(name, order_side):
-    m = re.search(r"k_gstream<(double|float), 8, 8, (true|false), (\d)>", name)
-    if m:
-        return ("item" if m.group(3) == "1" else "user") + "_half/gres_stage"
-    m = re.search(r"k_gres<(double|float), (\d+), (\d)(, (true|false))?>", name)  # the default streaming kernel
+    m = re.search(r"k_gres<(double|float), (\d+), (\d)(, \d+)?>", name)  # the streaming kernel (+ prefetch vectors)
     if m:
         return ("item" if m.group(3) == "1" else "user") + "_half/gres_stage"
     # Gram-block bins are several launches each (one per waves-per-row group, and the

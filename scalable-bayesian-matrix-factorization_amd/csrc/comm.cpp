@@ -3,6 +3,7 @@
 
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <sched.h>
 #include <sys/mman.h>
@@ -16,10 +17,55 @@
 #include <random>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 namespace sbmf {
 
 [[noreturn]] void comm_fail(const char* what, ncclResult_t r);
+
+// RCCL is loaded on first use (dlopen), not linked: a single-GPU process never
+// maps librccl.so or runs its initialisers, and a library user without RCCL can
+// still run one GPU.  The entry points are RCCL's own (rccl/rccl.h prototypes).
+namespace {
+struct Rccl {
+    decltype(&::ncclGetUniqueId) GetUniqueId;
+    decltype(&::ncclCommInitRank) CommInitRank;
+    decltype(&::ncclCommDestroy) CommDestroy;
+    decltype(&::ncclGetErrorString) GetErrorString;
+    decltype(&::ncclBroadcast) Broadcast;
+    decltype(&::ncclSend) Send;
+    decltype(&::ncclRecv) Recv;
+    decltype(&::ncclAllGather) AllGather;
+    decltype(&::ncclGroupStart) GroupStart;
+    decltype(&::ncclGroupEnd) GroupEnd;
+};
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) throw std::runtime_error(std::string("multi-GPU needs RCCL: dlopen(librccl.so.1) failed: ") + dlerror());
+        Rccl t{};
+        auto sym = [&](auto& f, const char* name) {
+            f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+            if (!f) throw std::runtime_error(std::string("RCCL symbol missing: ") + name);
+        };
+        sym(t.GetUniqueId, "ncclGetUniqueId");
+        sym(t.CommInitRank, "ncclCommInitRank");
+        sym(t.CommDestroy, "ncclCommDestroy");
+        sym(t.GetErrorString, "ncclGetErrorString");
+        sym(t.Broadcast, "ncclBroadcast");
+        sym(t.Send, "ncclSend");
+        sym(t.Recv, "ncclRecv");
+        sym(t.AllGather, "ncclAllGather");
+        sym(t.GroupStart, "ncclGroupStart");
+        sym(t.GroupEnd, "ncclGroupEnd");
+        return t;
+    }();
+    return r;
+}
+}  // namespace
+
+const char* rccl_error_string(int r) { return rccl().GetErrorString((ncclResult_t)r); }
 
 namespace {
 const char kHostMagic[8] = {'S', 'B', 'M', 'F', 'H', 'O', 'S', 'T'};
@@ -37,7 +83,7 @@ std::string host_name(const uint8_t id[128]) {
 }  // namespace
 
 Comm::~Comm() {
-    if (comm_) (void)ncclCommDestroy((ncclComm_t)comm_);
+    if (comm_) (void)rccl().CommDestroy((ncclComm_t)comm_);
     if (shm_) munmap(shm_, shm_bytes_);
 }
 
@@ -54,7 +100,7 @@ void Comm::unique_id(uint8_t id[128]) {
         return;
     }
     ncclUniqueId u;
-    ncclResult_t r = ncclGetUniqueId(&u);
+    ncclResult_t r = rccl().GetUniqueId(&u);
     if (r != ncclSuccess) comm_fail("ncclGetUniqueId", r);
     std::memcpy(id, &u, 128);
 }
@@ -98,7 +144,7 @@ void Comm::init(int nranks, int rank, const uint8_t id[128]) {
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
     ncclComm_t c;
-    ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
+    ncclResult_t r = rccl().CommInitRank(&c, nranks, u, rank);
     if (r != ncclSuccess) comm_fail("ncclCommInitRank", r);
     comm_ = c;
 }
@@ -130,16 +176,16 @@ void Comm::bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_
         return;
     }
     if (!comm_) return;
-    ncclResult_t r = ncclGroupStart();
+    ncclResult_t r = rccl().GroupStart();
     if (r != ncclSuccess) comm_fail("ncclGroupStart", r);
     for (int k = 0; k < nranks_; ++k) {
         const size_t bytes = (size_t)(bounds[k + 1] - bounds[k]) * unit_bytes;
         if (bytes == 0) continue;
         char* p = static_cast<char*>(base) + (size_t)bounds[k] * unit_bytes;
-        r = ncclBroadcast(p, p, bytes, ncclUint8, k, (ncclComm_t)comm_, st);
+        r = rccl().Broadcast(p, p, bytes, ncclUint8, k, (ncclComm_t)comm_, st);
         if (r != ncclSuccess) comm_fail("ncclBroadcast", r);
     }
-    r = ncclGroupEnd();
+    r = rccl().GroupEnd();
     if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
 }
 
@@ -165,16 +211,16 @@ void Comm::bcast_blocks(void* base, size_t unit_bytes, const std::vector<uint64_
         return;
     }
     if (!comm_) return;
-    ncclResult_t r = ncclGroupStart();
+    ncclResult_t r = rccl().GroupStart();
     if (r != ncclSuccess) comm_fail("ncclGroupStart", r);
     for (int k = 0; k < nranks_; ++k) {
         const size_t bytes = (size_t)(ends[k] - starts[k]) * unit_bytes;
         if (bytes == 0) continue;
         char* p = dev + (size_t)starts[k] * unit_bytes;
-        r = ncclBroadcast(p, p, bytes, ncclUint8, k, (ncclComm_t)comm_, st);
+        r = rccl().Broadcast(p, p, bytes, ncclUint8, k, (ncclComm_t)comm_, st);
         if (r != ncclSuccess) comm_fail("ncclBroadcast", r);
     }
-    r = ncclGroupEnd();
+    r = rccl().GroupEnd();
     if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
 }
 
@@ -212,31 +258,31 @@ void Comm::alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const
         return;
     }
     if (!comm_) return;
-    ncclResult_t r = ncclGroupStart();
+    ncclResult_t r = rccl().GroupStart();
     if (r != ncclSuccess) comm_fail("ncclGroupStart", r);
     for (int k = 0; k < nranks_; ++k) {
         if (k == rank_) continue;
         if (scnt[k]) {
-            r = ncclSend(static_cast<const char*>(sendbuf) + soff[k], scnt[k], ncclUint8, k, (ncclComm_t)comm_, st);
+            r = rccl().Send(static_cast<const char*>(sendbuf) + soff[k], scnt[k], ncclUint8, k, (ncclComm_t)comm_, st);
             if (r != ncclSuccess) comm_fail("ncclSend", r);
         }
         if (rcnt[k]) {
-            r = ncclRecv(static_cast<char*>(recvbuf) + roff[k], rcnt[k], ncclUint8, k, (ncclComm_t)comm_, st);
+            r = rccl().Recv(static_cast<char*>(recvbuf) + roff[k], rcnt[k], ncclUint8, k, (ncclComm_t)comm_, st);
             if (r != ncclSuccess) comm_fail("ncclRecv", r);
         }
     }
-    r = ncclGroupEnd();
+    r = rccl().GroupEnd();
     if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
 }
 
 void Comm::group_begin() {
     if (!comm_) return;
-    const ncclResult_t r = ncclGroupStart();
+    const ncclResult_t r = rccl().GroupStart();
     if (r != ncclSuccess) comm_fail("ncclGroupStart", r);
 }
 void Comm::group_end() {
     if (!comm_) return;
-    const ncclResult_t r = ncclGroupEnd();
+    const ncclResult_t r = rccl().GroupEnd();
     if (r != ncclSuccess) comm_fail("ncclGroupEnd", r);
 }
 
@@ -259,7 +305,7 @@ void Comm::allgather(const void* sendbuf, size_t bytes, void* recvbuf, hipStream
         return;
     }
     if (!comm_ || !bytes) return;
-    ncclResult_t r = ncclAllGather(sendbuf, recvbuf, bytes, ncclUint8, (ncclComm_t)comm_, st);
+    ncclResult_t r = rccl().AllGather(sendbuf, recvbuf, bytes, ncclUint8, (ncclComm_t)comm_, st);
     if (r != ncclSuccess) comm_fail("ncclAllGather", r);
 }
 

@@ -11,6 +11,9 @@
 
 namespace sbmf {
 
+// RCCL's message for an ncclResult_t (RCCL is dlopen'ed on first multi-GPU use).
+const char* rccl_error_string(int r);
+
 // Test-only alternative (SBMF_COMM=host when the id is made): the same
 // exchange through a POSIX shared-memory segment and a process-shared
 // barrier, so the multi-rank sampler can run as several processes on ONE GPU

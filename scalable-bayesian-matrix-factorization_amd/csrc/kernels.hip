@@ -220,11 +220,26 @@ __device__ __forceinline__ void lds_barrier() {
 
 // s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory operations are done
 // (the counter holds at most 63: a larger N waits for the oldest N - 63 of them too)
+// One wave's 1 KB LDS-DMA: lane l copies 16 bytes from its own global address src
+// to lds + 16 l (global_load_lds_dwordx4; lds wave-uniform).  Completion is
+// counted by vmcnt.  (The builtin exists only in the device pass; the host pass,
+// which only emits the kernel's launch stub, must not instantiate it.)
+__device__ __forceinline__ void lds_dma16(const void* src, void* lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+#endif
+}
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0, "vmcnt range");
     if constexpr (N >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
     else if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
@@ -669,6 +684,13 @@ struct GresOrder {
     static constexpr Arr arr = make();
     static constexpr const int* v = arr.a;
 };
+// position of vector j among the first NP vectors of GresOrder<VC> (-1: not among them)
+template <int VC, int NP>
+__host__ __device__ constexpr int gres_pidx(int j) {
+    for (int i = 0; i < NP; ++i)
+        if (GresOrder<VC>::v[i] == j) return i;
+    return -1;
+}
 template <typename T>
 struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of slices
     static constexpr int VW = sizeof(T) == 8 ? 32 : 64;
@@ -824,9 +846,39 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             // max(1, VC/16) vectors and updates their residuals in LDS -- 2 (VC - 1)
             // DPP moves instead of 4 VC row-sum steps.  The registers each level
             // frees take their next slices at once (next(j) = the gather of vector j).
+            // LDS-DMA prefetch (PFV > 0): the first NP vectors in gather-issue order
+            // (GresOrder), whose next-block slices a wave copies into pfL[wave]
+            // during a block's exchange and draws, in pairs (one 1 KB
+            // global_load_lds_dwordx4 per pair: lane l moves 16 bytes of rating
+            // (l >> 3) & 3 of the pair's vector l >> 5, so pfL holds [vector][rating][16])
+            constexpr int NP = (PFV < VC ? PFV : VC) / 2 * 2;
+            auto pidx = [](int j) { return gres_pidx<VC, NP>(j); };
+            auto pf_issue = [&](uint32_t t1) {
+                if constexpr (NP > 0) {
+                    const int h = lane >> 5, rq = (lane >> 3) & 3, pc = lane & 7;
+#pragma unroll
+                    for (int p = 0; p < NP / 2; ++p) {
+                        const int jv = h ? GresOrder<VC>::v[2 * p + 1] : GresOrder<VC>::v[2 * p];
+                        const uint32_t slot = 4 * wr_s + rq + jv * JS;
+                        const T* src = a.partner + (size_t)pjL[slot] + t1 * GB + 2 * pc;
+                        lds_dma16(src, &pfL[wr_s][2 * p][0]);
+                    }
+                }
+            };
+            // vector j of slice t: from pfL when it was prefetched, else gathered
+            auto nxt = [&](auto& s, int j, uint32_t t) {
+                const int i = pidx(j);
+                if (NP > 0 && i >= 0)
+                    s[j] = pfL[wr_s][i][rr * GB + ci];
+                else
+                    s[j] = gat(j, t);
+            };
             auto apply = [&](auto& s, T D, auto&& next) {
                 // VC rounded up to a power of two (VP); vectors VC..VP-1 are zero
                 constexpr int VP = VC <= 8 ? 8 : VC <= 16 ? 16 : VC <= 32 ? 32 : VC <= 64 ? 64 : 128;
+                // the prefetched slices have landed in LDS (this wave's own LDS-DMA: its vmcnt
+                // covers them; nothing else of this wave is in flight here)
+                if constexpr (NP > 0) wait_vmcnt<0>();
 #pragma unroll
                 for (int j = 0; j < VC; ++j) s[j] = s[j] * D;
                 bfly_level<0x128, VP>(s, ci & 8);
@@ -1027,14 +1079,18 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                             for (int j = 0; j < VC; ++j) s[j] = gat(j, t);
                         } else
 #endif
-                        apply(s, Dl, [&](int j) { s[j] = gat(j, t); });
+                        apply(s, Dl, [&](int j) { nxt(s, j, t); });
                     }
                     stamp(1);  // apply + gather issue
                     acc_t g = {T(0), T(0), T(0), T(0)};
                     T cc = T(0);
                     accumulate(s, g, cc);
                     stamp(2);  // gather wait + accumulate
-                    Dl = finish_block(g, cc, t, [] {}, std::integral_constant<int, 0>{});
+                    // LDS-DMA of slice t+1's first NP vectors, in flight through this block's
+                    // exchange and draws (the last block prefetches nothing)
+                    Dl = finish_block(g, cc, t, [&] {
+                        if (t + 1 < nblk) pf_issue(t + 1);
+                    }, std::integral_constant<int, NP / 2>{});
                 }
                 // apply the last block
                 apply(s, Dl, [](int) {});
@@ -1588,11 +1644,22 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
     return hipGetLastError();
 }
 
+// LDS-DMA prefetch vectors per wave (tune bit 25, f64): as many as the LDS left beside the
+// workgroups a CU holds (16-wave: one, 8-wave: two, 4-wave: four per CU) takes
+constexpr int gres_pfv(int nw) { return nw == 16 ? 8 : nw == 8 ? 4 : 2; }
+template <typename T, int NW>
+static const void* gres_fn(uint32_t tune, uint32_t side) {
+    if (sizeof(T) == 8 && (tune & 0x2000000u)) {
+        constexpr int P = sizeof(T) == 8 ? gres_pfv(NW) : 0;
+        return side ? (const void*)k_gres<T, NW, 1, P> : (const void*)k_gres<T, NW, 0, P>;
+    }
+    return side ? (const void*)k_gres<T, NW, 1> : (const void*)k_gres<T, NW, 0>;
+}
 template <typename T>
 static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
-    if (gres_nw(tune) == 4) return side ? (const void*)k_gres<T, 4, 1> : (const void*)k_gres<T, 4, 0>;
-    if (gres_nw(tune) == 16) return side ? (const void*)k_gres<T, 16, 1> : (const void*)k_gres<T, 16, 0>;
-    return side ? (const void*)k_gres<T, 8, 1> : (const void*)k_gres<T, 8, 0>;
+    if (gres_nw(tune) == 4) return gres_fn<T, 4>(tune, side);
+    if (gres_nw(tune) == 16) return gres_fn<T, 16>(tune, side);
+    return gres_fn<T, 8>(tune, side);
 }
 
 template <typename T>

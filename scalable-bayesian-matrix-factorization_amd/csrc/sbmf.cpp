@@ -44,7 +44,7 @@ struct sbmf_ctx;
 namespace sbmf {
 
 [[noreturn]] void comm_fail(const char* what, ncclResult_t r) {
-    fail(SBMF_E_COMM, "%s failed: %s", what, ncclGetErrorString(r));
+    fail(SBMF_E_COMM, "%s failed: %s", what, rccl_error_string((int)r));
 }
 
 // ------------------------------------------------------------------ host layout

@@ -55,3 +55,24 @@ def test_gpu_chain_collapses_with_the_reference(recompute_every):
     assert np.all(np.isnan(tau[n_ref + 2:]))
     # after the collapse every prediction is the clamp bound: the running mean drifts the same way
     assert abs(rmse[-1] - gold[-1]) < 1e-3
+
+
+@pytest.mark.timeout(600)
+def test_gpu_biased_chain_stalls_with_the_reference():
+    """The biased sampler (quirks bias2: top-level gibbs_sbpmf2.cpp:335-637) on the
+    ML-1M-shaped set, K=20, seed 1, reference stream: the compiled reference's 100
+    running-mean test RMSEs (tests/golden/ref_bias2_ml1msynth_k20_s1.txt, pinned to
+    the oracle by test_oracle_golden.py) stay at the bias-only fit (> 1.05, never
+    0.85); the GPU chain follows them to 1e-6 with the same shrunk factors."""
+    tr, te, dims = synth.generate("ml-1m")
+    gold = golden_rmse("ref_bias2_ml1msynth_k20_s1.txt")
+    L = FMLearnSBPMF(num_factor=20, seed=1, rng="ref", quirks="bias2")
+    L.set_data(Data(*tr), Data(*te))
+    L.learn(sweeps=100)
+    rmse = L.rmse_trajectory
+    U, V = L.factors()
+    L.close()
+    print("bias2 stall: max|dRMSE| %.2e, final %.6f (ref %.6f), mean|U| %.2e" % (
+        np.abs(rmse - gold).max(), rmse[-1], gold[-1], np.abs(U).mean()))
+    assert np.abs(rmse - gold).max() < 1e-6
+    assert rmse.min() > 1.05 and np.abs(U).mean() < 0.01 and np.abs(V).mean() < 0.01
