@@ -31,7 +31,9 @@ Fixtures written (all data, no reference source):
                                               (sbmf/synth.py), through its long-chain collapse
   ref_bias2_ml1msynth_k20_s1.txt              the top-level biased gibbs_sbpmf2.cpp on that set:
                                               stalls at the bias-only fit
-`make_golden.py vbo` / `make_golden.py libfm` / `make_golden.py collapse` regenerate only those fixtures.
+  ref_libfm_rlog_header_k20_g2.txt            bin/libFM's -rlog header (MCMC, K=20, two -meta groups)
+`make_golden.py vbo` / `make_golden.py libfm` / `make_golden.py rlog` / `make_golden.py collapse` regenerate
+only those fixtures.
 Only runnable in the build container (needs /root/reference).
 """
 import gzip
@@ -189,6 +191,34 @@ def libfm_goldens():
     shutil.rmtree(root)
 
 
+def rlog_golden():
+    """bin/libFM's -rlog header for an MCMC run with two attribute groups (users,
+    items: the SBPMF sampler's two hyperprior groups) at K=20: the compiled
+    libfm.cpp (fm_learn.h:82-127 then fm_learn_mcmc.h:1121-1148 register the
+    fields), run on ML-100k with a -meta file putting every user attribute in
+    group 0 and every item attribute in group 1."""
+    root = "/tmp/sbmf_rlog_%d" % os.getpid()
+    os.makedirs(root, exist_ok=True)
+    tr, te = os.path.join(GOLD, "ml100k_train.tsv.gz"), os.path.join(GOLD, "ml100k_test.tsv.gz")
+    I = max_user(tr, te) + 1
+    write_libfm(tr, os.path.join(root, "train.libfm"), I)
+    write_libfm(te, os.path.join(root, "test.libfm"), I)
+    mx = 0
+    for f in ("train.libfm", "test.libfm"):
+        for line in open(os.path.join(root, f)):
+            mx = max([mx] + [int(t.split(":")[0]) for t in line.split()[1:]])
+    with open(os.path.join(root, "meta.txt"), "w") as f:  # every attribute incl. libFM's +1 phantom one
+        f.write("".join("0\n" if a < I else "1\n" for a in range(mx + 2)))
+    subprocess.run([os.path.join(HERE, "_ref", "libFM"), "-task", "r", "-train", "train.libfm", "-test", "test.libfm",
+                    "-dim", "1,1,20", "-iter", "2", "-method", "mcmc", "-meta", "meta.txt", "-rlog", "rlog.tsv"],
+                   cwd=root, env=dict(os.environ, LIBFM_PIN_TIME="1"), capture_output=True, text=True, check=True)
+    head = open(os.path.join(root, "rlog.tsv")).readline().rstrip("\n")
+    shutil.rmtree(root)
+    with open(os.path.join(GOLD, "ref_libfm_rlog_header_k20_g2.txt"), "w") as f:
+        f.write(head + "\n")
+    print("golden rlog header", len(head.split("\t")), "fields")
+
+
 def collapse_golden():
     """The reference sampler through its long-chain collapse: gibbs_sbpmf_final
     (K=20, seed 1, 100 sweeps) on the ML-1M-shaped synthetic set of
@@ -232,6 +262,10 @@ def main():
         return 0
     if sys.argv[1:] == ["libfm"]:
         libfm_goldens()
+        rlog_golden()
+        return 0
+    if sys.argv[1:] == ["rlog"]:
+        rlog_golden()
         return 0
     os.makedirs(GOLD, exist_ok=True)
     ml_train = os.path.join(REF, "data", "m100k", "train_sbpmf")
@@ -265,6 +299,7 @@ def main():
             f.write(out)
     vbo_goldens()
     libfm_goldens()
+    rlog_golden()
     collapse_golden()
     return 0
 

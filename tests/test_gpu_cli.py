@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import golden_rmse
+from conftest import REPO, golden_rmse
 from sbmf._lib import CLI_PATH
 
 pytestmark = pytest.mark.gpu
@@ -82,9 +82,13 @@ def test_cli_mcmc_k20_matches_reference_golden(tmp_path, ml100k):
     assert vals.shape == gold.shape
     assert _close6(vals, gold)
     assert np.abs(_rlog(tmp_path / "rlog.tsv") - gold).max() < 1e-6
-    # libFM's -rlog columns first (the SBPMF sampler's two hyperprior groups), ours after them
+    # libFM's -rlog columns first (the SBPMF sampler's two hyperprior groups), ours after them:
+    # the header bin/libFM itself writes for two -meta groups at K=20 (oracle/make_golden.py rlog)
     head = (tmp_path / "rlog.tsv").read_text().splitlines()[0].split("\t")
-    assert head[:len(_libfm_rlog_header(20, groups=2))] == _libfm_rlog_header(20, groups=2)
+    with open(os.path.join(REPO, "tests", "golden", "ref_libfm_rlog_header_k20_g2.txt")) as f:
+        libfm_head = f.read().rstrip("\n").split("\t")
+    assert libfm_head == _libfm_rlog_header(20, groups=2)
+    assert head[:len(libfm_head)] == libfm_head
     assert _close6(_rlog(tmp_path / "rlog.tsv", "rmse"), gold)
     assert _close6(_rlog(tmp_path / "rlog.tsv", "rmse_mcmc_all"), gold)
     tau = _rlog(tmp_path / "rlog.tsv", "sbmf_tau")
