@@ -16,6 +16,14 @@ for t in 0 33554432; do
     python3 bench.py --steps 3 --warmup 1 --no-cpu --no-ttr --no-f32 --no-load --tune $t > $O/r04s2_kprof1_t$t.json 2> $O/r04s2_kprof1_t$t.log || { echo "kprof1 $t rc $?"; exit 1; }
 done
 echo kprof ok
+# CHECK=1 builds (every row-kernel index checked; a violation is printed and redirected, not
+# faulted): the default kernels, then round 3's two-step solve (SBMF_SOLVE2) that faulted in r03s3
+for b in build_check build_check_v2; do
+  SBMF_LIB=$R/scalable-bayesian-matrix-factorization_amd/$b/libsbmf.so timeout -k 10 200 \
+    python3 bench.py --steps 5 --warmup 2 --no-cpu --no-ttr --no-f32 --no-load > $O/r04s2_$b.json 2> $O/r04s2_$b.err \
+    || { echo "$b rc $?"; tail -20 $O/r04s2_$b.err; exit 1; }
+  echo "$b: $(grep -c 'sbmf check' $O/r04s2_$b.err || true) index violations"
+done
 zcat tests/golden/ml100k_train.tsv.gz > /tmp/ml100k_train.tsv && zcat tests/golden/ml100k_test.tsv.gz > /tmp/ml100k_test.tsv
 cd /tmp && export TMPDIR=/tmp
 rc=0

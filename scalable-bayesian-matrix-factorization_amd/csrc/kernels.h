@@ -33,6 +33,11 @@ struct HalfArgs {
     int e_from_dot;        // 1: e0 = r - own.partner (no gather; multi-GPU)
     uint32_t tune;         // kernel variant bits (sbmf_config.tune)
     unsigned long long* prof;  // [8] phase cycles of wave 0 (SBMF_KPROF diagnostics) or null
+    // extents of the arrays above, checked on every index by CHECK=1 builds (SBMF_CHECK_BUILD)
+    uint64_t lim_partner;  // elements of `partner` ((P+2) Kp)
+    uint64_t lim_other;    // elements of E_other (N + multi-GPU send area)
+    uint64_t lim_this;     // N (part, perm, E_this, r_this)
+    uint32_t lim_rows;     // R (own rows; zbuf rows)
 };
 
 // Gram-block (MFMA) row kernels.  Max ratings per row for each kind: f64
@@ -79,6 +84,8 @@ struct SplitSync {
     uint32_t* timeout;   // set to 1 if a spin gave up
     uint32_t cmax;       // ratings per task
     unsigned long long* prof;  // [8] phase cycles of wave 0 (SBMF_KPROF diagnostics) or null
+    uint64_t lim_slab;   // doubles of `slabs` (CHECK=1 builds)
+    uint32_t lim_chunk;  // entries of chunk_sq / chunk_tr (and rows of newown)
 };
 // Task capacity (ratings) of the streaming kernel k_gres for the variant `tune`:
 // 4 * waves * vectors-per-wave, the partner slices held in VGPRs.

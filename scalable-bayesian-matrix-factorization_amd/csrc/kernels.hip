@@ -220,6 +220,22 @@ __device__ __forceinline__ void lds_barrier() {
 
 // s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory operations are done
 // (the counter holds at most 63: a larger N waits for the oldest N - 63 of them too)
+// CHECK=1 builds: CHK(i, extent) validates a global index; a violation is printed
+// (the first 32 over the process) and the access goes to element 0 instead, so a bad
+// index is reported without faulting the device.  Other builds: CHK(i, n) is i.
+#ifdef SBMF_CHECK_BUILD
+__device__ unsigned int g_chk_count = 0;
+__device__ __noinline__ uint64_t chk_fail(uint64_t i, uint64_t lim, int line) {
+    if (atomicAdd(&g_chk_count, 1u) < 32u)
+        printf("[sbmf check] kernels.hip:%d index %llu >= extent %llu (block %u thread %u)\n", line,
+               (unsigned long long)i, (unsigned long long)lim, blockIdx.x, threadIdx.x);
+    return 0;
+}
+#define CHK(i, lim) ((uint64_t)(i) < (uint64_t)(lim) ? (uint64_t)(i) : chk_fail((uint64_t)(i), (uint64_t)(lim), __LINE__))
+#else
+#define CHK(i, lim) (i)
+#endif
+
 // One wave's 1 KB LDS-DMA: lane l copies 16 bytes from its own global address src
 // to lds + 16 l (global_load_lds_dwordx4; lds wave-uniform).  Completion is
 // counted by vmcnt.  (The builtin exists only in the device pass; the host pass,
@@ -269,14 +285,34 @@ __device__ __forceinline__ T gblock_solve(const T (&H)[GB], T gam) {
 
 // Same recurrence with the H row read from LDS (row `hrow`, scaled by Bq)
 // step by step, for kernels without the registers to hold it.
+// SOLVE2=1 builds (diagnostic, Makefile EXTRA=-DSBMF_SOLVE2): round 3's rejected
+// two-step form -- every lane forms d_{j+1} = gamma_{j+1} - H[j+1][j] d_j itself,
+// one readlane hop per pair of draws -- kept to re-run the fault it was dropped for
+// (CHECK=1 builds).
 template <typename T>
 __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, T gam) {
+#ifdef SBMF_SOLVE2
+    T H[GB];
+#pragma unroll
+    for (int j = 0; j < GB; ++j) H[j] = Bq * hrow[j];
+#pragma unroll
+    for (int j = 0; j < GB; j += 2) {
+        const T h10 = readlane(H[j], j + 1);
+        const T dj = readlane(gam, j);
+        const T g1 = readlane(gam, j + 1);
+        const T dj1 = g1 - h10 * dj;
+        gam -= H[j] * dj;
+        gam -= H[j + 1] * dj1;
+    }
+    return gam;
+#else
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
         const T dj = readlane(gam, j);
         gam -= (Bq * hrow[j]) * dj;
     }
     return gam;
+#endif
 }
 
 // Occupancy hints (waves/SIMD): 5 for 8 f64 vectors per wave (<= 102 VGPRs),
@@ -340,7 +376,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     __shared__ T eS[NWAVE][V * 4];
     {  // per-half normals (host reference stream or launch_philox_fill)
         const uint32_t k0 = NW > 1 ? threadIdx.x : lane, kst = NW > 1 ? 64 * NW : 64;
-        for (uint32_t k = k0; k < Kp; k += kst) zS[ws][k] = k < K ? a.zbuf[(size_t)row * K + k] : T(0);
+        for (uint32_t k = k0; k < Kp; k += kst) zS[ws][k] = k < K ? a.zbuf[(size_t)CHK(row, a.lim_rows) * K + k] : T(0);
     }
     // ratings of this wave: vector v covers ratings q = (wr*V + v)*4 + rr;
     // slots past the row's end gather the partner table's zero row
@@ -359,7 +395,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
 #pragma unroll
         for (int u = 0; u < SG; ++u) {
             const uint32_t q = (uint32_t)((wr * V + g0 + u) * 4 + rr);
-            const uint32_t qi = q < n ? beg + q : 0u;
+            const uint32_t qi = (uint32_t)CHK(q < n ? beg + q : 0u, a.lim_this);
             pjv[u] = a.part[qi];
             pmv[u] = a.perm[qi];
             ev[u] = a.e_from_dot ? T(0) : a.E_this[qi];
@@ -382,7 +418,8 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     asm volatile("" ::: "memory");  // read back by the other lanes of the wave (LDS keeps its order)
     const T* __restrict__ pbase = a.partner + ci;
 #define PROW(v) (pbase + pjR[4 * (v)])
-    auto gat = [&](int v, uint32_t k0) -> T { return PROW(v)[k0]; };  // vector v's slice at column k0
+    // vector v's slice at column k0
+    auto gat = [&](int v, uint32_t k0) -> T { return pbase[CHK(pjR[4 * v] + k0 + ci, a.lim_partner) - ci]; };
     if (a.e_from_dot) {  // validation mode (tune bit 1): e0 = r - own.partner
         T dot[V];
 #pragma unroll
@@ -402,7 +439,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     }
     asm volatile("" ::: "memory");  // read back by the other lanes of the wave (LDS keeps its order)
     const T tau = a.tau;
-    const T* __restrict__ orow = a.own + (size_t)row * Kp + ci;
+    const T* __restrict__ orow = a.own + (size_t)CHK(row, a.lim_rows) * Kp + ci;
     stamp(0);  // row setup (ids, residuals, normals)
     // software pipeline: block b+1's slices and own/sigma/mu values are in
     // flight while block b is reduced, solved and applied.  The prefetch past
@@ -566,7 +603,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     for (int v = 0; v < V; ++v) {
         const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
         if (q < n && ci == 0) {
-            a.E_other[pmS[wv][4 * v + rr]] = e[v];
+            a.E_other[CHK(pmS[wv][4 * v + rr], a.lim_other)] = e[v];
             sq += e[v] * e[v];
             if (want_r) {
                 const T r = Rs[(wv * V + v) * 4 + rr];
@@ -814,13 +851,14 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             const uint32_t npad = 4 * NW * VC;
             for (uint32_t x = threadIdx.x; x < npad; x += 64 * NW) {
                 const bool in = x < n;
-                pjL[x] = (in ? a.part[beg + x] : a.zrow) * Kp;  // host checks (P+2)*Kp < 2^32
-                pmL[x] = in ? a.perm[beg + x] : 0u;
-                if (!a.e_from_dot) eL[gres_slot<NW>(x)] = in ? a.E_this[beg + x] : T(0);
+                const uint32_t qx = in ? (uint32_t)CHK(beg + x, a.lim_this) : 0u;
+                pjL[x] = (in ? a.part[qx] : a.zrow) * Kp;  // host checks (P+2)*Kp < 2^32
+                pmL[x] = in ? a.perm[qx] : 0u;
+                if (!a.e_from_dot) eL[gres_slot<NW>(x)] = in ? a.E_this[qx] : T(0);
             }
             for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {  // per-half normals and old values of the row
-                zL[k] = k < K ? a.zbuf[(size_t)row * K + k] : T(0);
-                oL[k] = a.own[(size_t)row * Kp + k];  // padding columns are zero
+                zL[k] = k < K ? a.zbuf[(size_t)CHK(row, a.lim_rows) * K + k] : T(0);
+                oL[k] = a.own[(size_t)CHK(row, a.lim_rows) * Kp + k];  // padding columns are zero
             }
             __syncthreads();
             if (a.e_from_dot) {  // validation mode (tune bit 1): e0 = r - own.partner
@@ -838,7 +876,9 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             stamp(0);  // staging
             const T* __restrict__ pbase = a.partner + ci;
             // the gather of vector j's slice of block t
-            auto gat = [&](int j, uint32_t t) -> T { return pbase[(size_t)pjW[j * JS] + t * GB]; };
+            auto gat = [&](int j, uint32_t t) -> T {
+                return pbase[CHK((size_t)pjW[j * JS] + t * GB + ci, a.lim_partner) - ci];
+            };
             // Residual update e_v -= S_v D (vector v: 4 ratings x 16 columns, lane ci
             // holding column ci): s_v *= D in place, then a butterfly reduce-scatter
             // over the 16 lanes of each rating (row_ror:8, row_half_mirror, quad_perm
@@ -860,7 +900,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     for (int p = 0; p < NP / 2; ++p) {
                         const int jv = h ? GresOrder<VC>::v[2 * p + 1] : GresOrder<VC>::v[2 * p];
                         const uint32_t slot = 4 * wr_s + rq + jv * JS;
-                        const T* src = a.partner + (size_t)pjL[slot] + t1 * GB + 2 * pc;
+                        const T* src = a.partner + CHK((size_t)pjL[slot] + t1 * GB + 2 * pc, a.lim_partner);
                         lds_dma16(src, &pfL[wr_s][2 * p][0]);
                     }
                 }
@@ -982,6 +1022,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     // the chunks, the XP pieces added in piece order in LDS
                     const size_t cstride = (size_t)nblk * SL;  // between one chunk's slabs and the next's
                     const double* pb = sy.slabs + ((size_t)tk.slab0 * nblk + t) * SL;
+                    (void)CHK(((size_t)(tk.slab0 + nch - 1) * nblk + t) * SL + SL - 1, sy.lim_slab);  // the row's last slab
                     if (xin) st_sc1(const_cast<double*>(pb) + tk.chunk * cstride + xe, (double)val);
                     asm volatile("" ::: "memory");
                     pf();
@@ -993,7 +1034,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     else
                         wait_vmcnt<0>();
                     lds_barrier();
-                    uint32_t* cnt = sy.counters + (size_t)tk.cnt0 + t;
+                    uint32_t* cnt = sy.counters + CHK((size_t)tk.cnt0 + t, sy.ncounters);
                     if (threadIdx.x == 0) {
                         // no return value to wait for: the poll follows at once
                         __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1101,7 +1142,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             double sq = 0.0, trs = 0.0;
             for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) {
                 const T e = eL[gres_slot<NW>(x)];
-                a.E_other[pmL[x]] = e;
+                a.E_other[CHK(pmL[x], a.lim_other)] = e;
                 sq += (double)(e * e);
                 if (a.row_tr) {
                     const T r = a.r_this[beg + x];
@@ -1126,9 +1167,9 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
         if (tk.chunk == 0)
             for (uint32_t k = threadIdx.x; k < K; k += 64 * NW) {
                 if (nch > 1)
-                    static_cast<T*>(sy.newown)[(size_t)tk.slab0 * Kp + k] = newS[k];
+                    static_cast<T*>(sy.newown)[(size_t)CHK(tk.slab0, sy.lim_chunk) * Kp + k] = newS[k];
                 else
-                    a.own[(size_t)row * Kp + k] = newS[k];
+                    a.own[(size_t)CHK(row, a.lim_rows) * Kp + k] = newS[k];
             }
         double dsq = wave_sum(sums.sq);
         double dtr = wave_sum(sums.tr);
@@ -1145,8 +1186,8 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 dtr += red2[w][1];
             }
             if (nch > 1) {
-                sy.chunk_sq[tk.slab0 + tk.chunk] = dsq;
-                sy.chunk_tr[tk.slab0 + tk.chunk] = dtr;
+                sy.chunk_sq[CHK(tk.slab0 + tk.chunk, sy.lim_chunk)] = dsq;
+                sy.chunk_tr[CHK(tk.slab0 + tk.chunk, sy.lim_chunk)] = dtr;
             } else {
                 if (a.row_sq) a.row_sq[row] = dsq;
                 if (a.row_tr) a.row_tr[row] = dtr;

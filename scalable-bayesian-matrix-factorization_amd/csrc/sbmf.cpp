@@ -873,6 +873,10 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     a.sweep = c->sweep;
     a.lo = (T)c->lo;
     a.hi = (T)c->hi;
+    a.lim_partner = (uint64_t)((users ? c->J : c->I) + 2) * c->Kp;
+    a.lim_other = (uint64_t)c->tu.size() + (users ? c->users.nsend : c->items.nsend);
+    a.lim_this = c->tu.size();
+    a.lim_rows = users ? c->I : c->J;
     // tune bit 1: residuals from r - own.partner (the former multi-GPU form, kept for validation);
     // otherwise every rank reads the residuals the exchange delivered
     a.e_from_dot = (c->cfg.tune & 2u) ? 1 : 0;
@@ -931,6 +935,8 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 sy.newown = c->d_xnewown.as<T>() + ox * c->Kp;
                 sy.timeout = c->d_xtimeout.as<uint32_t>();
                 sy.cmax = S.cmax;
+                sy.lim_slab = (uint64_t)(c->d_xslabs.bytes / sizeof(double)) - ox * sy.nblk * (16 * 16 + 16);
+                sy.lim_chunk = (uint32_t)(c->d_xchunk_sq.bytes / sizeof(double) - ox);
                 sy.prof = c->kprof && set == c->kprof_set ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
                 HalfArgs<T> as = a;
                 as.tune = ovl ? S.tune | 0x1000000u : S.tune;
