@@ -18,9 +18,9 @@ O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 BENCH="$R/bench.py"
-SHORT="--no-cpu --no-f32 --no-ttr"
+SHORT="--no-cpu --no-f32 --no-ttr --no-load ${BENCH_ARGS:-}"  # BENCH_ARGS: e.g. "--shape ml-10m --K 100"
 case "$PASS" in
-  bench) timeout -k 10 500 python3 "$BENCH" > "$O/${TAG}_bench.json" 2> "$O/${TAG}_bench.err" ;;
+  bench) timeout -k 10 500 python3 "$BENCH" ${BENCH_ARGS:-} > "$O/${TAG}_bench.json" 2> "$O/${TAG}_bench.err" ;;
   trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${TAG}_trace" -o "$TAG" -- \
            python3 "$BENCH" --steps 10 --warmup 2 $SHORT > "$O/${TAG}_trace.log" 2>&1 ;;
   fetch) timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d "$O/${TAG}_pmc_fetch" -o "$TAG" -- \
