@@ -140,8 +140,8 @@ typedef struct sbmf_config {
                                  bit 30 = a half's two streaming sets (items: rows > 1024 and the
                                           rest) one after the other (default: side by side).
                                  Removed in round 4 with the variants they selected (measured
-                                 slower, kept in git history): bits 0, 5, 6, 8-10, 16, 20-22, 25,
-                                 28, 31; they are now ignored.                                   */
+                                 slower, kept in git history): bits 0, 5, 6, 8-10, 16, 20-22, 25
+                                 (also the round-4 LDS-DMA prefetch), 28, 31; they are ignored.  */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

@@ -236,15 +236,6 @@ __device__ __noinline__ uint64_t chk_fail(uint64_t i, uint64_t lim, int line) {
 #define CHK(i, lim) (i)
 #endif
 
-// One wave's 1 KB LDS-DMA: lane l copies 16 bytes from its own global address src
-// to lds + 16 l (global_load_lds_dwordx4; lds wave-uniform).  Completion is
-// counted by vmcnt.  (The builtin exists only in the device pass; the host pass,
-// which only emits the kernel's launch stub, must not instantiate it.)
-__device__ __forceinline__ void lds_dma16(const void* src, void* lds) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
-#endif
-}
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0, "vmcnt range");
@@ -721,24 +712,11 @@ struct GresOrder {
     static constexpr Arr arr = make();
     static constexpr const int* v = arr.a;
 };
-// position of vector j among the first NP vectors of GresOrder<VC> (-1: not among them)
-template <int VC, int NP>
-__host__ __device__ constexpr int gres_pidx(int j) {
-    for (int i = 0; i < NP; ++i)
-        if (GresOrder<VC>::v[i] == j) return i;
-    return -1;
-}
 template <typename T>
 struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of slices
     static constexpr int VW = sizeof(T) == 8 ? 32 : 64;
 };
-// PFV > 0 (f64): LDS-DMA prefetch.  Right after block t's accumulate, each wave
-// issues global_load_lds_dwordx4 copies of the first PFV vectors (in gather-issue
-// order, GresOrder) of slice t+1 into an LDS buffer of its own; the requests stay
-// in flight through block t's cross-wave sum, split-row exchange and draws (LDS-
-// only barriers do not drain them) and the apply of block t then takes those
-// vectors from LDS instead of issuing their gathers after D_t is known.
-template <typename T, int NW, int SIDE, int PFV = 0>
+template <typename T, int NW, int SIDE>
 __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict__ tasks, uint32_t ntask,
                                                            HalfArgs<T> a, SplitSync sy) {
     typedef typename MfmaT<T>::acc_t acc_t;
@@ -755,10 +733,6 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
     __shared__ uint32_t pjL[CAP];      // partner row offset (row * Kp) per rating slot (zero row past the end)
     __shared__ uint32_t pmL[CAP];      // residual scatter target per rating
     __shared__ T eL[CAP];              // residuals (bit-identical in the 16 lanes of a rating)
-    static_assert(PFV == 0 || sizeof(T) == 8, "LDS-DMA prefetch geometry is for f64 slices");
-    static_assert(PFV % 2 == 0, "prefetched vectors go in pairs (one 1 KB LDS-DMA per pair)");
-    // [wave][vector][4 ratings x 16 columns]: a pair of vectors = one wave's 1 KB LDS-DMA
-    __shared__ T pfL[PFV > 0 ? NW : 1][PFV > 0 ? PFV : 1][4 * GB];
     // per-wave block partials: the 16x17 image of G_B (row r, column c at r*GLD + c, all 256
     // entries as the MFMA leaves them) followed by c_B; Rr: the reduced entries in the same
     // layout, except that the diagonal goes to Rr[PW + r]: the image's diagonal and upper part
@@ -886,39 +860,9 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             // max(1, VC/16) vectors and updates their residuals in LDS -- 2 (VC - 1)
             // DPP moves instead of 4 VC row-sum steps.  The registers each level
             // frees take their next slices at once (next(j) = the gather of vector j).
-            // LDS-DMA prefetch (PFV > 0): the first NP vectors in gather-issue order
-            // (GresOrder), whose next-block slices a wave copies into pfL[wave]
-            // during a block's exchange and draws, in pairs (one 1 KB
-            // global_load_lds_dwordx4 per pair: lane l moves 16 bytes of rating
-            // (l >> 3) & 3 of the pair's vector l >> 5, so pfL holds [vector][rating][16])
-            constexpr int NP = (PFV < VC ? PFV : VC) / 2 * 2;
-            auto pidx = [](int j) { return gres_pidx<VC, NP>(j); };
-            auto pf_issue = [&](uint32_t t1) {
-                if constexpr (NP > 0) {
-                    const int h = lane >> 5, rq = (lane >> 3) & 3, pc = lane & 7;
-#pragma unroll
-                    for (int p = 0; p < NP / 2; ++p) {
-                        const int jv = h ? GresOrder<VC>::v[2 * p + 1] : GresOrder<VC>::v[2 * p];
-                        const uint32_t slot = 4 * wr_s + rq + jv * JS;
-                        const T* src = a.partner + CHK((size_t)pjL[slot] + t1 * GB + 2 * pc, a.lim_partner);
-                        lds_dma16(src, &pfL[wr_s][2 * p][0]);
-                    }
-                }
-            };
-            // vector j of slice t: from pfL when it was prefetched, else gathered
-            auto nxt = [&](auto& s, int j, uint32_t t) {
-                const int i = pidx(j);
-                if (NP > 0 && i >= 0)
-                    s[j] = pfL[wr_s][i][rr * GB + ci];
-                else
-                    s[j] = gat(j, t);
-            };
             auto apply = [&](auto& s, T D, auto&& next) {
                 // VC rounded up to a power of two (VP); vectors VC..VP-1 are zero
                 constexpr int VP = VC <= 8 ? 8 : VC <= 16 ? 16 : VC <= 32 ? 32 : VC <= 64 ? 64 : 128;
-                // the prefetched slices have landed in LDS (this wave's own LDS-DMA: its vmcnt
-                // covers them; nothing else of this wave is in flight here)
-                if constexpr (NP > 0) wait_vmcnt<0>();
 #pragma unroll
                 for (int j = 0; j < VC; ++j) s[j] = s[j] * D;
                 bfly_level<0x128, VP>(s, ci & 8);
@@ -1120,18 +1064,14 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                             for (int j = 0; j < VC; ++j) s[j] = gat(j, t);
                         } else
 #endif
-                        apply(s, Dl, [&](int j) { nxt(s, j, t); });
+                        apply(s, Dl, [&](int j) { s[j] = gat(j, t); });
                     }
                     stamp(1);  // apply + gather issue
                     acc_t g = {T(0), T(0), T(0), T(0)};
                     T cc = T(0);
                     accumulate(s, g, cc);
                     stamp(2);  // gather wait + accumulate
-                    // LDS-DMA of slice t+1's first NP vectors, in flight through this block's
-                    // exchange and draws (the last block prefetches nothing)
-                    Dl = finish_block(g, cc, t, [&] {
-                        if (t + 1 < nblk) pf_issue(t + 1);
-                    }, std::integral_constant<int, NP / 2>{});
+                    Dl = finish_block(g, cc, t, [] {}, std::integral_constant<int, 0>{});
                 }
                 // apply the last block
                 apply(s, Dl, [](int) {});
@@ -1685,22 +1625,11 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
     return hipGetLastError();
 }
 
-// LDS-DMA prefetch vectors per wave (tune bit 25, f64): as many as the LDS left beside the
-// workgroups a CU holds (16-wave: one, 8-wave: two, 4-wave: four per CU) takes
-constexpr int gres_pfv(int nw) { return nw == 16 ? 8 : nw == 8 ? 4 : 2; }
-template <typename T, int NW>
-static const void* gres_fn(uint32_t tune, uint32_t side) {
-    if (sizeof(T) == 8 && (tune & 0x2000000u)) {
-        constexpr int P = sizeof(T) == 8 ? gres_pfv(NW) : 0;
-        return side ? (const void*)k_gres<T, NW, 1, P> : (const void*)k_gres<T, NW, 0, P>;
-    }
-    return side ? (const void*)k_gres<T, NW, 1> : (const void*)k_gres<T, NW, 0>;
-}
 template <typename T>
 static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
-    if (gres_nw(tune) == 4) return gres_fn<T, 4>(tune, side);
-    if (gres_nw(tune) == 16) return gres_fn<T, 16>(tune, side);
-    return gres_fn<T, 8>(tune, side);
+    if (gres_nw(tune) == 4) return side ? (const void*)k_gres<T, 4, 1> : (const void*)k_gres<T, 4, 0>;
+    if (gres_nw(tune) == 16) return side ? (const void*)k_gres<T, 16, 1> : (const void*)k_gres<T, 16, 0>;
+    return side ? (const void*)k_gres<T, 8, 1> : (const void*)k_gres<T, 8, 0>;
 }
 
 template <typename T>
