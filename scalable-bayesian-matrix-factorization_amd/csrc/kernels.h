@@ -75,7 +75,7 @@ struct SplitRow {
 };
 struct SplitSync {
     double* slabs;       // [nchunk_total][nblk][16*16+16]
-    uint32_t* counters;  // [nsplit_rows * nblk], zeroed per launch; then the task-queue head (dynamic order)
+    uint32_t* counters;  // [nsplit_rows * nblk], then the task-queue head: zero at launch (the caller clears them)
     uint32_t ncounters;
     uint32_t nblk;       // ceil(K/16)
     double* chunk_sq;    // [nchunk_total]
@@ -100,7 +100,9 @@ int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune);
 // (<= residency) workgroups.  Tasks are one list, claimed in order from a queue
 // head by whichever workgroup is free; a split row's chunks are consecutive, so
 // a chunk only waits for peers that the next free workgroups claim.  Split rows
-// are then published by k_split_finish.
+// are then published by k_split_finish.  sy.counters[0..ncounters] must be zero
+// when the launch starts: sbmf.cpp clears every set's counters with one memset
+// per half, ahead of the half's launches.
 template <typename T>
 hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid, const SplitRow* srows, uint32_t nsrow,
                           const HalfArgs<T>& a, const SplitSync& sy, hipStream_t st);

@@ -1652,8 +1652,6 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     if (ntask == 0) return hipSuccess;
     if (a.K > 256 || sy.cmax == 0 || grid == 0) return hipErrorInvalidValue;
     hipError_t err;
-    err = hipMemsetAsync(sy.counters, 0, ((size_t)sy.ncounters + 1) * sizeof(uint32_t), st);  // + queue head
-    if (err != hipSuccess) return err;
     // Tasks are claimed from a queue in list order by running workgroups, so only
     // the most recently claimed split row can have chunks still unclaimed, and its
     // waiting chunks (fewer than its chunk count, far below the resident

@@ -437,7 +437,16 @@ static void prepare_T(sbmf_ctx* c) {
                 while (j < rows.size() &&
                        std::max(2u, (sd->ptr[rows[j] + 1] - sd->ptr[rows[j]] + per_wave - 1) / per_wave) == nw)
                     ++j;
-                g.gsub[k].push_back({nw, i, j - i});
+                // f64 rows of 5-8 eight-vector waves run as (nw + 1) / 2 sixteen-vector waves
+                // (launch_gblock_nw): groups that launch the same kernel shape are one launch
+                // (nw 5+6 and 7+8; the merged group carries its larger nw)
+                auto shape = [&](uint32_t w) { return f64 && w >= 5 ? 100 + (w + 1) / 2 : w; };
+                if (!g.gsub[k].empty() && shape(g.gsub[k].back()[0]) == shape(nw)) {
+                    auto& last = g.gsub[k].back();  // degree-descending: the earlier group has the larger nw
+                    last[2] += j - i;
+                } else {
+                    g.gsub[k].push_back({nw, i, j - i});
+                }
                 i = j;
             }
         }
@@ -531,7 +540,10 @@ static void prepare_T(sbmf_ctx* c) {
     {
         const size_t nx = c->xset_nx + std::max<size_t>(nxk[1], 1), nr = c->xset_nr + std::max<size_t>(nrk[1], 1);
         c->d_xslabs.alloc(nx * nblk * (16 * 16 + 16) * sizeof(double));
-        c->d_xcnt.alloc((nr * nblk + 2) * sizeof(uint32_t));  // + each set's task-queue head
+        // + each set's task-queue head; a whole number of 16-byte words, so that clearing it
+        // is one fill kernel (a ragged size is three, and on a stream beside a persistent
+        // launch the tail one waited for that launch: r04s4 trace)
+        c->d_xcnt.alloc((nr * nblk + 2 + 3) / 4 * 4 * sizeof(uint32_t));
         c->d_xchunk_sq.alloc(nx * sizeof(double));
         c->d_xchunk_tr.alloc(nx * sizeof(double));
         HIPCHK(hipMemsetAsync(c->d_xchunk_tr.p, 0, c->d_xchunk_tr.bytes, st));
@@ -901,6 +913,8 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     bool others = false;
     for (int k = 0; k < NBIN; ++k) others |= k != KIND_STREAM && !g.bin_rows[k].empty();
     const bool ovl = !(c->cfg.tune & 0x20000000u) && others && !g.bin_rows[KIND_STREAM].empty();
+    // the split-row counters and queue heads of both stream sets, zeroed before the fork
+    if (!g.bin_rows[KIND_STREAM].empty()) HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
     if (ovl) {
         HIPCHK(hipEventRecord(c->oev[0], st));
         HIPCHK(hipStreamWaitEvent(c->sto, c->oev[0], 0));
@@ -920,7 +934,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
             HIPCHK(launch_gblock<T>(k, g.d_bins[k].as<uint32_t>(), (uint32_t)g.bin_rows[k].size(), a, st));
         else {
             for (int q = 0; q < 2; ++q) {
-                const int set = sov ? 1 - q : q;
+                const int set = sov ? 1 - q : q;  // set 1 (the long rows) first
                 const Side::StreamSet& S = g.ss[set];
                 if (S.stasks.empty()) continue;
                 const hipStream_t ss = sov && set == 0 ? c->sto : st;
