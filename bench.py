@@ -585,10 +585,11 @@ def main():
 
 if __name__ == "__main__":
     from sbmf import _lib as _sbmf_lib
-    if os.environ.get("SBMF_EXIT") != "normal":
-        # before anything starts the HIP runtime: leave through libsbmf's exit handler
-        # after rocprofv3's (if any) has written its output -- the HIP runtime's library
-        # finalizer faults under rocprofv3 (ROCm 7.2, profiles/r03_rocprof_teardown.txt)
+    if os.environ.get("SBMF_EXIT") == "guard":
+        # opt-in (round 3's default): leave through libsbmf's exit handler after
+        # rocprofv3's has written its output.  The finalizer fault it skipped came with
+        # RCCL linked at load time; libsbmf now dlopens RCCL for a multi-GPU communicator
+        # only, and a plain exit under rocprofv3 is clean
         _sbmf_lib.exit_guard(1)
     rc = 0
     try:
@@ -599,6 +600,6 @@ if __name__ == "__main__":
             print(e.code, file=sys.stderr)
     sys.stdout.flush()
     sys.stderr.flush()
-    if os.environ.get("SBMF_EXIT") != "normal":
+    if os.environ.get("SBMF_EXIT") == "guard":
         _sbmf_lib.exit_guard(rc)
     sys.exit(rc)

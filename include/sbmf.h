@@ -295,7 +295,10 @@ int sbmf_partition_rows(const uint32_t* ptr, uint32_t R, int nranks, uint64_t* b
  * writer) have run, skipping the shared-library finalizers -- under rocprofv3
  * (ROCm 7.2) the HIP runtime's finalizer faults after the profiler has finished
  * (profiles/r03_rocprof_teardown.txt).  Call it before the first HIP call; later
- * calls only set rc.  The handler belongs to libsbmf: do not dlclose it after. */
+ * calls only set rc.  The handler belongs to libsbmf: do not dlclose it after.
+ * Opt-in since round 4 (SBMF_EXIT=guard in bench.py and the CLI): the fault came
+ * with RCCL linked at load time, and libsbmf now loads RCCL (dlopen) only for a
+ * multi-GPU communicator, so a single-GPU process exits normally under rocprofv3. */
 int sbmf_exit_guard(int rc);
 
 /* --- test hooks ---------------------------------------------------------------------------- */

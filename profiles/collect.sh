@@ -9,8 +9,8 @@
 #   bash profiles/collect.sh <tag> gather  --pmc FETCH_SIZE over tests/hip/gather_bench (known bytes: calibration)
 # Outputs land in gpurun_out/<tag>_<pass>*.  Since round 4 libsbmf loads RCCL only for a
 # multi-GPU communicator (dlopen), and a single-GPU process exits normally under
-# rocprofv3 (profiles/r04/r04s2_cli_rocprof_kernel_stats.csv): SBMF_EXIT=normal here, so the
-# profiler's own exit handler writes the files (SBMF_EXIT=guard: round 3's _Exit guard).
+# rocprofv3 (profiles/r04/r04s2_cli_rocprof_kernel_stats.csv): a plain exit, the profiler's
+# own exit handler writes the files (SBMF_EXIT=guard would restore round 3's _Exit guard).
 set -euo pipefail
 TAG=${1:-r01}
 PASS=${2:-bench}
@@ -18,7 +18,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-export SBMF_EXIT=${SBMF_EXIT:-normal}
 BENCH="$R/bench.py"
 SHORT="--no-cpu --no-f32 --no-ttr --no-load ${BENCH_ARGS:-}"  # BENCH_ARGS: e.g. "--shape ml-10m --K 100"
 case "$PASS" in

@@ -44,7 +44,8 @@ def main():
         for k in d["c"]:
             if k not in keys:
                 keys.append(k)
-    print("%-34s %7s %4s %9s " % ("kernel", "grid", "wg", "us") + " ".join("%14s" % k[:14] for k in keys))
+    print("counters: " + ", ".join(keys))
+    print("%-34s %7s %4s %9s " % ("kernel", "grid", "wg", "us") + " ".join("%14s" % k[-14:] for k in keys))
     for d in sel:
         if d["ns"] < 20000:
             continue

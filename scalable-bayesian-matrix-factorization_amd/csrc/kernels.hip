@@ -280,6 +280,25 @@ __device__ __forceinline__ T gblock_solve(const T (&H)[GB], T gam) {
 // two-step form -- every lane forms d_{j+1} = gamma_{j+1} - H[j+1][j] d_j itself,
 // one readlane hop per pair of draws -- kept to re-run the fault it was dropped for
 // (CHECK=1 builds).
+// Lane j of each 16-lane DPP row, broadcast to the row (row_newbcast: one 64-bit DPP move
+// on gfx950 where a readlane pair put the value through an SGPR pair and a wait state).
+// Every row of the solving wave holds the same 16-lane system, so each row broadcasting
+// its own lane j gives every lane what readlane(x, j) gave.
+template <int J>
+__device__ __forceinline__ double row_bcast(double v) {
+    return __longlong_as_double(__builtin_amdgcn_mov_dpp(__double_as_longlong(v), 0x150 + J, 0xf, 0xf, false));
+}
+template <int J>
+__device__ __forceinline__ float row_bcast(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + J, 0xf, 0xf, false));
+}
+template <int J, typename T>
+__device__ __forceinline__ void solve_steps(const T* __restrict__ hrow, T Bq, T& gam) {
+    const T dj = row_bcast<J>(gam);
+    gam -= (Bq * hrow[J]) * dj;
+    if constexpr (J + 1 < GB) solve_steps<J + 1>(hrow, Bq, gam);
+}
+
 template <typename T>
 __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, T gam) {
 #ifdef SBMF_SOLVE2
@@ -297,11 +316,7 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
     }
     return gam;
 #else
-#pragma unroll
-    for (int j = 0; j < GB; ++j) {
-        const T dj = readlane(gam, j);
-        gam -= (Bq * hrow[j]) * dj;
-    }
+    solve_steps<0>(hrow, Bq, gam);
     return gam;
 #endif
 }

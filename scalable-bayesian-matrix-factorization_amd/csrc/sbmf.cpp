@@ -469,6 +469,8 @@ static void prepare_T(sbmf_ctx* c) {
             // or an explicit workgroup-shape bit, keeps them on 8-wave workgroups
             const bool user4 = sd == &c->users && sizeof(T) == 8 && !(cf.tune & (128u | 0x20000u | 0x800000u));
             const uint32_t stunes[2] = {user4 ? cf.tune | 128u : cf.tune, cf.tune | 0x20000u};
+            // (user rows above 1024 / 2048 ratings on 16-wave workgroups as a second set: measured
+            // neutral to slower, r04s9)
             for (auto& gp : sd->stg) {
             std::vector<uint32_t> rows[2];
             for (uint32_t r : gp->bin_rows[KIND_STREAM])  // degree-descending

@@ -261,11 +261,12 @@ int on_sweep(const sbmf_sweep_info* in, void* user) {
     return 0;
 }
 
-// Leave through sbmf_exit_guard's handler (registered at main's start, before the
-// first HIP call): a profiler's exit handlers (rocprofv3 writes its output there)
-// still run, the HIP runtime's library finalizer -- which faults under rocprofv3
-// on ROCm 7.2 -- does not (profiles/r03_rocprof_teardown.txt).  Every file is
-// closed and the context destroyed by then.  SBMF_EXIT=normal: plain exit.
+// SBMF_EXIT=guard (opt-in; round 3's default): leave through sbmf_exit_guard's
+// handler (registered at main's start, before the first HIP call), so a profiler's
+// exit handlers still run and the shared-library finalizers do not.  The finalizer
+// fault it skipped under rocprofv3 came with RCCL linked at load time; libsbmf
+// dlopens RCCL only for a multi-GPU communicator now, and the CLI exits normally
+// under rocprofv3 (profiles/r04/r04s2_cli_rocprof_kernel_stats.csv).
 bool g_guarded = false;
 int leave(int rc) {
     std::cout.flush();
@@ -278,7 +279,7 @@ int leave(int rc) {
 
 int main(int argc, char** argv) {
     const char* em = std::getenv("SBMF_EXIT");
-    g_guarded = !(em && std::strcmp(em, "normal") == 0) && sbmf_exit_guard(1) == SBMF_OK;
+    g_guarded = em && std::strcmp(em, "guard") == 0 && sbmf_exit_guard(1) == SBMF_OK;
     try {
         CmdLine cl(argc, argv);
         std::cout << "----------------------------------------------------------------------------\n"
