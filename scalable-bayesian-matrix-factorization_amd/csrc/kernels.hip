@@ -414,6 +414,9 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
 #ifdef SBMF_ABLATIONS
             if (a.tune & 0x100u) pj = 0;  // ablation (wrong results): every gather hits one cached row
 #endif
+#ifdef SBMF_ABL_GATHER0
+            pj = 0;  // timing-only build (wrong results): every slice from partner row 0
+#endif
             if (ci == 0) {
                 pjS[wv][4 * v + rr] = pj * Kp;
                 pmS[wv][4 * v + rr] = q < n ? pmv[u] : 0u;
@@ -842,6 +845,9 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 const bool in = x < n;
                 const uint32_t qx = in ? (uint32_t)CHK(beg + x, a.lim_this) : 0u;
                 pjL[x] = (in ? a.part[qx] : a.zrow) * Kp;  // host checks (P+2)*Kp < 2^32
+#ifdef SBMF_ABL_GATHER0
+                pjL[x] = 0;  // timing-only build (wrong results): every slice from partner row 0
+#endif
                 pmL[x] = in ? a.perm[qx] : 0u;
                 if (!a.e_from_dot) eL[gres_slot<NW>(x)] = in ? a.E_this[qx] : T(0);
             }
