@@ -316,7 +316,9 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
     }
     return gam;
 #else
+#ifndef SBMF_ABL_NOSOLVE  // timing-only build (wrong results): no 16-step recurrence
     solve_steps<0>(hrow, Bq, gam);
+#endif
     return gam;
 #endif
 }
@@ -505,7 +507,11 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
                 g[v & 3] += s[v];
             else
 #endif
+#ifdef SBMF_ABL_NOMFMA
+            g[v & 3] += s[v];  // timing-only build (wrong results): no MFMA
+#else
             g = MfmaT<T>::mfma(s[v], g);
+#endif
             cc += s[v] * eR[4 * v];
         }
         cc += shfl_xor_t(cc, 16);
@@ -583,6 +589,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         stamp(4);  // solve + D hand-off
         // ---- 4. e -= S_B D_B (lane (r,i) holds D_i): one butterfly reduce-scatter of the
         // V row sums (row16_scatter), each lane updating the residuals its sums cover
+#ifndef SBMF_ABL_NOBFLY  // timing-only build (wrong results): no residual update
         {
 #pragma unroll
             for (int v = 0; v < V; ++v) s[v] = s[v] * dlt;
@@ -592,6 +599,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             for (int j = 0; j < RV; ++j) eR[4 * (vb + j)] = eR[4 * (vb + j)] - s[j];
             asm volatile("" ::: "memory");
         }
+#endif
         stamp(5);  // residual update
 #pragma unroll
         for (int v = 0; v < V; ++v) s[v] = sn[v];
@@ -882,6 +890,13 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             // DPP moves instead of 4 VC row-sum steps.  The registers each level
             // frees take their next slices at once (next(j) = the gather of vector j).
             auto apply = [&](auto& s, T D, auto&& next) {
+#ifdef SBMF_ABL_NOBFLY  // timing-only build (wrong results): no residual update, the gathers only
+                constexpr int VCn = sizeof(s) / sizeof(s[0]);
+                (void)D;
+#pragma unroll
+                for (int j = 0; j < VCn; ++j) next(j);
+                return;
+#endif
                 // VC rounded up to a power of two (VP); vectors VC..VP-1 are zero
                 constexpr int VP = VC <= 8 ? 8 : VC <= 16 ? 16 : VC <= 32 ? 32 : VC <= 64 ? 64 : 128;
 #pragma unroll
@@ -934,7 +949,11 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     // vectors in the order their gathers were issued (GresOrder): the first
                     // MFMAs wait only for the oldest loads, not for all of them
                     const int j = SBMF_GRES_ORD ? GresOrder<VC>::v[i] : i;
+#ifdef SBMF_ABL_NOMFMA
+                    g[j & 3] += s[j];  // timing-only build (wrong results): no MFMA
+#else
                     g = MfmaT<T>::mfma(s[j], g);
+#endif
                     cc += s[j] * eS(j);
                 }
                 cc += shfl_xor_t(cc, 16);
