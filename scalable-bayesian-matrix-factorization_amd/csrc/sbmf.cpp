@@ -468,25 +468,13 @@ static void prepare_T(sbmf_ctx* c) {
             // CU): measured user streaming 1.49 -> 1.40 ms against 8-wave (r03s10); tune bit 23,
             // or an explicit workgroup-shape bit, keeps them on 8-wave workgroups
             const bool user4 = sd == &c->users && sizeof(T) == 8 && !(cf.tune & (128u | 0x20000u | 0x800000u));
-            uint32_t stunes[2] = {user4 ? cf.tune | 128u : cf.tune, cf.tune | 0x20000u};
-            // (user rows above 1024 / 2048 ratings on 16-wave workgroups as a second set: measured
-            // neutral to slower, r04s9)
-            // EXPERIMENT SBMF_X_USERSET=<ratings>:<waves>: user rows above <ratings> as set 1 on
-            // <waves>-wave workgroups
-            uint32_t uthr = 0;
-            if (const char* e = std::getenv("SBMF_X_USERSET"))
-                if (sd == &c->users && sizeof(T) == 8) {
-                    uthr = (uint32_t)std::atoi(e);
-                    const char* w = std::strchr(e, ':');
-                    const int nw = w ? std::atoi(w + 1) : 16;
-                    stunes[1] = nw == 8 ? cf.tune : nw == 4 ? cf.tune | 128u : cf.tune | 0x20000u;
-                }
+            const uint32_t stunes[2] = {user4 ? cf.tune | 128u : cf.tune, cf.tune | 0x20000u};
+            // (a second user set -- rows above 1024 / 2048 ratings on 16-wave workgroups, or above
+            // 512 / 1024 on 8-wave ones -- measured neutral to slower: r04s9, r04s15)
             for (auto& gp : sd->stg) {
             std::vector<uint32_t> rows[2];
-            for (uint32_t r : gp->bin_rows[KIND_STREAM]) {  // degree-descending
-                const uint32_t d = sd->ptr[r + 1] - sd->ptr[r];
-                rows[(item16 && d > 1024u) || (uthr && d > uthr) ? 1 : 0].push_back(r);
-            }
+            for (uint32_t r : gp->bin_rows[KIND_STREAM])  // degree-descending
+                rows[item16 && sd->ptr[r + 1] - sd->ptr[r] > 1024u ? 1 : 0].push_back(r);
             for (int k = 0; k < 2; ++k) {
                 Side::StreamSet& S = gp->ss[k];
                 S.tune = stunes[k];
