@@ -298,7 +298,9 @@ int sbmf_partition_rows(const uint32_t* ptr, uint32_t R, int nranks, uint64_t* b
  * calls only set rc.  The handler belongs to libsbmf: do not dlclose it after.
  * Opt-in since round 4 (SBMF_EXIT=guard in bench.py and the CLI): the fault came
  * with RCCL linked at load time, and libsbmf now loads RCCL (dlopen) only for a
- * multi-GPU communicator, so a single-GPU process exits normally under rocprofv3. */
+ * multi-GPU communicator, so a single-GPU process of the default schedule exits
+ * normally under rocprofv3; a process that launched k_gres cooperatively (tune
+ * bit 29) still faults there. */
 int sbmf_exit_guard(int rc);
 
 /* --- test hooks ---------------------------------------------------------------------------- */
