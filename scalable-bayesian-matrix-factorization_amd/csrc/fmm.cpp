@@ -49,6 +49,11 @@ struct FMBin {
     std::vector<uint32_t> rows;
     DBuf d_rows;
     int tpr;
+    // one rank, the long-row bin: each row cut into chunks of at most fmm_chunk cases
+    // {row, first case, cases, row index in this bin}; row i owns [cfirst[i], cfirst[i+1])
+    std::vector<uint4> chunks;
+    std::vector<uint32_t> cfirst;
+    DBuf d_chunks, d_cfirst, d_csums, d_cdelta, d_cqq;
 };
 
 struct FMLearner {
@@ -210,6 +215,26 @@ struct FMLearner {
                 if (b.rows.empty()) continue;
                 a.rows = b.d_rows.as<uint32_t>();
                 a.nrows = (uint32_t)b.rows.size();
+                if (xmode == 0 && !b.chunks.empty()) {
+                    // one rank, long rows in chunks: the chunks' sums, the draw per row (chunk
+                    // sums in chunk order), then every chunk's residual update -- the row's
+                    // cases spread over many workgroups instead of one
+                    FMPassArgs c = a;
+                    c.chunks = b.d_chunks.as<uint4>();
+                    c.nrows = (uint32_t)b.chunks.size();
+                    c.xmode = 1;
+                    c.sums = b.d_csums.as<double2>();
+                    HIPCHK(vpass ? fmm_vpass(c, b.tpr, st) : fmm_wpass(c, b.tpr, st));
+                    HIPCHK(fmm_chunk_draw(a, b.d_rows.as<uint32_t>(), b.d_cfirst.as<uint32_t>(), a.nrows,
+                                          b.d_csums.as<double2>(), vpass ? 1 : 0, b.d_cdelta.as<double4>(),
+                                          b.d_cqq.as<double2>(), st));
+                    c.xmode = 2;
+                    c.delta = b.d_cdelta.as<double4>();
+                    c.qq = b.d_cqq.as<double2>();
+                    HIPCHK(vpass ? fmm_vpass(c, b.tpr, st) : fmm_wpass(c, b.tpr, st));
+                    n_launch += 3;
+                    continue;
+                }
                 HIPCHK(vpass ? fmm_vpass(a, b.tpr, st) : fmm_wpass(a, b.tpr, st));
                 ++n_launch;
             }
@@ -501,20 +526,57 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
         iperm[ipos[x]] = upos[x];
     }
     // rows binned by length: <= 256 cases 64 threads, <= 4096 256, longer 1024
-    // (users: this rank's range; items: every item row, each rank over its own cases)
-    auto bin = [](const std::vector<uint32_t>& ptr, uint32_t r0, uint32_t r1, FMBin* b) {
+    // (users: this rank's range; items: every item row, each rank over its own cases;
+    // SBMF_FMM_LONG moves the long-row bound, for tests of the chunked long rows)
+    uint32_t longb = 4096;
+    if (const char* e = std::getenv("SBMF_FMM_LONG")) longb = (uint32_t)std::max(256, std::atoi(e));
+    auto bin = [longb](const std::vector<uint32_t>& ptr, uint32_t r0, uint32_t r1, FMBin* b) {
         b[0].tpr = 64;
         b[1].tpr = 256;
         b[2].tpr = 1024;
         for (uint32_t k = r0; k < r1; ++k) {
             const uint32_t len = ptr[k + 1] - ptr[k];
-            b[len <= 256 ? 0 : len <= 4096 ? 1 : 2].rows.push_back(k);
+            b[len <= 256 ? 0 : len <= longb ? 1 : 2].rows.push_back(k);
         }
+        // longest rows first: blocks start roughly in index order, so a long row dispatched
+        // late would set the launch's tail (one block per row; rows are independent, so the
+        // order changes no result)
+        for (int j = 0; j < 3; ++j)
+            std::stable_sort(b[j].rows.begin(), b[j].rows.end(),
+                             [&](uint32_t x, uint32_t y) { return ptr[x + 1] - ptr[x] > ptr[y + 1] - ptr[y]; });
     };
     bin(uptr, u0, u1, L->ubins);
     bin(iptr, 0, L->RI, L->ibins);
     for (FMBin* bs : {L->ubins, L->ibins})
         for (int k = 0; k < 3; ++k) upload(bs[k].d_rows, bs[k].rows, st);
+    // one rank: the long-row bin's rows cut into chunks of at most `chunk` cases (the
+    // 1024-thread workgroup's four cases per thread), the chunks of one row consecutive
+    // (SBMF_FMM_CHUNK overrides the size, 0 turns the chunks off)
+    uint32_t chunk = 4096;
+    if (const char* e = std::getenv("SBMF_FMM_CHUNK")) chunk = (uint32_t)std::max(0, std::atoi(e));
+    if (L->R == 1 && chunk)
+        for (FMBin* bs : {L->ubins, L->ibins}) {
+            FMBin& b = bs[2];
+            const std::vector<uint32_t>& pt = bs == L->ubins ? uptr : iptr;
+            b.chunks.clear();
+            b.cfirst.assign(1, 0);
+            for (uint32_t i = 0; i < (uint32_t)b.rows.size(); ++i) {
+                const uint32_t r = b.rows[i], c0 = pt[r], len = pt[r + 1] - c0;
+                const uint32_t nch = (len + chunk - 1) / chunk;
+                for (uint32_t c = 0; c < nch; ++c) {
+                    const uint32_t cb = c0 + (uint32_t)((uint64_t)len * c / nch);
+                    const uint32_t ce = c0 + (uint32_t)((uint64_t)len * (c + 1) / nch);
+                    b.chunks.push_back(make_uint4(r, cb, ce - cb, i));
+                }
+                b.cfirst.push_back((uint32_t)b.chunks.size());
+            }
+            if (b.chunks.empty()) continue;
+            upload(b.d_chunks, b.chunks, st);
+            upload(b.d_cfirst, b.cfirst, st);
+            b.d_csums.alloc(b.chunks.size() * sizeof(double2));
+            b.d_cdelta.alloc(b.rows.size() * sizeof(double4));
+            b.d_cqq.alloc(b.rows.size() * sizeof(double2));
+        }
     upload(L->d_uptr, uptr, st);
     upload(L->d_iptr, iptr, st);
     upload(L->d_upart, upart, st);

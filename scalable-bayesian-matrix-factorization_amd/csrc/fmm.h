@@ -56,12 +56,23 @@ struct FMPassArgs {
     double* e_io;
     double4* rec;   // [p] by attribute: {old, value kept, keep, 0} of the attribute's last draw
     int pend;       // the other side's last pass: 0 none, 1 a w pass, 2 a v pass
+    // one rank, long rows cut into chunks (non-null: the pass runs over chunks {row, first
+    // case, cases, long-row index}): xmode 1 writes chunk ri's sums to sums[ri], xmode 2
+    // takes {old, new, keep} from delta[long-row index] and the user rows' {qo, qn} (the
+    // record the draw replaced) from qq[long-row index]
+    const uint4* chunks;
+    const double2* qq;
 };
 // several ranks: every item row's draw from every rank's local sums (recv
 // [R][nrows], rank order), the same on every rank; a.own / a.z / a.mu ... as for
 // the pass; writes own[a0 + row] and delta[row] = {old, new, keep}
 hipError_t fmm_item_update(const FMPassArgs& a, const double2* recv, int R, uint32_t nrows, int vpass, double4* delta,
                            hipStream_t st);
+// one rank, long rows in chunks: row i of `rows` (nlong rows) owns chunks [cfirst[i],
+// cfirst[i+1]); its chunk sums added in chunk order, the draw, own / rec written, and
+// delta[i] = {old, new, keep}, qq[i] = the record the draw replaced ({qo, qn})
+hipError_t fmm_chunk_draw(const FMPassArgs& a, const uint32_t* rows, const uint32_t* cfirst, uint32_t nlong,
+                          const double2* csums, int vpass, double4* delta, double2* qq, hipStream_t st);
 // draw_w (:670-719) over the rows of a bin
 hipError_t fmm_wpass(const FMPassArgs& a, int threads_per_row, hipStream_t st);
 // draw_v (:780-835) of one factor over the rows of a bin

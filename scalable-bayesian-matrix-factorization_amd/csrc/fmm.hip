@@ -53,20 +53,37 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
     const int sub = threadIdx.x / NT, lt = threadIdx.x % NT;
     const uint32_t ri = blockIdx.x * RPB + sub;
     if (NT == 64 && ri >= a.nrows) return;  // a whole wave: no block barriers on this path
-    const uint32_t row = a.rows[ri];
-    const uint32_t beg = a.ptr[row], n = a.ptr[row + 1] - beg;
+    uint32_t row, beg, n, di;  // di: the row's slot in sums / delta
+    if (a.chunks) {            // a chunk of a long row (one rank)
+        const uint4 ck = a.chunks[ri];
+        row = ck.x;
+        beg = ck.y;
+        n = ck.z;
+        di = ck.w;
+    } else {
+        row = a.rows[ri];
+        beg = a.ptr[row];
+        n = a.ptr[row + 1] - beg;
+        di = row;
+    }
     const uint32_t at = a.a0 + row;
     const int xm = a.xmode;
-    const double4 dl = xm == 2 ? a.delta[row] : make_double4(0.0, 0.0, 0.0, 0.0);
+    const double4 dl = xm == 2 ? a.delta[di] : make_double4(0.0, 0.0, 0.0, 0.0);
     const double old = xm == 2 ? dl.x : a.own[at];
     const float x = 1.0f;  // one-hot value (DATA_FLOAT)
     // IP: this user's values of the factor of the item pass to be applied on read
     double qo = 0.0, qn = 0.0;
     if constexpr (IP) {
         if (a.pend == 2 && !a.item_side) {
-            const double4 r = a.rec[at];
-            qo = r.x;
-            qn = r.y;
+            if (xm == 2) {  // chunks: the draw has replaced the record, its old one kept in qq
+                const double2 r = a.qq[di];
+                qo = r.x;
+                qn = r.y;
+            } else {
+                const double4 r = a.rec[at];
+                qo = r.x;
+                qn = r.y;
+            }
         }
     }
     // IP: the other side's last pass applied to case q's residual e (its record:
@@ -172,8 +189,8 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
             s2 += red[1][k];
         }
     }
-    if (xm == 1) {  // several ranks: this rank's share of the row's sums
-        if (lt == 0) a.sums[row] = make_double2(m, s2);
+    if (xm == 1) {  // several ranks: this rank's share of the row's sums (chunks: the chunk's)
+        if (lt == 0) a.sums[a.chunks ? ri : row] = make_double2(m, s2);
         return;
     }
     double nv;
@@ -193,8 +210,8 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
         const uint32_t k = lt + j * NT;
         if (k < n) {
             const uint32_t q = beg + k;
-            const bool cached = xm != 2;  // the forwarding pass (several ranks) summed nothing
-            const double e = cached ? ce[j] : a.e_in[q];
+            const bool cached = xm != 2;  // the forwarding pass (several ranks, chunks) summed nothing
+            const double e = cached ? ce[j] : (IP ? pend(q, ein[q]) : a.e_in[q]);
             double eo = e;
             if (!keep) {
                 const double h = MODE == 0 ? (double)x : (cached ? ch[j] : hval(q));
@@ -370,6 +387,32 @@ __global__ __launch_bounds__(256) void k_fmm_item(FMPassArgs a, const double2* _
     delta[row] = make_double4(old, nv, keep ? 1.0 : 0.0, 0.0);
 }
 
+// one rank, long rows in chunks: one thread per long row, chunk sums in chunk order
+template <int MODE>
+__global__ __launch_bounds__(256) void k_fmm_chunk_draw(FMPassArgs a, const uint32_t* __restrict__ rows,
+                                                        const uint32_t* __restrict__ cfirst, uint32_t nlong,
+                                                        const double2* __restrict__ csums, double4* __restrict__ delta,
+                                                        double2* __restrict__ qq) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nlong) return;
+    double m = 0.0, s2 = 0.0;
+    for (uint32_t c = cfirst[i]; c < cfirst[i + 1]; ++c) {
+        m += csums[c].x;
+        s2 += csums[c].y;
+    }
+    const uint32_t at = a.a0 + rows[i];
+    const double old = a.own[at];
+    bool keep;
+    const double nv = fmm_draw<MODE>(a, at, old, m, s2, keep);
+    a.own[at] = nv;
+    if (a.rec) {
+        const double4 r = a.rec[at];
+        qq[i] = make_double2(r.x, r.y);
+        a.rec[at] = make_double4(old, nv, keep ? 1.0 : 0.0, 0.0);
+    }
+    delta[i] = make_double4(old, nv, keep ? 1.0 : 0.0, 0.0);
+}
+
 template <int MODE, bool IP>
 hipError_t launch_pass_ip(const FMPassArgs& a, int tpr, hipStream_t st) {
     switch (tpr) {
@@ -391,7 +434,7 @@ template <int MODE>
 hipError_t launch_pass(const FMPassArgs& a, int tpr, hipStream_t st) {
     if (a.nrows == 0) return hipSuccess;
     if (a.e_io) {
-        if (a.xmode != 0 || !a.rec) return hipErrorInvalidValue;  // in place: one rank only
+        if ((a.xmode != 0 && !a.chunks) || !a.rec) return hipErrorInvalidValue;  // in place: one rank only
         return launch_pass_ip<MODE, true>(a, tpr, st);
     }
     return launch_pass_ip<MODE, false>(a, tpr, st);
@@ -406,6 +449,16 @@ hipError_t fmm_item_update(const FMPassArgs& a, const double2* recv, int R, uint
         k_fmm_item<1><<<(nrows + 255) / 256, 256, 0, st>>>(a, recv, R, nrows, delta);
     else
         k_fmm_item<0><<<(nrows + 255) / 256, 256, 0, st>>>(a, recv, R, nrows, delta);
+    return hipGetLastError();
+}
+
+hipError_t fmm_chunk_draw(const FMPassArgs& a, const uint32_t* rows, const uint32_t* cfirst, uint32_t nlong,
+                          const double2* csums, int vpass, double4* delta, double2* qq, hipStream_t st) {
+    if (nlong == 0) return hipSuccess;
+    if (vpass)
+        k_fmm_chunk_draw<1><<<(nlong + 255) / 256, 256, 0, st>>>(a, rows, cfirst, nlong, csums, delta, qq);
+    else
+        k_fmm_chunk_draw<0><<<(nlong + 255) / 256, 256, 0, st>>>(a, rows, cfirst, nlong, csums, delta, qq);
     return hipGetLastError();
 }
 

@@ -64,6 +64,32 @@ def test_libfm_chain_matches_reference(run, ml100k, ragged):
     assert _within_printed(pred, ref_pred)
 
 
+@pytest.mark.parametrize("method", ["mcmc", "als"])
+def test_libfm_long_rows_in_chunks_match_oracle(method, ml100k, monkeypatch):
+    """One rank cuts the long-row bin's rows into chunks (sums per chunk, the draw per row
+    from the chunk sums in chunk order, then each chunk's residual update).  ML-100k has no
+    row over the default 4096-case bound: SBMF_FMM_LONG=256 / SBMF_FMM_CHUNK=64 put its
+    users and items of more than 256 ratings into 5-12 chunks each, on both sides (the user
+    side's chunks replay the item pass's pending update from the record the draw replaced)."""
+    assert gpu_available()
+    tr, te = ml100k
+    regular = (0.0, 0.0, 10.0) if method == "als" else (0.0, 0.0, 0.0)
+    monkeypatch.setenv("SBMF_FMM_LONG", "256")
+    monkeypatch.setenv("SBMF_FMM_CHUNK", "64")
+    L = _gpu(tr, te, 8, 5, 1, method, 1, 1, regular)
+    monkeypatch.delenv("SBMF_FMM_LONG")
+    monkeypatch.delenv("SBMF_FMM_CHUNK")
+    o = oracle.run_fmm(tr, te, K=8, iters=5, seed=1, method=method, k0=1, k1=1, regular=regular)
+    h = L.history
+    np.testing.assert_allclose([x["rmse_train"] for x in h], o["rmse_train"], rtol=1e-9, atol=0)
+    np.testing.assert_allclose([x["rmse_avg"] for x in h], o["rmse_test"], rtol=1e-9, atol=0)
+    U, V = L.factors()
+    I = U.shape[0]
+    np.testing.assert_allclose(U, o["v"][:, :I].T, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(V, o["v"][:, I:I + V.shape[0]].T, rtol=0, atol=1e-8)
+    np.testing.assert_allclose(L.predict(), o["pred"], rtol=0, atol=1e-9)
+
+
 def test_libfm_als_is_deterministic_and_biases_exposed(ml100k):
     tr, te = ml100k
     a = _gpu(tr, te, 8, 4, 3, "als", 1, 1, (0.0, 0.0, 10.0))
