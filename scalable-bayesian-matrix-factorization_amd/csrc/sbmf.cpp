@@ -925,7 +925,11 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     // rest on 8-wave ones, set 0), set 1 runs on `st` and set 0 on `sto` beside it
     // (tune bit 30: one after the other), each with split-row areas of its own.
     const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && !g.ss[0].stasks.empty() && !g.ss[1].stasks.empty();
-    for (int k = NBIN - 1; k >= 0; --k) {
+    // EXPERIMENT (tune bit 31): with two stream sets, the Gram-block launches go on `sto` ahead
+    // of set 0 (they otherwise queue behind it and run after the streaming stage)
+    const bool gfirst = sov && (c->cfg.tune & 0x80000000u);
+    for (int kk = NBIN - 1; kk >= 0; --kk) {
+        const int k = gfirst ? (kk == 0 ? KIND_STREAM : kk - 1) : kk;
         if (g.bin_rows[k].empty()) continue;
         st = ovl && k != KIND_STREAM ? c->sto : c->st;
         HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
