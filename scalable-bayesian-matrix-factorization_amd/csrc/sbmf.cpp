@@ -1251,26 +1251,39 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             if (cf.eval_train) bcast_stage(c, c->items, p, c->d_rowtr_v.p, sizeof(double));
         });
         HIPCHK(hipEventRecord(c->ev[5], st));
-        if (overlap) {  // the next sweep's prologue kernels, ahead of the evaluation
-            prologue_gpu(c->sweep + 1);
-            HIPCHK(hipEventRecord(c->ev[7], st));
-        }
-        // ---- 5. evaluation
+        // ---- 5. evaluation (and, overlapped, the next sweep's prologue kernels ahead of it).
+        // EXPERIMENT (tune bit 28, one rank): the evaluation on the second stream beside the
+        // prologue kernels (both only read U and V; they write different result slots)
         const bool collect = q2 ? true : (c->sweep >= cf.burnin);
         if (collect) c->collected++;
         const double div = avg_collected(cf) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
         const uint64_t T_ = c->su.size();
-        if (cf.eval_test && T_) {
-            HIPCHK(launch_test<T>(c->d_tu.as<uint32_t>(), c->d_ti.as<uint32_t>(), c->d_tr.as<double>(), c->t0, c->t1,
-                                  c->d_U.as<T>(), c->d_V.as<T>(), K, c->Kp, (T)c->lo, (T)c->hi, collect ? 1 : 0, div,
-                                  c->d_tsum.as<double>(), c->d_tpart.as<double>(),
-                                  c->bias ? c->d_bu.as<double>() : nullptr, c->d_bv.as<double>(), c->b0, st));
-            if (c->nranks > 1) c->comm.bcast_ranges(c->d_tpart.p, 2 * sizeof(double), c->tbblocks, st);
-            const uint32_t nb = (uint32_t)((T_ + 255) / 256);
-            HIPCHK(launch_sum_cols(c->d_tpart.as<double>(), nb, 2, d_res + RES_TEST_AVG, st));
+        const bool par_eval = overlap && c->nranks == 1 && (cf.tune & 0x10000000u);
+        auto evaluate = [&](hipStream_t se) {
+            if (cf.eval_test && T_) {
+                HIPCHK(launch_test<T>(c->d_tu.as<uint32_t>(), c->d_ti.as<uint32_t>(), c->d_tr.as<double>(), c->t0,
+                                      c->t1, c->d_U.as<T>(), c->d_V.as<T>(), K, c->Kp, (T)c->lo, (T)c->hi,
+                                      collect ? 1 : 0, div, c->d_tsum.as<double>(), c->d_tpart.as<double>(),
+                                      c->bias ? c->d_bu.as<double>() : nullptr, c->d_bv.as<double>(), c->b0, se));
+                if (c->nranks > 1) c->comm.bcast_ranges(c->d_tpart.p, 2 * sizeof(double), c->tbblocks, se);
+                const uint32_t nb = (uint32_t)((T_ + 255) / 256);
+                HIPCHK(launch_sum_cols(c->d_tpart.as<double>(), nb, 2, d_res + RES_TEST_AVG, se));
+            }
+            if (cf.eval_train) HIPCHK(launch_sum(c->d_rowtr_v.as<double>(), c->J, d_res + RES_TRSQ, scratch, se));
+            HIPCHK(hipEventRecord(c->ev[6], se));
+        };
+        if (par_eval) {
+            HIPCHK(hipStreamWaitEvent(c->sto, c->ev[5], 0));
+            evaluate(c->sto);
         }
-        if (cf.eval_train) HIPCHK(launch_sum(c->d_rowtr_v.as<double>(), c->J, d_res + RES_TRSQ, scratch, st));
-        HIPCHK(hipEventRecord(c->ev[6], st));
+        if (overlap) {  // the next sweep's prologue kernels, ahead of the evaluation
+            prologue_gpu(c->sweep + 1);
+            HIPCHK(hipEventRecord(c->ev[7], st));
+        }
+        if (par_eval)
+            HIPCHK(hipStreamWaitEvent(st, c->ev[6], 0));
+        else
+            evaluate(st);
         HIPCHK(hipMemcpyAsync(c->h_res.data(), d_res, 8 * sizeof(double), hipMemcpyDeviceToHost, st));
         if (overlap) {  // the next sweep's draws while the evaluation runs; this sweep's values kept
             HIPCHK(hipEventSynchronize(c->ev[7]));
@@ -1358,7 +1371,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         c->timing.ms_user_half = ev_ms(c->ev[1], c->ev[2]);
         c->timing.ms_item_half = ev_ms(c->ev[3], c->ev[4]);
         c->timing.ms_comm = ev_ms(c->ev[2], c->ev[3]) + ev_ms(c->ev[4], c->ev[5]);
-        c->timing.ms_eval = ev_ms(c->ev[overlap ? 7 : 5], c->ev[6]);
+        c->timing.ms_eval = ev_ms(c->ev[overlap && !par_eval ? 7 : 5], c->ev[6]);
         for (int sd = 0; sd < 2; ++sd) {
             const Side& sdd = sd == 0 ? c->users : c->items;
             for (int k = 0; k < SBMF_NKIND; ++k) {
