@@ -195,7 +195,7 @@ struct FMLearner {
         a.item_side = items ? 1 : 0;
         if (R == 1) {
             a.e_io = (items ? d_ei : d_eu).as<double>();
-            a.rec = d_rec.as<double4>();
+            a.rec = d_rec.as<double2>();
             a.pend = items ? pend_i : pend_u;
         }
         return a;
@@ -602,7 +602,7 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
     L->d_vT.alloc(std::max<size_t>((size_t)p * L->Kp, 1) * sizeof(double));
     HIPCHK(hipMemsetAsync(L->d_vT.p, 0, L->d_vT.bytes, st));
     L->d_vold.alloc((size_t)std::max(I, 1u) * sizeof(double));
-    L->d_rec.alloc((size_t)p * sizeof(double4));
+    L->d_rec.alloc((size_t)p * sizeof(double2));
     L->d_zw.alloc((size_t)p * sizeof(double));
     L->d_zv.alloc(std::max<size_t>((size_t)K * p, 1) * sizeof(double));
     L->d_pthis.alloc(std::max<uint64_t>(nt, 1) * sizeof(double));

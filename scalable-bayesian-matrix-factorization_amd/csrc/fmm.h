@@ -54,7 +54,8 @@ struct FMPassArgs {
     // side's last pass is applied to a case on read, from that side's per-attribute
     // records -- the same operations the scatter form applied, in the same order
     double* e_io;
-    double4* rec;   // [p] by attribute: {old, value kept, keep, 0} of the attribute's last draw
+    double2* rec;   // [p] by attribute: {old, value kept} of the attribute's last draw (a kept
+                    // draw, non-finite in the reference's sense, records old twice)
     int pend;       // the other side's last pass: 0 none, 1 a w pass, 2 a v pass
     // one rank, long rows cut into chunks (non-null: the pass runs over chunks {row, first
     // case, cases, long-row index}): xmode 1 writes chunk ri's sums to sums[ri], xmode 2

@@ -80,21 +80,21 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
                 qo = r.x;
                 qn = r.y;
             } else {
-                const double4 r = a.rec[at];
+                const double2 r = a.rec[at];
                 qo = r.x;
                 qn = r.y;
             }
         }
     }
-    // IP: the other side's last pass applied to case q's residual e (its record:
-    // old, value kept, keep), with the h that pass used -- the scatter form's update
+    // IP: the other side's last pass applied to case q's residual e (its record: old,
+    // value kept -- a kept draw records old twice, so its update is e - h * 0 = e), with
+    // the h that pass used -- the scatter form's update
     auto pend = [&](uint32_t q, double e) -> double {
         if constexpr (!IP) {
             return e;
         } else {
             if (a.pend == 0) return e;
-            const double4 r = a.rec[a.pa0 + a.part[q]];
-            if (r.z != 0.0) return e;  // that draw was kept: nothing changed
+            const double2 r = a.rec[a.pa0 + a.part[q]];
             double h;
             if (a.pend == 1) {
                 h = (double)x;  // a w pass
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
         if (a.item_side) {
             double vo, vn;
             if constexpr (IP) {  // the user's record of this factor's user pass
-                const double4 r = a.rec[pr];
+                const double2 r = a.rec[pr];
                 vo = r.x;
                 vn = r.y;
             } else {
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
         nv = fmm_draw<MODE>(a, at, old, m, s2, keep);
         if (lt == 0) {
             a.own[at] = nv;
-            if constexpr (IP) a.rec[at] = make_double4(old, nv, keep ? 1.0 : 0.0, 0.0);
+            if constexpr (IP) a.rec[at] = make_double2(old, nv);  // nv == old when kept
         }
     }
 #pragma unroll
@@ -418,9 +418,8 @@ __global__ __launch_bounds__(256) void k_fmm_chunk_draw(FMPassArgs a, const uint
     const double nv = fmm_draw<MODE>(a, at, old, m, s2, keep);
     a.own[at] = nv;
     if (a.rec) {
-        const double4 r = a.rec[at];
-        qq[i] = make_double2(r.x, r.y);
-        a.rec[at] = make_double4(old, nv, keep ? 1.0 : 0.0, 0.0);
+        qq[i] = a.rec[at];
+        a.rec[at] = make_double2(old, nv);  // nv == old when kept
     }
     delta[i] = make_double4(old, nv, keep ? 1.0 : 0.0, 0.0);
 }
