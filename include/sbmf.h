@@ -139,14 +139,13 @@ typedef struct sbmf_config {
                                           the streaming launch then an ordinary one as bit 24),
                                  bit 30 = a half's two streaming sets (items: rows > 1024 and the
                                           rest) one after the other (default: side by side),
-                                 bit 28 = (launch-order experiment, one rank) the test evaluation on
-                                          the second stream beside the next sweep's prologue kernels,
-                                 bit 31 = (launch-order experiment) with two streaming sets, the
-                                          Gram-block launches on the second stream ahead of set 0;
-                                          28 and 31 change no result (disjoint writes).
+                                 bit 28 = (one rank) the test evaluation after the next sweep's
+                                          prologue kernels on the compute stream (default: on the
+                                          second stream beside them; the results are the same).
                                  Removed in round 4 with the variants they selected (measured
-                                 slower, kept in git history): bits 0, 5, 6, 8-10, 16, 20-22, 25
-                                 (also the round-4 LDS-DMA prefetch); they are ignored.  */
+                                 slower or neutral, kept in git history): bits 0, 5, 6, 8-10, 16,
+                                 20-22, 25 (also the round-4 LDS-DMA prefetch), 31; they are
+                                 ignored.  */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

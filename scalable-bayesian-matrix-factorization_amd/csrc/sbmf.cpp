@@ -925,11 +925,8 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     // rest on 8-wave ones, set 0), set 1 runs on `st` and set 0 on `sto` beside it
     // (tune bit 30: one after the other), each with split-row areas of its own.
     const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && !g.ss[0].stasks.empty() && !g.ss[1].stasks.empty();
-    // EXPERIMENT (tune bit 31): with two stream sets, the Gram-block launches go on `sto` ahead
-    // of set 0 (they otherwise queue behind it and run after the streaming stage)
-    const bool gfirst = sov && (c->cfg.tune & 0x80000000u);
-    for (int kk = NBIN - 1; kk >= 0; --kk) {
-        const int k = gfirst ? (kk == 0 ? KIND_STREAM : kk - 1) : kk;
+    // (the Gram-block launches on `sto` ahead of set 0 instead of behind it: neutral, r04s22)
+    for (int k = NBIN - 1; k >= 0; --k) {
         if (g.bin_rows[k].empty()) continue;
         st = ovl && k != KIND_STREAM ? c->sto : c->st;
         HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
@@ -1251,14 +1248,15 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             if (cf.eval_train) bcast_stage(c, c->items, p, c->d_rowtr_v.p, sizeof(double));
         });
         HIPCHK(hipEventRecord(c->ev[5], st));
-        // ---- 5. evaluation (and, overlapped, the next sweep's prologue kernels ahead of it).
-        // EXPERIMENT (tune bit 28, one rank): the evaluation on the second stream beside the
-        // prologue kernels (both only read U and V; they write different result slots)
+        // ---- 5. evaluation, and (overlap) the next sweep's prologue kernels.  One rank: the
+        // evaluation runs on the second stream beside the prologue kernels -- both only read
+        // U and V and they write different result slots, so nothing changes -- where it used
+        // to follow them (tune bit 28 restores that order; measured 7.64-7.73 -> 7.61 ms, r04s22)
         const bool collect = q2 ? true : (c->sweep >= cf.burnin);
         if (collect) c->collected++;
         const double div = avg_collected(cf) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
         const uint64_t T_ = c->su.size();
-        const bool par_eval = overlap && c->nranks == 1 && (cf.tune & 0x10000000u);
+        const bool par_eval = overlap && c->nranks == 1 && !(cf.tune & 0x10000000u);
         auto evaluate = [&](hipStream_t se) {
             if (cf.eval_test && T_) {
                 HIPCHK(launch_test<T>(c->d_tu.as<uint32_t>(), c->d_ti.as<uint32_t>(), c->d_tr.as<double>(), c->t0,
