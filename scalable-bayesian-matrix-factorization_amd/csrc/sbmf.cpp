@@ -286,6 +286,11 @@ struct sbmf_ctx {
     hipEvent_t& kev(uint32_t stage, int side, int kind, int e) {
         return kevs[(((size_t)stage * 2 + side) * SBMF_NKIND + kind) * 2 + e];
     }
+    // [stage][side][kind]: the kind launched just before this one on the same stream, whose
+    // end event is this kind's start (no begin event recorded), or -1.  Two timing events
+    // back to back on a stream cost ~12 us of idle device between the launches (r04f trace).
+    std::vector<int8_t> kprev;
+    int8_t& kpv(uint32_t stage, int side, int kind) { return kprev[((size_t)stage * 2 + side) * SBMF_NKIND + kind]; }
     uint32_t nstages = 1;          // stages per half (see Side::Stage); > 1 only with several ranks
     hipStream_t stc = nullptr;     // multi-GPU: the exchange of stage p runs here while stage p+1 computes
     std::vector<hipEvent_t> sev;   // [side][stage]: stage computed (compute stream)
@@ -309,14 +314,26 @@ struct sbmf_ctx {
     DBuf d_var3u, d_var3v, d_epart;              // reference-mode per-row bias variates; sum(E) partials
     std::vector<double> h_res;
     double* h_pre = nullptr;     // pinned: the prologue's sums (residual, column statistics)
+    // pinned: the sweep's results (8 doubles), the split-row timeout flag, and the staged
+    // hyperparameter upload [sig_u | mu_u | sig_v | mu_v] (4 Kp of T)
+    void* h_io = nullptr;
+    double* h_out() { return static_cast<double*>(h_io); }
+    uint32_t* h_timeout() { return reinterpret_cast<uint32_t*>(static_cast<char*>(h_io) + 64); }
+    void* h_hyper() { return static_cast<char*>(h_io) + 128; }
+    hipEvent_t hev = nullptr;  // the last upload from h_hyper done (the area is rewritten after it)
     // throughput mode: the next sweep's hyperparameters, drawn at the end of the
     // previous sweep while its test evaluation runs (run_sweeps_T)
     struct PreDraw {
         bool valid = false;
+        bool staged = false;  // uploaded to d_hyper, and the sweep's normals filled, ahead
         uint32_t sweep = 0;
         double tau = 0, b0 = 0, mu_b0 = 0, sig_b0 = 0, d0 = 0;
         std::vector<double> sig_u, mu_u, sig_v, mu_v;
     } pre;
+    // d_hyper holds the drawn-ahead values (pre), not the current ones: a sweep that does not
+    // use them (pre dropped by sbmf_set_factors) restores the current ones before its
+    // prologue, whose column statistics read the current mu from d_hyper
+    bool hyper_ahead = false;
     double* h_pinned = nullptr;  // pinned staging for z streams
     size_t h_pinned_bytes = 0;
     sbmf_timing timing{};
@@ -588,7 +605,11 @@ static void prepare_T(sbmf_ctx* c) {
     if (c->h_pre) (void)hipHostFree(c->h_pre);
     c->h_pre = nullptr;
     HIPCHK(hipHostMalloc((void**)&c->h_pre, c->h_res.size() * sizeof(double), hipHostMallocDefault));
+    if (c->h_io) (void)hipHostFree(c->h_io);
+    c->h_io = nullptr;
+    HIPCHK(hipHostMalloc(&c->h_io, 128 + 4 * (size_t)c->Kp * sizeof(T), hipHostMallocDefault));
     c->pre.valid = false;
+    c->hyper_ahead = false;
     const uint64_t big = std::max<uint64_t>({(uint64_t)c->I, (uint64_t)c->J, c->su.size() / 128 + 2});
     c->d_scratch.alloc((big / 1024 + 16) * 2 * sizeof(double));
     // test set
@@ -659,6 +680,7 @@ static void prepare_T(sbmf_ctx* c) {
     for (hipEvent_t e : c->kevs) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->sev) (void)hipEventDestroy(e);
     c->kevs.assign((size_t)c->nstages * 2 * SBMF_NKIND * 2, nullptr);
+    c->kprev.assign((size_t)c->nstages * 2 * SBMF_NKIND, (int8_t)-1);
     c->sev.assign((size_t)2 * c->nstages, nullptr);
     for (hipEvent_t& e : c->kevs) HIPCHK(hipEventCreate(&e));
     for (hipEvent_t& e : c->sev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -926,10 +948,14 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     // (tune bit 30: one after the other), each with split-row areas of its own.
     const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && !g.ss[0].stasks.empty() && !g.ss[1].stasks.empty();
     // (the Gram-block launches on `sto` ahead of set 0 instead of behind it: neutral, r04s22)
+    int last[2] = {-1, -1};  // the last kind launched on st / sto (its end event recorded there)
     for (int k = NBIN - 1; k >= 0; --k) {
         if (g.bin_rows[k].empty()) continue;
         st = ovl && k != KIND_STREAM ? c->sto : c->st;
-        HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
+        int& lk = last[st == c->st ? 0 : 1];
+        c->kpv(stage, sd, k) = (int8_t)lk;
+        if (lk < 0) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
+        lk = k;
         if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
             for (const auto& gs : g.gsub[k])
                 HIPCHK(launch_gblock_nw<T>((int)gs[0], g.d_bins[k].as<uint32_t>() + gs[1], gs[2], a, st));
@@ -1059,7 +1085,7 @@ static void run_half_pipelined(sbmf_ctx* c, bool users, F&& bcasts) {
         if (c->nranks > 1) HIPCHK(hipEventRecord(c->sev[(size_t)sd * c->nstages + p], c->st));
     }
     HIPCHK(hipEventRecord(c->ev[users ? 2 : 4], c->st));
-    if (c->nranks <= 1) return;
+    if (c->nranks <= 1) return;  // no exchange: ev[3] / ev[5] are not recorded (the sweep uses ev[2] / ev[4])
     for (uint32_t p = 0; p < c->nstages; ++p) {
         HIPCHK(hipStreamWaitEvent(c->stc, c->sev[(size_t)sd * c->nstages + p], 0));
         exchange_stage<T>(c, users, p, c->stc, bcasts);
@@ -1081,7 +1107,8 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
     // Throughput mode (Philox: the draws of sweep s depend only on (seed, s)): the
     // next sweep's prologue -- residual sum of squares, column statistics and the
     // host hyperparameter draws -- is issued at the end of this sweep, its kernels
-    // before the test evaluation and its host draws while the evaluation runs, so
+    // beside the test evaluation (one rank; before it otherwise) and its host draws
+    // while the evaluation runs, so
     // the GPU does not wait for the host round trip at the start of the next
     // sweep.  The inputs are the same (U, V and the residuals do not change in
     // between), so the chain is bitwise the same.  Tune bit 26 turns it off.
@@ -1173,10 +1200,36 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         }
         return d0;
     };
+    // one rank: nothing between the halves and after the item half, so their events are the
+    // halves' end events (two timing events back to back leave the device idle ~12 us)
+    hipEvent_t& ev3 = c->nranks > 1 ? c->ev[3] : c->ev[2];
+    hipEvent_t& ev5 = c->nranks > 1 ? c->ev[5] : c->ev[4];
+    // the sweep's hyperparameters [sig_u | mu_u | sig_v | mu_v] into the pinned staging area
+    // and on to d_hyper (stream order: after every launch already queued that reads it)
+    auto stage_hyper = [&](const std::vector<double>& su, const std::vector<double>& mu, const std::vector<double>& sv,
+                           const std::vector<double>& mv) {
+        const size_t Kp = c->Kp;
+        T* h = static_cast<T*>(c->h_hyper());
+        HIPCHK(hipEventSynchronize(c->hev));
+        std::fill(h, h + 4 * Kp, T(0));
+        for (uint32_t k = 0; k < K; ++k) {
+            h[k] = (T)su[k];
+            h[Kp + k] = (T)mu[k];
+            h[2 * Kp + k] = (T)sv[k];
+            h[3 * Kp + k] = (T)mv[k];
+        }
+        HIPCHK(hipMemcpyAsync(c->d_hyper.p, h, 4 * Kp * sizeof(T), hipMemcpyHostToDevice, st));
+        HIPCHK(hipEventRecord(c->hev, st));
+    };
     for (uint32_t it = 0; it < nsweeps; ++it) {
         c->timing.n_launch = 0;
         HIPCHK(hipEventRecord(c->ev[0], st));
         double d0;
+        // throughput mode: this sweep's hyperparameters already on the device and its normals
+        // filled (both queued at the end of the previous sweep)
+        const bool staged = c->pre.valid && c->pre.sweep == c->sweep && c->pre.staged;
+        if (!staged && c->hyper_ahead) stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v);
+        c->hyper_ahead = false;
         if (c->pre.valid && c->pre.sweep == c->sweep) {  // drawn at the end of the previous sweep
             c->tau = c->pre.tau;
             c->b0 = c->pre.b0;
@@ -1200,16 +1253,9 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             d0 = host_draw(hs);
         }
         c->pre.valid = false;
-        {
-            const size_t Kp = c->Kp;
-            std::vector<T> h(4 * Kp, T(0));
-            for (uint32_t k = 0; k < K; ++k) {
-                h[k] = (T)c->sig_u[k];
-                h[Kp + k] = (T)c->mu_u[k];
-                h[2 * Kp + k] = (T)c->sig_v[k];
-                h[3 * Kp + k] = (T)c->mu_v[k];
-            }
-            HIPCHK(hipMemcpyAsync(c->d_hyper.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st));
+        c->pre.staged = false;
+        if (!staged) {
+            stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v);
             if (ref && c->bias) {
                 fill_bias_variates<T>(c);
             } else if (ref) {  // user variates then item variates (:485 then :529)
@@ -1217,10 +1263,11 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 fill_z<T>(c, c->J, c->d_zV);
             }
             HIPCHK(hipStreamSynchronize(st));
+            HIPCHK(hipEventRecord(c->ev[1], st));
         }
-        HIPCHK(hipEventRecord(c->ev[1], st));
+        hipEvent_t& ev1 = staged ? c->ev[0] : c->ev[1];
         // ---- 3. user half-sweep (throughput mode: this half's normals first)
-        if (!ref)
+        if (!ref && !staged)
             HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep, TAG_USERS, st));
         if (c->bias)  // per-user bias hyperparameters + b_i draw + residual shift (:470-489, :515-530)
             HIPCHK(launch_bias_rows<T>(c->d_uptr.as<uint32_t>(), c->users.r0, c->users.r1, c->d_Eu.as<T>(),
@@ -1232,9 +1279,9 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             bcast_stage(c, c->users, p, c->d_U.p, c->Kp * sizeof(T));
             if (c->bias) bcast_stage(c, c->users, p, c->d_bu.p, sizeof(double));
         });
-        HIPCHK(hipEventRecord(c->ev[3], st));
+        if (c->nranks > 1) HIPCHK(hipEventRecord(c->ev[3], st));
         // ---- 4. item half-sweep
-        if (!ref)
+        if (!ref && !staged)
             HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep, TAG_ITEMS, st));
         if (c->bias)  // per-item (:492-511, :563-578)
             HIPCHK(launch_bias_rows<T>(c->d_vptr.as<uint32_t>(), c->items.r0, c->items.r1, c->d_Ev.as<T>(),
@@ -1247,7 +1294,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             bcast_stage(c, c->items, p, c->d_rowsq_v.p, sizeof(double));
             if (cf.eval_train) bcast_stage(c, c->items, p, c->d_rowtr_v.p, sizeof(double));
         });
-        HIPCHK(hipEventRecord(c->ev[5], st));
+        if (c->nranks > 1) HIPCHK(hipEventRecord(c->ev[5], st));
         // ---- 5. evaluation, and (overlap) the next sweep's prologue kernels.  One rank: the
         // evaluation runs on the second stream beside the prologue kernels -- both only read
         // U and V and they write different result slots, so nothing changes -- where it used
@@ -1271,18 +1318,22 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(hipEventRecord(c->ev[6], se));
         };
         if (par_eval) {
-            HIPCHK(hipStreamWaitEvent(c->sto, c->ev[5], 0));
+            HIPCHK(hipStreamWaitEvent(c->sto, ev5, 0));
             evaluate(c->sto);
         }
         if (overlap) {  // the next sweep's prologue kernels, ahead of the evaluation
             prologue_gpu(c->sweep + 1);
             HIPCHK(hipEventRecord(c->ev[7], st));
+            // and the next sweep's normals (Philox: a function of (seed, sweep) only; this
+            // sweep's halves, which read them, are queued before)
+            HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep + 1, TAG_USERS, st));
+            HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep + 1, TAG_ITEMS, st));
         }
         if (par_eval)
             HIPCHK(hipStreamWaitEvent(st, c->ev[6], 0));
         else
             evaluate(st);
-        HIPCHK(hipMemcpyAsync(c->h_res.data(), d_res, 8 * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(c->h_out(), d_res, 8 * sizeof(double), hipMemcpyDeviceToHost, st));
         if (overlap) {  // the next sweep's draws while the evaluation runs; this sweep's values kept
             HIPCHK(hipEventSynchronize(c->ev[7]));
             HostStream hs;
@@ -1309,11 +1360,18 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             c->mu_v.swap(mv0);
             c->pre.sweep = c->sweep + 1;
             c->pre.valid = true;
+            // the next sweep's hyperparameters to the device now (every launch of this sweep that
+            // reads d_hyper -- the halves and the prologue's column statistics -- is queued before)
+            stage_hyper(c->pre.sig_u, c->pre.mu_u, c->pre.sig_v, c->pre.mu_v);
+            c->pre.staged = true;
+            c->hyper_ahead = true;
         }
-        uint32_t split_timeout = 0;
+        *c->h_timeout() = 0;
         if (c->d_xtimeout.p)
-            HIPCHK(hipMemcpyAsync(&split_timeout, c->d_xtimeout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(c->h_timeout(), c->d_xtimeout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        std::copy(c->h_out(), c->h_out() + 8, c->h_res.begin());
+        const uint32_t split_timeout = *c->h_timeout();
         if (c->kprof) {
             unsigned long long h[96];
             HIPCHK(hipMemcpy(h, c->d_kprof.p, sizeof(h), hipMemcpyDeviceToHost));
@@ -1365,11 +1423,11 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         info.rmse_this = (cf.eval_test && T_) ? std::sqrt(c->h_res[RES_TEST_THIS] / T_) : NAN;
         info.rmse_train = cf.eval_train && N ? std::sqrt(c->h_res[RES_TRSQ] / N) : NAN;
         // with the overlap the prologue's kernels run between ev[5] and ev[7] (for the next sweep)
-        c->timing.ms_hyper = ev_ms(c->ev[0], c->ev[1]) + (overlap ? ev_ms(c->ev[5], c->ev[7]) : 0.0);
-        c->timing.ms_user_half = ev_ms(c->ev[1], c->ev[2]);
-        c->timing.ms_item_half = ev_ms(c->ev[3], c->ev[4]);
-        c->timing.ms_comm = ev_ms(c->ev[2], c->ev[3]) + ev_ms(c->ev[4], c->ev[5]);
-        c->timing.ms_eval = ev_ms(c->ev[overlap && !par_eval ? 7 : 5], c->ev[6]);
+        c->timing.ms_hyper = (staged ? 0.0 : ev_ms(c->ev[0], ev1)) + (overlap ? ev_ms(ev5, c->ev[7]) : 0.0);
+        c->timing.ms_user_half = ev_ms(ev1, c->ev[2]);
+        c->timing.ms_item_half = ev_ms(ev3, c->ev[4]);
+        c->timing.ms_comm = c->nranks > 1 ? ev_ms(c->ev[2], c->ev[3]) + ev_ms(c->ev[4], c->ev[5]) : 0.0;
+        c->timing.ms_eval = overlap && !par_eval ? ev_ms(c->ev[7], c->ev[6]) : ev_ms(ev5, c->ev[6]);
         for (int sd = 0; sd < 2; ++sd) {
             const Side& sdd = sd == 0 ? c->users : c->items;
             for (int k = 0; k < SBMF_NKIND; ++k) {
@@ -1377,12 +1435,13 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 for (uint32_t p = 0; p < c->nstages; ++p) {
                     const Side::Stage& g = *sdd.stg[p];
                     const bool ran = k < NBIN && !g.bin_rows[k].empty();
-                    if (ran) ms += ev_ms(c->kev(p, sd, k, 0), c->kev(p, sd, k, 1));
+                    const int kp = ran ? c->kpv(p, sd, k) : -1;
+                    if (ran) ms += ev_ms(kp >= 0 ? c->kev(p, sd, kp, 1) : c->kev(p, sd, k, 0), c->kev(p, sd, k, 1));
                 }
                 c->timing.kern_ms[sd][k] = ms;
             }
         }
-        info.ms_sweep = ev_ms(c->ev[0], c->ev[5]);
+        info.ms_sweep = ev_ms(c->ev[0], ev5);
         info.ms_eval = c->timing.ms_eval;
         c->sweep++;
         if (cb && cb(&info, user)) break;
@@ -1397,6 +1456,7 @@ sbmf_ctx::~sbmf_ctx() {
     fmm_destroy(fm);
     if (h_pinned) (void)hipHostFree(h_pinned);
     if (h_pre) (void)hipHostFree(h_pre);
+    if (h_io) (void)hipHostFree(h_io);
     for (auto& e : ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : kevs)
@@ -1407,6 +1467,7 @@ sbmf_ctx::~sbmf_ctx() {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : oev)
         if (e) (void)hipEventDestroy(e);
+    if (hev) (void)hipEventDestroy(hev);
     if (sto) (void)hipStreamDestroy(sto);
     if (stc) (void)hipStreamDestroy(stc);
     if (st) (void)hipStreamDestroy(st);
@@ -1532,6 +1593,7 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     for (auto& e : c->cev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->sto, hipStreamNonBlocking));
     for (auto& e : c->oev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->hev, hipEventDisableTiming));
     *out = c.release();
     API_END(ctx)
 }

@@ -128,6 +128,19 @@ def test_kernel_variants_match_oracle(ml100k, tune):
         assert np.abs(V - o["V"]).max() < 1e-7
 
 
+def test_evaluation_order_changes_nothing(ml100k):
+    """One rank evaluates the test RMSE on the second stream beside the next
+    sweep's prologue kernels; tune bit 28 puts it back after them on the compute
+    stream.  Both read U and V only and write different slots: the chain, the
+    printed RMSEs and the factors are the same bit for bit."""
+    tr, te = ml100k
+    a = _run(tr, te, 4, num_factor=30, seed=8, rng="philox")  # the overlapped schedule (device RNG)
+    b = _run(tr, te, 4, num_factor=30, seed=8, rng="philox", tune=1 << 28)
+    assert np.array_equal(a.rmse_trajectory, b.rmse_trajectory)
+    for x, y in zip(a.factors(), b.factors()):
+        assert np.array_equal(x, y)
+
+
 @pytest.mark.parametrize("kw", [{}, {"stream_threshold": 40, "split_chunk": 64}, {"stream_threshold": 16}])
 def test_multigpu_residual_mode_matches_oracle(ml100k, kw):
     """The residual form every rank uses with several GPUs (e0 = r - own.partner
