@@ -73,7 +73,11 @@ struct FMLearner {
     DBuf d_uptr, d_upart, d_uperm, d_uown, d_uy, d_iptr, d_ipart, d_iperm;
     DBuf d_eu, d_ei, d_w, d_v, d_vT, d_vold, d_zw, d_zv, d_su, d_si, d_sy, d_pthis, d_sum, d_part, d_tpart, d_res,
         d_scratch;
-    std::vector<double> h_w, h_v;
+    std::vector<double> h_w, h_v;  // the initial model (released after the upload)
+    // the hyperparameter draws' sums (k_fmm_hsums): per v column f and for w (index K),
+    // {mu, gm's initial value} in, {gm, m} out
+    DBuf d_hmg, d_hsum;
+    std::vector<double> h_mg, h_hs;
     // several ranks
     Comm* comm = nullptr;
     int R = 1;
@@ -127,16 +131,16 @@ struct FMLearner {
     // fm_learn_mcmc.h:951-1009 (one group: every attribute)
     template <class G>
     void draw_hyper_w(G& g) {
-        const double alpha_0 = 1.0, gamma_0 = 1.0, beta_0 = 1.0, mu_0 = 0.0;
+        const double alpha_0 = 1.0, beta_0 = 1.0, mu_0 = 0.0;
         if (do_multilevel) {
-            double gm = beta_0 * (w_mu - mu_0) * (w_mu - mu_0) + gamma_0;
-            for (uint32_t i = 0; i < p; ++i) gm += (h_w[i] - w_mu) * (h_w[i] - w_mu);
+            // gm = beta_0 (w_mu - mu_0)^2 + gamma_0 + sum_i (w_i - w_mu)^2 and m = sum_i w_i,
+            // summed on the device in this order (sweep_draws)
+            double gm = h_hs[2 * K];
             const double a = alpha_0 + p + 1;
             const double old = w_lambda;
             w_lambda = do_sample ? mt_gamma(g, a / 2.0) / (gm / 2.0) : a / gm;
             if (std::isnan(w_lambda) || std::isinf(w_lambda)) w_lambda = old;
-            double m = 0.0;
-            for (uint32_t i = 0; i < p; ++i) m += h_w[i];
+            double m = h_hs[2 * K + 1];
             m = (m + beta_0 * mu_0) / (p + beta_0);
             const double s2 = 1.0 / ((p + beta_0) * w_lambda);
             const double om = w_mu;
@@ -149,15 +153,15 @@ struct FMLearner {
     // fm_learn_mcmc.h:1011-1089 (a NaN / inf ends that draw's factor loop)
     template <class G>
     void draw_hyper_v(G& g) {
-        const double alpha_0 = 1.0, gamma_0 = 1.0, beta_0 = 1.0, mu_0 = 0.0;
+        const double alpha_0 = 1.0, beta_0 = 1.0, mu_0 = 0.0;
         if (!do_multilevel) {
             std::fill(v_mu.begin(), v_mu.end(), mu_0);
             return;
         }
+        // the sums over each column (device, the loops' order): gm from beta_0 (mu_f - mu_0)^2 +
+        // gamma_0 adding (v_fi - mu_f)^2, m = sum_i v_fi
         for (uint32_t f = 0; f < K; ++f) {
-            const double* v = h_v.data() + (size_t)f * p;
-            double gm = beta_0 * (v_mu[f] - mu_0) * (v_mu[f] - mu_0) + gamma_0;
-            for (uint32_t i = 0; i < p; ++i) gm += (v[i] - v_mu[f]) * (v[i] - v_mu[f]);
+            const double gm = h_hs[2 * f];
             const double a = alpha_0 + p + 1;
             const double old = v_lambda[f];
             v_lambda[f] = do_sample ? mt_gamma(g, a / 2.0) / (gm / 2.0) : a / gm;
@@ -167,9 +171,7 @@ struct FMLearner {
             }
         }
         for (uint32_t f = 0; f < K; ++f) {
-            const double* v = h_v.data() + (size_t)f * p;
-            double m = 0.0;
-            for (uint32_t i = 0; i < p; ++i) m += v[i];
+            double m = h_hs[2 * f + 1];
             m = (m + beta_0 * mu_0) / (p + beta_0);
             const double s2 = 1.0 / ((p + beta_0) * v_lambda[f]);
             const double old = v_mu[f];
@@ -297,8 +299,20 @@ struct FMLearner {
             gather_sums(res, 2, s);  // every rank's {sum e^2, sum (e - w0)}, rank order
         else
             HIPCHK(hipMemcpyAsync(s, res, sizeof s, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(h_w.data(), d_w.p, (size_t)p * sizeof(double), hipMemcpyDeviceToHost, st));
-        if (K) HIPCHK(hipMemcpyAsync(h_v.data(), d_v.p, (size_t)K * p * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (do_multilevel) {
+            // the hyperparameter draws' column sums (fm_learn_mcmc.h:951-1089) on the device, in
+            // the host loops' order: w and v do not change before the draws that read them
+            const double beta_0 = 1.0, gamma_0 = 1.0, mu_0 = 0.0;
+            for (uint32_t c = 0; c <= K; ++c) {
+                const double mu = c < K ? v_mu[c] : w_mu;
+                h_mg[2 * c] = mu;
+                h_mg[2 * c + 1] = beta_0 * (mu - mu_0) * (mu - mu_0) + gamma_0;
+            }
+            HIPCHK(hipMemcpyAsync(d_hmg.p, h_mg.data(), h_mg.size() * sizeof(double), hipMemcpyHostToDevice, st));
+            HIPCHK(fmm_hsums(d_v.as<double>(), d_w.as<double>(), p, K, d_hmg.as<double2>(), d_hsum.as<double2>(), st));
+            HIPCHK(hipMemcpyAsync(h_hs.data(), d_hsum.p, h_hs.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+            ++n_launch;
+        }
         HIPCHK(hipStreamSynchronize(st));
         n_launch += 2;
         if (!do_multilevel) {
@@ -611,6 +625,10 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
     L->d_part.alloc((std::max<uint64_t>((nl + 255) / 256, 2 * ((nl + 1023) / 1024)) + 2) * sizeof(double));
     L->d_tpart.alloc((2 * ((nt + 255) / 256) + 2) * sizeof(double));
     L->d_res.alloc(8 * sizeof(double));
+    L->d_hmg.alloc(2 * ((size_t)K + 1) * sizeof(double));
+    L->d_hsum.alloc(2 * ((size_t)K + 1) * sizeof(double));
+    L->h_mg.assign(2 * ((size_t)K + 1), 0.0);
+    L->h_hs.assign(2 * ((size_t)K + 1), 0.0);
     L->d_scratch.alloc(((nl + 255) / 256 / 1024 + 16) * 2 * sizeof(double));
     L->v_mu.assign(K, 0.0);
     // fm_learn_mcmc::init (:1099-1116) and the -regular values (libfm.cpp:484-513)
@@ -628,6 +646,8 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
     if (K) HIPCHK(hipMemcpyAsync(L->d_v.p, L->h_v.data(), (size_t)K * p * sizeof(double), hipMemcpyHostToDevice, st));
     L->predict_train();
     HIPCHK(hipStreamSynchronize(st));
+    std::vector<double>().swap(L->h_v);  // the host copies served the upload only
+    std::vector<double>().swap(L->h_w);
     for (auto& e : L->ev) HIPCHK(hipEventCreate(&e));
     return L.release();
 }

@@ -80,6 +80,10 @@ hipError_t fmm_wpass(const FMPassArgs& a, int threads_per_row, hipStream_t st);
 hipError_t fmm_vpass(const FMPassArgs& a, int threads_per_row, hipStream_t st);
 // part[b] = {sum e^2, sum (e - w0)} over 1024-case blocks
 hipError_t fmm_esums(const double* e, uint64_t n, double w0, double* part, hipStream_t st);
+// the hyperparameter sums {gm, m} of each v column (out[f]) and of w (out[K]) in the host's
+// order; mg[c] = {mu, gm's initial value} (fm_learn_mcmc.h:951-1089)
+hipError_t fmm_hsums(const double* v, const double* w, uint32_t p, uint32_t K, const double2* mg, double2* out,
+                     hipStream_t st);
 // e[q] -= d (the w0 update, :663-666)
 hipError_t fmm_shift(double* e, uint64_t n, double d, hipStream_t st);
 // [K][p] -> [p][Kp] (attribute-major rows for the predictions)

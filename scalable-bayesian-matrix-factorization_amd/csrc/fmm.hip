@@ -268,6 +268,63 @@ __global__ __launch_bounds__(256) void k_fmm_esums(const double* __restrict__ e,
     }
 }
 
+// The sums the hyperparameter draws of fm_learn_mcmc.h:951-1089 take over one column of the
+// model (v column f for blockIdx f < K, w for blockIdx K), in the host loop's order: one
+// sequential chain each, gm from its initial value (beta_0 (mu - mu_0)^2 + gamma_0, host)
+// adding (x_i - mu)^2 for i = 0..p-1, and m from 0 adding x_i -- so the result is the host
+// loop's, bit for bit (no contraction).  The whole workgroup stages 2048-value chunks of the
+// column and their squared deviations in LDS (double-buffered); thread 0 runs both chains.
+__global__ __launch_bounds__(256) void k_fmm_hsums(const double* __restrict__ v, const double* __restrict__ w,
+                                                   uint32_t p, uint32_t K, const double2* __restrict__ mg,
+                                                   double2* __restrict__ out) {
+#pragma clang fp contract(off)
+    constexpr uint32_t CH = 2048;
+    __shared__ double xs[2][CH], ds[2][CH];
+    const uint32_t c = blockIdx.x;
+    const double* __restrict__ x = c < K ? v + (size_t)c * p : w;
+    const double mu = mg[c].x;
+    double gm = mg[c].y, m = 0.0;
+    const uint32_t nch = (p + CH - 1) / CH;
+    auto stage = [&](uint32_t ch, int b) {
+        for (uint32_t i = threadIdx.x; i < CH; i += 256) {
+            const uint64_t q = (uint64_t)ch * CH + i;
+            const double t = q < p ? x[q] : 0.0;
+            const double d = t - mu;
+            xs[b][i] = t;
+            ds[b][i] = d * d;
+        }
+    };
+    stage(0, 0);
+    __syncthreads();
+    for (uint32_t ch = 0; ch < nch; ++ch) {
+        const int b = ch & 1;
+        if (ch + 1 < nch) stage(ch + 1, b ^ 1);
+        if (threadIdx.x == 0) {
+            const uint32_t n = min(CH, p - ch * CH);
+            uint32_t j = 0;
+            for (; j + 16 <= n; j += 16) {
+                double tx[16], td[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    tx[u] = xs[b][j + u];
+                    td[u] = ds[b][j + u];
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    gm = gm + td[u];
+                    m = m + tx[u];
+                }
+            }
+            for (; j < n; ++j) {
+                gm = gm + ds[b][j];
+                m = m + xs[b][j];
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[c] = make_double2(gm, m);
+}
+
 __global__ __launch_bounds__(256) void k_fmm_shift(double* __restrict__ e, uint64_t n, double d) {
     const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (q < n) e[q] -= d;
@@ -479,6 +536,13 @@ hipError_t fmm_vpass(const FMPassArgs& a, int tpr, hipStream_t st) { return laun
 hipError_t fmm_esums(const double* e, uint64_t n, double w0, double* part, hipStream_t st) {
     if (n == 0) return hipSuccess;
     k_fmm_esums<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(e, n, w0, part);
+    return hipGetLastError();
+}
+
+hipError_t fmm_hsums(const double* v, const double* w, uint32_t p, uint32_t K, const double2* mg, double2* out,
+                     hipStream_t st) {
+    if (p == 0) return hipSuccess;
+    k_fmm_hsums<<<K + 1, 256, 0, st>>>(v, w, p, K, mg, out);
     return hipGetLastError();
 }
 
