@@ -301,6 +301,7 @@ struct sbmf_ctx {
     DBuf d_U, d_V, d_Eu, d_Ev, d_zU, d_zV, d_hyper;
     DBuf d_rowsq_u, d_rowtr_u, d_rowsq_v, d_rowtr_v;
     DBuf d_colpart, d_res, d_scratch;
+    size_t scratch_half = 0;  // doubles: d_scratch + scratch_half is the evaluation's
 
     bool kprof = false; // SBMF_KPROF=1: streaming-kernel phase cycles printed per sweep
     int kprof_set = 0;  // SBMF_KPROF_SET: which streaming launch of a half is stamped (0: the 8-wave one)
@@ -611,7 +612,9 @@ static void prepare_T(sbmf_ctx* c) {
     c->pre.valid = false;
     c->hyper_ahead = false;
     const uint64_t big = std::max<uint64_t>({(uint64_t)c->I, (uint64_t)c->J, c->su.size() / 128 + 2});
-    c->d_scratch.alloc((big / 1024 + 16) * 2 * sizeof(double));
+    // two halves: the prologue's sums and the evaluation's, which run side by side (one rank)
+    c->d_scratch.alloc((big / 1024 + 16) * 4 * sizeof(double));
+    c->scratch_half = (big / 1024 + 16) * 2;
     // test set
     const uint64_t T_ = c->su.size();
     upload(c->d_tu, c->su, st);
@@ -1314,7 +1317,8 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 const uint32_t nb = (uint32_t)((T_ + 255) / 256);
                 HIPCHK(launch_sum_cols(c->d_tpart.as<double>(), nb, 2, d_res + RES_TEST_AVG, se));
             }
-            if (cf.eval_train) HIPCHK(launch_sum(c->d_rowtr_v.as<double>(), c->J, d_res + RES_TRSQ, scratch, se));
+            if (cf.eval_train)
+                HIPCHK(launch_sum(c->d_rowtr_v.as<double>(), c->J, d_res + RES_TRSQ, scratch + c->scratch_half, se));
             HIPCHK(hipEventRecord(c->ev[6], se));
         };
         if (par_eval) {

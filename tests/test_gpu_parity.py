@@ -134,9 +134,12 @@ def test_evaluation_order_changes_nothing(ml100k):
     stream.  Both read U and V only and write different slots: the chain, the
     printed RMSEs and the factors are the same bit for bit."""
     tr, te = ml100k
-    a = _run(tr, te, 4, num_factor=30, seed=8, rng="philox")  # the overlapped schedule (device RNG)
-    b = _run(tr, te, 4, num_factor=30, seed=8, rng="philox", tune=1 << 28)
+    kw = dict(num_factor=30, seed=8, rng="philox", eval_train=True)  # the overlapped schedule (device RNG)
+    a = _run(tr, te, 4, **kw)
+    b = _run(tr, te, 4, tune=1 << 28, **kw)
     assert np.array_equal(a.rmse_trajectory, b.rmse_trajectory)
+    # the train RMSE's sum runs beside the prologue's (separate scratch areas)
+    assert np.array_equal([h["rmse_train"] for h in a.history], [h["rmse_train"] for h in b.history])
     for x, y in zip(a.factors(), b.factors()):
         assert np.array_equal(x, y)
 
