@@ -142,10 +142,15 @@ def measure(args, world, rank, local, precision, train, test, uid):
     t0 = time.perf_counter()
     from sbmf._lib import NKIND
     kern_ms = np.zeros((2, NKIND))
-    for _ in range(args.steps):
-        L.learn(sweeps=1)
+
+    def per_sweep(_rec):  # each sweep's launch-kind times (HIP events), read from the callback
         t = L.timing()
-        kern_ms += np.array([[t.kern_ms[s][k] for k in range(NKIND)] for s in range(2)])
+        kern_ms[:] += np.array([[t.kern_ms[s][k] for k in range(NKIND)] for s in range(2)])
+        return False
+
+    # one run of K sweeps (sweep s+1's start is queued at the end of sweep s; the Gram-block
+    # kinds are timed on the run's first sweep, the streaming kind on every sweep)
+    L.learn(sweeps=args.steps, callback=per_sweep)
     device_sync()
     barrier(world)
     dt = time.perf_counter() - t0

@@ -232,7 +232,9 @@ int sbmf_get_biases(sbmf_ctx* ctx, double* bu, double* bv, double* b0);
  *         workgroups) ratings held in VGPRs -- whole rows, or chunks of longer
  *         rows on co-resident workgroups -- plus the publish of split rows,
  *   6..10 reserved (the removed per-coordinate and full-Gram row kernels: 0).
- * kern_bytes is the
+ * kern_ms of the streaming kind is the last sweep's; those of kinds 0..4 are timed on
+ * the first sweep of each sbmf_run call and kept (an event between two launches on a
+ * stream leaves the device idle for microseconds).  kern_bytes is the
  * algorithmic traffic of that launch per SURVEY.md §8(d): per rating
  * s*K (partner row) + 4 (partner id) + s (residual), per row 2*s*K (own row
  * read + write), s = 4 (f32) or 8 (f64). */

@@ -308,6 +308,8 @@ struct sbmf_ctx {
     DBuf d_kprof;
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
     DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
+    bool xcnt_clean = false;  // d_xcnt zeroed (queued) since its last use: the next streaming stage skips its clear
+    bool time_kinds = true;   // this sweep records every launch kind's events (else the streaming kind's only)
     size_t xset_nx = 1, xset_nr = 1;  // set 0's split chunks / rows: set 1's areas follow them
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
     DBuf d_uperm2, d_vperm2, d_uunpack, d_vunpack, d_xrecv;  // multi-GPU residual exchange
@@ -564,6 +566,7 @@ static void prepare_T(sbmf_ctx* c) {
         // is one fill kernel (a ragged size is three, and on a stream beside a persistent
         // launch the tail one waited for that launch: r04s4 trace)
         c->d_xcnt.alloc((nr * nblk + 2 + 3) / 4 * 4 * sizeof(uint32_t));
+        c->xcnt_clean = false;
         c->d_xchunk_sq.alloc(nx * sizeof(double));
         c->d_xchunk_tr.alloc(nx * sizeof(double));
         HIPCHK(hipMemsetAsync(c->d_xchunk_tr.p, 0, c->d_xchunk_tr.bytes, st));
@@ -941,7 +944,9 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     for (int k = 0; k < NBIN; ++k) others |= k != KIND_STREAM && !g.bin_rows[k].empty();
     const bool ovl = !(c->cfg.tune & 0x20000000u) && others && !g.bin_rows[KIND_STREAM].empty();
     // the split-row counters and queue heads of both stream sets, zeroed before the fork
-    if (!g.bin_rows[KIND_STREAM].empty()) HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
+    // (cleared at the end of the previous streaming stage on this stream, off the path, unless not)
+    if (!g.bin_rows[KIND_STREAM].empty() && !c->xcnt_clean) HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
+    if (!g.bin_rows[KIND_STREAM].empty()) c->xcnt_clean = false;
     if (ovl) {
         HIPCHK(hipEventRecord(c->oev[0], st));
         HIPCHK(hipStreamWaitEvent(c->sto, c->oev[0], 0));
@@ -955,10 +960,18 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     for (int k = NBIN - 1; k >= 0; --k) {
         if (g.bin_rows[k].empty()) continue;
         st = ovl && k != KIND_STREAM ? c->sto : c->st;
+        // launch-kind events: the streaming kind's every sweep (the bench's roofline), the
+        // others' on the first sweep of a run only (each event between two launches on a
+        // stream leaves the device idle ~6 us)
+        const bool timed = c->time_kinds || k == KIND_STREAM;
         int& lk = last[st == c->st ? 0 : 1];
-        c->kpv(stage, sd, k) = (int8_t)lk;
-        if (lk < 0) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
-        lk = k;
+        if (timed) {
+            c->kpv(stage, sd, k) = (int8_t)lk;
+            if (lk < 0) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
+            lk = k;
+        } else {
+            lk = -1;  // no end event behind this launch
+        }
         if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
             for (const auto& gs : g.gsub[k])
                 HIPCHK(launch_gblock_nw<T>((int)gs[0], g.d_bins[k].as<uint32_t>() + gs[1], gs[2], a, st));
@@ -994,7 +1007,11 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 HIPCHK(hipStreamWaitEvent(st, c->oev[2], 0));
             }
         }
-        HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
+        if (timed) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
+        if (k == KIND_STREAM && c->d_xcnt.p) {  // the next streaming stage's counters, cleared now
+            HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
+            c->xcnt_clean = true;
+        }
         c->timing.n_launch++;
     }
     if (ovl) {
@@ -1225,6 +1242,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         HIPCHK(hipEventRecord(c->hev, st));
     };
     for (uint32_t it = 0; it < nsweeps; ++it) {
+        c->time_kinds = it == 0;  // every launch kind timed on the first sweep of the run
         c->timing.n_launch = 0;
         HIPCHK(hipEventRecord(c->ev[0], st));
         double d0;
@@ -1435,6 +1453,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         for (int sd = 0; sd < 2; ++sd) {
             const Side& sdd = sd == 0 ? c->users : c->items;
             for (int k = 0; k < SBMF_NKIND; ++k) {
+                if (!c->time_kinds && k != KIND_STREAM) continue;  // kept from the run's first sweep
                 double ms = 0.0;
                 for (uint32_t p = 0; p < c->nstages; ++p) {
                     const Side::Stage& g = *sdd.stg[p];
