@@ -263,6 +263,7 @@ struct sbmf_ctx {
     Side users, items;
     uint64_t t0 = 0, t1 = 0;  // owned test range
     std::vector<uint64_t> tbounds, tbblocks;  // every rank's test range (ratings, 256-blocks)
+    std::vector<uint64_t> tperm;  // device test order (user order) -> file order
     // hyper state (fp64 host copy)
     std::vector<double> sig_u, mu_u, sig_v, mu_v;
     double tau = 1.0;
@@ -618,11 +619,30 @@ static void prepare_T(sbmf_ctx* c) {
     // two halves: the prologue's sums and the evaluation's, which run side by side (one rank)
     c->d_scratch.alloc((big / 1024 + 16) * 4 * sizeof(double));
     c->scratch_half = (big / 1024 + 16) * 2;
-    // test set
+    // test set, on the device in user order (a counting sort, stable: file order within a
+    // user), so the evaluation's consecutive ratings share their user's row in cache; the
+    // file order comes back through tperm in sbmf_predict.  The RMSE partial sums run in
+    // this order.
     const uint64_t T_ = c->su.size();
-    upload(c->d_tu, c->su, st);
-    upload(c->d_ti, c->si, st);
-    upload(c->d_tr, c->sr, st);
+    {
+        std::vector<uint64_t> start((size_t)c->I + 1, 0);
+        for (uint64_t x = 0; x < T_; ++x) ++start[c->su[x] + 1];
+        for (uint32_t u = 0; u < c->I; ++u) start[u + 1] += start[u];
+        c->tperm.resize(T_);
+        std::vector<uint32_t> su2(T_), si2(T_);
+        std::vector<double> sr2(T_);
+        for (uint64_t x = 0; x < T_; ++x) {
+            const uint64_t j = start[c->su[x]]++;
+            c->tperm[j] = x;
+            su2[j] = c->su[x];
+            si2[j] = c->si[x];
+            sr2[j] = c->sr[x];
+        }
+        upload(c->d_tu, su2, st);
+        upload(c->d_ti, si2, st);
+        upload(c->d_tr, sr2, st);
+        HIPCHK(hipStreamSynchronize(st));  // the sorted copies are locals
+    }
     c->d_tsum.alloc(std::max<uint64_t>(T_, 1) * sizeof(double));
     HIPCHK(hipMemsetAsync(c->d_tsum.p, 0, c->d_tsum.bytes, st));
     c->d_tpart.alloc(((T_ + 255) / 256 + 1) * 2 * sizeof(double));
@@ -1779,9 +1799,10 @@ int sbmf_predict(sbmf_ctx* ctx, double* out) {
     const uint64_t T_ = ctx->su.size();
     if (ctx->nranks > 1) ctx->comm.bcast_ranges(ctx->d_tsum.p, sizeof(double), ctx->tbounds, ctx->st);
     HIPCHK(hipStreamSynchronize(ctx->st));
-    HIPCHK(hipMemcpy(out, ctx->d_tsum.p, T_ * sizeof(double), hipMemcpyDeviceToHost));
+    std::vector<double> h(T_);
+    HIPCHK(hipMemcpy(h.data(), ctx->d_tsum.p, T_ * sizeof(double), hipMemcpyDeviceToHost));
     const double div = sbmf::avg_collected(ctx->cfg) ? (double)std::max(1u, ctx->collected) : (double)std::max(1u, ctx->sweep);
-    for (uint64_t t = 0; t < T_; ++t) out[t] /= div;
+    for (uint64_t j = 0; j < T_; ++j) out[ctx->tperm[j]] = h[j] / div;  // device (user) order -> file order
     API_END(ctx)
 }
 
