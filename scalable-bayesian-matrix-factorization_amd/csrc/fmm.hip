@@ -273,17 +273,19 @@ __global__ __launch_bounds__(256) void k_fmm_esums(const double* __restrict__ e,
 // sequential chain each, gm from its initial value (beta_0 (mu - mu_0)^2 + gamma_0, host)
 // adding (x_i - mu)^2 for i = 0..p-1, and m from 0 adding x_i -- so the result is the host
 // loop's, bit for bit (no contraction).  The whole workgroup stages 2048-value chunks of the
-// column and their squared deviations in LDS (double-buffered); thread 0 runs both chains.
+// column and their squared deviations in LDS (double-buffered); lane 0 runs the gm chain and
+// lane 1 the m chain, side by side in one instruction stream.
 __global__ __launch_bounds__(256) void k_fmm_hsums(const double* __restrict__ v, const double* __restrict__ w,
                                                    uint32_t p, uint32_t K, const double2* __restrict__ mg,
                                                    double2* __restrict__ out) {
 #pragma clang fp contract(off)
     constexpr uint32_t CH = 2048;
-    __shared__ double xs[2][CH], ds[2][CH];
+    __shared__ __align__(16) double xs[2][CH];
+    __shared__ __align__(16) double ds[2][CH];
     const uint32_t c = blockIdx.x;
     const double* __restrict__ x = c < K ? v + (size_t)c * p : w;
     const double mu = mg[c].x;
-    double gm = mg[c].y, m = 0.0;
+    double acc = threadIdx.x == 0 ? mg[c].y : 0.0;  // lane 0: gm, lane 1: m
     const uint32_t nch = (p + CH - 1) / CH;
     auto stage = [&](uint32_t ch, int b) {
         for (uint32_t i = threadIdx.x; i < CH; i += 256) {
@@ -299,30 +301,28 @@ __global__ __launch_bounds__(256) void k_fmm_hsums(const double* __restrict__ v,
     for (uint32_t ch = 0; ch < nch; ++ch) {
         const int b = ch & 1;
         if (ch + 1 < nch) stage(ch + 1, b ^ 1);
-        if (threadIdx.x == 0) {
+        if (threadIdx.x < 2) {
+            const double* __restrict__ src = threadIdx.x == 0 ? ds[b] : xs[b];
             const uint32_t n = min(CH, p - ch * CH);
             uint32_t j = 0;
-            for (; j + 16 <= n; j += 16) {
-                double tx[16], td[16];
+            for (; j + 32 <= n; j += 32) {
+                double2 t[16];  // 16-byte LDS reads, all issued before the first add
+#pragma unroll
+                for (int u = 0; u < 16; ++u) t[u] = reinterpret_cast<const double2*>(src + j)[u];
 #pragma unroll
                 for (int u = 0; u < 16; ++u) {
-                    tx[u] = xs[b][j + u];
-                    td[u] = ds[b][j + u];
-                }
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    gm = gm + td[u];
-                    m = m + tx[u];
+                    acc = acc + t[u].x;
+                    acc = acc + t[u].y;
                 }
             }
-            for (; j < n; ++j) {
-                gm = gm + ds[b][j];
-                m = m + xs[b][j];
-            }
+            for (; j < n; ++j) acc = acc + src[j];
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[c] = make_double2(gm, m);
+    __shared__ double res[2];
+    if (threadIdx.x < 2) res[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[c] = make_double2(res[0], res[1]);
 }
 
 __global__ __launch_bounds__(256) void k_fmm_shift(double* __restrict__ e, uint64_t n, double d) {
