@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--no-ttr", action="store_true", help="skip the time-to-RMSE runs")
     ap.add_argument("--no-load", action="store_true", help="skip the text / binary load timing")
     ap.add_argument("--tune", type=int, default=0, help="kernel-variant bits (sbmf_config.tune)")
-    ap.add_argument("--split-chunk", type=int, default=0, help="streaming task size (0 = LDS capacity)")
+    ap.add_argument("--split-chunk", type=int, default=0, help="streaming task size (0 = the register capacity of the workgroup shape: 512 / 1024 / 2048 f64 ratings for 4 / 8 / 16 waves)")
     ap.add_argument("--stream-threshold", type=int, default=0, help="rows above this use the streaming kernel")
     ap.add_argument("--device", type=int, default=-1,
                     help="HIP device for every rank (testing only; default: LOCAL_RANK)")

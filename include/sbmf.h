@@ -127,16 +127,16 @@ typedef struct sbmf_config {
                                  bit 17 = k_gres on 16-wave workgroups (both sides),
                                  bit 23 = f64 user streaming rows on 8-wave k_gres workgroups
                                           (default: 4-wave, 512-rating tasks),
-                                 bit 24 = k_gres as an ordinary launch instead of a cooperative one
-                                          (set internally under the launch overlap),
+                                 bit 24 = k_gres as a cooperative launch (experiments only; the
+                                          default is an ordinary launch in every schedule: tasks are
+                                          claimed in queue order, no co-residency needed),
                                  bit 26 = no overlap of the next sweep's prologue (sums, column
                                           statistics, host draws) with the test evaluation
                                           (Philox mode; the chain is the same either way),
                                  bit 27 = f64 item rows on 8-wave k_gres workgroups (default:
                                           rows > 1024 ratings on 16-wave ones, the rest 8-wave),
                                  bit 29 = a half's Gram-block launches after its streaming launch
-                                          on one stream (default: on a second stream beside it,
-                                          the streaming launch then an ordinary one as bit 24),
+                                          on one stream (default: on a second stream beside it),
                                  bit 30 = a half's two streaming sets (items: rows > 1024 and the
                                           rest) one after the other (default: side by side),
                                  bit 28 = (one rank) the test evaluation after the next sweep's
@@ -306,7 +306,7 @@ int sbmf_partition_rows(const uint32_t* ptr, uint32_t R, int nranks, uint64_t* b
  * with RCCL linked at load time, and libsbmf now loads RCCL (dlopen) only for a
  * multi-GPU communicator, so a single-GPU process of the default schedule exits
  * normally under rocprofv3; a process that launched k_gres cooperatively (tune
- * bit 29) still faults there. */
+ * bit 24, experiments only since round 5) faulted there. */
 int sbmf_exit_guard(int rc);
 
 /* --- test hooks ---------------------------------------------------------------------------- */
@@ -315,6 +315,37 @@ int sbmf_exit_guard(int rc);
 int sbmf_ref_stream(uint32_t seed, int kind, double shape, uint64_t n, double* out);
 /* Philox normals as the kernels draw them: z for (seed, sweep, tag, row, k<K). out [K]. */
 int sbmf_philox_normals(uint64_t seed, uint32_t sweep, uint32_t tag, uint32_t row, uint32_t K, double* out);
+
+/* Timing only: make this context rank `rank` of an `nranks`-rank sampler run on
+ * its one GPU, with every exchange skipped (no communicator: other ranks' rows
+ * keep their initial values, residuals from other ranks read as 0).  The rank
+ * runs exactly its own row blocks, stages, bins and streaming tasks, so its
+ * device time is the per-rank compute of the multi-GPU schedule; its numbers are
+ * not a chain.  Before sbmf_prepare; the SBPMF sampler only. */
+int sbmf_test_virtual_rank(sbmf_ctx* ctx, int nranks, int rank);
+/* A virtual rank's device time per stage of the last sweep's halves
+ * (HIP events on the compute stream): ms[side * nstages + stage]. */
+int sbmf_test_stage_ms(sbmf_ctx* ctx, double* ms, uint32_t cap, uint32_t* nstages);
+/* RCCL self-test on one GPU (a prepared one-rank sampler context after at least
+ * one sweep): a one-rank RCCL communicator through the library's own dlopen /
+ * dlsym table issues, per repetition and on the multi-GPU comm stream, the
+ * exchange's calls -- one group of three in-place ncclBroadcast over adjacent
+ * blocks of an nbytes buffer, the grouped ncclSend / ncclRecv of the residual
+ * exchange (to the rank itself), an ncclAllGather of nbytes/4 -- while the item
+ * half's persistent k_gres grids run on the compute streams.  Every byte is
+ * checked; the comm stream must finish within deadline_s (else SBMF_E_COMM). */
+typedef struct sbmf_rccl_selftest {
+    double ms_half;        /* the repetitions' item halves on the compute stream          */
+    double ms_rccl;        /* the RCCL calls on the comm stream, first to last            */
+    double ms_rccl_end;    /* from the first half's start to the last RCCL call's end     */
+    uint64_t bad_bcast;    /* bytes the in-place broadcasts changed (must be 0)           */
+    uint64_t bad_p2p;      /* received bytes that differ from the sent ones               */
+    uint64_t bad_allgather;
+    uint32_t n_calls;      /* RCCL collective / point-to-point calls issued               */
+    uint32_t overlapped;   /* 1: the RCCL calls finished while the halves were running    */
+} sbmf_rccl_selftest;
+int sbmf_test_rccl_selftest(sbmf_ctx* ctx, uint64_t nbytes, uint32_t reps, double deadline_s,
+                            sbmf_rccl_selftest* out);
 
 #ifdef __cplusplus
 }

@@ -32,7 +32,18 @@ Fixtures written (all data, no reference source):
   ref_bias2_ml1msynth_k20_s1.txt              the top-level biased gibbs_sbpmf2.cpp on that set:
                                               stalls at the bias-only fit
   ref_libfm_rlog_header_k20_g2.txt            bin/libFM's -rlog header (MCMC, K=20, two -meta groups)
-`make_golden.py vbo` / `make_golden.py libfm` / `make_golden.py rlog` / `make_golden.py collapse` regenerate
+  m1m100k_{train,test}_libfm.gz               the reference's own data/m1m/m100k/{train,test}_libfm
+                                              (users 0..942, items at their raw feature ids 943..2624)
+  ref_libfm_<method>_m1m100k_d118_s1_i10.txt  bin/libFM on those files with its exact argv
+                                              (-task r -dim '1,1,8' -iter 10 -method mcmc, and -method als
+                                              -regular '0,0,10'), time() pinned to 1; + _pred.txt.gz
+  ref_final_<data>_k20_seeds<N>.txt           gibbs_sbpmf_final over seeds 1..N (ml100k N=64, the ML-1M-shaped
+                                              synthetic set N=32): one line per seed, the first 20 sweeps'
+                                              running-mean test RMSE ("%.17g"), for the statistical check of
+                                              the throughput (Philox) chain against the reference chain
+  ref_final_m1m100k_k20_s1.txt                gibbs_sbpmf_final on the reference's converted
+                                              data/m1m/m100k/{train,test}_sbpmf (raw item ids kept)
+`make_golden.py seeds` / `make_golden.py refdata` / `make_golden.py vbo` / `make_golden.py libfm` / `make_golden.py rlog` / `make_golden.py collapse` regenerate
 only those fixtures.
 Only runnable in the build container (needs /root/reference).
 """
@@ -191,6 +202,78 @@ def libfm_goldens():
     shutil.rmtree(root)
 
 
+def refdata_goldens():
+    """bin/libFM and gibbs_sbpmf_final on the reference's own MovieLens files
+    data/m1m/m100k/{train,test}_libfm (libFM text: users first, items at raw
+    feature ids >= 943) and the {train,test}_sbpmf triples its
+    create_file_scalable_bpmf.py writes from them (raw ids kept).  libFM's argv
+    is exactly the one a user runs: no offsets, no seed (time() pinned to 1 =
+    sbmf's default -seed)."""
+    src = os.path.join(REF, "data", "m1m", "m100k")
+    for nm in ("train_libfm", "test_libfm"):
+        with open(os.path.join(src, nm), "rb") as f, \
+                gzip.GzipFile(os.path.join(GOLD, "m1m100k_%s.gz" % nm), "wb", mtime=0) as g:
+            g.write(f.read())
+    root = "/tmp/sbmf_refdata_%d" % os.getpid()
+    os.makedirs(root, exist_ok=True)
+    for nm in ("train_libfm", "test_libfm"):
+        shutil.copy(os.path.join(src, nm), os.path.join(root, nm))
+    for method, extra in (("mcmc", []), ("als", ["-regular", "0,0,10"])):
+        cmd = [os.path.join(HERE, "_ref", "libFM"), "-task", "r", "-train", "train_libfm", "-test", "test_libfm",
+               "-dim", "1,1,8", "-iter", "10", "-method", method, "-out", "pred.txt"] + extra
+        p = subprocess.run(cmd, cwd=root, env=dict(os.environ, LIBFM_PIN_TIME="1"), capture_output=True, text=True,
+                           check=True)
+        lines = [l for l in p.stdout.splitlines() if l.startswith("#Iter=")]
+        assert len(lines) == 10, p.stdout[-500:]
+        name = libfm_name(method, "m1m100k", "1,1,8", 1, 10)
+        with open(os.path.join(GOLD, name + ".txt"), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        with open(os.path.join(root, "pred.txt"), "rb") as f, \
+                gzip.GzipFile(os.path.join(GOLD, name + "_pred.txt.gz"), "wb", mtime=0) as g:
+            g.write(f.read())
+        print("golden libfm", name, lines[-1])
+    shutil.rmtree(root)
+    vals = run_ref(os.path.join(HERE, "_ref", "gibbs_sbpmf_final"), os.path.join(src, "train_sbpmf"),
+                   os.path.join(src, "test_sbpmf"), 1)
+    assert len(vals) == 100
+    with open(os.path.join(GOLD, "ref_final_m1m100k_k20_s1.txt"), "w") as f:
+        f.write("\n".join(vals) + "\n")
+    print("golden final m1m100k", vals[0], vals[-1])
+
+
+SEED_RUNS = [("ml100k", 64), ("ml1msynth", 32)]
+
+
+def seeds_goldens():
+    """The reference chain's seed-to-seed spread: gibbs_sbpmf_final (K=20) on
+    ML-100k for seeds 1..64 and on the ML-1M-shaped synthetic set for seeds 1..32,
+    the first 20 sweeps of each (before the ML-1M-shaped chain's collapse near
+    sweep 40).  tests/test_gpu_statistical.py compares the seed means of the
+    throughput-mode chains with these."""
+    sys.path.insert(0, os.path.join(REPO, "scalable-bayesian-matrix-factorization_amd"))
+    from sbmf import synth
+    root = "/tmp/sbmf_seeds_%d" % os.getpid()
+    os.makedirs(root, exist_ok=True)
+    tr, te, _ = synth.generate("ml-1m")
+    paths = {"ml100k": (os.path.join(REF, "data", "m100k", "train_sbpmf"), os.path.join(REF, "data", "m100k", "test_sbpmf"))}
+    pp = []
+    for nm, (u, i, r) in (("train", tr), ("test", te)):
+        pth = os.path.join(root, nm + ".tsv")
+        write_tsv(pth, zip(u.tolist(), i.tolist(), r.tolist()))
+        pp.append(pth)
+    paths["ml1msynth"] = tuple(pp)
+    for dname, n in SEED_RUNS:
+        rows = []
+        for seed in range(1, n + 1):
+            vals = run_ref(os.path.join(HERE, "_ref", "gibbs_sbpmf_final"), paths[dname][0], paths[dname][1], seed)
+            assert len(vals) == 100
+            rows.append(" ".join(vals[:20]))
+        with open(os.path.join(GOLD, "ref_final_%s_k20_seeds%d.txt" % (dname, n)), "w") as f:
+            f.write("\n".join(rows) + "\n")
+        print("golden seeds", dname, n)
+    shutil.rmtree(root)
+
+
 def rlog_golden():
     """bin/libFM's -rlog header for an MCMC run with two attribute groups (users,
     items: the SBPMF sampler's two hyperprior groups) at K=20: the compiled
@@ -264,6 +347,12 @@ def main():
         libfm_goldens()
         rlog_golden()
         return 0
+    if sys.argv[1:] == ["seeds"]:
+        seeds_goldens()
+        return 0
+    if sys.argv[1:] == ["refdata"]:
+        refdata_goldens()
+        return 0
     if sys.argv[1:] == ["rlog"]:
         rlog_golden()
         return 0
@@ -300,6 +389,8 @@ def main():
     vbo_goldens()
     libfm_goldens()
     rlog_golden()
+    refdata_goldens()
+    seeds_goldens()
     collapse_golden()
     return 0
 

@@ -149,8 +149,21 @@ void Comm::init(int nranks, int rank, const uint8_t id[128]) {
     comm_ = c;
 }
 
+void Comm::init_loopback() {
+    ncclUniqueId u;
+    ncclResult_t r = rccl().GetUniqueId(&u);
+    if (r != ncclSuccess) comm_fail("ncclGetUniqueId", r);
+    ncclComm_t c;
+    r = rccl().CommInitRank(&c, 1, u, 0);
+    if (r != ncclSuccess) comm_fail("ncclCommInitRank", r);
+    comm_ = c;
+    nranks_ = 1;
+    rank_ = 0;
+    loopback_ = true;
+}
+
 void Comm::bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_t>& bounds, hipStream_t st) {
-    if (nranks_ <= 1) return;
+    if (!live()) return;
     if (shm_) {  // host backend: windows of the whole range through the segment
         if (hipStreamSynchronize(st) != hipSuccess) throw std::runtime_error("hipStreamSynchronize failed");
         unsigned char* win = shm_ + kHostHeader;
@@ -191,7 +204,7 @@ void Comm::bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_
 
 void Comm::bcast_blocks(void* base, size_t unit_bytes, const std::vector<uint64_t>& starts,
                         const std::vector<uint64_t>& ends, hipStream_t st) {
-    if (nranks_ <= 1) return;
+    if (!live()) return;
     char* dev = static_cast<char*>(base);
     if (shm_) {  // host backend: each owner's block through the window, window by window
         if (hipStreamSynchronize(st) != hipSuccess) throw std::runtime_error("hipStreamSynchronize failed");
@@ -226,7 +239,7 @@ void Comm::bcast_blocks(void* base, size_t unit_bytes, const std::vector<uint64_
 
 void Comm::alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const std::vector<size_t>& scnt,
                      void* recvbuf, const std::vector<size_t>& roff, const std::vector<size_t>& rcnt, hipStream_t st) {
-    if (nranks_ <= 1) return;
+    if (!live()) return;
     if (shm_) {  // host backend: rank s publishes [offsets | its send buffer], every other rank takes its part
         if (hipStreamSynchronize(st) != hipSuccess) throw std::runtime_error("hipStreamSynchronize failed");
         unsigned char* win = shm_ + kHostHeader;
@@ -261,7 +274,7 @@ void Comm::alltoallv(const void* sendbuf, const std::vector<size_t>& soff, const
     ncclResult_t r = rccl().GroupStart();
     if (r != ncclSuccess) comm_fail("ncclGroupStart", r);
     for (int k = 0; k < nranks_; ++k) {
-        if (k == rank_) continue;
+        if (k == rank_ && !loopback_) continue;
         if (scnt[k]) {
             r = rccl().Send(static_cast<const char*>(sendbuf) + soff[k], scnt[k], ncclUint8, k, (ncclComm_t)comm_, st);
             if (r != ncclSuccess) comm_fail("ncclSend", r);
@@ -287,7 +300,7 @@ void Comm::group_end() {
 }
 
 void Comm::allgather(const void* sendbuf, size_t bytes, void* recvbuf, hipStream_t st) {
-    if (nranks_ <= 1) {
+    if (!live()) {
         if (bytes && hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
             throw std::runtime_error("allgather: copy failed");
         return;

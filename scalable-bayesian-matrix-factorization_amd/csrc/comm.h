@@ -26,6 +26,11 @@ class Comm {
     Comm& operator=(const Comm&) = delete;
     static void unique_id(uint8_t id[128]);
     void init(int nranks, int rank, const uint8_t id[128]);
+    // Test only (sbmf_test_rccl_selftest): a one-rank RCCL communicator whose calls
+    // are issued as with several ranks -- the block broadcasts with rank 0 as every
+    // owner, the point-to-point exchange including the rank itself -- so one GPU runs
+    // the exact RCCL calls of the exchange through the same dlsym table.
+    void init_loopback();
     bool active() const { return comm_ != nullptr || shm_ != nullptr; }
     // Rank k owns units [bounds[k], bounds[k+1]) of unit_bytes each, starting
     // at base; after the call every rank holds every rank's units.
@@ -52,7 +57,9 @@ class Comm {
 
   private:
     void host_barrier();
+    bool live() const { return nranks_ > 1 || loopback_; }
     void* comm_ = nullptr;  // ncclComm_t
+    bool loopback_ = false;
     unsigned char* shm_ = nullptr;  // host backend: [barrier header | window]
     size_t shm_bytes_ = 0;
     int sense_ = 0;

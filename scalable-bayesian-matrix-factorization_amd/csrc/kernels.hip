@@ -1695,9 +1695,10 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     // Tasks are claimed from a queue in list order by running workgroups, so only
     // the most recently claimed split row can have chunks still unclaimed, and its
     // waiting chunks (fewer than its chunk count, far below the resident
-    // workgroups) never block the claims that complete it: an ordinary launch.
-    // Tune bit 29 (no launch overlap) keeps the cooperative launch, which checks
-    // that the whole grid fits (the host sizes it to residency).
+    // workgroups) never block the claims that complete it: an ordinary launch in
+    // every schedule.  Tune bit 24 (experiments only) launches it cooperatively,
+    // which checks that the whole grid fits (the host sizes it to residency); a
+    // process that did so faulted in exit() under rocprofv3 (r04s16).
     const SplitTask* tp = tasks;
     HalfArgs<T> ap = a;
     SplitSync syp = sy;
@@ -1705,9 +1706,9 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     const void* fn = gstream_fn<T>(a.tune, a.tag == TAG_ITEMS ? 1u : 0u);
     const dim3 g(std::min(grid, ntask)), b(64 * gres_nw(a.tune));
     if (a.tune & 0x1000000u)
-        err = hipLaunchKernel(fn, g, b, args, 0, st);
-    else
         err = hipLaunchCooperativeKernel(fn, g, b, args, 0, st);
+    else
+        err = hipLaunchKernel(fn, g, b, args, 0, st);
     if (err != hipSuccess) return err;
     if (nsrow) {
         k_split_finish<T><<<nsrow, 64, 0, st>>>(srows, nsrow, a, sy);

@@ -24,6 +24,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sbmf.h"
@@ -295,6 +296,10 @@ struct sbmf_ctx {
     uint32_t nstages = 1;          // stages per half (see Side::Stage); > 1 only with several ranks
     hipStream_t stc = nullptr;     // multi-GPU: the exchange of stage p runs here while stage p+1 computes
     std::vector<hipEvent_t> sev;   // [side][stage]: stage computed (compute stream)
+    // sbmf_test_virtual_rank (timing only): one rank of an nranks-rank run on this GPU,
+    // every exchange skipped; tsev [side][stage + 1] times its stages on the compute stream
+    bool virt = false;
+    std::vector<hipEvent_t> tsev;
     hipEvent_t cev[2] = {};        // [side]: the half's exchange done (comm stream)
     hipStream_t sto = nullptr;     // a half's Gram-block launches, beside its streaming launch
     hipEvent_t oev[3] = {};        // [fork, join] of those launches, [2]: stream set 0 done
@@ -591,6 +596,7 @@ static void prepare_T(sbmf_ctx* c) {
         upload(c->d_uunpack, c->users.unpack, st);
         upload(c->d_vunpack, c->items.unpack, st);
         c->d_xrecv.alloc(std::max<size_t>(std::max(c->users.nrecv, c->items.nrecv), 1) * sizeof(T));
+        HIPCHK(hipMemsetAsync(c->d_xrecv.p, 0, c->d_xrecv.bytes, st));  // read as 0 by a virtual rank
     }
     HIPCHK(hipMemsetAsync(c->d_Eu.p, 0, c->d_Eu.bytes, st));
     HIPCHK(hipMemsetAsync(c->d_Ev.p, 0, c->d_Ev.bytes, st));
@@ -710,6 +716,9 @@ static void prepare_T(sbmf_ctx* c) {
     c->sev.assign((size_t)2 * c->nstages, nullptr);
     for (hipEvent_t& e : c->kevs) HIPCHK(hipEventCreate(&e));
     for (hipEvent_t& e : c->sev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t e : c->tsev) (void)hipEventDestroy(e);
+    c->tsev.assign(c->virt ? (size_t)2 * (c->nstages + 1) : 0, nullptr);
+    for (hipEvent_t& e : c->tsev) HIPCHK(hipEventCreate(&e));
     c->sweep = 0;
     c->collected = 0;
     fill_kernel_bytes(c);
@@ -957,9 +966,9 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     // launches fill the CU time the streaming launch's serial phases (solve,
     // split-row hand-offs) and its tail leave idle.  Rows of different bins are
     // disjoint and no launch reads another's outputs, so the results do not
-    // depend on the interleaving.  The streaming launch is then an ordinary one
-    // (tune bit 24): its claiming workgroups are resident by construction, while a
-    // cooperative launch would wait for the whole device.
+    // depend on the interleaving.  The streaming launch is an ordinary one in every
+    // schedule (its claiming workgroups are resident by construction; tune bit 24's
+    // cooperative launch, experiments only, would wait for the whole device).
     bool others = false;
     for (int k = 0; k < NBIN; ++k) others |= k != KIND_STREAM && !g.bin_rows[k].empty();
     const bool ovl = !(c->cfg.tune & 0x20000000u) && others && !g.bin_rows[KIND_STREAM].empty();
@@ -1018,7 +1027,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 sy.lim_chunk = (uint32_t)(c->d_xchunk_sq.bytes / sizeof(double) - ox);
                 sy.prof = c->kprof && set == c->kprof_set ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
                 HalfArgs<T> as = a;
-                as.tune = ovl ? S.tune | 0x1000000u : S.tune;
+                as.tune = S.tune;
                 HIPCHK(launch_gstream<T>(g.d_stasks[set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
                                          g.d_xrows[set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, ss));
             }
@@ -1120,9 +1129,12 @@ static void bcast_stage(sbmf_ctx* c, const Side& s, uint32_t p, void* base, size
 template <typename T, class F>
 static void run_half_pipelined(sbmf_ctx* c, bool users, F&& bcasts) {
     const int sd = users ? 0 : 1;
+    const size_t tb = (size_t)sd * (c->nstages + 1);
+    if (c->virt) HIPCHK(hipEventRecord(c->tsev[tb], c->st));
     for (uint32_t p = 0; p < c->nstages; ++p) {
         run_half<T>(c, users, p);
         if (c->nranks > 1) HIPCHK(hipEventRecord(c->sev[(size_t)sd * c->nstages + p], c->st));
+        if (c->virt) HIPCHK(hipEventRecord(c->tsev[tb + p + 1], c->st));
     }
     HIPCHK(hipEventRecord(c->ev[users ? 2 : 4], c->st));
     if (c->nranks <= 1) return;  // no exchange: ev[3] / ev[5] are not recorded (the sweep uses ev[2] / ev[4])
@@ -1506,6 +1518,8 @@ sbmf_ctx::~sbmf_ctx() {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : sev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : tsev)
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : cev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : oev)
@@ -1515,6 +1529,95 @@ sbmf_ctx::~sbmf_ctx() {
     if (stc) (void)hipStreamDestroy(stc);
     if (st) (void)hipStreamDestroy(st);
 }
+
+namespace sbmf {
+// sbmf_test_rccl_selftest: the exchange's RCCL calls through Comm's dlsym table on
+// a one-rank communicator, issued on the comm stream while the item half's
+// persistent k_gres grids (and its Gram-block launches) run on the compute
+// streams -- the situation of the pipelined multi-GPU half (stage p's exchange
+// beside stage p+1's compute), minus the peers.  Per repetition, one RCCL group of
+// three in-place ncclBroadcast calls over adjacent blocks of a patterned buffer
+// (as bcast_stage issues for U, the biases and the row sums), then the grouped
+// ncclSend / ncclRecv of alltoallv (here to the rank itself), then an
+// ncclAllGather.  Every byte is checked afterwards; the comm stream must finish
+// within the deadline.
+template <typename T>
+void rccl_selftest(sbmf_ctx* c, uint64_t nbytes, uint32_t reps, double deadline_s, sbmf_rccl_selftest* out) {
+    *out = sbmf_rccl_selftest{};
+    Comm loop;
+    loop.init_loopback();
+    const size_t n = (size_t)nbytes, nag = n / 4;
+    std::vector<uint8_t> pa(n), pb(n), pc(nag);
+    for (size_t x = 0; x < n; ++x) {
+        pa[x] = (uint8_t)(x * 2654435761u >> 13);
+        pb[x] = (uint8_t)(x * 40503u + 17u);
+    }
+    for (size_t x = 0; x < nag; ++x) pc[x] = (uint8_t)(x * 97u + 5u);
+    DBuf blk, snd, rcv, ags, agr;
+    blk.alloc(n);
+    snd.alloc(n);
+    rcv.alloc(n);
+    ags.alloc(nag);
+    agr.alloc(nag);
+    HIPCHK(hipMemcpy(blk.p, pa.data(), n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(snd.p, pb.data(), n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ags.p, pc.data(), nag, hipMemcpyHostToDevice));
+    HIPCHK(hipDeviceSynchronize());
+    hipEvent_t e[4];
+    for (hipEvent_t& x : e) HIPCHK(hipEventCreate(&x));
+    // three adjacent blocks of blk; the p2p segments [0, n/2) -> [n/2, n) and [n/2, n) -> [0, n/2)
+    const std::vector<uint64_t> b0{0}, b1{n / 3}, b2{2 * (n / 3)}, b3{n};
+    const std::vector<size_t> soff{0}, scnt{n / 2}, roff{n / 2}, rcnt{n / 2};
+    const std::vector<size_t> soff2{n / 2}, scnt2{n / 2}, roff2{0}, rcnt2{n / 2};
+    HIPCHK(hipEventRecord(e[0], c->st));
+    for (uint32_t r = 0; r < reps; ++r) {
+        run_half<T>(c, false, 0);  // the item half: persistent k_gres grids on st (+ sto)
+        if (r == 0) HIPCHK(hipEventRecord(e[2], c->stc));
+        loop.group_begin();
+        loop.bcast_blocks(blk.p, 1, b0, b1, c->stc);
+        loop.bcast_blocks(blk.p, 1, b1, b2, c->stc);
+        loop.bcast_blocks(blk.p, 1, b2, b3, c->stc);
+        loop.group_end();
+        loop.alltoallv(snd.p, r & 1 ? soff2 : soff, r & 1 ? scnt2 : scnt, rcv.p, r & 1 ? roff2 : roff,
+                       r & 1 ? rcnt2 : rcnt, c->stc);
+        loop.allgather(ags.p, nag, agr.p, c->stc);
+        out->n_calls += 3 + 2 + 1;
+    }
+    HIPCHK(hipEventRecord(e[1], c->st));
+    HIPCHK(hipEventRecord(e[3], c->stc));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(e[3]);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) fail(SBMF_E_COMM, "RCCL self-test: %s", hipGetErrorString(q));
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > deadline_s)
+            fail(SBMF_E_COMM, "RCCL self-test: the comm stream did not finish within %.1f s", deadline_s);
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    HIPCHK(hipEventSynchronize(e[1]));
+    float f = 0.f;
+    HIPCHK(hipEventElapsedTime(&f, e[0], e[1]));
+    out->ms_half = f;
+    HIPCHK(hipEventElapsedTime(&f, e[2], e[3]));
+    out->ms_rccl = f;
+    HIPCHK(hipEventElapsedTime(&f, e[0], e[3]));
+    out->ms_rccl_end = f;
+    for (hipEvent_t x : e) (void)hipEventDestroy(x);
+    std::vector<uint8_t> h(n);
+    HIPCHK(hipMemcpy(h.data(), blk.p, n, hipMemcpyDeviceToHost));
+    for (size_t x = 0; x < n; ++x) out->bad_bcast += h[x] != pa[x];
+    HIPCHK(hipMemcpy(h.data(), rcv.p, n, hipMemcpyDeviceToHost));
+    // even repetitions send snd[0, n/2) to rcv[n/2, n), odd ones snd[n/2, n) to rcv[0, n/2)
+    for (size_t x = 0; x < n; ++x) {
+        if (x < n / 2 && reps == 1) continue;  // never written
+        out->bad_p2p += h[x] != pb[x < n / 2 ? x + n / 2 : x - n / 2];
+    }
+    h.resize(nag);
+    HIPCHK(hipMemcpy(h.data(), agr.p, nag, hipMemcpyDeviceToHost));
+    for (size_t x = 0; x < nag; ++x) out->bad_allgather += h[x] != pc[x];
+    out->overlapped = out->ms_rccl_end < out->ms_half ? 1u : 0u;
+}
+}  // namespace sbmf
 
 #define API_BEGIN try {
 #define API_END(ctx)                                  \
@@ -1931,6 +2034,51 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
     ctx->nranks = nranks;
     ctx->rank = rank;
     if (nranks > 1) ctx->comm.init(nranks, rank, id);
+    API_END(ctx)
+}
+
+int sbmf_test_virtual_rank(sbmf_ctx* ctx, int nranks, int rank) {
+    API_BEGIN
+    if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (ctx->prepared) sbmf::fail(SBMF_E_STATE, "sbmf_test_virtual_rank must precede sbmf_prepare");
+    if (nranks < 2 || rank < 0 || rank >= nranks) sbmf::fail(SBMF_E_ARG, "bad rank %d / %d", rank, nranks);
+    if (ctx->cfg.method != SBMF_METHOD_MCMC) sbmf::fail(SBMF_E_ARG, "virtual ranks: the SBPMF sampler only");
+    if (ctx->comm.active()) sbmf::fail(SBMF_E_STATE, "context already joined a communicator");
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    ctx->virt = true;
+    API_END(ctx)
+}
+
+int sbmf_test_stage_ms(sbmf_ctx* ctx, double* ms, uint32_t cap, uint32_t* nstages) {
+    API_BEGIN
+    if (!ctx || !nstages) sbmf::fail(SBMF_E_ARG, "null argument");
+    if (!ctx->virt || !ctx->prepared) sbmf::fail(SBMF_E_STATE, "stage times need a prepared virtual rank");
+    *nstages = ctx->nstages;
+    if (ms && cap < 2 * ctx->nstages) sbmf::fail(SBMF_E_ARG, "need %u slots", 2 * ctx->nstages);
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    for (uint32_t sd = 0; ms && sd < 2; ++sd)
+        for (uint32_t p = 0; p < ctx->nstages; ++p) {
+            float f = 0.f;
+            const size_t tb = (size_t)sd * (ctx->nstages + 1);
+            HIPCHK(hipEventElapsedTime(&f, ctx->tsev[tb + p], ctx->tsev[tb + p + 1]));
+            ms[sd * ctx->nstages + p] = f;
+        }
+    API_END(ctx)
+}
+
+int sbmf_test_rccl_selftest(sbmf_ctx* ctx, uint64_t nbytes, uint32_t reps, double deadline_s,
+                            sbmf_rccl_selftest* out) {
+    API_BEGIN
+    if (!ctx || !out) sbmf::fail(SBMF_E_ARG, "null argument");
+    HIPCHK(hipSetDevice(ctx->cfg.device));
+    if (!ctx->prepared || ctx->nranks != 1 || ctx->cfg.method != SBMF_METHOD_MCMC)
+        sbmf::fail(SBMF_E_STATE, "the RCCL self-test needs a prepared one-rank sampler context");
+    if (nbytes < 64 || nbytes % 64 || reps == 0) sbmf::fail(SBMF_E_ARG, "nbytes a positive multiple of 64, reps >= 1");
+    if (ctx->cfg.precision == SBMF_F32)
+        sbmf::rccl_selftest<float>(ctx, nbytes, reps, deadline_s, out);
+    else
+        sbmf::rccl_selftest<double>(ctx, nbytes, reps, deadline_s, out);
     API_END(ctx)
 }
 

@@ -139,6 +139,35 @@ void load(const std::string& path, const std::string& fmt, uint32_t item_offset,
     if (rc != SBMF_OK) throw std::runtime_error(sbmf_loader_error());
 }
 
+// The users-first item offset of a libFM file loaded with offset 0 (user =
+// first feature, item = raw second feature): libFM's num_user, max user id + 1
+// over train and test (libfm.cpp:375).  The items are rebased onto it in place;
+// a file whose item ids do not all lie above every user id has no users-first
+// reading and is refused.
+uint32_t users_first_offset(sbmf_ratings& tr, sbmf_ratings& te) {
+    uint64_t umax = 0;
+    bool any = false;
+    for (const sbmf_ratings* r : {&tr, &te})
+        for (uint64_t q = 0; q < r->n; ++q) {
+            umax = std::max<uint64_t>(umax, r->user[q]);
+            any = true;
+        }
+    if (!any) return 0;
+    const uint32_t I = (uint32_t)(umax + 1);
+    for (sbmf_ratings* r : {&tr, &te})
+        for (uint64_t q = 0; q < r->n; ++q)
+            if (r->item[q] < I)
+                throw std::runtime_error(std::string("libFM input: ") + (r == &tr ? "train" : "test") + " case " +
+                                         std::to_string(q + 1) + " has item feature id " +
+                                         std::to_string(r->item[q]) + " <= the largest user feature id " +
+                                         std::to_string(umax) +
+                                         "; the learners read one user feature then one item feature per line, "
+                                         "users first (pass -item_offset to set the split)");
+    for (sbmf_ratings* r : {&tr, &te})
+        for (uint64_t q = 0; q < r->n; ++q) r->item[q] -= I;
+    return I;
+}
+
 struct RunState {
     std::string rmse_file;
     bool vb = false;  // online VB prints "#Iter=..\tTest=.." (fm_learn_vb_online_simultaneous.h:447)
@@ -320,11 +349,14 @@ int main(int argc, char** argv) {
         cl.reg("average", "running-mean divisor: default (quirk set) | collected (collected sweeps only) | "
                           "reference (sweep + 1, counts burn-in as gibbs_sbpmf_final.cpp:559 does)");
         cl.reg("format", "auto (default: <name>.x/.y binary if present, else triple or libfm text) | triple | libfm | binary");
-        cl.reg("item_offset", "libFM input: item feature id offset; default=0");
+        cl.reg("item_offset", "libFM input: item feature id offset; default: libFM's num_user (max user feature "
+                              "id + 1, libfm.cpp:375) for -method mcmc (libFM order) / als / vb, 0 for -order sbpmf");
         cl.reg("device", "HIP device ordinal; default=0");
         cl.reg("recompute_every", "recompute residuals from scratch every n sweeps; default=1");
         cl.reg("stream_threshold", "rows with more ratings take the streaming kernel; default=256 (f64) / 512 (f32)");
-        cl.reg("split_chunk", "streaming task size; longer rows are split over co-resident workgroups; default: LDS capacity (4096 f64 / ~8K f32)");
+        cl.reg("split_chunk", "streaming task size; longer rows are split into chunks on several workgroups; default: "
+                              "the register capacity of the workgroup shape (512 / 1024 / 2048 f64 ratings for 4 / 8 / "
+                              "16 waves), larger values are capped to it");
         if (cl.has("help") || argc == 1) {
             cl.print_help();
             return leave(0);
@@ -418,12 +450,18 @@ int main(int argc, char** argv) {
         }
         cfg.eval_test = 1;
 
-        const uint32_t off = (uint32_t)cl.getl("item_offset", 0);
+        uint32_t off = (uint32_t)cl.getl("item_offset", 0);
         std::cout << "Loading train...\t" << std::endl;
         sbmf_ratings tr{}, te{};
         load(cl.get("train", ""), fmt, off, tr);
         std::cout << "Loading test... \t" << std::endl;
         load(cl.get("test", ""), fmt, off, te);
+        // libFM's learners (fm_learn_mcmc, fm_learn_vb_online) take the file's feature ids as
+        // their attribute ids: num_user = max first feature id + 1 over train and test
+        // (libfm.cpp:219-221,263-265,375) and num_all_attribute = max feature id + 1 (:328).
+        // With one user and one item feature per line that is the users-first layout with
+        // item offset num_user, so no flag is needed (-item_offset overrides it).
+        if ((lfm || vb) && libfm_input && !cl.has("item_offset")) off = users_first_offset(tr, te);
 
         sbmf_ctx* ctx = nullptr;
         if (sbmf_create(&cfg, &ctx) != SBMF_OK) throw std::runtime_error(sbmf_last_global_error());
@@ -432,9 +470,9 @@ int main(int argc, char** argv) {
         };
         chk(sbmf_set_train(ctx, tr.n, tr.user, tr.item, tr.rating));
         chk(sbmf_set_test(ctx, te.n, te.user, te.item, te.rating));
-        // libFM's attributes are the file's feature ids: with a libFM input the
-        // users-first item offset is -item_offset
-        if (lfm && off) chk(sbmf_set_dims(ctx, off, 0));
+        // libFM's attributes are the file's feature ids: users first, items from the
+        // (inferred or given) item offset on
+        if ((lfm || vb) && off) chk(sbmf_set_dims(ctx, off, 0));
         chk(sbmf_prepare(ctx));
         uint32_t nu, ni;
         uint64_t ntr, nte;

@@ -150,6 +150,25 @@ def load_libfm(path, item_offset=0):
         lib.sbmf_free_ratings(C.byref(r))
 
 
+def libfm_users_first(train, test=None):
+    """libFM's attribute split of a users-first file loaded with item_offset=0:
+    num_user = max first feature id + 1 over train and test (libfm.cpp:219-221,
+    263-265,375).  Returns (train, test, num_user) with the item ids rebased onto
+    num_user -- pass num_user as set_data(..., num_users=num_user) so libFM's
+    learners see the file's attribute ids, as the CLI does.  A file whose item ids
+    do not all lie above every user id has no users-first reading: ValueError."""
+    sets = [d for d in (train, test) if d is not None and d.num_cases]
+    if not sets:
+        return train, test, 0
+    I = max(int(np.max(d.user)) for d in sets) + 1
+    for d in sets:
+        if int(np.min(d.item)) < I:
+            raise ValueError("libFM input: item feature id %d <= the largest user feature id %d: not users first"
+                             % (int(np.min(d.item)), I - 1))
+    rebase = lambda d: None if d is None else Data(d.user, np.asarray(d.item, np.int64) - I, d.rating)
+    return rebase(train), rebase(test), I
+
+
 def config_default():
     cfg = _lib.Config()
     lib.sbmf_config_default(C.byref(cfg))

@@ -65,6 +65,14 @@ _P_F64 = C.POINTER(C.c_double)
 _P_U8 = C.POINTER(C.c_uint8)
 
 # name -> (restype, argtypes); every function declared in include/sbmf.h
+class RcclSelftest(C.Structure):
+    _fields_ = [
+        ("ms_half", C.c_double), ("ms_rccl", C.c_double), ("ms_rccl_end", C.c_double),
+        ("bad_bcast", C.c_uint64), ("bad_p2p", C.c_uint64), ("bad_allgather", C.c_uint64),
+        ("n_calls", C.c_uint32), ("overlapped", C.c_uint32),
+    ]
+
+
 SIGNATURES = {
     "sbmf_config_default": (C.c_int, [C.POINTER(Config)]),
     "sbmf_create": (C.c_int, [C.POINTER(Config), C.POINTER(C.c_void_p)]),
@@ -96,6 +104,9 @@ SIGNATURES = {
     "sbmf_partition_rows": (C.c_int, [_P_U32, C.c_uint32, C.c_int, C.POINTER(C.c_uint64)]),
     "sbmf_ref_stream": (C.c_int, [C.c_uint32, C.c_int, C.c_double, C.c_uint64, _P_F64]),
     "sbmf_philox_normals": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P_F64]),
+    "sbmf_test_virtual_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "sbmf_test_stage_ms": (C.c_int, [C.c_void_p, _P_F64, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "sbmf_test_rccl_selftest": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_double, C.POINTER(RcclSelftest)]),
 }
 
 

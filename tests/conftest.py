@@ -56,6 +56,40 @@ def ragged():
     return tr, te
 
 
+def read_libfm_text(path):
+    """libFM text "r a:1 b:1" -> (first feature id, second feature id, target)."""
+    opener = gzip.open if path.endswith(".gz") else open
+    u, i, r = [], [], []
+    with opener(path, "rt") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 3:
+                r.append(float(parts[0]))
+                u.append(int(parts[1].split(":")[0]))
+                i.append(int(parts[2].split(":")[0]))
+    return np.array(u, np.uint32), np.array(i, np.uint32), np.array(r, np.float64)
+
+
+@pytest.fixture(scope="session")
+def m1m100k():
+    """The reference's own data/m1m/m100k/{train,test}_libfm (tests/golden/m1m100k_*_libfm.gz):
+    users 0..942 as the first feature, items at their raw feature ids 943..2624.  Triples with
+    the raw item ids are also exactly the {train,test}_sbpmf its converter writes."""
+    return (read_libfm_text(os.path.join(GOLD, "m1m100k_train_libfm.gz")),
+            read_libfm_text(os.path.join(GOLD, "m1m100k_test_libfm.gz")))
+
+
+def write_m1m100k_libfm(dirpath):
+    """Decompress the reference's libFM files into dirpath as train_libfm / test_libfm."""
+    out = []
+    for nm in ("train_libfm", "test_libfm"):
+        dst = os.path.join(str(dirpath), nm)
+        with gzip.open(os.path.join(GOLD, "m1m100k_%s.gz" % nm), "rb") as f, open(dst, "wb") as g:
+            g.write(f.read())
+        out.append(dst)
+    return out
+
+
 def golden_rmse(name):
     with open(os.path.join(GOLD, name)) as f:
         return np.array([float(x) for x in f.read().split()])

@@ -68,3 +68,16 @@ def test_binary_stem_loaded_before_device(tmp_path):
     r = run("-task", "r", "-train", stem, "-test", stem, "-dim", "1,1,8", "-iter", "2", "--format", "binary",
             "--item_offset", "3")
     assert r.returncode == 1 and "one user and one item" in r.stderr
+
+
+def test_libfm_input_must_be_users_first(tmp_path):
+    """libFM's learners read the file's feature ids as attributes with the users first
+    (num_user = max first feature + 1, libfm.cpp:375): an item feature id at or below a
+    user id has no such reading and is refused before any device work (no GPU needed)."""
+    tr = tmp_path / "t.libfm"
+    tr.write_text("5 0:1 3:1\n3 4:1 6:1\n")  # item 3 <= user 4
+    r = run("-task", "r", "-train", str(tr), "-test", str(tr), "-dim", "1,1,8", "-iter", "2", "-method", "mcmc")
+    assert r.returncode == 1 and "users first" in r.stderr and "item feature id 3" in r.stderr
+    # the SBPMF order reads the same file as raw (user, item) triples, as the reference's converter does
+    r = run("-task", "r", "-train", str(tr), "-test", str(tr), "-dim", "0,0,8", "-iter", "2", "-order", "sbpmf")
+    assert "users first" not in r.stderr

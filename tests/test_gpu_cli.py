@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import REPO, golden_rmse
+from conftest import REPO, golden_rmse, write_m1m100k_libfm
 from sbmf._lib import CLI_PATH
 
 pytestmark = pytest.mark.gpu
@@ -131,19 +131,22 @@ def _write_libfm(path, data, item_offset):
             f.write("%g %d:1 %d:1\n" % (c, a, item_offset + b))
 
 
-@pytest.mark.parametrize("method", ["mcmc", "als"])
-def test_cli_libfm_methods_reproduce_libfm_output(tmp_path, ml100k, method):
+@pytest.mark.parametrize("method,offset_flag", [("mcmc", False), ("als", False), ("mcmc", True)])
+def test_cli_libfm_methods_reproduce_libfm_output(tmp_path, ml100k, method, offset_flag):
     """`sbmf` as a drop-in for `bin/libFM -method mcmc|als` on the same libFM
     text files: the "#Iter=" lines equal libFM's own (tests/golden/ref_libfm_*,
     libfm.cpp compiled unmodified, time() pinned to the seed), the -out file
-    and test_rmse_118_mcmc within the printed digits."""
+    and test_rmse_118_mcmc within the printed digits.  The users-first split is
+    libFM's own num_user rule (libfm.cpp:375); -item_offset, when given, overrides it."""
     I = int(max(ml100k[0][0].max(), ml100k[1][0].max())) + 1
     tr, te = tmp_path / "train.libfm", tmp_path / "test.libfm"
     _write_libfm(tr, ml100k[0], I)
     _write_libfm(te, ml100k[1], I)
     extra = ["-order", "libfm"] if method == "mcmc" else ["-regular", "0,0,10"]
+    if offset_flag:
+        extra += ["-item_offset", str(I)]
     cmd = [CLI_PATH, "-task", "r", "-train", str(tr), "-test", str(te), "-dim", "1,1,8", "-iter", "10",
-           "-method", method, "-seed", "1", "-item_offset", str(I), "-out", str(tmp_path / "pred.txt"), *extra]
+           "-method", method, "-seed", "1", "-out", str(tmp_path / "pred.txt"), *extra]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr
     name = "ref_libfm_%s_ml100k_d118_s1_i10" % method
@@ -168,7 +171,7 @@ def test_cli_mcmc_on_libfm_input_is_libfms_chain(tmp_path, ml100k):
     _write_libfm(tr, ml100k[0], I)
     _write_libfm(te, ml100k[1], I)
     cmd = [CLI_PATH, "-task", "r", "-train", str(tr), "-test", str(te), "-dim", "1,1,8", "-iter", "10",
-           "-method", "mcmc", "-seed", "1", "-item_offset", str(I), "-rlog", str(tmp_path / "rlog.tsv")]
+           "-method", "mcmc", "-seed", "1", "-rlog", str(tmp_path / "rlog.tsv")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr
     assert "note" not in r.stdout
@@ -185,3 +188,69 @@ def test_cli_mcmc_on_libfm_input_is_libfms_chain(tmp_path, ml100k):
     r2 = subprocess.run(cmd[:-2] + ["-order", "sbpmf"], capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r2.returncode == 0, r2.stderr
     assert "note" in r2.stderr and "note" not in r2.stdout
+
+
+@pytest.mark.parametrize("method", ["mcmc", "als"])
+def test_cli_is_bin_libfm_on_the_reference_files(tmp_path, method):
+    """bin/libFM's exact command line on the reference's own data/m1m/m100k/{train,test}_libfm
+    (users 0..942, items at raw feature ids 943..2624), nothing added:
+        -task r -train train_libfm -test test_libfm -dim '1,1,8' -iter 10 -method mcmc
+        (-method als -regular '0,0,10')
+    libFM's attributes are the file's feature ids (num_user = max first feature + 1,
+    libfm.cpp:375; num_all_attribute = max feature + 1, :328), so the chain is libFM's:
+    "#Iter" lines equal as text to the compiled libfm.cpp's (time() pinned to 1 = sbmf's
+    default -seed), -out within libFM's printed digits, test_rmse_118_mcmc equal."""
+    write_m1m100k_libfm(tmp_path)
+    cmd = [CLI_PATH, "-task", "r", "-train", "train_libfm", "-test", "test_libfm", "-dim", "1,1,8", "-iter", "10",
+           "-method", method, "-out", "pred.txt"] + (["-regular", "0,0,10"] if method == "als" else [])
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    assert "#users=943\t#items=1682" in r.stdout  # libFM's 2625 attributes: 943 users + 1682 items
+    name = "ref_libfm_%s_m1m100k_d118_s1_i10" % method
+    gold_lines = open(os.path.join(REPO, "tests", "golden", name + ".txt")).read().splitlines()
+    lines = [l for l in r.stdout.splitlines() if l.startswith("#Iter")]
+    assert lines == gold_lines
+    import gzip
+    with gzip.open(os.path.join(REPO, "tests", "golden", name + "_pred.txt.gz"), "rt") as f:
+        ref_pred = np.array([float(x) for x in f.read().split()])
+    pred = np.loadtxt(tmp_path / "pred.txt")
+    ulp6 = 10.0 ** (np.floor(np.log10(np.abs(ref_pred))) - 5)
+    assert np.all(np.abs(pred - ref_pred) <= 0.5 * ulp6 * (1 + 1e-9) + 1e-12)
+    rm = (tmp_path / "test_rmse_118_mcmc").read_text().split()
+    assert rm == [l.split("Test=")[1] for l in gold_lines]
+
+
+def test_cli_sbpmf_order_on_the_reference_libfm_file(tmp_path):
+    """`-order sbpmf` on the same libFM file is gibbs_sbpmf_final on the reference's converted
+    data/m1m/m100k/{train,test}_sbpmf (create_file_scalable_bpmf.py keeps the raw item ids,
+    so items 0..942 are empty rows): K=20 (gibbs_sbpmf_final.cpp's baked D), 100 sweeps,
+    seed 1, the running-mean test RMSE of every sweep within the 6 printed digits."""
+    write_m1m100k_libfm(tmp_path)
+    cmd = [CLI_PATH, "-task", "r", "-train", "train_libfm", "-test", "test_libfm", "-dim", "1,1,20", "-iter", "100",
+           "-method", "mcmc", "-order", "sbpmf"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    assert "#users=943\t#items=2625" in r.stdout
+    gold = golden_rmse("ref_final_m1m100k_k20_s1.txt")
+    lines = [l for l in r.stdout.splitlines() if l.startswith("#Iter")]
+    assert len(lines) == 100
+    assert _close6([float(ITER_RE.match(l).group(3)) for l in lines], gold)
+    assert _close6([float(x) for x in (tmp_path / "test_rmse_1120_mcmc").read_text().split()], gold)
+
+
+def test_cli_vb_on_libfm_text_follows_reference_learner(tmp_path, ml100k):
+    """`-method vb` on users-first libFM text with libFM's own argv (no offset flag): the
+    online VB learner over the file's attributes, per-epoch "Test=" within the printed
+    digits of the reference learner's trajectory (tests/golden/ref_vbo_ml100k_k8_s1_e10.txt,
+    fm_learn_vb_online*.h compiled unmodified, oracle/ref_vbo_harness.cpp)."""
+    I = int(max(ml100k[0][0].max(), ml100k[1][0].max())) + 1
+    tr, te = tmp_path / "train.libfm", tmp_path / "test.libfm"
+    _write_libfm(tr, ml100k[0], I)
+    _write_libfm(te, ml100k[1], I)
+    cmd = [CLI_PATH, "-task", "r", "-train", str(tr), "-test", str(te), "-dim", "1,1,8", "-iter", "10",
+           "-method", "vb", "-seed", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    gold = golden_rmse("ref_vbo_ml100k_k8_s1_e10.txt")
+    vals = [float(l.split("Test=")[1]) for l in r.stdout.splitlines() if l.startswith("#Iter")]
+    assert len(vals) == 10 and _close6(vals, gold)

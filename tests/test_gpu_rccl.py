@@ -1,0 +1,77 @@
+"""The multi-GPU transport's RCCL calls on one GPU, and one rank's stage compute.
+
+RCCL refuses two ranks on one device, so the exchange (comm.cpp) cannot run
+between peers here.  What one GPU can show:
+
+* sbmf_test_rccl_selftest: a one-rank RCCL communicator created through the
+  library's own dlopen/dlsym table issues the exchange's exact calls -- grouped
+  in-place ncclBroadcast over adjacent blocks (bcast_stage), grouped
+  ncclSend/ncclRecv (alltoallv, here to the rank itself), ncclAllGather -- on the
+  multi-GPU comm stream while the item half's persistent k_gres grids run on the
+  compute streams, as in the pipelined half (stage p's exchange beside stage
+  p+1's compute; reference halves gibbs_sbpmf_final.cpp:453-535).  Every byte is
+  checked and the comm stream must finish within a deadline.
+* sbmf_test_virtual_rank: rank r of an N-rank run on this GPU with the exchange
+  skipped runs exactly its own blocks, stages, bins and tasks (timing only)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from sbmf import Data, FMLearnSBPMF, lib, synth
+from sbmf import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _learner(shape="ml-1m", K=50, **kw):
+    tr, te, _ = synth.generate(shape)
+    L = FMLearnSBPMF(num_factor=K, seed=3, rng="philox", recompute_every=0, **kw)
+    return L, Data(*tr), Data(*te)
+
+
+def test_rccl_calls_beside_persistent_kgres_grids():
+    L, tr, te = _learner()
+    L.set_data(tr, te)
+    L.learn(sweeps=1)
+    t = L.timing()
+    assert t.kern_rows[1][5] > 0  # the item half has streaming (k_gres) rows
+    out = _lib.RcclSelftest()
+    rc = lib.sbmf_test_rccl_selftest(L.ctx, 16 << 20, 8, 60.0, C.byref(out))
+    assert rc == 0, lib.sbmf_last_error(L.ctx).decode()
+    print("rccl self-test: half %.3f ms x8, rccl %.3f ms, rccl end %.3f ms, overlapped %d, calls %d"
+          % (out.ms_half, out.ms_rccl, out.ms_rccl_end, out.overlapped, out.n_calls))
+    assert out.n_calls == 8 * 6
+    assert out.bad_bcast == 0 and out.bad_p2p == 0 and out.bad_allgather == 0
+    assert out.ms_half > 0 and out.ms_rccl > 0
+    L.close()
+
+
+def test_rccl_selftest_argument_checks():
+    L, tr, te = _learner("ml-100k", K=8)
+    out = _lib.RcclSelftest()
+    L.init()
+    assert lib.sbmf_test_rccl_selftest(L.ctx, 1 << 20, 1, 10.0, C.byref(out)) != 0  # not prepared
+    L.set_data(tr, te)
+    assert lib.sbmf_test_rccl_selftest(L.ctx, 100, 1, 10.0, C.byref(out)) != 0  # not a multiple of 64
+    L.close()
+
+
+def test_virtual_rank_runs_its_stages():
+    """Config-4-like partitioning (8 ranks, 4 stages per half) of the ML-1M-shaped set: every
+    virtual rank runs; its stage times are positive and the stages add up to about the half."""
+    tr, te, _ = synth.generate("ml-1m")
+    for r in (0, 7):
+        L = FMLearnSBPMF(num_factor=50, seed=3, rng="philox", recompute_every=0)
+        L.init()
+        assert lib.sbmf_test_virtual_rank(L.ctx, 8, r) == 0
+        L.set_data(Data(*tr), Data(*te))
+        L.learn(sweeps=2)
+        ms = np.zeros(8)
+        ns = C.c_uint32()
+        assert lib.sbmf_test_stage_ms(L.ctx, ms.ctypes.data_as(C.POINTER(C.c_double)), 8, C.byref(ns)) == 0
+        assert ns.value == 4
+        assert np.all(ms > 0) and np.all(np.isfinite(ms)), ms
+        t = L.timing()
+        assert ms[:4].sum() <= t.ms_user_half * 1.05 + 0.05 and ms[4:].sum() <= t.ms_item_half * 1.05 + 0.05
+        L.close()

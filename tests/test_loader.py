@@ -60,6 +60,20 @@ def test_libfm_loader(tmp_path):
         sbmf.load_libfm(q, item_offset=944)
 
 
+def test_libfm_users_first_split_is_libfms_num_user(m1m100k, tmp_path):
+    """libFM's num_user = max first feature id + 1 over train and test (libfm.cpp:375): on the
+    reference's data/m1m/m100k/*_libfm that is 943 and the items rebase to 0..1681."""
+    from conftest import write_m1m100k_libfm
+    trp, tep = write_m1m100k_libfm(tmp_path)
+    tr, te = sbmf.load_libfm(trp), sbmf.load_libfm(tep)
+    assert np.array_equal(tr.item, m1m100k[0][1])
+    tr2, te2, I = sbmf.libfm_users_first(tr, te)
+    assert I == 943 and int(tr2.item.min()) == 0 and max(tr2.item.max(), te2.item.max()) == 2624 - 943
+    assert np.array_equal(tr2.item, tr.item - 943) and np.array_equal(te2.user, te.user)
+    with pytest.raises(ValueError):
+        sbmf.libfm_users_first(sbmf.Data([0, 4], [944, 3], [5.0, 3.0]))
+
+
 @pytest.mark.parametrize("bad", ["5 0:1\n", "5 0:1 3:1 4:1\n", "x 0:1 1:1\n", "5 0-1 1:1\n"])
 def test_libfm_loader_errors(tmp_path, bad):
     p = tmp_path / "bad.libfm"

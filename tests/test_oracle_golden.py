@@ -22,6 +22,17 @@ def test_oracle_bitwise_equals_reference(variant, data, seed, K, ml100k, ragged)
     assert np.array_equal(o["rmse"], gold), np.abs(o["rmse"] - gold).max()
 
 
+def test_oracle_bitwise_equals_reference_on_its_own_m1m100k_files(m1m100k):
+    """gibbs_sbpmf_final (K=20, seed 1) on the reference's converted data/m1m/m100k/{train,test}_sbpmf:
+    raw item ids 943..2624 kept by create_file_scalable_bpmf.py, so items 0..942 are empty rows
+    drawn from the prior every sweep."""
+    tr, te = m1m100k
+    gold = golden_rmse("ref_final_m1m100k_k20_s1.txt")
+    o = oracle.run(tr, te, K=20, iters=100, seed=1, want_factors=False)
+    assert np.array_equal(o["rmse"], gold), np.abs(o["rmse"] - gold).max()
+    assert o["num_items"] == 2625
+
+
 def test_oracle_dims_follow_reference_rule(ragged):
     """num_users/items = max id + 1 over train AND test (gibbs_sbpmf_final.cpp:146-148)."""
     tr, te = ragged

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import GOLD
+from conftest import GOLD, read_libfm_text
 
 # (method, data, dim, seed, iterations, -regular) -- as oracle/make_golden.py LIBFM_RUNS
 RUNS = [("mcmc", "ml100k", "1,1,8", 1, 10, None), ("als", "ml100k", "1,1,8", 1, 10, "0,0,10"),
@@ -52,3 +52,25 @@ def test_oracle_als_is_deterministic_and_seed_only_moves_the_init(ml100k):
     a = oracle.run_fmm(tr, te, K=4, iters=3, seed=5, method="als", regular=(0.0, 0.0, 10.0))
     b = oracle.run_fmm(tr, te, K=4, iters=3, seed=5, method="als", regular=(0.0, 0.0, 10.0))
     assert np.array_equal(a["rmse_test"], b["rmse_test"]) and np.array_equal(a["v"], b["v"])
+
+
+@pytest.mark.parametrize("method,reg", [("mcmc", None), ("als", "0,0,10")])
+def test_oracle_matches_libfm_on_the_reference_files(method, reg, m1m100k):
+    """bin/libFM -task r -dim '1,1,8' -iter 10 -method mcmc|als on the reference's own
+    data/m1m/m100k/{train,test}_libfm, argv unchanged (tests/golden/ref_libfm_*_m1m100k_*).
+    libFM's attributes are the file's feature ids: num_user = max first feature + 1
+    (libfm.cpp:375) = 943, items rebased onto it."""
+    (tu, ti, tr_), (su, si, sr) = m1m100k
+    I = int(max(tu.max(), su.max())) + 1
+    assert I == 943 and min(ti.min(), si.min()) >= I
+    regular = tuple(float(x) for x in reg.split(",")) if reg else (0.0, 0.0, 0.0)
+    o = oracle.run_fmm((tu, ti - I, tr_), (su, si - I, sr), K=8, iters=10, seed=1, method=method,
+                       regular=regular)
+    assert o["v"].shape[1] == int(max(ti.max(), si.max())) + 1 + 1  # libFM's p (+1: libfm.cpp:328)
+    name = golden_name(method, "m1m100k", "1,1,8", 1, 10)
+    with open(os.path.join(GOLD, name + ".txt")) as f:
+        assert iter_lines(o) == f.read().splitlines()
+    with gzip.open(os.path.join(GOLD, name + "_pred.txt.gz"), "rt") as f:
+        ref_pred = np.array([float(x) for x in f.read().split()])
+    ulp6 = 10.0 ** (np.floor(np.log10(np.abs(ref_pred))) - 5)
+    assert np.all(np.abs(o["pred"] - ref_pred) <= 0.5 * ulp6 * (1 + 1e-9))
