@@ -168,7 +168,12 @@ typedef struct sbmf_sweep_info {
     double rmse_this;          /* test RMSE of this sweep's sample alone                      */
     double rmse_train;         /* train RMSE of this sample (clamped), NaN if not evaluated   */
     double tau;                /* noise precision drawn this sweep                           */
-    double ms_sweep;           /* device time of the sweep (half-sweeps + hyper), ms          */
+    double ms_sweep;           /* device time of the sweep from its start to the end of the item
+                                  half, ms.  Throughput mode (overlapped start): the sweep's start
+                                  work -- residual sum, column statistics, both normal fills and
+                                  the hyperparameter upload -- was queued at the end of the
+                                  previous sweep, beside its test evaluation, and is not in here
+                                  (sbmf_timing.ms_hyper of the previous sweep holds it)        */
     double ms_eval;            /* device time of the test evaluation, ms                      */
 } sbmf_sweep_info;
 

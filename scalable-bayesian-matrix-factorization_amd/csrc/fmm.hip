@@ -105,7 +105,9 @@ __global__ __launch_bounds__(NT > 256 ? NT : 256) void k_fmm_pass(FMPassArgs a) 
                 const double qc = ((0.0 + qo * x) + r.x * x) - x * (qo - qn);
                 h = x * (qc - x * r.x);
             }
-            return e - h * (r.x - r.y);
+            // a draw that was not kept recorded {old, old}: leave e alone, as libFM does
+            // (e - h * 0 would turn a non-finite h into NaN and can flip a -0.0)
+            return r.x == r.y ? e : e - h * (r.x - r.y);
         }
     };
     // h of the case at position q (factor pass): x * (q_c - x * v) with the

@@ -26,9 +26,16 @@
 #include "kernels.h"
 #include "rng.h"
 
-// timing-only ablation switches (wrong results): KPROF=1 or ABLATE=1 builds
-#if defined(SBMF_KPROF_BUILD) || defined(SBMF_ABLATE_BUILD)
-#define SBMF_ABLATIONS 1
+// Diagnostic hooks: defined away here.  The diagnostic builds (Makefile CHECK=1 /
+// KPROF=1) pre-include kernels_instr.h, which defines them first; the product
+// build never includes it.
+//   CHK(i, extent)           a global index (CHECK=1: validated, printed, redirected)
+//   SBMF_GBLOCK_PHASES(on)   declares stamp(phase) in k_gblock (KPROF=1: wave 0's
+//   SBMF_GRES_PHASES(nch)    cycles per phase) / in k_gres' task loop
+#ifndef SBMF_KERNELS_INSTR_H_
+#define CHK(i, lim) (i)
+#define SBMF_GBLOCK_PHASES(on) auto stamp = [](int) {}
+#define SBMF_GRES_PHASES(nch) auto stamp = [](int) {}
 #endif
 
 namespace sbmf {
@@ -220,22 +227,6 @@ __device__ __forceinline__ void lds_barrier() {
 
 // s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory operations are done
 // (the counter holds at most 63: a larger N waits for the oldest N - 63 of them too)
-// CHECK=1 builds: CHK(i, extent) validates a global index; a violation is printed
-// (the first 32 over the process) and the access goes to element 0 instead, so a bad
-// index is reported without faulting the device.  Other builds: CHK(i, n) is i.
-#ifdef SBMF_CHECK_BUILD
-__device__ unsigned int g_chk_count = 0;
-__device__ __noinline__ uint64_t chk_fail(uint64_t i, uint64_t lim, int line) {
-    if (atomicAdd(&g_chk_count, 1u) < 32u)
-        printf("[sbmf check] kernels.hip:%d index %llu >= extent %llu (block %u thread %u)\n", line,
-               (unsigned long long)i, (unsigned long long)lim, blockIdx.x, threadIdx.x);
-    return 0;
-}
-#define CHK(i, lim) ((uint64_t)(i) < (uint64_t)(lim) ? (uint64_t)(i) : chk_fail((uint64_t)(i), (uint64_t)(lim), __LINE__))
-#else
-#define CHK(i, lim) (i)
-#endif
-
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0, "vmcnt range");
@@ -276,10 +267,6 @@ __device__ __forceinline__ T gblock_solve(const T (&H)[GB], T gam) {
 
 // Same recurrence with the H row read from LDS (row `hrow`, scaled by Bq)
 // step by step, for kernels without the registers to hold it.
-// SOLVE2=1 builds (diagnostic, Makefile EXTRA=-DSBMF_SOLVE2): round 3's rejected
-// two-step form -- every lane forms d_{j+1} = gamma_{j+1} - H[j+1][j] d_j itself,
-// one readlane hop per pair of draws -- kept to re-run the fault it was dropped for
-// (CHECK=1 builds).
 // Lane j of each 16-lane DPP row, broadcast to the row (row_newbcast: one 64-bit DPP move
 // on gfx950 where a readlane pair put the value through an SGPR pair and a wait state).
 // Every row of the solving wave holds the same 16-lane system, so each row broadcasting
@@ -301,26 +288,8 @@ __device__ __forceinline__ void solve_steps(const T* __restrict__ hrow, T Bq, T&
 
 template <typename T>
 __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, T gam) {
-#ifdef SBMF_SOLVE2
-    T H[GB];
-#pragma unroll
-    for (int j = 0; j < GB; ++j) H[j] = Bq * hrow[j];
-#pragma unroll
-    for (int j = 0; j < GB; j += 2) {
-        const T h10 = readlane(H[j], j + 1);
-        const T dj = readlane(gam, j);
-        const T g1 = readlane(gam, j + 1);
-        const T dj1 = g1 - h10 * dj;
-        gam -= H[j] * dj;
-        gam -= H[j + 1] * dj1;
-    }
-    return gam;
-#else
-#ifndef SBMF_ABL_NOSOLVE  // timing-only build (wrong results): no 16-step recurrence
     solve_steps<0>(hrow, Bq, gam);
-#endif
     return gam;
-#endif
 }
 
 // Occupancy hints (waves/SIMD): 5 for 8 f64 vectors per wave (<= 102 VGPRs),
@@ -328,13 +297,7 @@ __device__ __forceinline__ T gblock_solve_lds(const T* __restrict__ hrow, T Bq, 
 // hold because the per-rating values (partner-row offsets, residuals, scatter
 // targets) and the row's normals sit in LDS, and the block solve reads its H
 // row from LDS.
-#ifndef SBMF_GBLOCK_OCC64
-#define SBMF_GBLOCK_OCC64 5
-#endif
-#ifndef SBMF_GBLOCK_OCC_WIDE
-#define SBMF_GBLOCK_OCC_WIDE 4
-#endif
-#define GBLOCK_OCC(T, V) ((V) * sizeof(T) > 64 ? SBMF_GBLOCK_OCC_WIDE : (sizeof(T) == 8 ? SBMF_GBLOCK_OCC64 : 3))
+#define GBLOCK_OCC(T, V) ((V) * sizeof(T) > 64 ? 4 : (sizeof(T) == 8 ? 5 : 3))
 template <typename T, int V, int NW, int RPW>
 __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_gblock(const uint32_t* __restrict__ rows,
                                                                      uint32_t nrows, HalfArgs<T> a) {
@@ -345,20 +308,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
     const int wr = NW > 1 ? wv : 0;           // wave within the row
     const uint32_t ri = NW > 1 ? blockIdx.x : blockIdx.x * RPW + wv;
     if (ri >= nrows) return;                  // NW>1: whole block; RPW: this wave only (no block barriers)
-    // optional phase profile (build with KPROF=1, run with SBMF_KPROF=1;
-    // multi-wave rows): wave 0's cycles per phase
-#ifdef SBMF_KPROF_BUILD
-    unsigned long long tp = (a.prof && threadIdx.x == 0) ? clock64() : 0ull;
-    auto stamp = [&](int ph) {
-        if (NW > 1 && a.prof && threadIdx.x == 0) {
-            const unsigned long long now = clock64();
-            atomicAdd(&a.prof[ph], now - tp);
-            tp = now;
-        }
-    };
-#else
-    auto stamp = [](int) {};
-#endif
+    SBMF_GBLOCK_PHASES(NW > 1);  // stamp(phase): the diagnostic phase profile (multi-wave rows)
     const uint32_t row = rows[ri];
     const uint32_t beg = a.ptr[row];
     const uint32_t n = a.ptr[row + 1] - beg;
@@ -412,13 +362,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         for (int u = 0; u < SG; ++u) {
             const int v = g0 + u;
             const uint32_t q = (uint32_t)((wr * V + v) * 4 + rr);
-            uint32_t pj = q < n ? pjv[u] : a.zrow;
-#ifdef SBMF_ABLATIONS
-            if (a.tune & 0x100u) pj = 0;  // ablation (wrong results): every gather hits one cached row
-#endif
-#ifdef SBMF_ABL_GATHER0
-            pj = 0;  // timing-only build (wrong results): every slice from partner row 0
-#endif
+            const uint32_t pj = q < n ? pjv[u] : a.zrow;
             if (ci == 0) {
                 pjS[wv][4 * v + rr] = pj * Kp;
                 pmS[wv][4 * v + rr] = q < n ? pmv[u] : 0u;
@@ -481,15 +425,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
 #pragma unroll
     for (int v = 0; v < V; ++v) s[v] = gat(v, 0);
     T oldc = orow[0], sgc = a.sig[ci], muc = a.mu[ci];
-#ifdef SBMF_ABLATIONS
-    // ablation (wrong results): tune 0x800 runs the block loop twice (block index wraps)
-    const uint32_t Kr = (K + GB - 1) / GB * GB;
-    const uint32_t KL = (a.tune & 0x800u) ? 2 * Kr : K;
-    for (uint32_t bl = 0; bl < KL; bl += GB) {
-        const uint32_t b0 = bl % Kr;
-#else
     for (uint32_t b0 = 0; b0 < K; b0 += GB) {
-#endif
         const uint32_t kk = b0 + ci;
         const bool kin = kk < K;
         const uint32_t kn = b0 + GB;
@@ -502,16 +438,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         T cc = T(0);
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-#ifdef SBMF_ABLATIONS
-            if (a.tune & 0x1000u)  // ablation (wrong results): no MFMA
-                g[v & 3] += s[v];
-            else
-#endif
-#ifdef SBMF_ABL_NOMFMA
-            g[v & 3] += s[v];  // timing-only build (wrong results): no MFMA
-#else
             g = MfmaT<T>::mfma(s[v], g);
-#endif
             cc += s[v] * eR[4 * v];
         }
         cc += shfl_xor_t(cc, 16);
@@ -566,11 +493,6 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             const T sd = a.sd_is_var ? var : tsqrt(var);
             const T A = var * sg * mu + sd * z;
             const T Bq = var * tau;
-#ifdef SBMF_ABLATIONS
-            if (a.tune & 0x200u)  // ablation (wrong results): no 16-step recurrence
-                dlt = A - old + Bq * (Cs[ws][ci] + P * old);
-            else
-#endif
             dlt = gblock_solve_lds(&Ls[ws][ci][0], Bq, A - old + Bq * (Cs[ws][ci] + P * old));
             const T nwv = old + dlt;
             if constexpr (NW > 1) {
@@ -589,7 +511,6 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         stamp(4);  // solve + D hand-off
         // ---- 4. e -= S_B D_B (lane (r,i) holds D_i): one butterfly reduce-scatter of the
         // V row sums (row16_scatter), each lane updating the residuals its sums cover
-#ifndef SBMF_ABL_NOBFLY  // timing-only build (wrong results): no residual update
         {
 #pragma unroll
             for (int v = 0; v < V; ++v) s[v] = s[v] * dlt;
@@ -599,7 +520,6 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             for (int j = 0; j < RV; ++j) eR[4 * (vb + j)] = eR[4 * (vb + j)] - s[j];
             asm volatile("" ::: "memory");
         }
-#endif
         stamp(5);  // residual update
 #pragma unroll
         for (int v = 0; v < V; ++v) s[v] = sn[v];
@@ -689,33 +609,16 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 struct GresSums {
     double sq, tr;
 };
-#ifdef SBMF_KPROF_BUILD
-constexpr uint32_t GRES_ALLREAD = 16;  // phase-profile class boundary
-#endif
-// Residual slot of rating q (of a task) in LDS.  The butterfly residual update
-// has lane ci of a rating write the residuals of vectors vb(ci) + j, whose
-// slots are 4*NW apart: plain slots put all 16 lanes of a rating on one bank
-// pair (16-way conflicts).  XOR-ing bits 1-4 of the slot with a 4-bit hash of
-// the vector index J = q / (4 NW) spreads them over 16 bank pairs; the map is a
-// permutation inside each aligned group of 32 slots, so the staging and the
-// epilogue (consecutive slots per lane) stay conflict-free as well.
-#ifndef SBMF_GRES_SWZ
-#define SBMF_GRES_SWZ 0  // measured 5 % slower on the item stage (r03b): off
-#endif
-template <int NW>
-__device__ __forceinline__ uint32_t gres_swz(uint32_t J) {
-    return SBMF_GRES_SWZ ? (((J ^ (J >> 4)) & 15u) << 1) : 0u;
-}
-template <int NW>
-__device__ __forceinline__ uint32_t gres_slot(uint32_t q) {
-    return q ^ gres_swz<NW>(q / (4 * NW));
-}
+// Residual slot of rating q (of a task) in LDS: slot q.  The butterfly residual
+// update has lane ci of a rating write the residuals of vectors vb(ci) + j, whose
+// slots are 4*NW apart, so all 16 lanes of a rating hit one bank pair (16-way
+// conflicts on two writes per lane per block); an XOR swizzle that removed them
+// measured 5 % slower on the item stage (VGPR spills, r03b), a pad slot per 32
+// 1 % slower.
 // The order in which k_gres' residual update issues the next block's gathers:
 // the butterfly frees vectors [VP/2, VC) first, then [VP/4, VP/2), ..., and the
 // vectors whose residuals the lane updates ([0, RV)) last.
-#ifndef SBMF_GRES_ORD
-#define SBMF_GRES_ORD 1  // measured: item streaming 3.56 -> 3.49 ms, user 1.515 -> 1.49 (r03s3)
-#endif
+// (measured: item streaming 3.56 -> 3.49 ms, user 1.515 -> 1.49 against index order, r03s3)
 template <int VC>
 struct GresOrder {
     static constexpr int VP = VC <= 8 ? 8 : VC <= 16 ? 16 : VC <= 32 ? 32 : VC <= 64 ? 64 : 128;
@@ -798,19 +701,11 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
     // this lane's slots: vector j of wave wr is rating 4*(wr + j*NW) + rr, i.e.
     // a fixed per-lane base plus j*4*NW (an immediate LDS offset)
     const uint32_t* const pjW = pjL + 4 * wr + rr;
-    const uint32_t lb = 4 * wr + rr;  // this lane's slot in every vector (before the swizzle)
+    const uint32_t lb = 4 * wr + rr;  // this lane's slot in every vector
     constexpr int JS = 4 * NW;
-    // residual slot of this lane's rating in vector j of its wave (j = vector index / NW)
-    // (lb is re-read through an opaque move at each use so the compiler does not hoist
-    // VC swizzled addresses out of the block loop into VGPRs)
-    auto eS = [&](uint32_t j) -> T& {
-        uint32_t lbo = lb;
-        if constexpr (SBMF_GRES_SWZ) asm volatile("v_mov_b32 %0, %1" : "=v"(lbo) : "v"(lb));
-        if constexpr (JS % 32 == 0)  // the XOR stays inside the lane-slot field: an immediate offset per j
-            return eL[j * JS + (lbo ^ gres_swz<NW>(j))];
-        else
-            return eL[gres_slot<NW>(j * JS + lbo)];
-    };
+    // residual slot of this lane's rating in vector j of its wave (j = vector index / NW):
+    // a fixed per-lane base plus an immediate offset per j
+    auto eS = [&](uint32_t j) -> T& { return eL[j * JS + lb]; };
 
     // task order: a queue claimed in list order, one returning atomic per task,
     // so a split row's chunks start as soon as enough workgroups are free
@@ -827,24 +722,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
         if (n == 0) continue;  // empty round slot (uniform)
         const uint32_t row = tk.row, beg = tk.beg, nch = tk.nch;
         const uint32_t vpw = ((n + 3) / 4 + NW - 1) / NW;  // vectors per wave
-        // optional phase profile (build with KPROF=1, run with SBMF_KPROF=1): wave 0's cycles per phase
-#ifdef SBMF_KPROF_BUILD
-        unsigned long long tp = (sy.prof && threadIdx.x == 0) ? clock64() : 0ull;
-        // per chunk-count class (whole rows / 2..GRES_ALLREAD chunks / more): [32 + 24*SIDE + 8*cls]
-        unsigned long long* const pcls =
-            sy.prof ? sy.prof - 8 * SIDE + 32 + 24 * SIDE + 8 * (nch == 1 ? 0 : nch <= GRES_ALLREAD ? 1 : 2) : nullptr;
-        if (sy.prof && threadIdx.x == 0) atomicAdd(&pcls[7], 1ull);
-        auto stamp = [&](int ph) {
-            if (sy.prof && threadIdx.x == 0) {
-                const unsigned long long now = clock64();
-                atomicAdd(&sy.prof[ph], now - tp);
-                atomicAdd(&pcls[ph], now - tp);
-                tp = now;
-            }
-        };
-#else
-        auto stamp = [](int) {};
-#endif
+        SBMF_GRES_PHASES(nch);  // stamp(phase): the diagnostic phase profile
         // size class: the task's vectors per wave, rounded up to VW/4, VW/2, 3VW/4 or VW
         auto body = [&](auto vc) {
             constexpr int VC = decltype(vc)::value;
@@ -853,11 +731,8 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 const bool in = x < n;
                 const uint32_t qx = in ? (uint32_t)CHK(beg + x, a.lim_this) : 0u;
                 pjL[x] = (in ? a.part[qx] : a.zrow) * Kp;  // host checks (P+2)*Kp < 2^32
-#ifdef SBMF_ABL_GATHER0
-                pjL[x] = 0;  // timing-only build (wrong results): every slice from partner row 0
-#endif
                 pmL[x] = in ? a.perm[qx] : 0u;
-                if (!a.e_from_dot) eL[gres_slot<NW>(x)] = in ? a.E_this[qx] : T(0);
+                if (!a.e_from_dot) eL[x] = in ? a.E_this[qx] : T(0);
             }
             for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {  // per-half normals and old values of the row
                 zL[k] = k < K ? a.zbuf[(size_t)CHK(row, a.lim_rows) * K + k] : T(0);
@@ -872,7 +747,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     for (uint32_t k0 = 0; k0 < K; k0 += GB)
                         d += a.partner[(size_t)pj + k0 + ci] * a.own[(size_t)row * Kp + k0 + ci];
                     d = row16_sum(d);
-                    if (ci == 0) eL[gres_slot<NW>(q)] = q < n ? a.r_this[beg + q] - d : T(0);
+                    if (ci == 0) eL[q] = q < n ? a.r_this[beg + q] - d : T(0);
                 }
                 __syncthreads();
             }
@@ -890,13 +765,6 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             // DPP moves instead of 4 VC row-sum steps.  The registers each level
             // frees take their next slices at once (next(j) = the gather of vector j).
             auto apply = [&](auto& s, T D, auto&& next) {
-#ifdef SBMF_ABL_NOBFLY  // timing-only build (wrong results): no residual update, the gathers only
-                constexpr int VCn = sizeof(s) / sizeof(s[0]);
-                (void)D;
-#pragma unroll
-                for (int j = 0; j < VCn; ++j) next(j);
-                return;
-#endif
                 // VC rounded up to a power of two (VP); vectors VC..VP-1 are zero
                 constexpr int VP = VC <= 8 ? 8 : VC <= 16 ? 16 : VC <= 32 ? 32 : VC <= 64 ? 64 : 128;
 #pragma unroll
@@ -937,23 +805,12 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             // G_t = S_t^T S_t by MFMA, c_t = S_t^T e (this lane's column, summed over
             // the 4 ratings of each vector)
             auto accumulate = [&](auto& s, acc_t& g, T& cc) {
-#ifdef SBMF_ABLATIONS
-                if (a.tune & 0x80000u) {  // ablation (wrong results): no MFMA (c only, G from one vector)
-                    g = MfmaT<T>::mfma(s[0], g);
-#pragma unroll
-                    for (int j = 0; j < VC; ++j) cc += s[j] * eS(j);
-                } else
-#endif
 #pragma unroll
                 for (int i = 0; i < VC; ++i) {
                     // vectors in the order their gathers were issued (GresOrder): the first
                     // MFMAs wait only for the oldest loads, not for all of them
-                    const int j = SBMF_GRES_ORD ? GresOrder<VC>::v[i] : i;
-#ifdef SBMF_ABL_NOMFMA
-                    g[j & 3] += s[j];  // timing-only build (wrong results): no MFMA
-#else
+                    const int j = GresOrder<VC>::v[i];
                     g = MfmaT<T>::mfma(s[j], g);
-#endif
                     cc += s[j] * eS(j);
                 }
                 cc += shfl_xor_t(cc, 16);
@@ -993,11 +850,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     for (int w = 0; w < NW; ++w)
                         val += Pw[w][xo];
                 }
-#ifdef SBMF_ABLATIONS
-                const bool xchg = nch > 1 && !(a.tune & 0x4000u);  // ablation (wrong results): no hand-off
-#else
                 const bool xchg = nch > 1;
-#endif
                 if (xchg) {
                     // cross-chunk sum over the row's chunks (see the header comment):
                     // every chunk stores its packed partial, adds once to the block's
@@ -1072,11 +925,6 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     if (!a.sd_is_var) sd = tsqrt(var);
                     const T A = var * sg * mu + sd * z;
                     const T Bq = var * tau;
-#ifdef SBMF_ABLATIONS
-                    if (a.tune & 0x8000u)  // ablation (wrong results): no 16-step recurrence
-                        dlt = A - old + Bq * (Cc + P * old);
-                    else
-#endif
                     dlt = gblock_solve_lds(&Rr[ci * GLD], Bq, A - old + Bq * (Cc + P * old));
                     if (lane < GB) {
                         if (kin) newS[kk] = old + dlt;
@@ -1098,12 +946,6 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     asm volatile("" ::: "memory");
                     if (t > 0) {
                         // apply block t-1 with the held slice, then gather slice t into it
-#ifdef SBMF_ABLATIONS
-                        if (a.tune & 0x40000u) {  // ablation (wrong results): no residual update
-#pragma unroll
-                            for (int j = 0; j < VC; ++j) s[j] = gat(j, t);
-                        } else
-#endif
                         apply(s, Dl, [&](int j) { s[j] = gat(j, t); });
                     }
                     stamp(1);  // apply + gather issue
@@ -1121,7 +963,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
             __syncthreads();
             double sq = 0.0, trs = 0.0;
             for (uint32_t x = threadIdx.x; x < n; x += 64 * NW) {
-                const T e = eL[gres_slot<NW>(x)];
+                const T e = eL[x];
                 a.E_other[CHK(pmL[x], a.lim_other)] = e;
                 sq += (double)(e * e);
                 if (a.row_tr) {

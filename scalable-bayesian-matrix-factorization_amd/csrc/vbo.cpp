@@ -139,6 +139,8 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
         comm = cm;
         R = cm->nranks();
         rank = cm->rank();
+        // VGItem.mask holds one bit per rank's part (the combine kernels test bit r)
+        if (R > 32) fail(SBMF_E_ARG, "online VB: at most 32 ranks (%d given)", R);
     }
     K = c.num_factor;
     Kp = (K + 15) / 16 * 16;
@@ -441,7 +443,7 @@ void VBLearner::build_layout(VBLayout& L, uint32_t ep) {
             for (uint32_t a = 0; a < J; ++a)
                 if (cnt[(size_t)b * J + a]) {
                     gidx[(size_t)b * J + a] = (uint32_t)L.gitems.size() - L.gitem0[b];
-                    L.gitems.push_back(VGItem{I + a, cnt[(size_t)b * J + a], XS > 1 ? 0u : R >= 32 ? ~0u : (1u << R) - 1});
+                    L.gitems.push_back(VGItem{I + a, cnt[(size_t)b * J + a], XS > 1 ? 0u : R == 32 ? ~0u : (1u << R) - 1});
                 }
             gmax = std::max(gmax, (uint32_t)L.gitems.size() - L.gitem0[b]);
         }

@@ -610,7 +610,7 @@ __global__ __launch_bounds__(256) void k_item_v(const VGItem* __restrict__ gi, u
     const uint32_t a = gi[g].attr, n = gi[g].n;
     double e1 = 0.0, e2 = 0.0;
     for (int r = 0; r < R; ++r)
-        if (r >= 32 || (gi[g].mask >> r & 1u)) {  // ranks >= 32: mask ~0u (no shift past 31)
+        if (gi[g].mask >> r & 1u) {  // r < 32: vbo.cpp refuses more ranks
             e1 += recv[(size_t)r * nG + g].x;
             e2 += recv[(size_t)r * nG + g].y;
         }
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256) void k_item_w(const VGItem* __restrict__ gi, u
     const uint32_t a = gi[g].attr, n = gi[g].n;
     double e1 = 0.0, e2 = 0.0;
     for (int r = 0; r < R; ++r)
-        if (r >= 32 || (gi[g].mask >> r & 1u)) {  // ranks >= 32: mask ~0u (no shift past 31)
+        if (gi[g].mask >> r & 1u) {  // r < 32: vbo.cpp refuses more ranks
             e1 += recv[(size_t)r * nG + g].x;
             e2 += recv[(size_t)r * nG + g].y;
         }

@@ -80,3 +80,34 @@ def test_oracle_follows_biased_reference_stall():
     assert np.array_equal(o["rmse"], gold[:40])
     assert gold.min() > 1.05 and abs(gold[-1] - te[2].std()) < 0.01
     assert np.abs(o["U"]).mean() < 0.01 and np.abs(o["V"]).mean() < 0.01
+
+
+def _seeds_golden(name):
+    import os
+    from conftest import GOLD
+    with open(os.path.join(GOLD, name)) as f:
+        return np.array([[float(x) for x in line.split()] for line in f if line.strip()])
+
+
+def test_seed_sweep_golden_is_the_reference_chain(ml100k):
+    """tests/golden/ref_final_ml100k_k20_seeds64.txt (the compiled gibbs_sbpmf_final over
+    seeds 1..64, first 20 sweeps) is the reference-stream chain: the oracle reproduces
+    sampled rows bit for bit."""
+    ref = _seeds_golden("ref_final_ml100k_k20_seeds64.txt")
+    assert ref.shape == (64, 20)
+    for seed in (1, 33, 64):
+        o = oracle.run(*ml100k, K=20, iters=20, seed=seed, want_factors=False)
+        assert np.array_equal(o["rmse"], ref[seed - 1])
+
+
+def test_oracle_philox_chain_matches_reference_chain_in_distribution(ml100k):
+    """The throughput stream's restatement (the oracle's Philox mode, which the GPU
+    follows to ~1e-9) against the 64 reference chains: seed means at sweeps 10 and 20
+    within two standard errors (the criterion of tests/test_gpu_statistical.py)."""
+    ref = _seeds_golden("ref_final_ml100k_k20_seeds64.txt")
+    ph = np.array([oracle.run(*ml100k, K=20, iters=20, seed=s, rng="philox", want_factors=False)["rmse"]
+                   for s in range(1, 65)])
+    for k in (9, 19):
+        d = ph[:, k].mean() - ref[:, k].mean()
+        se = np.sqrt(ph[:, k].var(ddof=1) / 64 + ref[:, k].var(ddof=1) / 64)
+        assert abs(d) <= 2 * se, (k, d, se)
