@@ -4,6 +4,7 @@ The CPU restatement of the reference sampler (sbpmf_oracle.c), used only by
 tests/, __graft_entry__.smoke() (as the checker) and bench.py's cpu_baseline.
 """
 import ctypes as C
+import time
 import os
 
 import numpy as np
@@ -209,15 +210,17 @@ def run_fmm(train, test, K=8, iters=10, seed=1, method="mcmc", k0=1, k1=1, init_
         res.w, res.v = _p(w, C.c_double), _p(v, C.c_double)
     a0, a1 = (np.ascontiguousarray(x, np.uint32) for x in ta)
     b0, b1 = (np.ascontiguousarray(x, np.uint32) for x in sa)
+    t0 = time.perf_counter()
     rc = L.oracle_fmm_run(C.byref(cfg), C.c_uint64(len(ty)), _p(a0, C.c_uint32), _p(a1, C.c_uint32),
                           _p(ty, C.c_double), C.c_uint64(len(sy)), _p(b0, C.c_uint32), _p(b1, C.c_uint32),
                           _p(sy, C.c_double), C.c_uint32(p_train), C.c_uint32(p_test), C.byref(res))
+    seconds = time.perf_counter() - t0  # set-up + the iterations
     if rc != 0:
         raise ValueError("oracle_fmm_run failed (%d)" % rc)
     n = res.iters_done
     return {"rmse_test": rt[:n], "rmse_this": rh[:n], "rmse_train": rr[:n], "alpha": al[:n],
             "pred": pred[:len(sy)], "w": w, "v": v, "w0": res.w0, "num_attribute": res.num_attribute,
-            "num_users": I}
+            "num_users": I, "seconds": seconds}
 
 
 def stream(seed, kind, n, shape=1.0):
