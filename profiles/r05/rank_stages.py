@@ -5,7 +5,7 @@ BASELINE config 4 (ML-20M-shaped, K=200, f64) as rank r of an N=8 run, every ran
 in turn, through sbmf_test_virtual_rank: the rank runs exactly its own row blocks,
 4 nnz-balanced stages per half, bins and streaming tasks, with the exchange
 skipped (timing only; other ranks' rows keep their initial values, their
-residuals read 0).  Per rank and stage: the device time on the compute stream
+residuals read 0; SBMF_STAGES sets the stages per half).  Per rank and stage: the device time on the compute stream
 (HIP events), the stage's rows / ratings and its longest row.  The stage holding
 the rank's longest split item row is marked.  Philox stream, residuals carried
 (recompute_every 0): the benchmarked configuration.
@@ -58,7 +58,8 @@ def main():
     N = args.ranks
     ub, ib = partition_rows(uptr, N), partition_rows(iptr, N)
     trd, ted = Data(*tr), Data(*te)
-    out = {"shape": args.shape, "K": args.K, "ranks": N, "stages": 4, "n_train": int(len(tr[0])), "per_rank": []}
+    NST = int(os.environ.get("SBMF_STAGES", "4"))
+    out = {"shape": args.shape, "K": args.K, "ranks": N, "stages": NST, "n_train": int(len(tr[0])), "per_rank": []}
     ranks = [args.only] if args.only >= 0 else list(range(N))
     for r in ranks:
         L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", recompute_every=0)
@@ -70,9 +71,10 @@ def main():
         prep = time.time() - t0
         L.learn(sweeps=1)  # warm-up (first sweep: residual recompute, launch-kind events)
         L.learn(sweeps=args.sweeps)
-        ms = np.zeros(8)
+        ms = np.zeros(2 * NST)
         ns = C.c_uint32()
-        assert lib.sbmf_test_stage_ms(L.ctx, ms.ctypes.data_as(C.POINTER(C.c_double)), 8, C.byref(ns)) == 0
+        assert lib.sbmf_test_stage_ms(L.ctx, ms.ctypes.data_as(C.POINTER(C.c_double)), 2 * NST, C.byref(ns)) == 0
+        assert ns.value == NST
         t = L.timing()
         hist = L.history[-args.sweeps:]
         rec = {"rank": r, "prepare_s": prep, "ms_sweep": float(np.mean([h["ms_sweep"] for h in hist])),
@@ -80,14 +82,14 @@ def main():
                "ms_eval": t.ms_eval, "halves": {}}
         for sd, (name, ptr, bnd) in enumerate((("user", uptr, ub), ("item", iptr, ib))):
             b0, b1 = int(bnd[r]), int(bnd[r + 1])
-            sb = stage_cuts(ptr, b0, b1, 4)
+            sb = stage_cuts(ptr, b0, b1, NST)
             deg = np.diff(ptr.astype(np.int64))
             longest = int(np.argmax(deg[b0:b1])) + b0 if b1 > b0 else -1
             stages = []
-            for p in range(4):
+            for p in range(NST):
                 s0, s1 = sb[p], sb[p + 1]
                 d = deg[s0:s1]
-                stages.append({"ms": float(ms[sd * 4 + p]), "rows": s1 - s0, "ratings": int(d.sum()),
+                stages.append({"ms": float(ms[sd * NST + p]), "rows": s1 - s0, "ratings": int(d.sum()),
                                "longest_row": int(d.max()) if len(d) else 0,
                                "split_rows_gt1024": int((d > 1024).sum()),
                                "holds_longest_row": bool(s0 <= longest < s1)})
@@ -107,7 +109,7 @@ def main():
         # runs while p+1 computes, so the compute critical path is max over ranks per half
         out["max_over_ranks"] = {h: max(sum(s["ms"] for s in x["halves"][h]["stages"]) for x in pr)
                                  for h in ("user", "item")}
-        out["max_stage_ms"] = {h: [max(x["halves"][h]["stages"][p]["ms"] for x in pr) for p in range(4)]
+        out["max_stage_ms"] = {h: [max(x["halves"][h]["stages"][p]["ms"] for x in pr) for p in range(NST)]
                                for h in ("user", "item")}
     print(json.dumps(out))
 

@@ -121,11 +121,12 @@ hipError_t launch_resid(const ResidTask* tasks, uint32_t ntask, const uint32_t* 
                         uint32_t K, uint32_t Kp, T* E_other, double* task_sq, double* row_sq, const double* b_own,
                         const double* b_part, double b0, hipStream_t st);
 
-// Column partials over table rows [r0,r1): out[c][0..K) = sum (x-mu)^2,
-// out[c][K..2K) = sum x, c = chunk of 256 rows (global chunk index).
+// Column partials of two tables in one launch, over rows [0, rA) of A and [0, rB)
+// of B: out[c][0..K) = sum (x-mu)^2, out[c][K..2K) = sum x, c = chunk of 64 rows
+// (outA: (rA+63)/64 chunks, outB: (rB+63)/64).
 template <typename T>
-hipError_t launch_colstats(const T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, const T* mu,
-                           double* out, hipStream_t st);
+hipError_t launch_colstats(const T* tabA, uint32_t rA, const T* muA, double* outA, const T* tabB, uint32_t rB,
+                           const T* muB, double* outB, uint32_t K, uint32_t Kp, hipStream_t st);
 
 // Test predictions: pred = clamp(dot(U[u],V[i])) (+ b0 + bu[u] + bv[i] when bu
 // is non-null: the biased sampler); sum[t] += pred if collect;
@@ -166,6 +167,9 @@ hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, h
 hipError_t launch_sum(const double* in, uint64_t n, double* out, double* scratch, hipStream_t st);
 // out[w] = sum_c in[c*width + w], c ascending (width columns, nchunk rows)
 hipError_t launch_sum_cols(const double* in, uint32_t nchunk, uint32_t width, double* out, hipStream_t st);
+// The same for two arrays of the same width in one launch.
+hipError_t launch_sum_cols2(const double* in, uint32_t nchunk, double* out, const double* in2, uint32_t nchunk2,
+                            double* out2, uint32_t width, hipStream_t st);
 
 // Philox init: tab[r][k] = sd * z(seed, sweep=0xffffffff, tag, r, k), rows [r0,r1).
 // z[row][k] = N(0,1) Philox normal (seed, sweep, tag, row, pair k/2) for rows [r0, r1):

@@ -103,10 +103,24 @@ __device__ __forceinline__ void load_slice(const float* p, float (&o)[8]) {
 
 template <typename T>
 __device__ __forceinline__ T tsqrt(T x);
+template <typename T>
+__device__ __forceinline__ T tsqrt_if(T x, int want);
 template <>
 __device__ __forceinline__ float tsqrt<float>(float x) { return sqrtf(x); }
 template <>
 __device__ __forceinline__ double tsqrt<double>(double x) { return sqrt(x); }
+// sqrt(x) if `want` (a kernel argument: wave-uniform), else x -- as a real branch: the
+// compiler if-converts the plain select and runs the whole f64 square-root sequence
+// (about 20 dependent instructions) on the solving wave's critical path even under the
+// variance-as-stdev quirk, where it is never used
+template <typename T>
+__device__ __forceinline__ T tsqrt_if(T x, int want) {
+    if (__builtin_amdgcn_readfirstlane(want)) {
+        asm volatile("" ::: "memory");
+        x = tsqrt(x);
+    }
+    return x;
+}
 
 // One coordinate draw, shared by all row paths.
 template <typename T>
@@ -490,7 +504,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
             const T old = oldc, sg = sgc, mu = muc;
             const T z = zS[ws][kk];
             const T var = kin ? T(1) / (sg + tau * P) : T(0);  // k >= K: var = 0 -> d = -old = 0
-            const T sd = a.sd_is_var ? var : tsqrt(var);
+            const T sd = tsqrt_if(var, !a.sd_is_var);
             const T A = var * sg * mu + sd * z;
             const T Bq = var * tau;
             dlt = gblock_solve_lds(&Ls[ws][ci][0], Bq, A - old + Bq * (Cs[ws][ci] + P * old));
@@ -921,8 +935,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     const T P = Rr[PW + ci];
                     const T Cc = Rr[GB * GLD + ci];
                     const T var = kin ? T(1) / (sg + tau * P) : T(0);
-                    T sd = var;  // a uniform branch: no square root under the variance-as-stdev quirk
-                    if (!a.sd_is_var) sd = tsqrt(var);
+                    const T sd = tsqrt_if(var, !a.sd_is_var);  // no square root under the quirk
                     const T A = var * sg * mu + sd * z;
                     const T Bq = var * tau;
                     dlt = gblock_solve_lds(&Rr[ci * GLD], Bq, A - old + Bq * (Cc + P * old));
@@ -1092,15 +1105,26 @@ __global__ __launch_bounds__(256) void k_resid_rows(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------------------ column statistics
-template <typename T>
-__global__ __launch_bounds__(256) void k_colstats(const T* __restrict__ tab, uint32_t K, uint32_t Kp, uint32_t r0,
-                                                   uint32_t r1, const T* __restrict__ mu, double* __restrict__ out) {
-    // wave w sums rows rb + w, rb + w + 4, ... of the chunk (one coalesced row
-    // segment per load, every lane busy), lane l columns l, l + 64, ...; the four
-    // waves' partials are then added in wave order (fixed: bitwise repeatable)
-    constexpr int CPL = 4;  // columns per lane: K <= 256
-    const uint32_t c = r0 / 256 + blockIdx.x;  // global chunk index (r0 is chunk aligned)
-    const uint32_t rb = max(c * 256, r0), re = min(c * 256 + 256, r1);
+// Both tables in one launch: blocks [0, nA) take table A's 64-row chunks, the rest
+// table B's.  Wave w sums rows 16w .. 16w+15 of its chunk (all of them loaded
+// before the first add: one coalesced row segment per load, lane l on columns
+// l, l + 64, ...), in row order; the four waves' partials are added in wave order
+// (fixed: bitwise repeatable, and the same for any 256-aligned rank split).  The
+// round-4 form -- 256-row chunks, four rows in flight per wave -- ran the two
+// tables at 1.3 / 0.35 TB/s (98 / 71 us at ML-20M K=100): too few waves in flight.
+template <typename T, int CPL>
+__global__ __launch_bounds__(256) void k_colstats(const T* __restrict__ tabA, uint32_t rA, const T* __restrict__ muA,
+                                                   double* __restrict__ outA, uint32_t nA, const T* __restrict__ tabB,
+                                                   uint32_t rB, const T* __restrict__ muB, double* __restrict__ outB,
+                                                   uint32_t K, uint32_t Kp) {
+    constexpr int RW = 16;                   // rows per wave
+    constexpr int RB = CPL <= 2 ? 16 : 8;    // rows loaded at once (<= 32 doubles in flight per lane)
+    const bool first = blockIdx.x < nA;
+    const T* __restrict__ tab = first ? tabA : tabB;
+    const T* __restrict__ mu = first ? muA : muB;
+    double* __restrict__ out = first ? outA : outB;
+    const uint32_t R = first ? rA : rB;
+    const uint32_t c = first ? blockIdx.x : blockIdx.x - nA;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double m[CPL], s1[CPL], s2[CPL];
 #pragma unroll
@@ -1110,16 +1134,25 @@ __global__ __launch_bounds__(256) void k_colstats(const T* __restrict__ tab, uin
         s1[j] = 0.0;
         s2[j] = 0.0;
     }
-    uint32_t r = rb + w;
-#pragma unroll 4
-    for (; r < re; r += 4) {
-        const T* row = tab + (size_t)r * Kp + lane;
+    const uint32_t rb = c * 64 + w * RW;
 #pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-            if (lane + 64 * j < K) {
-                const double x = (double)row[64 * j];
-                s2[j] += (x - m[j]) * (x - m[j]);
-                s1[j] += x;
+    for (int b0 = 0; b0 < RW; b0 += RB) {
+        double x[RB][CPL];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+            const uint32_t r = rb + b0 + i;
+            const T* row = tab + (size_t)(r < R ? r : 0) * Kp + lane;
+#pragma unroll
+            for (int j = 0; j < CPL; ++j) x[i][j] = lane + 64 * j < Kp ? (double)row[64 * j] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+            if (rb + b0 + i < R) {
+#pragma unroll
+                for (int j = 0; j < CPL; ++j) {
+                    s2[j] += (x[i][j] - m[j]) * (x[i][j] - m[j]);
+                    s1[j] += x[i][j];
+                }
             }
         }
     }
@@ -1137,8 +1170,13 @@ __global__ __launch_bounds__(256) void k_colstats(const T* __restrict__ tab, uin
 }
 
 // ------------------------------------------------------------------ test evaluation
-// 256 test ratings per block; each wave takes 4 at a time with 16 lanes per
-// rating (coalesced 128-byte reads of both factor rows).
+// 256 test ratings per block: each 16-lane group of a wave takes 16 consecutive
+// ratings (user order), two at a time, 16 lanes per rating (coalesced 128-byte
+// reads of both factor rows).  Lane i of a group first loads everything rating i
+// of its 16 needs besides the rows -- ids, target, running sum -- in one round
+// trip; the ids reach the group's lanes by shuffles, and lane i updates rating
+// i's running sum itself.  (Round 4 loaded the ids of each pair, then the rows,
+// then the sum and target: three dependent round trips per pair.)
 template <typename T>
 __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ti,
                                                const double* __restrict__ tr, uint64_t t0, uint64_t t1,
@@ -1149,25 +1187,27 @@ __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, c
                                                double b0) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ci = lane & 15, rr = lane >> 4;
-    const uint64_t base = t0 + (uint64_t)blockIdx.x * 256 + (uint64_t)w * 64;
+    // group rr of wave w: ratings gbase + 0..15
+    const uint64_t gbase = t0 + (uint64_t)blockIdx.x * 256 + (uint64_t)w * 64 + (uint64_t)rr * 16;
     const uint32_t nb = Kp / 16;  // k-blocks; the padding columns are zero in both tables
+    const uint64_t mt = gbase + ci;  // this lane's own rating
+    const bool mok = mt < t1;
+    const uint64_t mtc = mok ? mt : t0;
+    const uint32_t myu = tu[mtc], myi = ti[mtc];
+    const double myr = tr[mtc], mys = sum[mtc];
+    double myb = 0.0;
+    if (bu) myb = (b0 + bu[myu]) + bv[myi];
     double a2 = 0.0, t2 = 0.0;
-    // two ratings per 16-lane group at a time, their ids and every row slice of a chunk of up
-    // to CB k-blocks loaded before the first product (the per-block masked loads of one rating
-    // at a time were a dependent round trip each); products summed in k order, the zero
-    // padding columns adding +0 (the clamped prediction is the same)
+    // products summed in k order, the zero padding columns adding +0 (the clamped
+    // prediction is the same as over K columns)
     constexpr int PR = 2, CB = 8;
     for (int it = 0; it < 16; it += PR) {
         uint32_t uu[PR], ii[PR];
-        uint64_t tt[PR];
-        bool ok[PR];
 #pragma unroll
         for (int j = 0; j < PR; ++j) {
-            tt[j] = base + (it + j) * 4 + rr;
-            ok[j] = tt[j] < t1;
-            const uint64_t tc = ok[j] ? tt[j] : t0;
-            uu[j] = tu[tc];
-            ii[j] = ti[tc];
+            const int src = (lane & 48) + it + j;  // lane it+j of this group
+            uu[j] = (uint32_t)__shfl((int)myu, src);
+            ii[j] = (uint32_t)__shfl((int)myi, src);
         }
         T p[PR];
 #pragma unroll
@@ -1190,20 +1230,19 @@ __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, c
         }
 #pragma unroll
         for (int j = 0; j < PR; ++j) {
-            T pj = row16_sum(p[j]);
-            const uint64_t t = tt[j];
-            if (ok[j] && ci == 0) {
-                if (bu) pj = (T)((b0 + bu[uu[j]]) + bv[ii[j]]) + pj;  // biased sampler (gibbs_sbpmf2.cpp:614-618)
+            T pj = row16_sum(p[j]);  // the same value in the group's 16 lanes
+            if (ci == it + j && mok) {
+                if (bu) pj = (T)myb + pj;  // biased sampler (gibbs_sbpmf2.cpp:614-618)
                 pj = (pj < hi) ? pj : hi;
                 pj = (lo < pj) ? pj : lo;
-                double s = sum[t];
+                double s = mys;
                 if (collect) {
                     s += (double)pj;
-                    sum[t] = s;
+                    sum[mt] = s;
                 }
-                const double d = tr[t] - s / div;
+                const double d = myr - s / div;
                 a2 += d * d;
-                const double dt = tr[t] - (double)pj;
+                const double dt = myr - (double)pj;
                 t2 += dt * dt;
             }
         }
@@ -1240,10 +1279,18 @@ __global__ __launch_bounds__(256) void k_sum_blocks(const double* __restrict__ i
 }
 
 // out[w] = sum over chunks of in[c][w]: one block per column, thread t sums
-// chunks t, t+256, ... in order, then a fixed tree -> deterministic.
+// chunks t, t+256, ... in order, then a fixed tree -> deterministic.  Blocks
+// [width, 2 width) do the same for a second array (in2, nchunk2 -> out2).
 __global__ __launch_bounds__(256) void k_sum_cols(const double* __restrict__ in, uint32_t nchunk, uint32_t width,
-                                                   double* __restrict__ out) {
-    const uint32_t w = blockIdx.x;
+                                                   double* __restrict__ out, const double* __restrict__ in2,
+                                                   uint32_t nchunk2, double* __restrict__ out2) {
+    uint32_t w = blockIdx.x;
+    if (w >= width) {
+        w -= width;
+        in = in2;
+        nchunk = nchunk2;
+        out = out2;
+    }
     double s = 0.0;
     for (uint32_t c = threadIdx.x; c < nchunk; c += 256) s += in[(size_t)c * width + w];
     s = wave_sum(s);
@@ -1573,11 +1620,17 @@ hipError_t launch_resid(const ResidTask* tasks, uint32_t ntask, const uint32_t* 
 }
 
 template <typename T>
-hipError_t launch_colstats(const T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, const T* mu, double* out,
-                           hipStream_t st) {
-    if (r1 <= r0) return hipSuccess;
-    const uint32_t c0 = r0 / 256, c1 = (r1 + 255) / 256;
-    k_colstats<T><<<c1 - c0, 256, 0, st>>>(tab, K, Kp, r0, r1, mu, out);
+hipError_t launch_colstats(const T* tabA, uint32_t rA, const T* muA, double* outA, const T* tabB, uint32_t rB,
+                           const T* muB, double* outB, uint32_t K, uint32_t Kp, hipStream_t st) {
+    const uint32_t nA = (rA + 63) / 64, nB = (rB + 63) / 64;
+    if (nA + nB == 0) return hipSuccess;
+    if (K > 256 || Kp > 256) return hipErrorInvalidValue;
+    if (Kp <= 64)
+        k_colstats<T, 1><<<nA + nB, 256, 0, st>>>(tabA, rA, muA, outA, nA, tabB, rB, muB, outB, K, Kp);
+    else if (Kp <= 128)
+        k_colstats<T, 2><<<nA + nB, 256, 0, st>>>(tabA, rA, muA, outA, nA, tabB, rB, muB, outB, K, Kp);
+    else
+        k_colstats<T, 4><<<nA + nB, 256, 0, st>>>(tabA, rA, muA, outA, nA, tabB, rB, muB, outB, K, Kp);
     return hipGetLastError();
 }
 
@@ -1612,7 +1665,12 @@ hipError_t launch_sum(const double* in, uint64_t n, double* out, double* scratch
 }
 
 hipError_t launch_sum_cols(const double* in, uint32_t nchunk, uint32_t width, double* out, hipStream_t st) {
-    k_sum_cols<<<width, 256, 0, st>>>(in, nchunk, width, out);
+    k_sum_cols<<<width, 256, 0, st>>>(in, nchunk, width, out, nullptr, 0, nullptr);
+    return hipGetLastError();
+}
+hipError_t launch_sum_cols2(const double* in, uint32_t nchunk, double* out, const double* in2, uint32_t nchunk2,
+                            double* out2, uint32_t width, hipStream_t st) {
+    k_sum_cols<<<2 * width, 256, 0, st>>>(in, nchunk, width, out, in2, nchunk2, out2);
     return hipGetLastError();
 }
 
@@ -1678,8 +1736,8 @@ hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, h
                                         hipStream_t);                                                                \
     template hipError_t launch_philox_fill<T>(T*, uint32_t, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t,        \
                                               hipStream_t);                                                          \
-    template hipError_t launch_colstats<T>(const T*, uint32_t, uint32_t, uint32_t, uint32_t, const T*, double*,     \
-                                           hipStream_t);                                                             \
+    template hipError_t launch_colstats<T>(const T*, uint32_t, const T*, double*, const T*, uint32_t, const T*,    \
+                                           double*, uint32_t, uint32_t, hipStream_t);                                \
     template hipError_t launch_test<T>(const uint32_t*, const uint32_t*, const double*, uint64_t, uint64_t,         \
                                        const T*, const T*, uint32_t, uint32_t, T, T, int, double, double*, double*, \
                                        const double*, const double*, double, hipStream_t);                          \

@@ -609,7 +609,7 @@ static void prepare_T(sbmf_ctx* c) {
     // [sig_u | mu_u | sig_v | mu_v], each Kp long and zero padded, + 16 slack for prefetch
     c->d_hyper.alloc((4 * (size_t)c->Kp + 16) * sizeof(T));
     HIPCHK(hipMemsetAsync(c->d_hyper.p, 0, c->d_hyper.bytes, st));
-    const uint32_t nchunk = (std::max(c->I, c->J) + 255) / 256;
+    const uint32_t nchunk = (c->I + 63) / 64 + (c->J + 63) / 64;  // both tables' 64-row chunks
     c->d_colpart.alloc((size_t)nchunk * 2 * c->K * sizeof(double));
     c->h_res.assign(RES_COL + 4 * (size_t)c->K, 0.0);
     c->d_res.alloc(c->h_res.size() * sizeof(double));
@@ -1194,11 +1194,12 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // ---- column statistics with the current mu (:378-381, :397-401)
         const T* hyp = c->d_hyper.as<T>();
         double* colpart = c->d_colpart.as<double>();
-        HIPCHK(launch_colstats<T>(c->d_U.as<T>(), K, c->Kp, 0, c->I, hyp + c->Kp, colpart, st));
-        HIPCHK(launch_sum_cols(colpart, (c->I + 255) / 256, 2 * K, d_res + RES_COL, st));
-        HIPCHK(launch_colstats<T>(c->d_V.as<T>(), K, c->Kp, 0, c->J, hyp + 3 * c->Kp, colpart, st));
-        HIPCHK(launch_sum_cols(colpart, (c->J + 255) / 256, 2 * K, d_res + RES_COL + 2 * K, st));
-        c->timing.n_launch += 5;
+        double* colpart_v = colpart + (size_t)((c->I + 63) / 64) * 2 * K;
+        HIPCHK(launch_colstats<T>(c->d_U.as<T>(), c->I, hyp + c->Kp, colpart, c->d_V.as<T>(), c->J, hyp + 3 * c->Kp,
+                                  colpart_v, K, c->Kp, st));
+        HIPCHK(launch_sum_cols2(colpart, (c->I + 63) / 64, d_res + RES_COL, colpart_v, (c->J + 63) / 64,
+                                d_res + RES_COL + 2 * K, 2 * K, st));
+        c->timing.n_launch += 3;
         HIPCHK(hipMemcpyAsync(c->h_pre, d_res, c->h_res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
     };
     // ---- 2. host draws (:339-342, :375-414) from the prologue's sums: updates
