@@ -130,6 +130,9 @@ typedef struct sbmf_config {
                                  bit 24 = k_gres as a cooperative launch (experiments only; the
                                           default is an ordinary launch in every schedule: tasks are
                                           claimed in queue order, no co-residency needed),
+                                 bit 25 = a half's Gram-block kinds all on one side stream
+                                          (default since round 5: alternating between two side
+                                          streams, beside each other and the streaming launch),
                                  bit 26 = no overlap of the next sweep's prologue (sums, column
                                           statistics, host draws) with the test evaluation
                                           (Philox mode; the chain is the same either way),
@@ -144,8 +147,8 @@ typedef struct sbmf_config {
                                           second stream beside them; the results are the same).
                                  Removed in round 4 with the variants they selected (measured
                                  slower or neutral, kept in git history): bits 0, 5, 6, 8-10, 16,
-                                 20-22, 25 (also the round-4 LDS-DMA prefetch), 31; they are
-                                 ignored.  */
+                                 20-22, 31; they are ignored (bit 25 was the round-4 LDS-DMA
+                                 prefetch before its round-5 use above).  */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--shape", default="ml-20m")
     ap.add_argument("--sweeps", type=int, default=3)
     ap.add_argument("--only", type=int, default=-1)
+    ap.add_argument("--tune", type=int, default=0)
     args = ap.parse_args()
     tr, te, dims = synth.generate(args.shape)
     I, J = dims
@@ -59,10 +60,10 @@ def main():
     ub, ib = partition_rows(uptr, N), partition_rows(iptr, N)
     trd, ted = Data(*tr), Data(*te)
     NST = int(os.environ.get("SBMF_STAGES", "4"))
-    out = {"shape": args.shape, "K": args.K, "ranks": N, "stages": NST, "n_train": int(len(tr[0])), "per_rank": []}
+    out = {"shape": args.shape, "K": args.K, "ranks": N, "stages": NST, "tune": args.tune, "n_train": int(len(tr[0])), "per_rank": []}
     ranks = [args.only] if args.only >= 0 else list(range(N))
     for r in ranks:
-        L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", recompute_every=0)
+        L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", recompute_every=0, tune=args.tune)
         L.init()
         rc = lib.sbmf_test_virtual_rank(L.ctx, N, r)
         assert rc == 0, lib.sbmf_last_error(L.ctx).decode()

@@ -156,8 +156,10 @@ SBMF_HD void philox_normal_pair(uint64_t seed, uint32_t row, uint32_t sweep, uin
     const double u2 = (double)b * (1.0 / 9007199254740992.0);        // [0,1)
     const double rr = sqrt(-2.0 * log(u1));
     const double th = 6.283185307179586476925286766559 * u2;
-    z0 = rr * cos(th);
-    z1 = rr * sin(th);
+    double sn, cs;
+    sincos(th, &sn, &cs);  // one argument reduction for both (the values of sin / cos)
+    z0 = rr * cs;
+    z1 = rr * sn;
 }
 
 // Host-side sequential uniform stream over Philox (hyperparameter draws in

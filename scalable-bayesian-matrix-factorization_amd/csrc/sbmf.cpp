@@ -302,7 +302,8 @@ struct sbmf_ctx {
     std::vector<hipEvent_t> tsev;
     hipEvent_t cev[2] = {};        // [side]: the half's exchange done (comm stream)
     hipStream_t sto = nullptr;     // a half's Gram-block launches, beside its streaming launch
-    hipEvent_t oev[3] = {};        // [fork, join] of those launches, [2]: stream set 0 done
+    hipStream_t sto2 = nullptr;    // tune bit 25: half of them on a second side stream
+    hipEvent_t oev[4] = {};        // [fork, join] of those launches, [2]: stream set 0 done, [3]: sto2 join
     DBuf d_uptr, d_upart, d_uperm, d_ur, d_vptr, d_vpart, d_vperm, d_vr;
     DBuf d_U, d_V, d_Eu, d_Ev, d_zU, d_zV, d_hyper;
     DBuf d_rowsq_u, d_rowtr_u, d_rowsq_v, d_rowtr_v;
@@ -969,31 +970,41 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     // depend on the interleaving.  The streaming launch is an ordinary one in every
     // schedule (its claiming workgroups are resident by construction; tune bit 24's
     // cooperative launch, experiments only, would wait for the whole device).
-    bool others = false;
-    for (int k = 0; k < NBIN; ++k) others |= k != KIND_STREAM && !g.bin_rows[k].empty();
-    const bool ovl = !(c->cfg.tune & 0x20000000u) && others && !g.bin_rows[KIND_STREAM].empty();
+    int others = 0;
+    for (int k = 0; k < NBIN; ++k) others += k != KIND_STREAM && !g.bin_rows[k].empty();
+    const bool serial = (c->cfg.tune & 0x20000000u) != 0;
+    const bool ovl = !serial && others && !g.bin_rows[KIND_STREAM].empty();
+    // The Gram-block kinds alternate between two side streams (sto, sto2), so they also run
+    // beside each other: a small stage's kinds are each bound by one row's latency through
+    // its k-blocks, which a chain of launches adds up (r05s2 per-rank trace).  Per-rank
+    // compute of the 8-way split, 4 stages: K=100 2.06 -> 1.96 ms, K=200 3.09 -> 2.76 ms;
+    // the single-GPU sweep is unchanged (7.33 both ways, r05s5).  Tune bit 25: one side stream.
+    const bool two = !serial && others >= 2 && !(c->cfg.tune & 0x2000000u);
+    const bool side = ovl || two;
     // the split-row counters and queue heads of both stream sets, zeroed before the fork
     // (cleared at the end of the previous streaming stage on this stream, off the path, unless not)
     if (!g.bin_rows[KIND_STREAM].empty() && !c->xcnt_clean) HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
     if (!g.bin_rows[KIND_STREAM].empty()) c->xcnt_clean = false;
-    if (ovl) {
+    if (side) {
         HIPCHK(hipEventRecord(c->oev[0], st));
         HIPCHK(hipStreamWaitEvent(c->sto, c->oev[0], 0));
+        if (two) HIPCHK(hipStreamWaitEvent(c->sto2, c->oev[0], 0));
     }
     // With two stream sets (items: rows > 1024 on 16-wave workgroups, set 1, and the
     // rest on 8-wave ones, set 0), set 1 runs on `st` and set 0 on `sto` beside it
     // (tune bit 30: one after the other), each with split-row areas of its own.
     const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && !g.ss[0].stasks.empty() && !g.ss[1].stasks.empty();
     // (the Gram-block launches on `sto` ahead of set 0 instead of behind it: neutral, r04s22)
-    int last[2] = {-1, -1};  // the last kind launched on st / sto (its end event recorded there)
+    int last[3] = {-1, -1, -1};  // the last kind launched on st / sto / sto2 (its end event recorded there)
+    int nside = 0;  // Gram-block kinds launched so far (two: even ones on sto, odd ones on sto2)
     for (int k = NBIN - 1; k >= 0; --k) {
         if (g.bin_rows[k].empty()) continue;
-        st = ovl && k != KIND_STREAM ? c->sto : c->st;
+        st = side && k != KIND_STREAM ? (two && (nside++ & 1) ? c->sto2 : c->sto) : c->st;
         // launch-kind events: the streaming kind's every sweep (the bench's roofline), the
         // others' on the first sweep of a run only (each event between two launches on a
         // stream leaves the device idle ~6 us)
         const bool timed = c->time_kinds || k == KIND_STREAM;
-        int& lk = last[st == c->st ? 0 : 1];
+        int& lk = last[st == c->st ? 0 : st == c->sto ? 1 : 2];
         if (timed) {
             c->kpv(stage, sd, k) = (int8_t)lk;
             if (lk < 0) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
@@ -1044,9 +1055,13 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         if (timed) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
         c->timing.n_launch++;
     }
-    if (ovl) {
+    if (side) {
         HIPCHK(hipEventRecord(c->oev[1], c->sto));
         HIPCHK(hipStreamWaitEvent(c->st, c->oev[1], 0));
+        if (two) {
+            HIPCHK(hipEventRecord(c->oev[3], c->sto2));
+            HIPCHK(hipStreamWaitEvent(c->st, c->oev[3], 0));
+        }
     }
 }
 
@@ -1530,6 +1545,7 @@ sbmf_ctx::~sbmf_ctx() {
         if (e) (void)hipEventDestroy(e);
     if (hev) (void)hipEventDestroy(hev);
     if (sto) (void)hipStreamDestroy(sto);
+    if (sto2) (void)hipStreamDestroy(sto2);
     if (stc) (void)hipStreamDestroy(stc);
     if (st) (void)hipStreamDestroy(st);
 }
@@ -1742,6 +1758,7 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
     for (auto& e : c->cev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->sto, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->sto2, hipStreamNonBlocking));
     for (auto& e : c->oev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->hev, hipEventDisableTiming));
     *out = c.release();
