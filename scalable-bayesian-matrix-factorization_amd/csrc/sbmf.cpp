@@ -432,8 +432,13 @@ static void prepare_T(sbmf_ctx* c) {
         c->items.perm[pos_v[x]] = pos_u[x];
     }
     // stages per half: the multi-GPU exchange of a stage overlaps the next stage's
-    // compute; one rank needs no exchange (SBMF_STAGES overrides, for tests)
-    c->nstages = c->nranks > 1 ? 4u : 1u;
+    // compute; one rank needs no exchange (SBMF_STAGES overrides, for tests).  Two: each
+    // extra stage costs its launches' fixed latency -- per-rank compute of the 8-way split
+    // at 1 / 2 / 4 stages is 1.25 / 1.50 / 1.99 ms at K=100 and 2.01 / 2.31 / 2.90 ms at
+    // K=200 (virtual ranks, r05s6) -- against about half the exchange hidden per doubling
+    // (0.6 / 0.9 ms per sweep at an assumed 330 GB/s all-gather): two stages are the best
+    // or tied over 150-600 GB/s at both K
+    c->nstages = c->nranks > 1 ? 2u : 1u;
     if (const char* e = std::getenv("SBMF_STAGES")) c->nstages = std::max(1, std::min(16, std::atoi(e)));
     partition(c->users, c->nranks, c->rank, c->nstages);
     partition(c->items, c->nranks, c->rank, c->nstages);

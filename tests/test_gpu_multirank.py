@@ -194,7 +194,7 @@ def _config4(tmp_path_factory, relabel):
 def test_config4_ml20m_k200_ranks_match_single_rank(tmp_path, tmp_path_factory, nranks, relabel):
     """BASELINE config 4's split (ML-20M K=200, user and item row blocks over ranks,
     /root/reference/src/libfm/gibbs_sbpmf_final.cpp:453-535 sharded) at its own shape
-    and at 2, 4 and its own 8 ranks, reference stream, one sweep, default 4 stages per
+    and at 2, 4 and its own 8 ranks, reference stream, one sweep, default 2 stages per
     half: every rank (host comm backend, all on one GPU) ends with the single-rank U, V,
     tau and RMSE bit for bit.  The single-rank run is pinned to the oracle by
     test_gpu_production.py::test_ml20m_k200_reference_stream_one_sweep.  With shuffled
