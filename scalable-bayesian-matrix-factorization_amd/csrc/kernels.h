@@ -122,8 +122,8 @@ hipError_t launch_resid(const ResidTask* tasks, uint32_t ntask, const uint32_t* 
                         const double* b_part, double b0, hipStream_t st);
 
 // Column partials of two tables in one launch, over rows [0, rA) of A and [0, rB)
-// of B: out[c][0..K) = sum (x-mu)^2, out[c][K..2K) = sum x, c = chunk of 64 rows
-// (outA: (rA+63)/64 chunks, outB: (rB+63)/64).
+// of B: out[c][0..K) = sum (x-mu)^2, out[c][K..2K) = sum x, c = chunk of 256 rows
+// (outA: (rA+255)/256 chunks, outB: (rB+255)/256).
 template <typename T>
 hipError_t launch_colstats(const T* tabA, uint32_t rA, const T* muA, double* outA, const T* tabB, uint32_t rB,
                            const T* muB, double* outB, uint32_t K, uint32_t Kp, hipStream_t st);

@@ -1105,19 +1105,19 @@ __global__ __launch_bounds__(256) void k_resid_rows(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------------------ column statistics
-// Both tables in one launch: blocks [0, nA) take table A's 64-row chunks, the rest
-// table B's.  Wave w sums rows 16w .. 16w+15 of its chunk (all of them loaded
-// before the first add: one coalesced row segment per load, lane l on columns
-// l, l + 64, ...), in row order; the four waves' partials are added in wave order
-// (fixed: bitwise repeatable, and the same for any 256-aligned rank split).  The
-// round-4 form -- 256-row chunks, four rows in flight per wave -- ran the two
-// tables at 1.3 / 0.35 TB/s (98 / 71 us at ML-20M K=100): too few waves in flight.
+// Both tables in one launch: blocks [0, nA) take table A's 256-row chunks, the rest
+// table B's.  Wave w sums rows 64w .. 64w+63 of its chunk in row order, loading RB
+// rows at a time before their adds (one coalesced row segment per load, lane l on
+// columns l, l + 64, ...); the four waves' partials are added in wave order (fixed:
+// bitwise repeatable, and the same for any 256-aligned rank split).  Round 4 had
+// four rows in flight per wave: the two tables ran at 1.3 / 0.35 TB/s (98 / 71 us at
+// ML-20M K=100).
 template <typename T, int CPL>
 __global__ __launch_bounds__(256) void k_colstats(const T* __restrict__ tabA, uint32_t rA, const T* __restrict__ muA,
                                                    double* __restrict__ outA, uint32_t nA, const T* __restrict__ tabB,
                                                    uint32_t rB, const T* __restrict__ muB, double* __restrict__ outB,
                                                    uint32_t K, uint32_t Kp) {
-    constexpr int RW = 16;                   // rows per wave
+    constexpr int RW = 64;                   // rows per wave
     constexpr int RB = CPL <= 2 ? 16 : 8;    // rows loaded at once (<= 32 doubles in flight per lane)
     const bool first = blockIdx.x < nA;
     const T* __restrict__ tab = first ? tabA : tabB;
@@ -1134,8 +1134,7 @@ __global__ __launch_bounds__(256) void k_colstats(const T* __restrict__ tabA, ui
         s1[j] = 0.0;
         s2[j] = 0.0;
     }
-    const uint32_t rb = c * 64 + w * RW;
-#pragma unroll
+    const uint32_t rb = c * 256 + w * RW;
     for (int b0 = 0; b0 < RW; b0 += RB) {
         double x[RB][CPL];
 #pragma unroll
@@ -1177,7 +1176,7 @@ __global__ __launch_bounds__(256) void k_colstats(const T* __restrict__ tabA, ui
 // trip; the ids reach the group's lanes by shuffles, and lane i updates rating
 // i's running sum itself.  (Round 4 loaded the ids of each pair, then the rows,
 // then the sum and target: three dependent round trips per pair.)
-template <typename T>
+template <typename T, int PR, int CB>
 __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ti,
                                                const double* __restrict__ tr, uint64_t t0, uint64_t t1,
                                                const T* __restrict__ U, const T* __restrict__ V, uint32_t K,
@@ -1199,8 +1198,8 @@ __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, c
     if (bu) myb = (b0 + bu[myu]) + bv[myi];
     double a2 = 0.0, t2 = 0.0;
     // products summed in k order, the zero padding columns adding +0 (the clamped
-    // prediction is the same as over K columns)
-    constexpr int PR = 2, CB = 8;
+    // prediction is the same as over K columns); PR ratings per group at a time, CB
+    // k-blocks of each loaded before the first product
     for (int it = 0; it < 16; it += PR) {
         uint32_t uu[PR], ii[PR];
 #pragma unroll
@@ -1622,7 +1621,7 @@ hipError_t launch_resid(const ResidTask* tasks, uint32_t ntask, const uint32_t* 
 template <typename T>
 hipError_t launch_colstats(const T* tabA, uint32_t rA, const T* muA, double* outA, const T* tabB, uint32_t rB,
                            const T* muB, double* outB, uint32_t K, uint32_t Kp, hipStream_t st) {
-    const uint32_t nA = (rA + 63) / 64, nB = (rB + 63) / 64;
+    const uint32_t nA = (rA + 255) / 256, nB = (rB + 255) / 256;
     if (nA + nB == 0) return hipSuccess;
     if (K > 256 || Kp > 256) return hipErrorInvalidValue;
     if (Kp <= 64)
@@ -1640,8 +1639,9 @@ hipError_t launch_test(const uint32_t* tu, const uint32_t* ti, const double* tr,
                        double* part, const double* bu, const double* bv, double b0, hipStream_t st) {
     if (t1 <= t0) return hipSuccess;
     const uint64_t nb = (t1 - t0 + 255) / 256;
-    k_test<T><<<(uint32_t)nb, 256, 0, st>>>(tu, ti, tr, t0, t1, U, V, K, Kp, lo, hi, collect, div, sum, part, bu, bv,
-                                            b0);
+    // (4 ratings x 4 k-blocks per load round instead of 2 x 8: neutral, r05s7)
+    k_test<T, 2, 8><<<(uint32_t)nb, 256, 0, st>>>(tu, ti, tr, t0, t1, U, V, K, Kp, lo, hi, collect, div, sum, part,
+                                                  bu, bv, b0);
     return hipGetLastError();
 }
 

@@ -513,6 +513,9 @@ static void prepare_T(sbmf_ctx* c) {
                 // task capacity: the kernel's on-chip maximum, or smaller if split_chunk asks
                 S.cmax = gstream_cmax<T>(S.tune);
                 if (cf.split_chunk) S.cmax = std::min(S.cmax, std::max(cf.split_chunk, 1u));
+                // (fewer persistent workgroups per CU, leaving CU slots to the Gram-block launches
+                // beside the streaming one from its start: user 3 / 2 per CU +0.03 / +0.13 ms, item
+                // 8-wave set 1 per CU +0.2 ms per sweep, r05s8)
                 const int per_cu =
                     std::max(1, std::min(gstream_wg_target(S.tune), gstream_blocks_per_cu<T>(S.cmax, S.tune)));
                 build_stream_tasks(*sd, S, rows[k], (uint32_t)(dev_cus * per_cu), nblk);
@@ -615,7 +618,7 @@ static void prepare_T(sbmf_ctx* c) {
     // [sig_u | mu_u | sig_v | mu_v], each Kp long and zero padded, + 16 slack for prefetch
     c->d_hyper.alloc((4 * (size_t)c->Kp + 16) * sizeof(T));
     HIPCHK(hipMemsetAsync(c->d_hyper.p, 0, c->d_hyper.bytes, st));
-    const uint32_t nchunk = (c->I + 63) / 64 + (c->J + 63) / 64;  // both tables' 64-row chunks
+    const uint32_t nchunk = (c->I + 255) / 256 + (c->J + 255) / 256;  // both tables' 256-row chunks
     c->d_colpart.alloc((size_t)nchunk * 2 * c->K * sizeof(double));
     c->h_res.assign(RES_COL + 4 * (size_t)c->K, 0.0);
     c->d_res.alloc(c->h_res.size() * sizeof(double));
@@ -1214,10 +1217,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // ---- column statistics with the current mu (:378-381, :397-401)
         const T* hyp = c->d_hyper.as<T>();
         double* colpart = c->d_colpart.as<double>();
-        double* colpart_v = colpart + (size_t)((c->I + 63) / 64) * 2 * K;
+        double* colpart_v = colpart + (size_t)((c->I + 255) / 256) * 2 * K;
         HIPCHK(launch_colstats<T>(c->d_U.as<T>(), c->I, hyp + c->Kp, colpart, c->d_V.as<T>(), c->J, hyp + 3 * c->Kp,
                                   colpart_v, K, c->Kp, st));
-        HIPCHK(launch_sum_cols2(colpart, (c->I + 63) / 64, d_res + RES_COL, colpart_v, (c->J + 63) / 64,
+        HIPCHK(launch_sum_cols2(colpart, (c->I + 255) / 256, d_res + RES_COL, colpart_v, (c->J + 255) / 256,
                                 d_res + RES_COL + 2 * K, 2 * K, st));
         c->timing.n_launch += 3;
         HIPCHK(hipMemcpyAsync(c->h_pre, d_res, c->h_res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
