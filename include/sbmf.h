@@ -124,6 +124,12 @@ typedef struct sbmf_config {
                                  bit 3 = f64 rows of 33..64 ratings on two 8-vector waves instead
                                          of one 16-vector wave,
                                  bit 7 = k_gres on 4-wave workgroups (both sides),
+                                 bit 8 = f64 rows of 65..128 ratings as 3-4-wave Gram-block rows
+                                         (default: one-wave k_grow workgroups),
+                                 bit 9 = f64 rows of 129..256 ratings as 3-4-wave Gram-block rows
+                                         (default: two-wave k_grow workgroups),
+                                 bit 10 = f64 rows of 9..64 ratings on the one-wave Gram-block
+                                          kind (default: one-wave k_grow workgroups),
                                  bit 17 = k_gres on 16-wave workgroups (both sides),
                                  bit 23 = f64 user streaming rows on 8-wave k_gres workgroups
                                           (default: 4-wave, 512-rating tasks),
@@ -146,7 +152,7 @@ typedef struct sbmf_config {
                                           prologue kernels on the compute stream (default: on the
                                           second stream beside them; the results are the same).
                                  Removed in round 4 with the variants they selected (measured
-                                 slower or neutral, kept in git history): bits 0, 5, 6, 8-10, 16,
+                                 slower or neutral, kept in git history): bits 0, 5, 6, 16,
                                  20-22, 31; they are ignored (bit 25 was the round-4 LDS-DMA
                                  prefetch before its round-5 use above).  */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */

@@ -57,6 +57,12 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
 template <typename T>
 hipError_t launch_gblock(int kind, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
 
+// Whole rows of a Gram-block bin on the streaming kernel's code (k_grow), one workgroup of
+// nw (1 or 2) waves per row: rows of at most grow_maxdeg(nw, f64) ratings.
+template <typename T>
+hipError_t launch_grow(int nw, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st);
+uint32_t grow_maxdeg(int nw, bool f64);
+
 // Streaming-kernel task: at most `cmax` ratings of one row (the whole row,
 // or one chunk of a row split over `nch` co-resident workgroups).  A task
 // with len == 0 is an empty slot (round padding).

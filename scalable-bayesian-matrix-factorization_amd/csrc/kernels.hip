@@ -9,14 +9,17 @@
 //     E_n += v_nk (old - new).
 // Rows are independent given the partner table, so a half-sweep is one
 // launch per degree bin:
-//   * k_gblock<T, V, NW, RPW>  rows of <= 256 ratings (f64): 1 wave per row (RPW
-//     rows per block) or NW waves per row; per 16-wide k-block the row's
-//     partner slices sit in VGPRs, G_B = S^T S by MFMA, the 16 draws as the
-//     exact recurrence over G_B, e -= S_B D_B by DPP;
+//   * k_gblock<T, V, NW, RPW>  rows of <= 8 ratings (f64; <= 256 with tune bits
+//     8-10, and f32): 1 wave per row (RPW rows per block) or NW waves per row; per
+//     16-wide k-block the row's partner slices sit in VGPRs, G_B = S^T S by MFMA,
+//     the 16 draws as the exact recurrence over G_B, e -= S_B D_B
+//     by DPP;
 //   * k_gres<T, NW, SIDE>  longer rows and the chunks of split rows: one
 //     persistent launch, the same per-block steps with a task's slices held in
 //     the VGPRs of NW waves and split rows' (G_B, c_B) partials summed across
-//     workgroups in chunk order.
+//     workgroups in chunk order;
+//   * k_grow<T, NW, SIDE>  f64 rows of 9..256 ratings: k_gres' code on whole
+//     rows, one workgroup of one (<= 128 ratings) or two waves per row.
 // Layout: factor tables row-major [rows][Kp] (Kp = K padded to 16), so a
 // partner row is one contiguous 4K/8K-byte record; ratings in CSR (users)
 // and CSC (items) order; residuals kept per orientation and gathered through
@@ -661,10 +664,19 @@ template <typename T>
 struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of slices
     static constexpr int VW = sizeof(T) == 8 ? 32 : 64;
 };
-template <typename T, int NW, int SIDE>
-__global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict__ tasks, uint32_t ntask,
-                                                           HalfArgs<T> a, SplitSync sy) {
+// LIST: whole rows of a Gram-block bin, one workgroup per row of the list (k_grow; NW 1 or 2,
+// no split rows), instead of tasks claimed from a queue (k_gres).  One wave (NW = 1) takes
+// its G_B straight from the MFMA registers into the solve's image and its D from its own
+// solve, with no cross-wave sum and no hand-off: the per-row LDS is small enough for four
+// one-wave workgroups per SIMD.
+template <typename T, int NW, int SIDE, bool LIST>
+__device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, const uint32_t* __restrict__ lrows,
+                                         uint32_t ntask, const HalfArgs<T>& a, const SplitSync& sy) {
     typedef typename MfmaT<T>::acc_t acc_t;
+    constexpr bool ONE = NW == 1;
+    // whole rows of a list: the solving wave writes the new own row itself and reads sigma and
+    // mu from memory (no LDS copy of either)
+    constexpr bool DIRECT = LIST;
     constexpr int VW = GresW<T>::VW;
     constexpr uint32_t CAP = 4 * NW * VW;
     constexpr int SL = GB * GB + GB;  // slab doubles per (chunk, block): 16x16 image (lower + diagonal) | c
@@ -683,22 +695,24 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
     // layout, except that the diagonal goes to Rr[PW + r]: the image's diagonal and upper part
     // stay zero (cleared once), so the solve reads whole H rows unmasked
     constexpr int PW = GB * GLD + GB;
-    __shared__ T Pw[NW][PW];
+    __shared__ T Pw[NW][ONE ? 1 : PW];
     __shared__ T Rr[PW + GB];
-    __shared__ T Dsh[GB];
-    __shared__ T newS[256];
+    __shared__ T newS[DIRECT ? 1 : 256];
     __shared__ double red2[NW][2];
     // packed exchange entries: SLP = 136 (lower triangle incl. diagonal) + 16 (c);
     // thread x < SLP owns entry x; XP threads per entry share a split row's chunk sum
+    // (NW >= 3; one- and two-wave workgroups take whole rows only and loop over the entries)
     constexpr int SLP = GB * (GB + 1) / 2 + GB;
-    constexpr int XP = (64 * NW) / SLP;
+    constexpr bool XCH = NW >= 3;
+    constexpr int XP = XCH ? (64 * NW) / SLP : 1;
     static_assert(XP >= 1 && SLP <= SL, "exchange geometry");
-    __shared__ double xsum[XP][SLP];
+    __shared__ double xsum[XP][XCH ? SLP : 1];
     // packed entry x -> its offset in a partial image, and in Rr (computed once: no per-block geometry)
-    __shared__ uint16_t xoff[SLP], xdst[SLP];
+    __shared__ uint16_t xoff[ONE ? 1 : SLP], xdst[ONE ? 1 : SLP];
     // the row's normals and old values, sigma and mu: read by the solving wave from LDS
     // (kept out of the VGPRs the held slices need)
-    __shared__ T zL[256], oL[256], sgL[256], muL[256];
+    __shared__ T zL[256], oL[256], sgL[DIRECT ? 1 : 256], muL[DIRECT ? 1 : 256];
+    if constexpr (!ONE)
     for (int x = threadIdx.x; x < SLP; x += 64 * NW) {
         int r = 0;
         while ((r + 1) * (r + 2) / 2 <= x && r < GB) ++r;  // row of the packed triangle
@@ -710,6 +724,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
     // this wave's index as a scalar, and the lane: the thread id is rebuilt from them in the
     // block loop (no VGPR held across it, no spill slot to reload)
     const int wr_s = __builtin_amdgcn_readfirstlane(wr);
+    if constexpr (!DIRECT)
     for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {
         sgL[k] = a.sig[k];
         muL[k] = a.mu[k];
@@ -726,14 +741,28 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
     // task order: a queue claimed in list order, one returning atomic per task,
     // so a split row's chunks start as soon as enough workgroups are free
     __shared__ uint32_t qti;
-    for (;;) {
-        if (threadIdx.x == 0)
-            qti = __hip_atomic_fetch_add(sy.counters + sy.ncounters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const uint32_t ti = qti;
-        __syncthreads();  // every thread has its ticket before thread 0 claims the next
-        if (ti >= ntask) break;
-        const SplitTask tk = tasks[ti];
+    // (the task loop in this form, also for the one-task LIST case: written as a task lambda
+    // called once or in the loop, k_grow compiles to 50-70 spilled VGPRs instead of 1-2)
+    for (uint32_t it = 0;; ++it) {
+        uint32_t ti;
+        if constexpr (LIST) {
+            ti = blockIdx.x;
+            if (it > 0 || ti >= ntask) break;
+        } else {
+            if (threadIdx.x == 0)
+                qti = __hip_atomic_fetch_add(sy.counters + sy.ncounters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            ti = qti;
+            __syncthreads();  // every thread has its ticket before thread 0 claims the next
+            if (ti >= ntask) break;
+        }
+        SplitTask tk;
+        if constexpr (LIST) {
+            const uint32_t r = lrows[ti];
+            tk = SplitTask{r, a.ptr[r], a.ptr[r + 1] - a.ptr[r], 1u, 0u, 0u, 0u, 0u};
+        } else {
+            tk = tasks[ti];
+        }
         const uint32_t n = tk.len;
         if (n == 0) continue;  // empty round slot (uniform)
         const uint32_t row = tk.row, beg = tk.beg, nch = tk.nch;
@@ -843,14 +872,39 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 constexpr int NPF = decltype(npf)::value;
                 T Dl;
                 if (nch == 1) pf();
-                {
+                if constexpr (ONE) {
+                    // one wave: the image straight from the MFMA registers (strict lower part,
+                    // the diagonal apart, c after it); its upper part stays zero
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = MfmaT<T>::row(lane, j);
+                        if (ci < r)
+                            Rr[r * GLD + ci] = g[j];
+                        else if (ci == r)
+                            Rr[PW + r] = g[j];
+                    }
+                    if (lane < GB) Rr[GB * GLD + lane] = cc;
+                    lds_barrier();
+                } else {
                     T* const pw = &Pw[wr_s][0];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) pw[MfmaT<T>::row(lane, j) * GLD + ci] = g[j];
                     if (lane < GB) pw[GB * GLD + lane] = cc;
+                    lds_barrier();
                 }
-                lds_barrier();
                 stamp(3);  // wait for the other waves
+                if constexpr (NW == 2) {  // two waves: each thread sums its entries in wave order
+                    const int tid = wr_s * 64 + (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+                    for (int x = tid; x < SLP; x += 64 * NW) {
+                        const int xo = xoff[x];
+                        T val = T(0);
+#pragma unroll
+                        for (int w = 0; w < NW; ++w) val += Pw[w][xo];
+                        Rr[xdst[x]] = val;
+                    }
+                    lds_barrier();
+                }
+                if constexpr (XCH) {
                 // cross-wave sum in wave order: thread x < SLP holds packed entry x
                 // (lower triangle incl. the diagonal, then c); the entry's geometry is
                 // recomputed here from an opaque thread id so it holds no VGPRs across
@@ -926,14 +980,25 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                 }
                 if (xin) Rr[xd] = val;
                 lds_barrier();
+                }  // XCH
                 stamp(4);  // cross-wave sum + split-row exchange
-                // the 16 draws: wave 0, D handed over in LDS
-                T dlt = T(0);
-                if (wr == 0) {
+                // the 16 draws: every wave draws the same 16 from the same LDS image (the same
+                // bits), so D needs no hand-off -- one barrier per block fewer than wave 0 drawing
+                // and handing D over in LDS (item stage 3.49-3.54 -> 3.44 ms, r05s13)
+                T dlt;
+                {
                     const uint32_t kk = t * GB + ci;
                     const bool kin = kk < K;
                     // the block's old values, hyperparameters and normals (zero padded)
-                    const T old = oL[kk], sg = sgL[kk], mu = muL[kk], z = zL[kk];
+                    T sg, mu;
+                    if constexpr (DIRECT) {
+                        sg = a.sig[kk];
+                        mu = a.mu[kk];
+                    } else {
+                        sg = sgL[kk];
+                        mu = muL[kk];
+                    }
+                    const T old = oL[kk], z = zL[kk];
                     const T P = Rr[PW + ci];
                     const T Cc = Rr[GB * GLD + ci];
                     const T var = kin ? T(1) / (sg + tau * P) : T(0);
@@ -941,13 +1006,15 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
                     const T A = var * sg * mu + sd * z;
                     const T Bq = var * tau;
                     dlt = gblock_solve_lds(&Rr[ci * GLD], Bq, A - old + Bq * (Cc + P * old));
-                    if (lane < GB) {
-                        if (kin) newS[kk] = old + dlt;
-                        Dsh[lane] = dlt;
+                    if (lane < GB && wr == 0) {
+                        if constexpr (DIRECT) {
+                            if (kin) a.own[(size_t)CHK(row, a.lim_rows) * Kp + kk] = old + dlt;
+                        } else {
+                            if (kin) newS[kk] = old + dlt;
+                        }
                     }
                 }
-                lds_barrier();
-                Dl = Dsh[ci];
+                Dl = dlt;  // every 16-lane row of every wave solved the same system
                 stamp(5);  // solve
                 return Dl;
             };
@@ -1001,7 +1068,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
         else
             sums = body(std::integral_constant<int, VW>{});
         // ---- new own row: whole rows write it, split rows stage it (k_split_finish publishes)
-        if (tk.chunk == 0)
+        if (!DIRECT && tk.chunk == 0)
             for (uint32_t k = threadIdx.x; k < K; k += 64 * NW) {
                 if (nch > 1)
                     static_cast<T*>(sy.newown)[(size_t)CHK(tk.slab0, sy.lim_chunk) * Kp + k] = newS[k];
@@ -1033,6 +1100,17 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(const SplitTask* __restrict
         __syncthreads();  // LDS (ids, residuals, newS, red2) is reused by the next task
         stamp(6);  // epilogue
     }
+}
+template <typename T, int NW, int SIDE>
+__global__ __launch_bounds__(64 * NW, 4) void k_gres(
+    const SplitTask* __restrict__ tasks, uint32_t ntask, HalfArgs<T> a, SplitSync sy) {
+    gres_run<T, NW, SIDE, false>(tasks, nullptr, ntask, a, sy);
+}
+template <typename T, int NW, int SIDE>
+__global__ __launch_bounds__(64 * NW, 4) void k_grow(
+    const uint32_t* __restrict__ rows, uint32_t nrows, HalfArgs<T> a) {
+    const SplitSync sy{};
+    gres_run<T, NW, SIDE, true>(nullptr, rows, nrows, a, sy);
 }
 
 // Split rows: publish the new own rows and fold the chunk partial sums.
@@ -1581,6 +1659,30 @@ hipError_t launch_gblock_nw(int nw, const uint32_t* rows, uint32_t nrows, const 
     return hipGetLastError();
 }
 
+// Whole rows of a Gram-block bin on the streaming kernel's code, one workgroup per row:
+// one wave per row (nw = 1: rows of <= 128 f64 / 256 f32 ratings) or two (nw = 2: twice that)
+template <typename T>
+hipError_t launch_grow(int nw, const uint32_t* rows, uint32_t nrows, const HalfArgs<T>& a, hipStream_t st) {
+    if (nrows == 0) return hipSuccess;
+    if (a.K > 256) return hipErrorInvalidValue;
+    const bool side = a.tag == TAG_ITEMS;
+    if (nw == 1) {
+        if (side)
+            k_grow<T, 1, 1><<<nrows, 64, 0, st>>>(rows, nrows, a);
+        else
+            k_grow<T, 1, 0><<<nrows, 64, 0, st>>>(rows, nrows, a);
+    } else if (nw == 2) {
+        if (side)
+            k_grow<T, 2, 1><<<nrows, 128, 0, st>>>(rows, nrows, a);
+        else
+            k_grow<T, 2, 0><<<nrows, 128, 0, st>>>(rows, nrows, a);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+uint32_t grow_maxdeg(int nw, bool f64) { return 4u * (uint32_t)nw * (f64 ? GresW<double>::VW : GresW<float>::VW); }
+
 template <typename T>
 static const void* gstream_fn(uint32_t tune, uint32_t side = 0) {
     if (gres_nw(tune) == 4) return side ? (const void*)k_gres<T, 4, 1> : (const void*)k_gres<T, 4, 0>;
@@ -1762,6 +1864,7 @@ hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, h
     template hipError_t launch_gstream<T>(const SplitTask*, uint32_t, uint32_t, const SplitRow*, uint32_t,           \
                                           const HalfArgs<T>&, const SplitSync&, hipStream_t);                        \
     template int gstream_blocks_per_cu<T>(uint32_t, uint32_t);                                                      \
+    template hipError_t launch_grow<T>(int, const uint32_t*, uint32_t, const HalfArgs<T>&, hipStream_t);            \
     template uint32_t gstream_cmax<T>(uint32_t);                                                                    \
     template hipError_t launch_resid<T>(const ResidTask*, uint32_t, const uint32_t*, uint32_t, uint32_t,              \
                                         const uint32_t*, const uint32_t*, const T*, const T*, const T*, uint32_t,     \

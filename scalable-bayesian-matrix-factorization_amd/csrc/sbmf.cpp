@@ -1020,7 +1020,21 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         } else {
             lk = -1;  // no end event behind this launch
         }
-        if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
+        // f64 rows of 65..128 ratings on one-wave k_grow workgroups, 129..256 on two-wave ones
+        // (the streaming kernel's code on whole rows: 32 vectors per wave, one wave with no
+        // cross-wave sum or D hand-off) instead of 3-4-wave Gram-block rows: user half
+        // 3.20-3.24 -> 2.93-3.04 ms, sweep 7.22-7.25 -> 7.02-7.06 (r05s11, 2 interleaved
+        // rounds); the 9..64-rating bin too, on one-wave k_grow workgroups (sweep 6.99-7.03 ->
+        // 6.90-6.95, r05s12).  Tune bits 8 / 9 / 10 keep the Gram-block kinds of these bins.
+        const uint32_t tn = c->cfg.tune;
+        const int gw = sizeof(T) != 8                                 ? 0
+                       : k == GK_B4 && !(tn & 0x100u)                 ? 1
+                       : k == GK_B8 && !(tn & 0x200u)                 ? 2
+                       : k == GK_W16 && !(tn & 0x400u) && !(tn & 8u)  ? 1
+                                                                      : 0;
+        if (gw) {
+            HIPCHK(launch_grow<T>(gw, g.d_bins[k].as<uint32_t>(), (uint32_t)g.bin_rows[k].size(), a, st));
+        } else if (k < GK_NUM && k >= GK_B2 && !(c->cfg.tune & 4u)) {
             for (const auto& gs : g.gsub[k])
                 HIPCHK(launch_gblock_nw<T>((int)gs[0], g.d_bins[k].as<uint32_t>() + gs[1], gs[2], a, st));
         } else if (k < GK_NUM)
