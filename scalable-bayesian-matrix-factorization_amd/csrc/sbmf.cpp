@@ -987,7 +987,14 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     // its k-blocks, which a chain of launches adds up (r05s2 per-rank trace).  Per-rank
     // compute of the 8-way split, 4 stages: K=100 2.06 -> 1.96 ms, K=200 3.09 -> 2.76 ms;
     // the single-GPU sweep is unchanged (7.33 both ways, r05s5).  Tune bit 25: one side stream.
-    const bool two = !serial && others >= 2 && !(c->cfg.tune & 0x2000000u);
+    // With two stream sets (items: rows > 1024 on 16-wave workgroups, set 1, and the
+    // rest on 8-wave ones, set 0), set 1 runs on `st` and set 0 on `sto` beside it
+    // (tune bit 30: one after the other), each with split-row areas of its own.
+    const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && !g.ss[0].stasks.empty() && !g.ss[1].stasks.empty();
+    // Beside two streaming sets every Gram-block kind goes to sto2: on sto it would queue behind
+    // set 0 (r05s14 trace: two item kinds, 0.18 ms, ran after the stage; measured neutral, 6.91
+    // ms both ways, r05s15: the persistent sets hold every CU, so the kinds' work only moves)
+    const bool two = !serial && (others >= 2 || sov) && !(c->cfg.tune & 0x2000000u);
     const bool side = ovl || two;
     // the split-row counters and queue heads of both stream sets, zeroed before the fork
     // (cleared at the end of the previous streaming stage on this stream, off the path, unless not)
@@ -998,16 +1005,12 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         HIPCHK(hipStreamWaitEvent(c->sto, c->oev[0], 0));
         if (two) HIPCHK(hipStreamWaitEvent(c->sto2, c->oev[0], 0));
     }
-    // With two stream sets (items: rows > 1024 on 16-wave workgroups, set 1, and the
-    // rest on 8-wave ones, set 0), set 1 runs on `st` and set 0 on `sto` beside it
-    // (tune bit 30: one after the other), each with split-row areas of its own.
-    const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && !g.ss[0].stasks.empty() && !g.ss[1].stasks.empty();
     // (the Gram-block launches on `sto` ahead of set 0 instead of behind it: neutral, r04s22)
     int last[3] = {-1, -1, -1};  // the last kind launched on st / sto / sto2 (its end event recorded there)
     int nside = 0;  // Gram-block kinds launched so far (two: even ones on sto, odd ones on sto2)
     for (int k = NBIN - 1; k >= 0; --k) {
         if (g.bin_rows[k].empty()) continue;
-        st = side && k != KIND_STREAM ? (two && (nside++ & 1) ? c->sto2 : c->sto) : c->st;
+        st = side && k != KIND_STREAM ? (two && (sov || (nside++ & 1)) ? c->sto2 : c->sto) : c->st;
         // launch-kind events: the streaming kind's every sweep (the bench's roofline), the
         // others' on the first sweep of a run only (each event between two launches on a
         // stream leaves the device idle ~6 us)

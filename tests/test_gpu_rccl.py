@@ -66,8 +66,9 @@ def test_rccl_selftest_argument_checks():
 
 
 def test_virtual_rank_runs_its_stages():
-    """Config-4-like partitioning (8 ranks, 4 stages per half) of the ML-1M-shaped set: every
-    virtual rank runs; its stage times are positive and the stages add up to about the half."""
+    """Config-4-like partitioning (8 ranks, the default 2 stages per half) of the ML-1M-shaped
+    set: every virtual rank runs; its stage times are positive and the stages add up to about
+    the half."""
     tr, te, _ = synth.generate("ml-1m")
     for r in (0, 7):
         L = FMLearnSBPMF(num_factor=50, seed=3, rng="philox", recompute_every=0)
@@ -75,11 +76,13 @@ def test_virtual_rank_runs_its_stages():
         assert lib.sbmf_test_virtual_rank(L.ctx, 8, r) == 0
         L.set_data(Data(*tr), Data(*te))
         L.learn(sweeps=2)
-        ms = np.zeros(8)
         ns = C.c_uint32()
-        assert lib.sbmf_test_stage_ms(L.ctx, ms.ctypes.data_as(C.POINTER(C.c_double)), 8, C.byref(ns)) == 0
-        assert ns.value == 4
+        assert lib.sbmf_test_stage_ms(L.ctx, None, 0, C.byref(ns)) == 0
+        assert ns.value == 2  # sbmf.cpp: two stages per half for several ranks
+        n = ns.value
+        ms = np.zeros(2 * n)
+        assert lib.sbmf_test_stage_ms(L.ctx, ms.ctypes.data_as(C.POINTER(C.c_double)), 2 * n, C.byref(ns)) == 0
         assert np.all(ms > 0) and np.all(np.isfinite(ms)), ms
         t = L.timing()
-        assert ms[:4].sum() <= t.ms_user_half * 1.05 + 0.05 and ms[4:].sum() <= t.ms_item_half * 1.05 + 0.05
+        assert ms[:n].sum() <= t.ms_user_half * 1.05 + 0.05 and ms[n:].sum() <= t.ms_item_half * 1.05 + 0.05
         L.close()
