@@ -130,6 +130,8 @@ typedef struct sbmf_config {
                                          (default: two-wave k_grow workgroups),
                                  bit 10 = f64 rows of 9..64 ratings on the one-wave Gram-block
                                           kind (default: one-wave k_grow workgroups),
+                                 bit 11 = f32 rows of 17..512 ratings on the Gram-block kinds
+                                          (default: one- / two-wave k_grow workgroups),
                                  bit 17 = k_gres on 16-wave workgroups (both sides),
                                  bit 23 = f64 user streaming rows on 8-wave k_gres workgroups
                                           (default: 4-wave, 512-rating tasks),

@@ -9,8 +9,8 @@
 //     E_n += v_nk (old - new).
 // Rows are independent given the partner table, so a half-sweep is one
 // launch per degree bin:
-//   * k_gblock<T, V, NW, RPW>  rows of <= 8 ratings (f64; <= 256 with tune bits
-//     8-10, and f32): 1 wave per row (RPW rows per block) or NW waves per row; per
+//   * k_gblock<T, V, NW, RPW>  rows of <= 8 ratings f64 / 16 f32 (<= 256 / 512 with tune bits
+//     8-11): 1 wave per row (RPW rows per block) or NW waves per row; per
 //     16-wide k-block the row's partner slices sit in VGPRs, G_B = S^T S by MFMA,
 //     the 16 draws as the exact recurrence over G_B, e -= S_B D_B
 //     by DPP;
@@ -18,8 +18,8 @@
 //     persistent launch, the same per-block steps with a task's slices held in
 //     the VGPRs of NW waves and split rows' (G_B, c_B) partials summed across
 //     workgroups in chunk order;
-//   * k_grow<T, NW, SIDE>  f64 rows of 9..256 ratings: k_gres' code on whole
-//     rows, one workgroup of one (<= 128 ratings) or two waves per row.
+//   * k_grow<T, NW, SIDE>  rows of 9..256 ratings f64 / 17..512 f32: k_gres' code on whole
+//     rows, one workgroup of one (<= 128 f64 / 256 f32 ratings) or two waves per row.
 // Layout: factor tables row-major [rows][Kp] (Kp = K padded to 16), so a
 // partner row is one contiguous 4K/8K-byte record; ratings in CSR (users)
 // and CSC (items) order; residuals kept per orientation and gathered through

@@ -1030,7 +1030,12 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         // rounds); the 9..64-rating bin too, on one-wave k_grow workgroups (sweep 6.99-7.03 ->
         // 6.90-6.95, r05s12).  Tune bits 8 / 9 / 10 keep the Gram-block kinds of these bins.
         const uint32_t tn = c->cfg.tune;
-        const int gw = sizeof(T) != 8                                 ? 0
+        // f32 rows of 17..256 ratings on one-wave k_grow workgroups, 257..512 on two-wave ones (64
+        // vectors per f32 wave): f32 sweep 5.46 -> 4.63 ms (r05s18); tune bit 11 keeps the
+        // Gram-block kinds
+        const bool g32 = sizeof(T) == 4 && !(tn & 0x800u);
+        const int gw = g32 ? (k == GK_W16 || k == GK_B2 || k == GK_B4 ? 1 : k == GK_B8 ? 2 : 0)
+                       : sizeof(T) != 8                               ? 0
                        : k == GK_B4 && !(tn & 0x100u)                 ? 1
                        : k == GK_B8 && !(tn & 0x200u)                 ? 2
                        : k == GK_W16 && !(tn & 0x400u) && !(tn & 8u)  ? 1

@@ -69,10 +69,13 @@ def test_ragged_edge_cases_track_reference(ragged, name, quirks, seed):
     assert np.abs(L.rmse_trajectory - gold).max() < 1e-6
 
 
-def test_f32_ref_stream_within_north_star_tolerance(ml100k):
+@pytest.mark.parametrize("tune", [0, 2048])
+def test_f32_ref_stream_within_north_star_tolerance(ml100k, tune):
+    """f32 against the reference trajectory; tune bit 11 runs the f32 rows of 17..512 ratings
+    on the Gram-block kinds instead of k_grow workgroups."""
     tr, te = ml100k
     gold = golden_rmse("ref_final_ml100k_k20_s1.txt")
-    L = _run(tr, te, 100, num_factor=20, seed=1, precision="f32")
+    L = _run(tr, te, 100, num_factor=20, seed=1, precision="f32", tune=tune)
     err = np.abs(L.rmse_trajectory - gold)
     print("f32 max |dRMSE| = %.3e" % err.max())
     assert err.max() < 1e-3
