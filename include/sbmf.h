@@ -132,6 +132,8 @@ typedef struct sbmf_config {
                                           kind (default: one-wave k_grow workgroups),
                                  bit 11 = f32 rows of 17..512 ratings on the Gram-block kinds
                                           (default: one- / two-wave k_grow workgroups),
+                                 bit 12 = k_grow reads sigma and mu from memory at every K
+                                          (default: from LDS when Kp <= 128),
                                  bit 17 = k_gres on 16-wave workgroups (both sides),
                                  bit 23 = f64 user streaming rows on 8-wave k_gres workgroups
                                           (default: 4-wave, 512-rating tasks),

@@ -669,14 +669,17 @@ struct GresW {  // vectors (of 4 ratings) per wave held in VGPRs: 64 VGPRs of sl
 // its G_B straight from the MFMA registers into the solve's image and its D from its own
 // solve, with no cross-wave sum and no hand-off: the per-row LDS is small enough for four
 // one-wave workgroups per SIMD.
-template <typename T, int NW, int SIDE, bool LIST>
+template <typename T, int NW, int SIDE, bool LIST, int KL = 256>
 __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, const uint32_t* __restrict__ lrows,
                                          uint32_t ntask, const HalfArgs<T>& a, const SplitSync& sy) {
     typedef typename MfmaT<T>::acc_t acc_t;
     constexpr bool ONE = NW == 1;
-    // whole rows of a list: the solving wave writes the new own row itself and reads sigma and
-    // mu from memory (no LDS copy of either)
+    // whole rows of a list: the solving waves write the new own row themselves; KL (>= Kp) sizes
+    // the row's LDS copies of its normals, old values, sigma and mu.  At KL = 256 a list kernel
+    // reads sigma and mu from memory (four one-wave workgroups per SIMD fit the LDS only
+    // without those copies), which puts an L2 round trip in front of every block's draws
     constexpr bool DIRECT = LIST;
+    constexpr bool SMG = LIST && KL > 128;
     constexpr int VW = GresW<T>::VW;
     constexpr uint32_t CAP = 4 * NW * VW;
     constexpr int SL = GB * GB + GB;  // slab doubles per (chunk, block): 16x16 image (lower + diagonal) | c
@@ -711,7 +714,7 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
     __shared__ uint16_t xoff[ONE ? 1 : SLP], xdst[ONE ? 1 : SLP];
     // the row's normals and old values, sigma and mu: read by the solving wave from LDS
     // (kept out of the VGPRs the held slices need)
-    __shared__ T zL[256], oL[256], sgL[DIRECT ? 1 : 256], muL[DIRECT ? 1 : 256];
+    __shared__ T zL[KL], oL[KL], sgL[SMG ? 1 : KL], muL[SMG ? 1 : KL];
     if constexpr (!ONE)
     for (int x = threadIdx.x; x < SLP; x += 64 * NW) {
         int r = 0;
@@ -724,7 +727,7 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
     // this wave's index as a scalar, and the lane: the thread id is rebuilt from them in the
     // block loop (no VGPR held across it, no spill slot to reload)
     const int wr_s = __builtin_amdgcn_readfirstlane(wr);
-    if constexpr (!DIRECT)
+    if constexpr (!SMG)
     for (uint32_t k = threadIdx.x; k < Kp; k += 64 * NW) {
         sgL[k] = a.sig[k];
         muL[k] = a.mu[k];
@@ -991,7 +994,7 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
                     const bool kin = kk < K;
                     // the block's old values, hyperparameters and normals (zero padded)
                     T sg, mu;
-                    if constexpr (DIRECT) {
+                    if constexpr (SMG) {
                         sg = a.sig[kk];
                         mu = a.mu[kk];
                     } else {
@@ -1106,11 +1109,11 @@ __global__ __launch_bounds__(64 * NW, 4) void k_gres(
     const SplitTask* __restrict__ tasks, uint32_t ntask, HalfArgs<T> a, SplitSync sy) {
     gres_run<T, NW, SIDE, false>(tasks, nullptr, ntask, a, sy);
 }
-template <typename T, int NW, int SIDE>
+template <typename T, int NW, int SIDE, int KL>
 __global__ __launch_bounds__(64 * NW, 4) void k_grow(
     const uint32_t* __restrict__ rows, uint32_t nrows, HalfArgs<T> a) {
     const SplitSync sy{};
-    gres_run<T, NW, SIDE, true>(nullptr, rows, nrows, a, sy);
+    gres_run<T, NW, SIDE, true, KL>(nullptr, rows, nrows, a, sy);
 }
 
 // Split rows: publish the new own rows and fold the chunk partial sums.
@@ -1666,20 +1669,26 @@ hipError_t launch_grow(int nw, const uint32_t* rows, uint32_t nrows, const HalfA
     if (nrows == 0) return hipSuccess;
     if (a.K > 256) return hipErrorInvalidValue;
     const bool side = a.tag == TAG_ITEMS;
-    if (nw == 1) {
-        if (side)
-            k_grow<T, 1, 1><<<nrows, 64, 0, st>>>(rows, nrows, a);
-        else
-            k_grow<T, 1, 0><<<nrows, 64, 0, st>>>(rows, nrows, a);
-    } else if (nw == 2) {
-        if (side)
-            k_grow<T, 2, 1><<<nrows, 128, 0, st>>>(rows, nrows, a);
-        else
-            k_grow<T, 2, 0><<<nrows, 128, 0, st>>>(rows, nrows, a);
-    } else {
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+    // Kp <= 128: the row's sigma and mu in LDS too (KL = 128); larger K: from memory (KL = 256)
+    auto go = [&](auto kl) {
+        constexpr int KL = decltype(kl)::value;
+        if (nw == 1) {
+            if (side)
+                k_grow<T, 1, 1, KL><<<nrows, 64, 0, st>>>(rows, nrows, a);
+            else
+                k_grow<T, 1, 0, KL><<<nrows, 64, 0, st>>>(rows, nrows, a);
+        } else if (nw == 2) {
+            if (side)
+                k_grow<T, 2, 1, KL><<<nrows, 128, 0, st>>>(rows, nrows, a);
+            else
+                k_grow<T, 2, 0, KL><<<nrows, 128, 0, st>>>(rows, nrows, a);
+        } else {
+            return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    };
+    return a.Kp <= 128 && !(a.tune & 0x1000u) ? go(std::integral_constant<int, 128>{})
+                                               : go(std::integral_constant<int, 256>{});
 }
 uint32_t grow_maxdeg(int nw, bool f64) { return 4u * (uint32_t)nw * (f64 ? GresW<double>::VW : GresW<float>::VW); }
 
