@@ -699,7 +699,7 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
     // stay zero (cleared once), so the solve reads whole H rows unmasked
     constexpr int PW = GB * GLD + GB;
     __shared__ T Pw[NW][ONE ? 1 : PW];
-    __shared__ T Rr[PW + GB];
+    __shared__ T Rr[PW + GB + (ONE ? 64 : 0)];  // (one wave: + a slot per lane for the upper part)
     __shared__ T newS[DIRECT ? 1 : 256];
     __shared__ double red2[NW][2];
     // packed exchange entries: SLP = 136 (lower triangle incl. diagonal) + 16 (c);
@@ -877,14 +877,12 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
                 if (nch == 1) pf();
                 if constexpr (ONE) {
                     // one wave: the image straight from the MFMA registers (strict lower part,
-                    // the diagonal apart, c after it); its upper part stays zero
+                    // the diagonal apart, c after it); its upper part stays zero: those entries
+                    // go to a slot of their lane past the image (no exec-mask branches)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int r = MfmaT<T>::row(lane, j);
-                        if (ci < r)
-                            Rr[r * GLD + ci] = g[j];
-                        else if (ci == r)
-                            Rr[PW + r] = g[j];
+                        Rr[ci < r ? r * GLD + ci : ci == r ? PW + r : PW + GB + lane] = g[j];
                     }
                     if (lane < GB) Rr[GB * GLD + lane] = cc;
                     lds_barrier();
