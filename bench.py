@@ -546,9 +546,12 @@ def main():
     n_train = len(train[0])
     value = n_train * args.steps / main_res["seconds"]
     ms = 1e3 * main_res["seconds"] / args.steps
-    # dominant kernel: the (half, bin) with the largest device time
+    # dominant kernel: the (half, bin) that moves the most algorithmic bytes (the item streaming
+    # stage on every sampler line).  Not the largest HIP-event time: a small Gram-block kind that
+    # waits for CU slots beside the persistent streaming launch spans about as long as that launch
+    # (the r05s3 / r05s23 bias2 lines picked such a window, 0.02 of peak)
     km = main_res["kern_ms"]
-    s, k = np.unravel_index(np.argmax(km), km.shape)
+    s, k = np.unravel_index(np.argmax(main_res["kern_bytes"]), km.shape)
     achieved = main_res["kern_bytes"][s, k] / (km[s, k] * 1e-3) / 1e9
     kernel = "%s_half/%s" % ("user" if s == 0 else "item", KIND_NAMES[k])
     traffic = None
@@ -622,9 +625,12 @@ def main():
                      "sweep_alg_GBs": main_res["bytes_alg"] / (main_res["seconds"] / args.steps) / 1e9,
                      "bins": bins,
                      "bins_overlap": None if args.tune & (1 << 29) else
-                     "a half's Gram-block launches run on a second stream beside its streaming launch "
+                     "a half's Gram-block launches run on two side streams beside its streaming launch "
                      "(and the item half's two streaming sets side by side unless tune bit 30): a bin's ms is "
-                     "its start-to-end time while it shares the device, so the bins of a half overlap"},
+                     "its start-to-end time while it shares the device, so the bins of a half overlap",
+                     "bins_kernels": "bins are row-length classes; by default (f64) gblock_w16 (9-64 ratings) and "
+                     "gblock_b4 (65-128) run k_grow<double,1>, gblock_b8 (129-256) k_grow<double,2>, "
+                     "gblock_w4 (<= 8) k_gblock, gres_stage k_gres (DESIGN.md 3.1b); f32: k_grow for 17-512"},
     }
     if f32 is not None:
         out["f32_value"] = n_train * args.steps / f32["seconds"]

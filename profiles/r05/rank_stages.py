@@ -3,7 +3,7 @@
 
 BASELINE config 4 (ML-20M-shaped, K=200, f64) as rank r of an N=8 run, every rank
 in turn, through sbmf_test_virtual_rank: the rank runs exactly its own row blocks,
-4 nnz-balanced stages per half, bins and streaming tasks, with the exchange
+nnz-balanced stages per half (2, the default for several ranks), bins and streaming tasks, with the exchange
 skipped (timing only; other ranks' rows keep their initial values, their
 residuals read 0; SBMF_STAGES sets the stages per half).  Per rank and stage: the device time on the compute stream
 (HIP events), the stage's rows / ratings and its longest row.  The stage holding
@@ -59,7 +59,7 @@ def main():
     N = args.ranks
     ub, ib = partition_rows(uptr, N), partition_rows(iptr, N)
     trd, ted = Data(*tr), Data(*te)
-    NST = int(os.environ.get("SBMF_STAGES", "4"))
+    NST = int(os.environ.get("SBMF_STAGES", "2"))  # the library's default for several ranks
     out = {"shape": args.shape, "K": args.K, "ranks": N, "stages": NST, "tune": args.tune, "n_train": int(len(tr[0])), "per_rank": []}
     ranks = [args.only] if args.only >= 0 else list(range(N))
     for r in ranks:
