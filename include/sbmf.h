@@ -134,9 +134,13 @@ typedef struct sbmf_config {
                                           (default: one- / two-wave k_grow workgroups),
                                  bit 12 = k_grow reads sigma and mu from memory at every K
                                           (default: from LDS when Kp <= 128),
+                                 bit 13 = f64 user streaming rows all on one 4-wave k_gres set
+                                          (default: rows above 512 ratings on a second, 8-wave set),
+                                 bit 14 = (experiment) that second user set on 16-wave workgroups,
                                  bit 17 = k_gres on 16-wave workgroups (both sides),
-                                 bit 23 = f64 user streaming rows on 8-wave k_gres workgroups
-                                          (default: 4-wave, 512-rating tasks),
+                                 bit 23 = f64 user streaming rows all on 8-wave k_gres workgroups
+                                          (default: up to 512 ratings on 4-wave ones, 512-rating
+                                          tasks, longer rows on a second, 8-wave set),
                                  bit 24 = k_gres as a cooperative launch (experiments only; the
                                           default is an ordinary launch in every schedule: tasks are
                                           claimed in queue order, no co-residency needed),

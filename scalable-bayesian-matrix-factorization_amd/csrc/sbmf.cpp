@@ -500,13 +500,23 @@ static void prepare_T(sbmf_ctx* c) {
             // CU): measured user streaming 1.49 -> 1.40 ms against 8-wave (r03s10); tune bit 23,
             // or an explicit workgroup-shape bit, keeps them on 8-wave workgroups
             const bool user4 = sd == &c->users && sizeof(T) == 8 && !(cf.tune & (128u | 0x20000u | 0x800000u));
-            const uint32_t stunes[2] = {user4 ? cf.tune | 128u : cf.tune, cf.tune | 0x20000u};
-            // (a second user set -- rows above 1024 / 2048 ratings on 16-wave workgroups, or above
-            // 512 / 1024 on 8-wave ones -- measured neutral to slower: r04s9, r04s15)
+            // f64 user rows above 512 ratings as a second set on 8-wave workgroups (1024-rating tasks:
+            // rows up to 1024 whole, longer ones in half as many chunks) beside the 4-wave set of the
+            // rest: the r05s26 phase profile had the 4-wave set's split-row chunks 63 % in the hand-off
+            // phase; user half 2.85-2.89 -> 2.80-2.81 ms (r05s27, 3 rounds).  Tune bit 13 keeps one
+            // 4-wave set; bit 14 (experiment) puts the long rows on 16-wave workgroups instead (slower)
+            const bool user2 = user4 && (!(cf.tune & 0x2000u) || (cf.tune & 0x4000u));
+            const uint32_t stunes[2] = {user4 ? cf.tune | 128u : cf.tune,
+                                        user2 && !(cf.tune & 0x4000u) ? cf.tune : cf.tune | 0x20000u};
+            // (round 4 measured a second user set neutral to slower -- rows above 1024 / 2048 ratings
+            // on 16-wave workgroups, above 512 / 1024 on 8-wave ones: r04s9, r04s15 -- with the user
+            // rows of 9..256 ratings still on the Gram-block kinds)
             for (auto& gp : sd->stg) {
             std::vector<uint32_t> rows[2];
-            for (uint32_t r : gp->bin_rows[KIND_STREAM])  // degree-descending
-                rows[item16 && sd->ptr[r + 1] - sd->ptr[r] > 1024u ? 1 : 0].push_back(r);
+            for (uint32_t r : gp->bin_rows[KIND_STREAM]) {  // degree-descending
+                const uint32_t d = sd->ptr[r + 1] - sd->ptr[r];
+                rows[(item16 && d > 1024u) || (user2 && d > 512u) ? 1 : 0].push_back(r);
+            }
             for (int k = 0; k < 2; ++k) {
                 Side::StreamSet& S = gp->ss[k];
                 S.tune = stunes[k];

@@ -110,7 +110,7 @@ def test_split_rows_match_oracle(ml100k, chunk, K):
 
 @pytest.mark.parametrize("tune", [0, 4, 8, 12, 128, 131072, 1 << 23, 1 << 24, 1 << 25, 1 << 27, 1 << 29, 1 << 30,
                                   (1 << 30) | (1 << 27), (1 << 29) | 128, (1 << 30) | 131072, (1 << 25) | 128, 256, 512,
-                                  768, 1024, 1792, 4096])
+                                  768, 1024, 1792, 4096, 8192, 16384])
 def test_kernel_variants_match_oracle(ml100k, tune):
     """Kernel variants (sbmf_config.tune, include/sbmf.h): bit 2 power-of-two
     waves per Gram-block row, bit 3 two 8-vector waves for 33..64-rating f64
@@ -121,7 +121,9 @@ def test_kernel_variants_match_oracle(ml100k, tune):
     streaming sets one after the other instead of side by side; bits 8 / 9 / 10:
     the 65..128 / 129..256 / 9..64-rating f64 bins as Gram-block rows instead of
     one- / two- / one-wave k_grow workgroups; bit 12: k_grow's KL = 256 form (sigma
-    and mu read from memory) at a K whose default is the KL = 128 one.  Under the
+    and mu read from memory) at a K whose default is the KL = 128 one; bit 13: one 4-wave
+    user streaming set (default: rows above 512 ratings on a second, 8-wave set); bit 14:
+    that set on 16-wave workgroups.  Under the
     default overlap the two item streaming sets run concurrently on two streams
     beside the Gram-block launches, their split rows handing partials over while
     the other launches hold CUs: split_chunk 16 splits the longest rows into
