@@ -1064,8 +1064,8 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
             sums = body(std::integral_constant<int, VW / 4>{});
         else if (vpw <= (uint32_t)VW / 2)
             sums = body(std::integral_constant<int, VW / 2>{});
-        else if (SIDE == 0 && vpw <= (uint32_t)(3 * VW / 4))  // user rows (measured: 3 % faster there,
-            sums = body(std::integral_constant<int, 3 * VW / 4>{});  // 1 % slower on the item side)
+        else if (vpw <= (uint32_t)(3 * VW / 4))  // (user rows: 3 % faster, r03; item rows since round 5:
+            sums = body(std::integral_constant<int, 3 * VW / 4>{});  // stage 3.51-3.55 -> 3.47-3.48 ms, r05s33)
         else
             sums = body(std::integral_constant<int, VW>{});
         // ---- new own row: whole rows write it, split rows stage it (k_split_finish publishes)
