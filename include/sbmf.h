@@ -300,6 +300,29 @@ int sbmf_load_libfm(const char* path, uint32_t item_offset, sbmf_ratings* out);
  * one-user-one-item rule and item_offset meaning as sbmf_load_libfm.  Replaces
  * the binary branch of Data::load (Data.h:115-160). */
 int sbmf_load_libfm_binary(const char* stem, uint32_t item_offset, sbmf_ratings* out);
+/* The transpose <stem>.xt + <stem>.y (or .datat + .target, preferred): the
+ * file tools/transpose.cpp:54-172 writes from a .x, one sparse row per
+ * feature listing its cases.  This is what bin/libFM -method mcmc|als reads:
+ * its data sets are built with has_x = false (libfm.cpp:132-149), so Data::load
+ * (Data.h:113-117,143-151) opens only the transpose.  Each case must hold two
+ * features; the lower id is the user, the higher the item (item_offset as
+ * above).  Replaces the has_xt branch of Data::load. */
+int sbmf_load_libfm_binary_t(const char* stem, uint32_t item_offset, sbmf_ratings* out);
+/* Data::load's choice of input (Data.h:112-117) for a data set that needs the
+ * row-major cases (has_x) and / or the transpose (has_xt): 1 = <stem>.data
+ * [+ .datat] + .target, 2 = <stem>.x [+ .xt] + .y, 0 = neither (Data::load
+ * then parses <stem> as libFM text); SBMF_E_ARG if both flags are 0. */
+int sbmf_libfm_binary_kind(const char* stem, int has_x, int has_xt);
+/* Data::load (Data.h:106-283) for rating data: the binary input
+ * sbmf_libfm_binary_kind picks for (has_x, has_xt) -- the cases read from the
+ * row-major file when has_x, from the transpose otherwise -- else <stem> as libFM text
+ * (sbmf_load_libfm).  bin/libFM's sets: has_x = 0, has_xt = 1 for -method
+ * mcmc and als, both 1 for the other methods (libfm.cpp:132-149). */
+int sbmf_load_libfm_data(const char* stem, int has_x, int has_xt, uint32_t item_offset, sbmf_ratings* out);
+/* Writes <stem>.xt / <stem>.y: what tools/convert.cpp then tools/transpose.cpp
+ * write for the same cases, byte for byte (rows per feature 0..num_cols-1,
+ * ascending case ids, value 1). */
+int sbmf_save_libfm_binary_t(const char* stem, const sbmf_ratings* in, uint32_t item_offset, uint32_t num_cols);
 /* Writes <stem>.x / <stem>.y in that format (the convert tool's output for
  * rating data): row q = {user[q]:1, item_offset + item[q]:1}, f32 targets;
  * num_cols = max(num_cols, largest feature id + 1). */
@@ -368,6 +391,24 @@ typedef struct sbmf_rccl_selftest {
 } sbmf_rccl_selftest;
 int sbmf_test_rccl_selftest(sbmf_ctx* ctx, uint64_t nbytes, uint32_t reps, double deadline_s,
                             sbmf_rccl_selftest* out);
+/* The self-test runs `reps` extra item halves on the context's live chain, so the
+ * context is spent afterwards: sbmf_run returns SBMF_E_STATE on it (create a new
+ * one).  On a timeout the communicator is aborted (ncclCommAbort), the buffers
+ * are left allocated, and sbmf_destroy leaks the context instead of waiting on
+ * its queued work. */
+
+/* Resource audit: hipMemGetInfo of `device` and what the library holds in this
+ * process right now, counted where it is created and released (every device
+ * buffer, pinned host buffer, stream, event, context and RCCL communicator of
+ * every learner kind).  A process that has destroyed all of its contexts holds
+ * nothing: the counts return to zero. */
+typedef struct sbmf_device_usage {
+    uint64_t device_free, device_total; /* hipMemGetInfo                                  */
+    int64_t dev_bytes, dev_allocs;      /* device buffers the library holds              */
+    int64_t pinned_bytes, pinned_allocs;/* pinned host buffers                           */
+    int64_t streams, events, contexts, comms;
+} sbmf_device_usage;
+int sbmf_test_device_usage(int device, sbmf_device_usage* out);
 
 #ifdef __cplusplus
 }

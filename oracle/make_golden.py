@@ -43,7 +43,12 @@ Fixtures written (all data, no reference source):
                                               the throughput (Philox) chain against the reference chain
   ref_final_m1m100k_k20_s1.txt                gibbs_sbpmf_final on the reference's converted
                                               data/m1m/m100k/{train,test}_sbpmf (raw item ids kept)
-`make_golden.py seeds` / `make_golden.py refdata` / `make_golden.py vbo` / `make_golden.py libfm` / `make_golden.py rlog` / `make_golden.py collapse` regenerate
+  m1m100k_{train,test}_libfm.{x,y,xt}.gz       libFM's binary files of those: tools/convert.cpp (.x/.y) and
+                                              tools/transpose.cpp (.xt), compiled unmodified (oracle/Makefile)
+  ref_libfm_<method>_m1m100k_xt_d118_s1_i10.txt
+                                              bin/libFM with the same argv in a directory holding only
+                                              .xt + .y (the files -method mcmc|als reads); + _pred.txt.gz
+`make_golden.py bindata` / `make_golden.py seeds` / `make_golden.py refdata` / `make_golden.py vbo` / `make_golden.py libfm` / `make_golden.py rlog` / `make_golden.py collapse` regenerate
 only those fixtures.
 Only runnable in the build container (needs /root/reference).
 """
@@ -241,6 +246,48 @@ def refdata_goldens():
     print("golden final m1m100k", vals[0], vals[-1])
 
 
+def bindata_goldens():
+    """libFM's binary input for the reference's own data/m1m/m100k/{train,test}_libfm:
+    the compiled tools/convert.cpp writes <stem>.x/.y, the compiled
+    tools/transpose.cpp the feature-major <stem>.xt, all stored gzipped as
+    m1m100k_<stem>.{x,y,xt}.gz.  Then bin/libFM (libfm.cpp compiled unmodified,
+    time() pinned to 1) runs its exact argv in a directory holding only .xt + .y:
+    -method mcmc|als build their sets with has_x = false (libfm.cpp:140-149), so
+    Data::load opens the transpose (Data.h:113-117,143-151).  Its #Iter lines and
+    -out predictions are stored as ref_libfm_<method>_m1m100k_xt_d118_s1_i10*."""
+    src = os.path.join(REF, "data", "m1m", "m100k")
+    root = "/tmp/sbmf_bindata_%d" % os.getpid()
+    os.makedirs(os.path.join(root, "bin"), exist_ok=True)
+    for nm in ("train_libfm", "test_libfm"):
+        shutil.copy(os.path.join(src, nm), os.path.join(root, nm))
+        subprocess.run([os.path.join(HERE, "_ref", "convert"), "--ifile", nm, "--ofilex", nm + ".x", "--ofiley",
+                        nm + ".y"], cwd=root, capture_output=True, text=True, check=True)
+        subprocess.run([os.path.join(HERE, "_ref", "transpose"), "--ifile", nm + ".x", "--ofile", nm + ".xt"],
+                       cwd=root, capture_output=True, text=True, check=True)
+        for ext in ("x", "y", "xt"):
+            with open(os.path.join(root, nm + "." + ext), "rb") as f, \
+                    gzip.GzipFile(os.path.join(GOLD, "m1m100k_%s.%s.gz" % (nm, ext)), "wb", mtime=0) as g:
+                g.write(f.read())
+        for ext in ("xt", "y"):
+            shutil.copy(os.path.join(root, nm + "." + ext), os.path.join(root, "bin", nm + "." + ext))
+    for method, extra in (("mcmc", []), ("als", ["-regular", "0,0,10"])):
+        cmd = [os.path.join(HERE, "_ref", "libFM"), "-task", "r", "-train", "train_libfm", "-test", "test_libfm",
+               "-dim", "1,1,8", "-iter", "10", "-method", method, "-out", "pred.txt"] + extra
+        p = subprocess.run(cmd, cwd=os.path.join(root, "bin"), env=dict(os.environ, LIBFM_PIN_TIME="1"),
+                           capture_output=True, text=True, check=True)
+        assert "data transpose..." in p.stdout, p.stdout[-800:]  # Data.h:144: the binary branch ran
+        lines = [l for l in p.stdout.splitlines() if l.startswith("#Iter=")]
+        assert len(lines) == 10, p.stdout[-500:]
+        name = "ref_libfm_%s_m1m100k_xt_d118_s1_i10" % method
+        with open(os.path.join(GOLD, name + ".txt"), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        with open(os.path.join(root, "bin", "pred.txt"), "rb") as f, \
+                gzip.GzipFile(os.path.join(GOLD, name + "_pred.txt.gz"), "wb", mtime=0) as g:
+            g.write(f.read())
+        print("golden libfm binary", name, lines[-1])
+    shutil.rmtree(root)
+
+
 SEED_RUNS = [("ml100k", 64), ("ml1msynth", 32)]
 
 
@@ -353,6 +400,9 @@ def main():
     if sys.argv[1:] == ["refdata"]:
         refdata_goldens()
         return 0
+    if sys.argv[1:] == ["bindata"]:
+        bindata_goldens()
+        return 0
     if sys.argv[1:] == ["rlog"]:
         rlog_golden()
         return 0
@@ -390,6 +440,7 @@ def main():
     libfm_goldens()
     rlog_golden()
     refdata_goldens()
+    bindata_goldens()
     seeds_goldens()
     collapse_golden()
     return 0

@@ -1,5 +1,6 @@
 // comm.cpp -- RCCL exchange (see comm.h).
 #include "comm.h"
+#include "common.h"
 
 #include <rccl/rccl.h>
 
@@ -31,6 +32,7 @@ struct Rccl {
     decltype(&::ncclGetUniqueId) GetUniqueId;
     decltype(&::ncclCommInitRank) CommInitRank;
     decltype(&::ncclCommDestroy) CommDestroy;
+    decltype(&::ncclCommAbort) CommAbort;
     decltype(&::ncclGetErrorString) GetErrorString;
     decltype(&::ncclBroadcast) Broadcast;
     decltype(&::ncclSend) Send;
@@ -52,6 +54,7 @@ const Rccl& rccl() {
         sym(t.GetUniqueId, "ncclGetUniqueId");
         sym(t.CommInitRank, "ncclCommInitRank");
         sym(t.CommDestroy, "ncclCommDestroy");
+        sym(t.CommAbort, "ncclCommAbort");
         sym(t.GetErrorString, "ncclGetErrorString");
         sym(t.Broadcast, "ncclBroadcast");
         sym(t.Send, "ncclSend");
@@ -83,9 +86,35 @@ std::string host_name(const uint8_t id[128]) {
 }  // namespace
 
 Comm::~Comm() {
-    if (comm_) (void)rccl().CommDestroy((ncclComm_t)comm_);
+    if (comm_) {
+        (void)rccl().CommDestroy((ncclComm_t)comm_);
+        audit().comms--;
+    }
     if (shm_) munmap(shm_, shm_bytes_);
 }
+
+void Comm::abort() {
+    if (!comm_) return;
+    (void)rccl().CommAbort((ncclComm_t)comm_);
+    audit().comms--;
+    comm_ = nullptr;
+}
+
+namespace {
+// ncclCommInitRank's failure, with what this process holds at that moment: free
+// device memory and the library's live resources (the audit of common.h)
+[[noreturn]] void init_fail(ncclResult_t r) {
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    const Audit& a = audit();
+    fail(SBMF_E_COMM,
+         "ncclCommInitRank failed: %s [device free %.1f of %.1f GiB; library holds %lld contexts, %lld streams, "
+         "%lld events, %lld device buffers (%.1f MiB), %lld pinned buffers (%.1f MiB), %lld RCCL communicators]",
+         rccl_error_string((int)r), fr / 1073741824.0, tot / 1073741824.0, a.contexts.load(), a.streams.load(),
+         a.events.load(), a.dev_allocs.load(), a.dev_bytes.load() / 1048576.0, a.pinned_allocs.load(),
+         a.pinned_bytes.load() / 1048576.0, a.comms.load());
+}
+}  // namespace
 
 void Comm::unique_id(uint8_t id[128]) {
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
@@ -145,8 +174,9 @@ void Comm::init(int nranks, int rank, const uint8_t id[128]) {
     std::memcpy(&u, id, 128);
     ncclComm_t c;
     ncclResult_t r = rccl().CommInitRank(&c, nranks, u, rank);
-    if (r != ncclSuccess) comm_fail("ncclCommInitRank", r);
+    if (r != ncclSuccess) init_fail(r);
     comm_ = c;
+    audit().comms++;
 }
 
 void Comm::init_loopback() {
@@ -155,8 +185,9 @@ void Comm::init_loopback() {
     if (r != ncclSuccess) comm_fail("ncclGetUniqueId", r);
     ncclComm_t c;
     r = rccl().CommInitRank(&c, 1, u, 0);
-    if (r != ncclSuccess) comm_fail("ncclCommInitRank", r);
+    if (r != ncclSuccess) init_fail(r);
     comm_ = c;
+    audit().comms++;
     nranks_ = 1;
     rank_ = 0;
     loopback_ = true;

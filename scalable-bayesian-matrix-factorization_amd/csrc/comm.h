@@ -32,6 +32,9 @@ class Comm {
     // the exact RCCL calls of the exchange through the same dlsym table.
     void init_loopback();
     bool active() const { return comm_ != nullptr || shm_ != nullptr; }
+    // ncclCommAbort: tear the communicator down without waiting for its queued
+    // work (a stuck self-test); the object is inactive afterwards.
+    void abort();
     // Rank k owns units [bounds[k], bounds[k+1]) of unit_bytes each, starting
     // at base; after the call every rank holds every rank's units.
     void bcast_ranges(void* base, size_t unit_bytes, const std::vector<uint64_t>& bounds, hipStream_t st);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -32,6 +33,50 @@ struct Error {
                                          __FILE__, __LINE__);                                         \
     } while (0)
 
+// Resource audit (sbmf_test_device_usage): what the library holds right now,
+// counted where it is created and released -- device and pinned host bytes,
+// streams, events, contexts and RCCL communicators.  Every stream, event and
+// pinned buffer goes through the helpers below, every device buffer through DBuf.
+struct Audit {
+    std::atomic<long long> dev_bytes{0}, dev_allocs{0}, pinned_bytes{0}, pinned_allocs{0};
+    std::atomic<long long> streams{0}, events{0}, contexts{0}, comms{0};
+};
+Audit& audit();
+inline void stream_create(hipStream_t* s) {
+    HIPCHK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+    audit().streams++;
+}
+inline void stream_destroy(hipStream_t& s) {
+    if (!s) return;
+    (void)hipStreamDestroy(s);
+    audit().streams--;
+    s = nullptr;
+}
+inline void event_create(hipEvent_t* e, unsigned flags = hipEventDefault) {
+    HIPCHK(hipEventCreateWithFlags(e, flags));
+    audit().events++;
+}
+inline void event_destroy(hipEvent_t& e) {
+    if (!e) return;
+    (void)hipEventDestroy(e);
+    audit().events--;
+    e = nullptr;
+}
+// pinned host memory: the byte count is kept by the caller (freed with the same size)
+inline void pinned_alloc(void** p, size_t bytes) {
+    HIPCHK(hipHostMalloc(p, bytes, hipHostMallocDefault));
+    audit().pinned_bytes += (long long)bytes;
+    audit().pinned_allocs++;
+}
+template <typename P>
+inline void pinned_free(P*& p, size_t bytes) {
+    if (!p) return;
+    (void)hipHostFree((void*)p);
+    audit().pinned_bytes -= (long long)bytes;
+    audit().pinned_allocs--;
+    p = nullptr;
+}
+
 // Owning device allocation.
 struct DBuf {
     void* p = nullptr;
@@ -41,7 +86,11 @@ struct DBuf {
     DBuf& operator=(const DBuf&) = delete;
     ~DBuf() { release(); }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            audit().dev_bytes -= (long long)bytes;
+            audit().dev_allocs--;
+        }
         p = nullptr;
         bytes = 0;
     }
@@ -49,8 +98,17 @@ struct DBuf {
         release();
         if (b == 0) b = 16;
         hipError_t e = hipMalloc(&p, b);
-        if (e != hipSuccess) fail(SBMF_E_NOMEM, "hipMalloc(%zu) failed: %s", b, hipGetErrorString(e));
+        if (e != hipSuccess) {
+            p = nullptr;
+            fail(SBMF_E_NOMEM, "hipMalloc(%zu) failed: %s", b, hipGetErrorString(e));
+        }
         bytes = b;
+        audit().dev_bytes += (long long)b;
+        audit().dev_allocs++;
+    }
+    void leak() {  // give the allocation up without freeing it (it stays counted as held)
+        p = nullptr;
+        bytes = 0;
     }
     void ensure(size_t b) {  // grow-only (per-epoch staging)
         if (b > bytes) alloc(b);

@@ -110,8 +110,7 @@ struct FMLearner {
     }
 
     ~FMLearner() {
-        for (auto& e : ev)
-            if (e) (void)hipEventDestroy(e);
+        for (auto& e : ev) event_destroy(e);
     }
 
     template <class G>
@@ -648,7 +647,7 @@ FMLearner* fmm_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
     HIPCHK(hipStreamSynchronize(st));
     std::vector<double>().swap(L->h_v);  // the host copies served the upload only
     std::vector<double>().swap(L->h_w);
-    for (auto& e : L->ev) HIPCHK(hipEventCreate(&e));
+    for (auto& e : L->ev) event_create(&e);
     return L.release();
 }
 

@@ -18,6 +18,7 @@
 // two exactly representable values -- the value strtod (strtof) returns
 // (Clinger's fast path); anything else goes through strtod / strtof itself.
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -522,21 +523,52 @@ bool file_exists(const std::string& f) {
 }
 }  // namespace
 
+namespace {
+int load_x(const std::string& xf, const std::string& yf, uint32_t item_offset, sbmf_ratings* out);
+int load_xt(const std::string& xf, const std::string& yf, uint32_t item_offset, sbmf_ratings* out);
+}  // namespace
+
 int sbmf_load_libfm_binary(const char* stem, uint32_t item_offset, sbmf_ratings* out) {
     if (!stem || !out) return SBMF_E_ARG;
     std::memset(out, 0, sizeof *out);
     const std::string s(stem);
-    std::string xf, yf;
-    if (file_exists(s + ".data") && file_exists(s + ".target")) {
-        xf = s + ".data";
-        yf = s + ".target";
-    } else if (file_exists(s + ".x") && file_exists(s + ".y")) {
-        xf = s + ".x";
-        yf = s + ".y";
-    } else {
-        g_lerr = "unable to open " + s + ".x/.y (or .data/.target)";
-        return SBMF_E_IO;
-    }
+    if (file_exists(s + ".data") && file_exists(s + ".target")) return load_x(s + ".data", s + ".target", item_offset, out);
+    if (file_exists(s + ".x") && file_exists(s + ".y")) return load_x(s + ".x", s + ".y", item_offset, out);
+    g_lerr = "unable to open " + s + ".x/.y (or .data/.target)";
+    return SBMF_E_IO;
+}
+
+int sbmf_load_libfm_binary_t(const char* stem, uint32_t item_offset, sbmf_ratings* out) {
+    if (!stem || !out) return SBMF_E_ARG;
+    std::memset(out, 0, sizeof *out);
+    const std::string s(stem);
+    if (file_exists(s + ".datat") && file_exists(s + ".target"))
+        return load_xt(s + ".datat", s + ".target", item_offset, out);
+    if (file_exists(s + ".xt") && file_exists(s + ".y")) return load_xt(s + ".xt", s + ".y", item_offset, out);
+    g_lerr = "unable to open " + s + ".xt/.y (or .datat/.target)";
+    return SBMF_E_IO;
+}
+
+// Data::load (Data.h:106-283) for rating data: the binary files of
+// sbmf_libfm_binary_kind when present (the row-major file when the set has one;
+// the transpose for a set without, which is what bin/libFM's MCMC / ALS sets
+// read), else <stem> as libFM text.
+int sbmf_load_libfm_data(const char* stem, int has_x, int has_xt, uint32_t item_offset, sbmf_ratings* out) {
+    if (!stem || !out || (!has_x && !has_xt)) return SBMF_E_ARG;
+    std::memset(out, 0, sizeof *out);
+    const std::string s(stem);
+    const int kind = sbmf_libfm_binary_kind(stem, has_x, has_xt);
+    if (kind == 1)
+        return has_x ? load_x(s + ".data", s + ".target", item_offset, out)
+                     : load_xt(s + ".datat", s + ".target", item_offset, out);
+    if (kind == 2)
+        return has_x ? load_x(s + ".x", s + ".y", item_offset, out) : load_xt(s + ".xt", s + ".y", item_offset, out);
+    return sbmf_load_libfm(stem, item_offset, out);
+}
+
+namespace {
+int load_x(const std::string& xf, const std::string& yf, uint32_t item_offset, sbmf_ratings* out) {
+    std::memset(out, 0, sizeof *out);
     InFile xin, yin;
     if (!open_in(xf.c_str(), xin) || !open_in(yf.c_str(), yin)) {
         g_lerr = "unable to open " + xf + " / " + yf;
@@ -640,6 +672,251 @@ int sbmf_load_libfm_binary(const char* stem, uint32_t item_offset, sbmf_ratings*
         return SBMF_E_IO;
     }
     out->n = R;
+    return SBMF_OK;
+}
+}  // namespace
+
+// Data::load's file choice (Data.h:112-117): 1 = <stem>.data/.datat/.target,
+// 2 = <stem>.x/.xt/.y, each file of the pair required only when the data set
+// needs that orientation (has_x: row-major cases; has_xt: the transpose, rows
+// per feature), 0 = neither, Data::load reads <stem> as text.  bin/libFM builds
+// its train / test sets with has_x = (method != "mcmc") after rewriting als to
+// mcmc, and has_xt = true except for sgd / sgda (libfm.cpp:132-149): the MCMC
+// and ALS chains read only the transpose.
+int sbmf_libfm_binary_kind(const char* stem, int has_x, int has_xt) {
+    if (!stem || (!has_x && !has_xt)) return SBMF_E_ARG;
+    const std::string s(stem);
+    if ((!has_x || file_exists(s + ".data")) && (!has_xt || file_exists(s + ".datat")) && file_exists(s + ".target"))
+        return 1;
+    if ((!has_x || file_exists(s + ".x")) && (!has_xt || file_exists(s + ".xt")) && file_exists(s + ".y")) return 2;
+    return 0;
+}
+
+// libFM's transpose <stem>.xt + <stem>.y (or .datat + .target, preferred as
+// Data::load does, Data.h:113-117,143-151): the file tools/transpose.cpp:54-172
+// writes from a .x, with the .x header's roles swapped (num_rows = features,
+// num_cols = cases) and one sparse row per feature {u32 size; size x {u32 case
+// id; f32 value}}, case ids ascending.  This is the only file bin/libFM -method
+// mcmc|als reads (has_x = false, libfm.cpp:140-149).  For rating data a
+// feature's row is its user's or item's rating list, so the per-case pair is
+// rebuilt: each case must hold exactly two features, the lower id is the user,
+// the higher the item (users-first ids), and item_offset has the meaning of
+// sbmf_load_libfm_binary.
+namespace {
+int load_xt(const std::string& xf, const std::string& yf, uint32_t item_offset, sbmf_ratings* out) {
+    std::memset(out, 0, sizeof *out);
+    InFile xin, yin;
+    if (!open_in(xf.c_str(), xin) || !open_in(yf.c_str(), yin)) {
+        g_lerr = "unable to open " + xf + " / " + yf;
+        return SBMF_E_IO;
+    }
+    const char* const xb = xin.p;
+    const char* const yb = yin.p;
+    const size_t xn = xin.n, yn = yin.n;
+    if (yn < 12) {
+        g_lerr = yf + ": truncated header";
+        return SBMF_E_IO;
+    }
+    uint32_t yh[3];
+    std::memcpy(yh, yb, 12);
+    if (yh[0] != 1 || yh[1] != sizeof(float) || yn < 12 + (size_t)yh[2] * sizeof(float)) {
+        g_lerr = yf + ": not a libFM DVector<float> file (version 1, 4-byte values)";
+        return SBMF_E_IO;
+    }
+    FmHeader h;
+    if (xn < sizeof h) {
+        g_lerr = xf + ": truncated header";
+        return SBMF_E_IO;
+    }
+    std::memcpy(&h, xb, sizeof h);
+    if (h.id != 2 || h.float_size != sizeof(float)) {
+        g_lerr = xf + ": not a libFM sparse matrix file (id 2, 4-byte values)";
+        return SBMF_E_IO;
+    }
+    // the transpose's columns are the cases; Data::load takes num_cases from the
+    // targets (Data.h:167), so the two must agree
+    if (h.num_cols != yh[2]) {
+        g_lerr = xf + ": " + std::to_string(h.num_cols) + " cases but " + std::to_string(yh[2]) + " targets";
+        return SBMF_E_IO;
+    }
+    const uint32_t F = h.num_rows;
+    const size_t C = h.num_cols, m = C ? C : 1;
+    // pass 1 (serial, one u32 per feature row): row offsets and the value count
+    std::vector<size_t> off((size_t)F + 1);
+    size_t at = sizeof h;
+    for (uint32_t f = 0; f < F; ++f) {
+        uint32_t sz;
+        if (at + 4 > xn) {
+            g_lerr = xf + ": truncated at feature row " + std::to_string(f);
+            return SBMF_E_IO;
+        }
+        std::memcpy(&sz, xb + at, 4);
+        if (at + 4 + (size_t)sz * 8 > xn) {
+            g_lerr = xf + ": truncated at feature row " + std::to_string(f);
+            return SBMF_E_IO;
+        }
+        off[f] = at;
+        at += 4 + (size_t)sz * 8;
+    }
+    off[F] = at;
+    const uint64_t nv = (at - sizeof h - 4ull * F) / 8;
+    if (nv != h.num_values) {
+        g_lerr = xf + ": header says " + std::to_string(h.num_values) + " values, rows hold " + std::to_string(nv);
+        return SBMF_E_IO;
+    }
+    out->user = static_cast<uint32_t*>(big_alloc(m * sizeof(uint32_t)));
+    out->item = static_cast<uint32_t*>(big_alloc(m * sizeof(uint32_t)));
+    out->rating = static_cast<double*>(big_alloc(m * sizeof(double)));
+    std::unique_ptr<std::atomic<uint32_t>[]> cnt(new (std::nothrow) std::atomic<uint32_t>[m]);
+    if (!out->user || !out->item || !out->rating || !cnt) {
+        sbmf_free_ratings(out);
+        return SBMF_E_NOMEM;
+    }
+    const size_t nc = std::max<size_t>(1, std::min<size_t>((size_t)nthreads(), C >> 16));
+    parallel_for(nc, [&](size_t t) {
+        for (size_t c = C * t / nc, e = C * (t + 1) / nc; c < e; ++c) cnt[c].store(0, std::memory_order_relaxed);
+    });
+    // pass 2: feature rows cut into nt ranges of about equal value counts; a
+    // case's first two features land in user[] / item[] in any order (sorted
+    // below), a third one or a case id past the targets is an error
+    const size_t nt = std::max<size_t>(1, std::min<size_t>((size_t)nthreads(), (size_t)(nv >> 17)));
+    std::vector<uint32_t> fcut(nt + 1, F);
+    fcut[0] = 0;
+    for (size_t t = 1, f = 0; t < nt; ++t) {
+        const size_t want = sizeof h + (off[F] - sizeof h) * t / nt;
+        while (f < F && off[f] < want) ++f;
+        fcut[t] = (uint32_t)f;
+    }
+    std::vector<uint64_t> bad(nt, UINT64_MAX);  // (kind << 56) | case / feature
+    parallel_for(nt, [&](size_t t) {
+        for (uint32_t f = fcut[t]; f < fcut[t + 1]; ++f) {
+            uint32_t sz;
+            std::memcpy(&sz, xb + off[f], 4);
+            const char* rec = xb + off[f] + 4;
+            for (uint32_t k = 0; k < sz; ++k, rec += 8) {
+                uint32_t c;
+                std::memcpy(&c, rec, 4);
+                if (c >= C) {
+                    bad[t] = (1ull << 56) | f;
+                    return;
+                }
+                const uint32_t slot = cnt[c].fetch_add(1, std::memory_order_relaxed);
+                if (slot == 0) out->user[c] = f;
+                else if (slot == 1) out->item[c] = f;
+            }
+        }
+    });
+    for (uint64_t b : bad)
+        if (b != UINT64_MAX) {
+            g_lerr = xf + " feature row " + std::to_string(b & 0xffffffffull) + ": case id past the " +
+                     std::to_string(C) + " targets";
+            sbmf_free_ratings(out);
+            return SBMF_E_IO;
+        }
+    std::vector<uint64_t> first_bad(nc, UINT64_MAX);
+    parallel_for(nc, [&](size_t t) {
+        for (size_t c = C * t / nc, e = C * (t + 1) / nc; c < e; ++c) {
+            const uint32_t a = out->user[c], b = out->item[c];
+            const uint32_t lo = std::min(a, b), hi = std::max(a, b);
+            if (cnt[c].load(std::memory_order_relaxed) != 2 || hi < item_offset ||
+                (item_offset > 0 && lo >= item_offset)) {
+                first_bad[t] = c;
+                return;
+            }
+            float y;
+            std::memcpy(&y, yb + 12 + c * 4, 4);
+            out->user[c] = lo;
+            out->item[c] = hi - item_offset;
+            out->rating[c] = (double)y;
+        }
+    });
+    for (uint64_t c : first_bad)
+        if (c != UINT64_MAX) {
+            g_lerr = xf + " case " + std::to_string(c) + ": the learners need exactly one user and one item feature "
+                     "per case (" + std::to_string(cnt[c].load()) + " features" +
+                     (item_offset > 0 ? "; user id < item_offset <= item id)" : ")");
+            sbmf_free_ratings(out);
+            return SBMF_E_IO;
+        }
+    out->n = C;
+    return SBMF_OK;
+}
+}  // namespace
+
+// tools/transpose.cpp:54-172 for rating data: <stem>.xt holds one row per
+// feature 0..num_cols-1 (num_cols = max(num_cols, largest feature id + 1), as
+// the .x writer), each the ascending case ids of that feature with value 1, and
+// <stem>.y the f32 targets -- byte for byte what convert + transpose write for
+// the same cases (a .x row {user, item} with value 1 each).
+int sbmf_save_libfm_binary_t(const char* stem, const sbmf_ratings* in, uint32_t item_offset, uint32_t num_cols) {
+    if (!stem || !in || (in->n && (!in->user || !in->item || !in->rating))) return SBMF_E_ARG;
+    if (in->n > 0xffffffffull) return SBMF_E_ARG;
+    uint64_t cols = num_cols;
+    for (uint64_t q = 0; q < in->n; ++q) {
+        cols = std::max<uint64_t>(cols, (uint64_t)in->user[q] + 1);
+        cols = std::max<uint64_t>(cols, (uint64_t)item_offset + in->item[q] + 1);
+    }
+    if (cols > 0xffffffffull) {
+        g_lerr = "feature id past UINT32_MAX - 1 (item_offset + item id): not representable in the .xt format";
+        return SBMF_E_ARG;
+    }
+    for (uint64_t q = 0; q < in->n; ++q)
+        if (in->user[q] == (uint64_t)item_offset + in->item[q]) {
+            g_lerr = "case " + std::to_string(q) + ": user and item feature ids coincide";
+            return SBMF_E_ARG;
+        }
+    // counting sort of the 2n (feature, case) entries by feature, cases ascending
+    std::vector<uint64_t> start(cols + 1, 0);
+    for (uint64_t q = 0; q < in->n; ++q) {
+        ++start[in->user[q] + 1];
+        ++start[(uint64_t)item_offset + in->item[q] + 1];
+    }
+    for (uint64_t f = 0; f < cols; ++f) start[f + 1] += start[f];
+    std::vector<uint32_t> cs(2 * in->n);
+    {
+        std::vector<uint64_t> fill(start.begin(), start.end() - 1);
+        for (uint64_t q = 0; q < in->n; ++q) {
+            cs[fill[in->user[q]]++] = (uint32_t)q;
+            cs[fill[(uint64_t)item_offset + in->item[q]]++] = (uint32_t)q;
+        }
+    }
+    const std::string s(stem);
+    FILE* fx = std::fopen((s + ".xt").c_str(), "wb");
+    FILE* fy = fx ? std::fopen((s + ".y").c_str(), "wb") : nullptr;
+    if (!fx || !fy) {
+        if (fx) std::fclose(fx);
+        g_lerr = "unable to write " + s + ".xt/.y";
+        return SBMF_E_IO;
+    }
+    const FmHeader h{2, (uint32_t)sizeof(float), 2 * in->n, (uint32_t)cols, (uint32_t)in->n};
+    bool ok = std::fwrite(&h, sizeof h, 1, fx) == 1;
+    std::vector<char> buf;
+    const float one = 1.0f;
+    for (uint64_t f = 0; ok && f < cols; ++f) {
+        const uint32_t sz = (uint32_t)(start[f + 1] - start[f]);
+        buf.resize(4 + (size_t)sz * 8);
+        std::memcpy(buf.data(), &sz, 4);
+        for (uint32_t k = 0; k < sz; ++k) {
+            std::memcpy(buf.data() + 4 + 8 * (size_t)k, &cs[start[f] + k], 4);
+            std::memcpy(buf.data() + 8 + 8 * (size_t)k, &one, 4);
+        }
+        ok = std::fwrite(buf.data(), 1, buf.size(), fx) == buf.size();
+    }
+    const uint32_t yh[3] = {1, (uint32_t)sizeof(float), (uint32_t)in->n};
+    ok = ok && std::fwrite(yh, sizeof yh, 1, fy) == 1;
+    constexpr size_t CH = 1 << 16;
+    std::vector<float> yb(CH);
+    for (uint64_t q0 = 0; ok && q0 < in->n; q0 += CH) {
+        const size_t m = (size_t)std::min<uint64_t>(CH, in->n - q0);
+        for (size_t k = 0; k < m; ++k) yb[k] = (float)in->rating[q0 + k];
+        ok = std::fwrite(yb.data(), 4, m, fy) == m;
+    }
+    ok = (std::fclose(fx) == 0) & ok;
+    ok = (std::fclose(fy) == 0) & ok;
+    if (!ok) {
+        g_lerr = "write error on " + s + ".xt/.y";
+        return SBMF_E_IO;
+    }
     return SBMF_OK;
 }
 

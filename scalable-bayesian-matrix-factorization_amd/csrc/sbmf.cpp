@@ -244,13 +244,23 @@ static void build_bins(const Side& s, Side::Stage& g, uint32_t stream_thr, bool 
     }
 }
 
+Audit& audit() {
+    static Audit a;
+    return a;
+}
+
 }  // namespace sbmf
 
 using namespace sbmf;
 
 struct sbmf_ctx {
+    sbmf_ctx() { sbmf::audit().contexts++; }
     sbmf_config cfg{};
     std::string err;
+    // sbmf_test_rccl_selftest ran extra item halves on this chain (it is no longer
+    // the sampler's): sweeps are refused.  dead: the self-test timed out with RCCL
+    // work still queued; sbmf_destroy then leaks the context instead of waiting.
+    bool spent = false, dead = false;
     // host data
     std::vector<uint32_t> tu, ti, su, si;
     std::vector<double> tr, sr;
@@ -345,7 +355,7 @@ struct sbmf_ctx {
     // prologue, whose column statistics read the current mu from d_hyper
     bool hyper_ahead = false;
     double* h_pinned = nullptr;  // pinned staging for z streams
-    size_t h_pinned_bytes = 0;
+    size_t h_pinned_bytes = 0, h_pre_bytes = 0, h_io_bytes = 0;
     sbmf_timing timing{};
     VBLearner* vb = nullptr;  // -method vb (vbo.cpp)
     FMLearner* fm = nullptr;  // -method mcmc --order libfm / als (fmm.cpp)
@@ -387,9 +397,9 @@ static void download_table(sbmf_ctx* c, const DBuf& d, double* dst, uint32_t R) 
 
 static void ensure_pinned(sbmf_ctx* c, size_t bytes) {
     if (c->h_pinned_bytes >= bytes) return;
-    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
-    c->h_pinned = nullptr;
-    HIPCHK(hipHostMalloc((void**)&c->h_pinned, bytes, hipHostMallocDefault));
+    pinned_free(c->h_pinned, c->h_pinned_bytes);
+    c->h_pinned_bytes = 0;
+    pinned_alloc((void**)&c->h_pinned, bytes);
     c->h_pinned_bytes = bytes;
 }
 
@@ -632,12 +642,12 @@ static void prepare_T(sbmf_ctx* c) {
     c->d_colpart.alloc((size_t)nchunk * 2 * c->K * sizeof(double));
     c->h_res.assign(RES_COL + 4 * (size_t)c->K, 0.0);
     c->d_res.alloc(c->h_res.size() * sizeof(double));
-    if (c->h_pre) (void)hipHostFree(c->h_pre);
-    c->h_pre = nullptr;
-    HIPCHK(hipHostMalloc((void**)&c->h_pre, c->h_res.size() * sizeof(double), hipHostMallocDefault));
-    if (c->h_io) (void)hipHostFree(c->h_io);
-    c->h_io = nullptr;
-    HIPCHK(hipHostMalloc(&c->h_io, 128 + 4 * (size_t)c->Kp * sizeof(T), hipHostMallocDefault));
+    pinned_free(c->h_pre, c->h_pre_bytes);
+    c->h_pre_bytes = c->h_res.size() * sizeof(double);
+    pinned_alloc((void**)&c->h_pre, c->h_pre_bytes);
+    pinned_free(c->h_io, c->h_io_bytes);
+    c->h_io_bytes = 128 + 4 * (size_t)c->Kp * sizeof(T);
+    pinned_alloc(&c->h_io, c->h_io_bytes);
     c->pre.valid = false;
     c->hyper_ahead = false;
     const uint64_t big = std::max<uint64_t>({(uint64_t)c->I, (uint64_t)c->J, c->su.size() / 128 + 2});
@@ -728,16 +738,16 @@ static void prepare_T(sbmf_ctx* c) {
         c->d_kprof.alloc(96 * sizeof(unsigned long long));
         HIPCHK(hipMemset(c->d_kprof.p, 0, 96 * sizeof(unsigned long long)));
     }
-    for (hipEvent_t e : c->kevs) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->sev) (void)hipEventDestroy(e);
+    for (hipEvent_t& e : c->kevs) event_destroy(e);
+    for (hipEvent_t& e : c->sev) event_destroy(e);
     c->kevs.assign((size_t)c->nstages * 2 * SBMF_NKIND * 2, nullptr);
     c->kprev.assign((size_t)c->nstages * 2 * SBMF_NKIND, (int8_t)-1);
     c->sev.assign((size_t)2 * c->nstages, nullptr);
-    for (hipEvent_t& e : c->kevs) HIPCHK(hipEventCreate(&e));
-    for (hipEvent_t& e : c->sev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (hipEvent_t e : c->tsev) (void)hipEventDestroy(e);
+    for (hipEvent_t& e : c->kevs) event_create(&e);
+    for (hipEvent_t& e : c->sev) event_create(&e, hipEventDisableTiming);
+    for (hipEvent_t& e : c->tsev) event_destroy(e);
     c->tsev.assign(c->virt ? (size_t)2 * (c->nstages + 1) : 0, nullptr);
-    for (hipEvent_t& e : c->tsev) HIPCHK(hipEventCreate(&e));
+    for (hipEvent_t& e : c->tsev) event_create(&e);
     c->sweep = 0;
     c->collected = 0;
     fill_kernel_bytes(c);
@@ -1568,26 +1578,22 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
 sbmf_ctx::~sbmf_ctx() {
     vbo_destroy(vb);
     fmm_destroy(fm);
-    if (h_pinned) (void)hipHostFree(h_pinned);
-    if (h_pre) (void)hipHostFree(h_pre);
-    if (h_io) (void)hipHostFree(h_io);
-    for (auto& e : ev)
-        if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : kevs)
-        if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : sev)
-        if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : tsev)
-        if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : cev)
-        if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : oev)
-        if (e) (void)hipEventDestroy(e);
-    if (hev) (void)hipEventDestroy(hev);
-    if (sto) (void)hipStreamDestroy(sto);
-    if (sto2) (void)hipStreamDestroy(sto2);
-    if (stc) (void)hipStreamDestroy(stc);
-    if (st) (void)hipStreamDestroy(st);
+    using namespace sbmf;
+    pinned_free(h_pinned, h_pinned_bytes);
+    pinned_free(h_pre, h_pre_bytes);
+    pinned_free(h_io, h_io_bytes);
+    for (hipEvent_t& e : ev) event_destroy(e);
+    for (hipEvent_t& e : kevs) event_destroy(e);
+    for (hipEvent_t& e : sev) event_destroy(e);
+    for (hipEvent_t& e : tsev) event_destroy(e);
+    for (hipEvent_t& e : cev) event_destroy(e);
+    for (hipEvent_t& e : oev) event_destroy(e);
+    event_destroy(hev);
+    stream_destroy(sto);
+    stream_destroy(sto2);
+    stream_destroy(stc);
+    stream_destroy(st);
+    audit().contexts--;
 }
 
 namespace sbmf {
@@ -1623,8 +1629,16 @@ void rccl_selftest(sbmf_ctx* c, uint64_t nbytes, uint32_t reps, double deadline_
     HIPCHK(hipMemcpy(snd.p, pb.data(), n, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ags.p, pc.data(), nag, hipMemcpyHostToDevice));
     HIPCHK(hipDeviceSynchronize());
-    hipEvent_t e[4];
-    for (hipEvent_t& x : e) HIPCHK(hipEventCreate(&x));
+    struct Events {  // destroyed on every path but a timeout (below)
+        hipEvent_t e[4] = {};
+        bool keep = false;
+        ~Events() {
+            if (!keep)
+                for (hipEvent_t& x : e) event_destroy(x);
+        }
+    } evs;
+    hipEvent_t* e = evs.e;
+    for (int x = 0; x < 4; ++x) event_create(&e[x]);
     // three adjacent blocks of blk; the p2p segments [0, n/2) -> [n/2, n) and [n/2, n) -> [0, n/2)
     const std::vector<uint64_t> b0{0}, b1{n / 3}, b2{2 * (n / 3)}, b3{n};
     const std::vector<size_t> soff{0}, scnt{n / 2}, roff{n / 2}, rcnt{n / 2};
@@ -1650,8 +1664,17 @@ void rccl_selftest(sbmf_ctx* c, uint64_t nbytes, uint32_t reps, double deadline_
         const hipError_t q = hipEventQuery(e[3]);
         if (q == hipSuccess) break;
         if (q != hipErrorNotReady) fail(SBMF_E_COMM, "RCCL self-test: %s", hipGetErrorString(q));
-        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > deadline_s)
-            fail(SBMF_E_COMM, "RCCL self-test: the comm stream did not finish within %.1f s", deadline_s);
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > deadline_s) {
+            // RCCL work is still queued on stc: abort the communicator instead of
+            // destroying it, and leave the buffers and events in place (freeing them
+            // would wait on the stuck stream); the context is dead from here on
+            loop.abort();
+            evs.keep = true;
+            for (DBuf* b : {&blk, &snd, &rcv, &ags, &agr}) b->leak();
+            c->dead = true;
+            fail(SBMF_E_COMM, "RCCL self-test: the comm stream did not finish within %.1f s (communicator aborted, "
+                              "context unusable)", deadline_s);
+        }
         std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
     HIPCHK(hipEventSynchronize(e[1]));
@@ -1662,7 +1685,6 @@ void rccl_selftest(sbmf_ctx* c, uint64_t nbytes, uint32_t reps, double deadline_
     out->ms_rccl = f;
     HIPCHK(hipEventElapsedTime(&f, e[0], e[3]));
     out->ms_rccl_end = f;
-    for (hipEvent_t x : e) (void)hipEventDestroy(x);
     std::vector<uint8_t> h(n);
     HIPCHK(hipMemcpy(h.data(), blk.p, n, hipMemcpyDeviceToHost));
     for (size_t x = 0; x < n; ++x) out->bad_bcast += h[x] != pa[x];
@@ -1793,20 +1815,20 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     c->lo = cfg->clamp_lo >= 0 ? cfg->clamp_lo : (q2 ? 0.5 : 1.0);
     c->hi = cfg->clamp_hi;
     c->sd_is_var = cfg->quirks == SBMF_QUIRKS_NONE ? 0 : 1;
-    HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->stc, hipStreamNonBlocking));
-    for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
-    for (auto& e : c->cev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(hipStreamCreateWithFlags(&c->sto, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->sto2, hipStreamNonBlocking));
-    for (auto& e : c->oev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->hev, hipEventDisableTiming));
+    sbmf::stream_create(&c->st);
+    sbmf::stream_create(&c->stc);
+    for (auto& e : c->ev) sbmf::event_create(&e);
+    for (auto& e : c->cev) sbmf::event_create(&e, hipEventDisableTiming);
+    sbmf::stream_create(&c->sto);
+    sbmf::stream_create(&c->sto2);
+    for (auto& e : c->oev) sbmf::event_create(&e, hipEventDisableTiming);
+    sbmf::event_create(&c->hev, hipEventDisableTiming);
     *out = c.release();
     API_END(ctx)
 }
 
 void sbmf_destroy(sbmf_ctx* ctx) {
-    if (!ctx) return;
+    if (!ctx || ctx->dead) return;  // dead: work may still be queued (see sbmf_ctx::dead); leaked
     (void)hipSetDevice(ctx->cfg.device);
     (void)hipStreamSynchronize(ctx->st);
     delete ctx;
@@ -1912,6 +1934,9 @@ int sbmf_prepare(sbmf_ctx* ctx) {
 int sbmf_run(sbmf_ctx* ctx, uint32_t sweeps, sbmf_sweep_cb cb, void* user) {
     API_BEGIN
     if (!ctx) sbmf::fail(SBMF_E_ARG, "null context");
+    if (ctx->spent || ctx->dead)
+        sbmf::fail(SBMF_E_STATE, "sbmf_test_rccl_selftest ran extra item halves on this context: its chain is no "
+                                 "longer the sampler's; create a new context");
     HIPCHK(hipSetDevice(ctx->cfg.device));
     if (!ctx->prepared && ctx->cfg.method == SBMF_METHOD_VB) {
         if (ctx->tu.empty()) sbmf::fail(SBMF_E_STATE, "no training data (sbmf_set_train)");
@@ -2136,10 +2161,37 @@ int sbmf_test_rccl_selftest(sbmf_ctx* ctx, uint64_t nbytes, uint32_t reps, doubl
     if (!ctx->prepared || ctx->nranks != 1 || ctx->cfg.method != SBMF_METHOD_MCMC)
         sbmf::fail(SBMF_E_STATE, "the RCCL self-test needs a prepared one-rank sampler context");
     if (nbytes < 64 || nbytes % 64 || reps == 0) sbmf::fail(SBMF_E_ARG, "nbytes a positive multiple of 64, reps >= 1");
+    if (ctx->spent || ctx->dead) sbmf::fail(SBMF_E_STATE, "the RCCL self-test already ran on this context");
+    ctx->spent = true;  // from the first extra half on, the chain is not the sampler's
     if (ctx->cfg.precision == SBMF_F32)
         sbmf::rccl_selftest<float>(ctx, nbytes, reps, deadline_s, out);
     else
         sbmf::rccl_selftest<double>(ctx, nbytes, reps, deadline_s, out);
+    API_END(ctx)
+}
+
+int sbmf_test_device_usage(int device, sbmf_device_usage* out) {
+    sbmf_ctx* ctx = nullptr;
+    API_BEGIN
+    if (!out) sbmf::fail(SBMF_E_ARG, "null argument");
+    *out = sbmf_device_usage{};
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        sbmf::fail(SBMF_E_DEVICE, "no HIP device %d", device);
+    HIPCHK(hipSetDevice(device));
+    size_t fr = 0, tot = 0;
+    HIPCHK(hipMemGetInfo(&fr, &tot));
+    out->device_free = fr;
+    out->device_total = tot;
+    const sbmf::Audit& a = sbmf::audit();
+    out->dev_bytes = a.dev_bytes.load();
+    out->dev_allocs = a.dev_allocs.load();
+    out->pinned_bytes = a.pinned_bytes.load();
+    out->pinned_allocs = a.pinned_allocs.load();
+    out->streams = a.streams.load();
+    out->events = a.events.load();
+    out->contexts = a.contexts.load();
+    out->comms = a.comms.load();
     API_END(ctx)
 }
 

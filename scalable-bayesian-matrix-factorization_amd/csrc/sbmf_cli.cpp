@@ -122,15 +122,35 @@ bool looks_libfm(const std::string& path) {
 
 bool exists(const std::string& f) { return std::ifstream(f).good(); }
 
-// Data::load (Data.h:113-117) takes the binary pair <stem>.data/.target or
-// <stem>.x/.y when it exists, before the text file itself
-bool has_binary(const std::string& stem) {
-    return (exists(stem + ".data") && exists(stem + ".target")) || (exists(stem + ".x") && exists(stem + ".y"));
+// Data::load (Data.h:112-117) takes <stem>.data/.datat/.target or <stem>.x/.xt/.y,
+// each orientation only when the data set needs it, before the text file itself.
+// bin/libFM's sets (libfm.cpp:132-149): -method mcmc and als (rewritten to mcmc
+// first) have no row-major data, has_x = 0, so they read only the transpose
+// (.xt / .datat, tools/transpose.cpp); the other methods need both files.
+bool has_binary(const std::string& stem, bool has_x) { return sbmf_libfm_binary_kind(stem.c_str(), has_x, 1) > 0; }
+
+// The row-major pair alone (.x/.y, .data/.target: tools/convert.cpp's output), with
+// no transpose beside it and no text file of that name: libFM would fail to open
+// <stem>; sbmf reads the pair (an extension, noted on stderr).
+bool rowmajor_only(const std::string& stem) {
+    return !exists(stem) && ((exists(stem + ".x") && exists(stem + ".y")) ||
+                             (exists(stem + ".data") && exists(stem + ".target")));
 }
 
-void load(const std::string& path, const std::string& fmt, uint32_t item_offset, sbmf_ratings& r) {
+void load(const std::string& path, const std::string& fmt, uint32_t item_offset, bool has_x, sbmf_ratings& r) {
     int rc;
-    if (fmt == "binary" || (fmt == "auto" && has_binary(path))) {
+    if (fmt == "binary" || (fmt == "auto" && has_binary(path, has_x))) {
+        if (has_binary(path, has_x)) {
+            rc = sbmf_load_libfm_data(path.c_str(), has_x, 1, item_offset, &r);
+        } else if (rowmajor_only(path) || fmt == "binary") {
+            rc = sbmf_load_libfm_binary(path.c_str(), item_offset, &r);
+        } else {
+            rc = sbmf_load_libfm(path.c_str(), item_offset, &r);
+        }
+    } else if (fmt == "auto" && rowmajor_only(path)) {
+        std::cerr << "note: " << path << ": no " << (has_x ? "" : "transpose (.xt/.datat) or ")
+                  << "text file of that name (bin/libFM would stop here); reading the row-major binary pair"
+                  << std::endl;
         rc = sbmf_load_libfm_binary(path.c_str(), item_offset, &r);
     } else {
         const bool libfm = fmt == "libfm" || (fmt == "auto" && looks_libfm(path));
@@ -348,7 +368,9 @@ int main(int argc, char** argv) {
         cl.reg("burnin", "burn-in sweeps before collection; default=0");
         cl.reg("average", "running-mean divisor: default (quirk set) | collected (collected sweeps only) | "
                           "reference (sweep + 1, counts burn-in as gibbs_sbpmf_final.cpp:559 does)");
-        cl.reg("format", "auto (default: <name>.x/.y binary if present, else triple or libfm text) | triple | libfm | binary");
+        cl.reg("format", "auto (default: libFM's binary files if present -- <name>.xt/.y or .datat/.target for "
+                          "-method mcmc|als, <name>.x/.xt/.y or .data/.datat/.target for vb (Data.h:112-117) --, else "
+                          "triple or libfm text) | triple | libfm | binary");
         cl.reg("item_offset", "libFM input: item feature id offset; default: libFM's num_user (max user feature "
                               "id + 1, libfm.cpp:375) for -method mcmc (libFM order) / als / vb, 0 for -order sbpmf");
         cl.reg("device", "HIP device ordinal; default=0");
@@ -372,8 +394,11 @@ int main(int argc, char** argv) {
         // bin/libFM -method mcmc runs fm_learn_mcmc on libFM data (libfm.cpp:411-419); the SBPMF
         // sampler reads the triple files of gibbs_sbpmf_final.cpp:43
         const std::string trainf = cl.get("train", "");
+        // the MCMC and ALS sets carry no row-major data (libfm.cpp:140-149): they read the transpose
+        const bool has_x = vb;
         const bool libfm_input = fmt == "libfm" || fmt == "binary" ||
-                                 (fmt == "auto" && (has_binary(trainf) || looks_libfm(trainf)));
+                                 (fmt == "auto" && (has_binary(trainf, has_x) || rowmajor_only(trainf) ||
+                                                    looks_libfm(trainf)));
         const std::string order = cl.get("order", libfm_input ? "libfm" : "sbpmf");
         if (order != "sbpmf" && order != "libfm") throw std::runtime_error("unknown -order " + order);
         const bool als = method == "als";
@@ -453,9 +478,9 @@ int main(int argc, char** argv) {
         uint32_t off = (uint32_t)cl.getl("item_offset", 0);
         std::cout << "Loading train...\t" << std::endl;
         sbmf_ratings tr{}, te{};
-        load(cl.get("train", ""), fmt, off, tr);
+        load(cl.get("train", ""), fmt, off, has_x, tr);
         std::cout << "Loading test... \t" << std::endl;
-        load(cl.get("test", ""), fmt, off, te);
+        load(cl.get("test", ""), fmt, off, has_x, te);
         // libFM's learners (fm_learn_mcmc, fm_learn_vb_online) take the file's feature ids as
         // their attribute ids: num_user = max first feature id + 1 over train and test
         // (libfm.cpp:219-221,263-265,375) and num_all_attribute = max feature id + 1 (:328).

@@ -112,11 +112,9 @@ struct VBLearner {
 
     ~VBLearner() {
         if (worker.joinable()) worker.join();
-        for (auto& e : ev)
-            if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : {uev[0], uev[1], done[0], done[1]})
-            if (e) (void)hipEventDestroy(e);
-        if (ust) (void)hipStreamDestroy(ust);
+        for (auto& e : ev) event_destroy(e);
+        for (hipEvent_t* e : {&uev[0], &uev[1], &done[0], &done[1]}) event_destroy(*e);
+        stream_destroy(ust);
     }
 
     void init(const sbmf_config& c, uint64_t n, const uint32_t* u, const uint32_t* i, const double* r, uint64_t nt,
@@ -278,12 +276,12 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     tb.I = I;
     shuffle.resize(N);
     for (uint32_t x = 0; x < N; ++x) shuffle[x] = x + 1;
-    for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    for (auto& e : ev) event_create(&e);
     HIPCHK(hipGetDevice(&dev));
-    HIPCHK(hipStreamCreateWithFlags(&ust, hipStreamNonBlocking));
+    stream_create(&ust);
     for (int k = 0; k < 2; ++k) {
-        HIPCHK(hipEventCreateWithFlags(&uev[k], hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
+        event_create(&uev[k], hipEventDisableTiming);
+        event_create(&done[k], hipEventDisableTiming);
         HIPCHK(hipEventRecord(done[k], st));
     }
     HIPCHK(hipStreamSynchronize(st));

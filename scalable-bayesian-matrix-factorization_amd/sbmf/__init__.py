@@ -23,7 +23,7 @@ from . import _lib
 from ._lib import (F32, F64, METHOD_ALS, METHOD_LIBFM_MCMC, METHOD_MCMC, METHOD_VB, QUIRKS_BIAS2, QUIRKS_BIAS22, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
                    SBMF_E_COMM, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_NOMEM, SBMF_E_STATE, SBMF_OK)
 
-__all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "load_libfm_binary", "save_libfm_binary", "save_triples", "config_default",
+__all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "load_libfm_binary", "save_libfm_binary", "libfm_binary_kind", "device_usage", "save_triples", "config_default",
            "RNG_REFERENCE", "RNG_PHILOX", "QUIRKS_FINAL", "QUIRKS_SBPMF2", "QUIRKS_NONE",
            "QUIRKS_BIAS2", "QUIRKS_BIAS22", "F64", "F32"]
 
@@ -94,11 +94,14 @@ def load_triples(path):
         lib.sbmf_free_ratings(C.byref(r))
 
 
-def load_libfm_binary(stem, item_offset=0):
+def load_libfm_binary(stem, item_offset=0, transpose=False):
     """libFM binary <stem>.x/.y (or .data/.target), Data.h:113-160; one user and
-    one item feature per row."""
+    one item feature per row.  transpose=True reads the feature-major
+    <stem>.xt/.y (or .datat/.target) that tools/transpose.cpp writes and
+    bin/libFM -method mcmc|als loads (libfm.cpp:140-149)."""
     r = _lib.Ratings()
-    rc = lib.sbmf_load_libfm_binary(str(stem).encode(), item_offset, C.byref(r))
+    fn = lib.sbmf_load_libfm_binary_t if transpose else lib.sbmf_load_libfm_binary
+    rc = fn(str(stem).encode(), item_offset, C.byref(r))
     if rc != SBMF_OK:
         raise SBMFError(rc, lib.sbmf_loader_error().decode())
     try:
@@ -107,8 +110,18 @@ def load_libfm_binary(stem, item_offset=0):
         lib.sbmf_free_ratings(C.byref(r))
 
 
-def save_libfm_binary(stem, data, item_offset=0, num_cols=0):
-    """Write <stem>.x / <stem>.y as tools/convert.cpp does for rating data."""
+def libfm_binary_kind(stem, has_x, has_xt):
+    """Data::load's file choice (Data.h:112-117): 1 = .data/.datat/.target,
+    2 = .x/.xt/.y, 0 = none (libFM text)."""
+    rc = lib.sbmf_libfm_binary_kind(str(stem).encode(), int(has_x), int(has_xt))
+    if rc < 0:
+        raise SBMFError(rc, "has_x or has_xt must be set")
+    return rc
+
+
+def save_libfm_binary(stem, data, item_offset=0, num_cols=0, transpose=False):
+    """Write <stem>.x / <stem>.y as tools/convert.cpp does for rating data
+    (transpose=True: <stem>.xt / <stem>.y, convert then tools/transpose.cpp)."""
     u, i = _u32(data.user), _u32(data.item)  # refuses negative / >= 2^32 ids before the cast
     # the .x format holds feature ids (user, item_offset + item) as uint32 with num_cols = max + 1
     if len(u) and (int(u.max()) > 0xfffffffe or int(i.max()) + int(item_offset) > 0xfffffffe):
@@ -119,7 +132,8 @@ def save_libfm_binary(stem, data, item_offset=0, num_cols=0):
     r.user = u.ctypes.data_as(C.POINTER(C.c_uint32))
     r.item = i.ctypes.data_as(C.POINTER(C.c_uint32))
     r.rating = v.ctypes.data_as(C.POINTER(C.c_double))
-    rc = lib.sbmf_save_libfm_binary(str(stem).encode(), C.byref(r), item_offset, num_cols)
+    fn = lib.sbmf_save_libfm_binary_t if transpose else lib.sbmf_save_libfm_binary
+    rc = fn(str(stem).encode(), C.byref(r), item_offset, num_cols)
     if rc != SBMF_OK:
         raise SBMFError(rc, lib.sbmf_loader_error().decode())
 
@@ -352,6 +366,16 @@ class FMLearnVBOnline(FMLearnSBPMF):
     def __init__(self, num_factor=8, num_iter=100, seed=1, rng="ref", device=0, vb_batches=0, **kw):
         super().__init__(num_factor=num_factor, num_iter=num_iter, seed=seed, rng=rng, device=device, method="vb",
                          vb_batches=vb_batches, **kw)
+
+
+def device_usage(device=0):
+    """sbmf_test_device_usage: hipMemGetInfo plus the library's live device / pinned
+    buffers, streams, events, contexts and RCCL communicators (a dict)."""
+    u = _lib.DeviceUsage()
+    rc = lib.sbmf_test_device_usage(device, C.byref(u))
+    if rc != SBMF_OK:
+        raise SBMFError(rc, lib.sbmf_last_global_error().decode())
+    return {f: getattr(u, f) for f, _ in u._fields_}
 
 
 def comm_unique_id():

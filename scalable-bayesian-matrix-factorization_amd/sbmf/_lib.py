@@ -73,6 +73,15 @@ class RcclSelftest(C.Structure):
     ]
 
 
+class DeviceUsage(C.Structure):
+    _fields_ = [
+        ("device_free", C.c_uint64), ("device_total", C.c_uint64),
+        ("dev_bytes", C.c_int64), ("dev_allocs", C.c_int64), ("pinned_bytes", C.c_int64),
+        ("pinned_allocs", C.c_int64), ("streams", C.c_int64), ("events", C.c_int64),
+        ("contexts", C.c_int64), ("comms", C.c_int64),
+    ]
+
+
 SIGNATURES = {
     "sbmf_config_default": (C.c_int, [C.POINTER(Config)]),
     "sbmf_create": (C.c_int, [C.POINTER(Config), C.POINTER(C.c_void_p)]),
@@ -99,6 +108,10 @@ SIGNATURES = {
     "sbmf_load_libfm": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(Ratings)]),
     "sbmf_load_libfm_binary": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(Ratings)]),
     "sbmf_save_libfm_binary": (C.c_int, [C.c_char_p, C.POINTER(Ratings), C.c_uint32, C.c_uint32]),
+    "sbmf_load_libfm_binary_t": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(Ratings)]),
+    "sbmf_save_libfm_binary_t": (C.c_int, [C.c_char_p, C.POINTER(Ratings), C.c_uint32, C.c_uint32]),
+    "sbmf_libfm_binary_kind": (C.c_int, [C.c_char_p, C.c_int, C.c_int]),
+    "sbmf_load_libfm_data": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.POINTER(Ratings)]),
     "sbmf_save_triples": (C.c_int, [C.c_char_p, C.POINTER(Ratings)]),
     "sbmf_free_ratings": (None, [C.POINTER(Ratings)]),
     "sbmf_partition_rows": (C.c_int, [_P_U32, C.c_uint32, C.c_int, C.POINTER(C.c_uint64)]),
@@ -107,6 +120,7 @@ SIGNATURES = {
     "sbmf_test_virtual_rank": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "sbmf_test_stage_ms": (C.c_int, [C.c_void_p, _P_F64, C.c_uint32, C.POINTER(C.c_uint32)]),
     "sbmf_test_rccl_selftest": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_double, C.POINTER(RcclSelftest)]),
+    "sbmf_test_device_usage": (C.c_int, [C.c_int, C.POINTER(DeviceUsage)]),
 }
 
 

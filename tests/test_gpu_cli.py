@@ -220,6 +220,38 @@ def test_cli_is_bin_libfm_on_the_reference_files(tmp_path, method):
     assert rm == [l.split("Test=")[1] for l in gold_lines]
 
 
+@pytest.mark.parametrize("method", ["mcmc", "als"])
+def test_cli_reads_the_transpose_as_bin_libfm_does(tmp_path, method):
+    """A reference user who ran tools/convert then tools/transpose and points -train / -test at
+    the stem: bin/libFM -method mcmc|als builds its sets with has_x = false (libfm.cpp:132-149),
+    so Data::load opens <stem>.xt + <stem>.y (Data.h:113-117,143-151).  The directory holds
+    only those files (the reference tools' own output on data/m1m/m100k, compiled from source:
+    `make_golden.py bindata`); the argv is bin/libFM's, nothing added.  The "#Iter" lines equal
+    as text the compiled libfm.cpp's on the same files (time() pinned to 1), -out within
+    libFM's printed digits, test_rmse_118_mcmc equal."""
+    import gzip
+    for nm in ("train_libfm", "test_libfm"):
+        for ext in ("xt", "y"):
+            with gzip.open(os.path.join(REPO, "tests", "golden", "m1m100k_%s.%s.gz" % (nm, ext)), "rb") as f:
+                (tmp_path / ("%s.%s" % (nm, ext))).write_bytes(f.read())
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["test_libfm.xt", "test_libfm.y", "train_libfm.xt",
+                                                          "train_libfm.y"]
+    cmd = [CLI_PATH, "-task", "r", "-train", "train_libfm", "-test", "test_libfm", "-dim", "1,1,8", "-iter", "10",
+           "-method", method, "-out", "pred.txt"] + (["-regular", "0,0,10"] if method == "als" else [])
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    assert "#users=943\t#items=1682" in r.stdout
+    name = "ref_libfm_%s_m1m100k_xt_d118_s1_i10" % method
+    gold_lines = open(os.path.join(REPO, "tests", "golden", name + ".txt")).read().splitlines()
+    assert [l for l in r.stdout.splitlines() if l.startswith("#Iter")] == gold_lines
+    with gzip.open(os.path.join(REPO, "tests", "golden", name + "_pred.txt.gz"), "rt") as f:
+        ref_pred = np.array([float(x) for x in f.read().split()])
+    pred = np.loadtxt(tmp_path / "pred.txt")
+    ulp6 = 10.0 ** (np.floor(np.log10(np.abs(ref_pred))) - 5)
+    assert np.all(np.abs(pred - ref_pred) <= 0.5 * ulp6 * (1 + 1e-9) + 1e-12)
+    assert (tmp_path / "test_rmse_118_mcmc").read_text().split() == [l.split("Test=")[1] for l in gold_lines]
+
+
 def test_cli_sbpmf_order_on_the_reference_libfm_file(tmp_path):
     """`-order sbpmf` on the same libFM file is gibbs_sbpmf_final on the reference's converted
     data/m1m/m100k/{train,test}_sbpmf (create_file_scalable_bpmf.py keeps the raw item ids,
