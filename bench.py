@@ -121,17 +121,17 @@ def device_sync():
         raise RuntimeError("hipDeviceSynchronize failed: %d" % rc)
 
 
-def make_learner(args, world, rank, local, precision, uid):
+def make_learner(args, world, rank, local, precision, comm):
     from sbmf import Data, FMLearnSBPMF
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=precision, device=local,
                      quirks=args.quirks, recompute_every=0, eval_train=False, tune=args.tune,
                      split_chunk=args.split_chunk, stream_threshold=args.stream_threshold)
-    L.init(comm=(world, rank, uid) if world > 1 else None)
+    L.init(comm=comm)
     return L, Data
 
 
-def measure(args, world, rank, local, precision, train, test, uid):
-    L, Data = make_learner(args, world, rank, local, precision, uid)
+def measure(args, world, rank, local, precision, train, test, comm):
+    L, Data = make_learner(args, world, rank, local, precision, comm)
     t0 = time.time()
     L.set_data(Data(*train), Data(*test))
     prep_s = time.time() - t0
@@ -168,7 +168,29 @@ def measure(args, world, rank, local, precision, train, test, uid):
     return res
 
 
-def time_to_rmse(args, world, rank, local, train, test, uid, burnin, quirks="final", target=0.85, max_sweeps=200):
+def standalone_kinds(args, local, train, test, reps=3):
+    """Every launch kind's device time ALONE: the serial schedule (tune bit 29: a half's
+    launches one after the other on one stream, nothing beside them), the kinds timed with
+    HIP events on the first sweep of each run.  The default schedule overlaps a half's
+    launches, so its per-kind windows include the time a kind waits for CU slots beside
+    the persistent streaming launch; these are the rates the bins quote."""
+    from sbmf import Data, FMLearnSBPMF
+    from sbmf._lib import NKIND
+    L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=args.precision, device=local,
+                     quirks=args.quirks, recompute_every=0, eval_train=False, tune=args.tune | (1 << 29),
+                     split_chunk=args.split_chunk, stream_threshold=args.stream_threshold)
+    L.set_data(Data(*train), Data(*test))
+    L.learn(sweeps=1)
+    acc = np.zeros((2, NKIND))
+    for _ in range(reps):
+        L.learn(sweeps=1)  # a run's first sweep times every kind
+        t = L.timing()
+        acc += np.array([[t.kern_ms[s][k] for k in range(NKIND)] for s in range(2)])
+    L.close()
+    return acc / reps
+
+
+def time_to_rmse(args, world, rank, local, train, test, comm, burnin, quirks="final", target=0.85, max_sweeps=200):
     """Wall-clock from the end of data load to the first sweep whose running-mean
     test RMSE <= target, with the reference's averaging rule.
     Two clocks: `seconds` starts after set_data (host CSR/CSC build, task lists,
@@ -185,7 +207,7 @@ def time_to_rmse(args, world, rank, local, train, test, uid, burnin, quirks="fin
                      recompute_every=0, burnin=burnin, tune=args.tune,
                      split_chunk=args.split_chunk, stream_threshold=args.stream_threshold,
                      quirks=quirks, average="collected" if burnin else "reference")
-    L.init(comm=(world, rank, uid) if world > 1 else None)
+    L.init(comm=comm)
     barrier(world)
     tl = time.perf_counter()
     L.set_data(Data(*train), Data(*test))
@@ -294,6 +316,12 @@ RESTATEMENT_VS_REFERENCE = {
 }
 
 
+# the reference source each oracle quirk set restates (oracle/sbpmf_oracle.c)
+QUIRK_SOURCE = {"final": "gibbs_sbpmf_final.cpp", "sbpmf2": "src/libfm/gibbs_sbpmf2.cpp",
+                "none": "gibbs_sbpmf_final.cpp with sqrt(variance) as the stdev (no reference file)",
+                "bias2": "the top-level biased gibbs_sbpmf2.cpp", "bias22": "src/libfm/gibbs_sbpmf22.cpp"}
+
+
 def cpu_baseline(train, test, dims, K, seconds, quirks="final"):
     """The oracle (serial CPU restatement of gibbs_sbpmf_final.cpp -- or, quirks
     bias2, of the top-level biased gibbs_sbpmf2.cpp -- 1 thread) on a bounded
@@ -301,19 +329,27 @@ def cpu_baseline(train, test, dims, K, seconds, quirks="final"):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     n = len(train[0])
-    # ~0.46 M ratings/s for the reference on one core: size one sweep to ~`seconds`
-    take = int(min(n, max(100_000, 0.46e6 * seconds * 0.8)))
-    idx = np.random.default_rng(7).permutation(n)[:take]
-    sub = tuple(a[idx] for a in train)
     tsub = tuple(a[:1000] for a in test)
+    # one sweep of the FULL set when it fits ~`seconds` at the oracle's speed on one core (measured
+    # 1.24 M ratings/s at K=100 on the GPU box, r05; scaled by 100 / K): ML-20M K=100 is ~15 s.
+    # Larger sets: a random subsample sized to `seconds`, and the line says so.
+    est = 1.24e6 * 100.0 / max(K, 1)
+    take = n if n <= est * seconds else int(max(100_000, est * seconds))
+    if take < n:
+        idx = np.random.default_rng(7).permutation(n)[:take]
+        sub = tuple(a[idx] for a in train)
+    else:
+        sub = train
     r = oracle.run(sub, tsub, K=K, iters=1, seed=1, num_users=dims[0], num_items=dims[1], want_factors=False,
                    quirks=quirks)
-    src = "the top-level biased gibbs_sbpmf2.cpp" if quirks == "bias2" else "gibbs_sbpmf_final.cpp"
+    src = QUIRK_SOURCE.get(quirks, QUIRK_SOURCE["final"])
+    what = ("1 sweep of the full %d-rating set" % n if take == n else
+            "1 sweep on a random %d-rating subsample of the %d-rating set (all users and items kept; the rate "
+            "per rating is the measured one, not extrapolated to the full set)" % (take, n))
     out = {"value": take / r["seconds"], "unit": "ratings/s", "cores": 1, "kind": "port",
-           "sample": "oracle (serial C restatement of %s, glibc RNG, f64) for 1 sweep "
-                     "on a random %d-rating subsample of the same synthetic set (all %d users x %d "
-                     "items kept), K=%d, %.1f s" % (src, take, dims[0], dims[1], K, r["seconds"]),
-           "restatement_vs_reference": RESTATEMENT_VS_REFERENCE["bias2" if quirks == "bias2" else "final"]}
+           "sample": "oracle (serial C restatement of %s, glibc RNG, f64): %s, %d users x %d items, K=%d, %.1f s"
+                     % (src, what, dims[0], dims[1], K, r["seconds"]),
+           "restatement_vs_reference": RESTATEMENT_VS_REFERENCE.get(quirks)}
     if quirks != "final":
         return out
     # the same restatement, rows of each half in parallel
@@ -327,15 +363,17 @@ def cpu_baseline(train, test, dims, K, seconds, quirks="final"):
     return out
 
 
-def mk_uid(world, rank):
-    """A fresh RCCL unique id from rank 0, shared over the gloo bootstrap group."""
+def mk_comm(world, rank):
+    """The process's one communicator (sbmf_comm_create: ncclCommInitRank once), from a
+    fresh RCCL unique id made by rank 0 and shared over the gloo bootstrap group; every
+    learner of this process attaches to it in turn (sbmf_comm_attach)."""
     if world == 1:
         return None
     import torch.distributed as dist
-    from sbmf import comm_unique_id
+    from sbmf import Communicator, comm_unique_id
     obj = [comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
-    return obj[0]
+    return Communicator(world, rank, obj[0])
 
 
 def vb_main(args):
@@ -348,9 +386,9 @@ def vb_main(args):
     train, test, dims = synth.generate(args.shape)
     say("[bench vb] %d train ratings in %.0f s" % (len(train[0]), time.time() - t0))
     n_train = len(train[0])
-    uid = mk_uid(world, rank)
+    comm = mk_comm(world, rank)
     L = FMLearnVBOnline(num_factor=args.K, seed=2015, rng="philox", device=local)
-    L.init(comm=(world, rank, uid) if world > 1 else None)
+    L.init(comm=comm)
     t0 = time.time()
     L.set_data(Data(*train), Data(*test))
     prep_s = time.time() - t0
@@ -413,6 +451,8 @@ def vb_main(args):
                                "restatement_vs_reference": RESTATEMENT_VS_REFERENCE["vb"]}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
@@ -457,10 +497,10 @@ def libfm_main(args):
     train, test, dims = synth.generate(args.shape)
     n_train, n_test, K = len(train[0]), len(test[0]), args.K
     als = args.method == "als"
-    uid = mk_uid(world, rank)
+    comm = mk_comm(world, rank)
     L = FMLearnSBPMF(num_factor=K, seed=2015, rng="philox", method="als" if als else "mcmc", order="libfm",
                      regular=(0.0, 0.0, 10.0) if als else (0.0, 0.0, 0.0), init_stdev=0.1, device=local)
-    L.init(comm=(world, rank, uid) if world > 1 else None)
+    L.init(comm=comm)
     L.set_data(Data(*train), Data(*test))
     L.learn(sweeps=args.warmup)
     barrier(world)
@@ -506,6 +546,8 @@ def libfm_main(args):
         out["cpu_baseline"] = libfm_cpu_baseline(train, test, dims, K, als, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
@@ -531,16 +573,18 @@ def main():
     from sbmf import synth
     world, rank, local = dist_setup(args)
     from sbmf._lib import KIND_NAMES, NKIND
+    KIND_STREAM_IDX = list(KIND_NAMES).index("gres_stage")
     train, test, dims = synth.generate(args.shape)
-    main_res = measure(args, world, rank, local, args.precision, train, test, mk_uid(world, rank))
+    comm = mk_comm(world, rank)  # one communicator for every leg below
+    main_res = measure(args, world, rank, local, args.precision, train, test, comm)
     if args.quirks != "final":  # the extra legs (f32, time-to-RMSE, loads) belong to the headline sampler
         args.no_f32 = args.no_ttr = args.no_load = True
     f32 = None
     if not args.no_f32 and args.precision != "f32":
-        f32 = measure(args, world, rank, local, "f32", train, test, mk_uid(world, rank))
+        f32 = measure(args, world, rank, local, "f32", train, test, comm)
     # time to 0.85: the reference sampler (final) and the paper's biased SBMF-P model (bias2),
     # burn-in 0 and 50 each
-    ttr = [time_to_rmse(args, world, rank, local, train, test, mk_uid(world, rank), b, q)
+    ttr = [time_to_rmse(args, world, rank, local, train, test, comm, b, q)
            for q in ("final", "bias2") for b in (0, 50)] if not args.no_ttr else []
     loads = None if args.no_load else load_times(train, world, rank)
     n_train = len(train[0])
@@ -554,42 +598,57 @@ def main():
     s, k = np.unravel_index(np.argmax(main_res["kern_bytes"]), km.shape)
     achieved = main_res["kern_bytes"][s, k] / (km[s, k] * 1e-3) / 1e9
     kernel = "%s_half/%s" % ("user" if s == 0 else "item", KIND_NAMES[k])
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    # the PMC pass was taken on the default single-rank ML-20M K=100 f64 run: only that config quotes it
-    profiled = world == 1 and args.shape == "ml-20m" and args.K == 100 and args.quirks == "final"
-    if profiled and os.path.exists(pmc):
+    # HBM traffic and LDS bank conflicts of the dominant launch come from separate rocprofv3 --pmc
+    # passes (profiles/collect.sh fetch / write / lds, never in this run); the line names the file
+    # and the run they were taken in
+    traffic = traffic_src = None
+    lds = None
+    # the PMC passes were taken on the default single-rank ML-20M K=100 f64 line: only that config quotes them
+    profiled = world == 1 and args.shape == "ml-20m" and args.K == 100 and args.quirks == "final" and not args.tune
+    if profiled:
         try:
-            traffic = json.load(open(pmc)).get(kernel)
+            pm = json.load(open(os.path.join(REPO, "profiles", "pmc_traffic.json")))
+            traffic = pm.get(kernel)
+            traffic_src = "profiles/pmc_traffic.json (%s)" % pm.get("_run", "run not recorded")
         except Exception:
             traffic = None
-    # LDS bank-conflict share of the dominant kernel (profiles/pmc_lds.py, rocprofv3 --pmc pass)
-    lds_frac = None
-    pmc = os.path.join(REPO, "profiles", "pmc_lds.json")
-    if profiled and os.path.exists(pmc):
         try:
-            e = json.load(open(pmc)).get(kernel) or {}
-            bc, act = e.get("bank_conflict_cycles"), e.get("lds_active_cycles")
-            # share of the LDS pipe's cycles (issuing + conflict-stalled) lost to bank conflicts
-            lds_frac = bc / (bc + act) if bc is not None and act else None
+            pl = json.load(open(os.path.join(REPO, "profiles", "pmc_lds.json")))
+            e = pl.get(kernel) or {}
+            bc = e.get("bank_conflict_cycles")
+            if bc is not None:
+                # conflict cycles per CU-cycle of the launch (its live HIP-event time here, every CU
+                # at the 2.4 GHz engine clock): the share of the CU time the LDS pipe stalls
+                cu_cycles = km[s, k] * 1e-3 * 2.4e9 * 256
+                lds = {"conflict_cycles_per_launch": bc, "lds_issue_cycles_per_launch": e.get("lds_active_cycles"),
+                       "conflict_cycles_per_cu_cycle": bc / cu_cycles,
+                       "source": "profiles/pmc_lds.json (%s)" % pl.get("_run", "run not recorded")}
         except Exception:
-            lds_frac = None
+            lds = None
     # every launch kind of both halves against its own bound: algorithmic bytes (per
-    # launch) / HIP-event time; the user side gathers from the 24 MB V table (measured random-row
-    # gather ceiling 8.1 TB/s), the item side from the 124 MB U table (6.3 TB/s;
-    # profiles/r01_gather_ceiling.txt), both quoted as fractions of the 8 TB/s spec too
+    # launch) / its standalone device time (serial schedule, standalone_kinds); the user side gathers
+    # from the 24 MB V table (measured random-row gather ceiling 8.1 TB/s), the item side from the
+    # 124 MB U table (6.3 TB/s; profiles/r01_gather_ceiling.txt), both quoted as fractions of the
+    # 8 TB/s spec too.  The default schedule's per-kind windows are reported beside them, without a
+    # rate: a kind waiting for CU slots beside the persistent streaming launch spans that wait too.
+    solo = standalone_kinds(args, local, train, test) if world == 1 else None
     ceil = {0: 8100.0, 1: 6300.0}
     bins = {}
     for s_ in range(2):
         for k_ in range(NKIND):
             if km[s_, k_] <= 0:
                 continue
-            gbs = main_res["kern_bytes"][s_, k_] / (km[s_, k_] * 1e-3) / 1e9
-            bins[("user_" if s_ == 0 else "item_") + KIND_NAMES[k_]] = {
-                "ms": round(float(km[s_, k_]), 4), "rows": int(main_res["kern_rows"][s_, k_]),
-                "GB": round(float(main_res["kern_bytes"][s_, k_]) / 1e9, 4), "GB/s": round(float(gbs), 1),
-                "frac_peak": round(float(gbs / HBM_PEAK_GBS), 4),
-                "frac_gather_ceiling": round(float(gbs / ceil[s_]), 4)}
+            e = {"rows": int(main_res["kern_rows"][s_, k_]),
+                 "GB": round(float(main_res["kern_bytes"][s_, k_]) / 1e9, 4),
+                 "ms_default_window": round(float(km[s_, k_]), 4)}
+            if k_ != KIND_STREAM_IDX and not (args.tune & (1 << 29)):
+                e["overlapped"] = True  # the window shares the device: not a rate
+            if solo is not None and solo[s_, k_] > 0:
+                gbs = main_res["kern_bytes"][s_, k_] / (solo[s_, k_] * 1e-3) / 1e9
+                e.update({"ms_standalone": round(float(solo[s_, k_]), 4), "GB/s": round(float(gbs), 1),
+                          "frac_peak": round(float(gbs / HBM_PEAK_GBS), 4),
+                          "frac_gather_ceiling": round(float(gbs / ceil[s_]), 4)})
+            bins[("user_" if s_ == 0 else "item_") + KIND_NAMES[k_]] = e
     # several ranks on one device (SBMF_COMM=host or --device): a protocol rehearsal, not a scaling point
     one_device = world > 1 and (os.environ.get("SBMF_COMM") == "host" or args.device >= 0)
     out = {
@@ -618,16 +677,17 @@ def main():
                    "kernel_ms": {("user_" if s_ == 0 else "item_") + KIND_NAMES[k_]: round(float(km[s_, k_]), 4)
                                  for s_ in range(2) for k_ in range(NKIND) if km[s_, k_] > 0}},
         "roofline": {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "lds_bank_conflict_frac": lds_frac,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "lds_bank_conflicts": lds,
                      "bytes_per_launch": float(main_res["kern_bytes"][s, k]),
                      "rows_per_launch": int(main_res["kern_rows"][s, k]),
                      "ms_per_launch": float(km[s, k]),
                      "sweep_alg_GBs": main_res["bytes_alg"] / (main_res["seconds"] / args.steps) / 1e9,
                      "bins": bins,
-                     "bins_overlap": None if args.tune & (1 << 29) else
-                     "a half's Gram-block launches run on two side streams beside its streaming launch "
-                     "(and the item half's two streaming sets side by side unless tune bit 30): a bin's ms is "
-                     "its start-to-end time while it shares the device, so the bins of a half overlap",
+                     "bins_note": "rates from each kind's standalone device time (serial schedule, tune bit 29, "
+                     "measured in this run); ms_default_window is the kind's start-to-end span in the default "
+                     "schedule, where a half's Gram-block launches run on two side streams beside its "
+                     "streaming launch (overlapped: no rate)",
                      "bins_kernels": "bins are row-length classes; by default (f64) gblock_w16 (9-64 ratings) and "
                      "gblock_b4 (65-128) run k_grow<double,1>, gblock_b8 (129-256) k_grow<double,2>, "
                      "gblock_w4 (<= 8) k_gblock, gres_stage k_gres (DESIGN.md 3.1b); f32: k_grow for 17-512"},
@@ -639,6 +699,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(train, test, dims, args.K, args.cpu_seconds, args.quirks)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -137,6 +137,8 @@ typedef struct sbmf_config {
                                  bit 13 = f64 user streaming rows all on one 4-wave k_gres set
                                           (default: rows above 512 ratings on a second, 8-wave set),
                                  bit 14 = (experiment) that second user set on 16-wave workgroups,
+                                 bit 16 = k_gres claims from one task queue (default since round 6:
+                                          per-XCD queues, each split row on one XCD),
                                  bit 17 = k_gres on 16-wave workgroups (both sides),
                                  bit 23 = f64 user streaming rows all on 8-wave k_gres workgroups
                                           (default: up to 512 ratings on 4-wave ones, 512-rating
@@ -159,10 +161,13 @@ typedef struct sbmf_config {
                                  bit 28 = (one rank) the test evaluation after the next sweep's
                                           prologue kernels on the compute stream (default: on the
                                           second stream beside them; the results are the same).
-                                 Removed in round 4 with the variants they selected (measured
-                                 slower or neutral, kept in git history): bits 0, 5, 6, 16,
-                                 20-22, 31; they are ignored (bit 25 was the round-4 LDS-DMA
-                                 prefetch before its round-5 use above).  */
+                                 Every other bit is refused (SBMF_E_ARG): bits 0, 4-6, 15, 18-22
+                                 and 31 selected variants removed in rounds 1-5 (measured slower
+                                 or neutral, kept in git history).  Bits whose meaning changed
+                                 between rounds: 16 (round-4 ablation, now the
+                                 single queue), 24 (round 4: ordinary launch; since round 5 the
+                                 cooperative one), 25 (round-4 LDS-DMA prefetch; since round 5 one
+                                 side stream).  */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */
@@ -276,6 +281,16 @@ int sbmf_comm_unique_id(uint8_t id[128]);
 /* Join an nranks-wide communicator; users and items are then block-partitioned
  * (nnz-balanced) and U / V blocks are all-gathered between half-sweeps. */
 int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]);
+/* One communicator for the whole process, shared by several contexts in turn (a
+ * driver running many learners on the same ranks, e.g. bench.py's legs): RCCL's
+ * set-up (ncclCommInitRank) runs once.  sbmf_comm_attach joins a context to it
+ * in place of sbmf_comm_init (before sbmf_prepare); the communicator must
+ * outlive every context attached to it.  Contexts attached to one communicator
+ * must not run at the same time. */
+typedef struct sbmf_comm sbmf_comm;
+int sbmf_comm_create(int nranks, int rank, const uint8_t id[128], sbmf_comm** out);
+int sbmf_comm_attach(sbmf_ctx* ctx, sbmf_comm* comm);
+void sbmf_comm_destroy(sbmf_comm* comm);
 
 /* --- loaders (the reference's input formats) ------------------------------------------------ */
 typedef struct sbmf_ratings {

@@ -2,7 +2,7 @@
 """LDS bank-conflict share per launch of the hot kernels from a rocprofv3
 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS pass (profiles/collect.sh lds).
 
-usage: python profiles/pmc_lds.py <counter_collection.csv> [out.json]
+usage: python profiles/pmc_lds.py <counter_collection.csv> [out.json [run]]
 conflict_per_active = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS: the cycles the
 LDS pipe stalls on bank conflicts per cycle spent issuing LDS instructions,
 summed over every SIMD of the launch and averaged over the profiled sweeps;
@@ -49,6 +49,8 @@ def main():
         out[k] = {"bank_conflict_cycles": bc / n, "lds_active_cycles": act / n, "lds_insts": ins / n,
                   "conflict_per_active": bc / act if act else None,
                   "frac": bc / (bc + act) if bc + act else None}
+    if len(sys.argv) > 3:
+        out["_run"] = sys.argv[3]  # the gpurun step the pass came from (quoted by bench.py)
     s = json.dumps(out, indent=1)
     print(s)
     if len(sys.argv) > 2:

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """HBM/fabric traffic per launch of the hot kernels from rocprofv3 PMC passes.
 
-usage: python profiles/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> [out.json]
+usage: python profiles/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> [out.json [run]]
+(run: the tag of the gpurun step the passes came from, stored as "_run" and quoted by bench.py)
 
 Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE (kB) counts the L2's
 memory-side read requests and reports half the bytes of wide streaming reads
@@ -72,6 +73,8 @@ def main():
     res["_note"] = ("bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (kB x 1024), averaged over the profiled "
                     "sweeps; x2 per MI355X_MICROARCH.md gfx950 note, checked for these 8 B/lane gathers on "
                     "tests/hip/gather_bench (ratio 2.05, r02_pmc_gather_calibration.txt)")
+    if len(sys.argv) > 4:
+        res["_run"] = sys.argv[4]
     txt = json.dumps(res, indent=1, sort_keys=True)
     print(txt)
     if out_path:

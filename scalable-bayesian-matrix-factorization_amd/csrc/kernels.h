@@ -92,7 +92,17 @@ struct SplitSync {
     unsigned long long* prof;  // [8] phase cycles of wave 0 (SBMF_KPROF diagnostics) or null
     uint64_t lim_slab;   // doubles of `slabs` (CHECK=1 builds)
     uint32_t lim_chunk;  // entries of chunk_sq / chunk_tr (and rows of newown)
+    // Per-XCD task queues (nq = 9; nq = 0: the single queue at counters[ncounters]):
+    // queue q holds tasks [qoff[q], qoff[q+1]); queue 0 takes the rows too long to keep
+    // on one XCD, queue 1 + x the rest of XCD x's share.  A workgroup reads its XCD
+    // from HW_REG_XCC_ID and claims from queue 0, then its own XCD's, then the others'
+    // (x+1, x+2, ...), each through its head heads[16 q] (one 64-byte line per head).
+    uint32_t* heads;
+    const uint32_t* qoff;
+    uint32_t nq;
 };
+constexpr uint32_t XCD_QUEUES = 9;  // queue 0 + one per XCD
+constexpr uint32_t HEAD_STRIDE = 16;
 // Task capacity (ratings) of the streaming kernel k_gres for the variant `tune`:
 // 4 * waves * vectors-per-wave, the partner slices held in VGPRs.
 template <typename T>
@@ -103,9 +113,10 @@ int gstream_wg_target(uint32_t tune);
 template <typename T>
 int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune);
 // All streaming tasks of a half-sweep in one persistent launch of `grid`
-// (<= residency) workgroups.  Tasks are one list, claimed in order from a queue
-// head by whichever workgroup is free; a split row's chunks are consecutive, so
-// a chunk only waits for peers that the next free workgroups claim.  Split rows
+// (<= residency) workgroups.  Tasks are claimed in order from queue heads by
+// whichever workgroup is free (one queue, or per-XCD queues: SplitSync); a
+// split row's chunks are consecutive in its queue, so a chunk only waits for
+// peers that the next free workgroups claim.  Split rows
 // are then published by k_split_finish.  sy.counters[0..ncounters] must be zero
 // when the launch starts: sbmf.cpp clears every set's counters with one memset
 // per half, ahead of the half's launches.

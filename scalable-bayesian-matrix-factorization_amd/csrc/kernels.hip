@@ -742,8 +742,17 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
     auto eS = [&](uint32_t j) -> T& { return eL[j * JS + lb]; };
 
     // task order: a queue claimed in list order, one returning atomic per task,
-    // so a split row's chunks start as soon as enough workgroups are free
+    // so a split row's chunks start as soon as enough workgroups are free.  Per-XCD
+    // queues (sy.nq = 9, the default): the workgroup's XCD from HW_REG_XCC_ID (hwreg
+    // 20, bits 3:0; tests/hip/xcc_probe.hip), queue 0 first, then its own XCD's, then
+    // the other XCDs' in turn once its own is drained.  Only the head a workgroup
+    // claims from decides where a task runs: results never depend on it.  A split
+    // row's chunks sit consecutively in one queue, so each queue has at most one
+    // partly claimed row; the host caps the chunk counts so that all those rows'
+    // waiting chunks together stay below the resident workgroups (build_stream_tasks).
     __shared__ uint32_t qti;
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 7u;
+    uint32_t qdone = 0;  // thread 0: queues found drained
     // (the task loop in this form, also for the one-task LIST case: written as a task lambda
     // called once or in the loop, k_grow compiles to 50-70 spilled VGPRs instead of 1-2)
     for (uint32_t it = 0;; ++it) {
@@ -752,8 +761,29 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
             ti = blockIdx.x;
             if (it > 0 || ti >= ntask) break;
         } else {
-            if (threadIdx.x == 0)
-                qti = __hip_atomic_fetch_add(sy.counters + sy.ncounters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (threadIdx.x == 0) {
+                if (sy.nq == 0) {
+                    qti = __hip_atomic_fetch_add(sy.counters + sy.ncounters, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    uint32_t got = ntask;
+                    for (uint32_t i = 0; i < sy.nq; ++i) {
+                        const uint32_t q = i == 0 ? 0u : 1u + ((xcc + i - 1u) & 7u);
+                        if (qdone & (1u << q)) continue;
+                        const uint32_t b = sy.qoff[q], e = sy.qoff[q + 1];
+                        if (b < e) {
+                            const uint32_t k = __hip_atomic_fetch_add(sy.heads + HEAD_STRIDE * q, 1u, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT);
+                            if (k < e - b) {
+                                got = b + k;
+                                break;
+                            }
+                        }
+                        qdone |= 1u << q;
+                    }
+                    qti = got;
+                }
+            }
             __syncthreads();
             ti = qti;
             __syncthreads();  // every thread has its ticket before thread 0 claims the next

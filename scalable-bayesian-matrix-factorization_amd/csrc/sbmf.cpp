@@ -69,6 +69,7 @@ struct Side {
         uint32_t sgrid = 0;             // persistent grid of the launch
         uint32_t cmax = 0;              // task capacity (ratings)
         uint32_t tune = 0;              // kernel variant bits of the launch
+        std::vector<uint32_t> qoff;     // per-XCD queues: [XCD_QUEUES + 1] task bounds (empty: one queue)
     };
     // A stage: the rows [r0, r1) of this rank's block, binned for their own launches.
     // One stage per half unless the multi-GPU exchange is pipelined: then the block is
@@ -80,7 +81,7 @@ struct Side {
         std::vector<uint32_t> bin_rows[NBIN];  // kinds: GK_* (0..4), KIND_STREAM (5)
         StreamSet ss[2];
         std::vector<std::array<uint32_t, 3>> gsub[GK_NUM];  // multi-wave bins: (waves, offset, count) sub-ranges
-        DBuf d_bins[NBIN], d_stasks[2], d_xrows[2];
+        DBuf d_bins[NBIN], d_stasks[2], d_xrows[2], d_qoff[2];
         // multi-GPU residual exchange of this stage: [peer] segments of the send / receive areas
         std::vector<size_t> soff, scnt, roff, rcnt;
         size_t rbeg = 0, rend = 0;  // this stage's receive elements [rbeg, rend)
@@ -290,7 +291,8 @@ struct sbmf_ctx {
     GlibcRand grand{1};
     // multi-GPU
     int nranks = 1, rank = 0;
-    Comm comm;
+    Comm own_comm;            // this context's communicator (sbmf_comm_init) ...
+    Comm* comm = &own_comm;   // ... or a process-wide one it borrows (sbmf_comm_attach)
     // device
     hipStream_t st = nullptr;
     hipEvent_t ev[9] = {};
@@ -356,6 +358,7 @@ struct sbmf_ctx {
     bool hyper_ahead = false;
     double* h_pinned = nullptr;  // pinned staging for z streams
     size_t h_pinned_bytes = 0, h_pre_bytes = 0, h_io_bytes = 0;
+    size_t xheads_off = 0;  // d_xcnt: first per-XCD queue head (uint32 index)
     sbmf_timing timing{};
     VBLearner* vb = nullptr;  // -method vb (vbo.cpp)
     FMLearner* fm = nullptr;  // -method mcmc --order libfm / als (fmm.cpp)
@@ -405,7 +408,7 @@ static void ensure_pinned(sbmf_ctx* c, size_t bytes) {
 
 static void fill_kernel_bytes(sbmf_ctx* c);
 static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vector<uint32_t>& rows, uint32_t gres,
-                               uint32_t nblk);
+                               uint32_t nblk, uint32_t rmin, bool xcd);
 
 // ------------------------------------------------------------------ prepare
 template <typename T>
@@ -527,18 +530,28 @@ static void prepare_T(sbmf_ctx* c) {
                 const uint32_t d = sd->ptr[r + 1] - sd->ptr[r];
                 rows[(item16 && d > 1024u) || (user2 && d > 512u) ? 1 : 0].push_back(r);
             }
+            bool splits[2] = {false, false};  // the set has rows longer than one task
             for (int k = 0; k < 2; ++k) {
                 Side::StreamSet& S = gp->ss[k];
                 S.tune = stunes[k];
                 // task capacity: the kernel's on-chip maximum, or smaller if split_chunk asks
                 S.cmax = gstream_cmax<T>(S.tune);
                 if (cf.split_chunk) S.cmax = std::min(S.cmax, std::max(cf.split_chunk, 1u));
+                for (uint32_t r : rows[k]) splits[k] = splits[k] || sd->ptr[r + 1] - sd->ptr[r] > S.cmax;
+            }
+            for (int k = 0; k < 2; ++k) {
+                Side::StreamSet& S = gp->ss[k];
                 // (fewer persistent workgroups per CU, leaving CU slots to the Gram-block launches
                 // beside the streaming one from its start: user 3 / 2 per CU +0.03 / +0.13 ms, item
                 // 8-wave set 1 per CU +0.2 ms per sweep, r05s8)
                 const int per_cu =
                     std::max(1, std::min(gstream_wg_target(S.tune), gstream_blocks_per_cu<T>(S.cmax, S.tune)));
-                build_stream_tasks(*sd, S, rows[k], (uint32_t)(dev_cus * per_cu), nblk);
+                // per-XCD task queues (default; tune bit 16 keeps the single queue).  The residency
+                // every launch reaches: its workgroups on every CU (the two sets of a half run side
+                // by side: on half the CUs when the other set has split rows too, whose waiting
+                // chunks may hold the rest)
+                const uint32_t rmin = (uint32_t)(splits[1 - k] ? dev_cus / 2 : dev_cus) * (uint32_t)per_cu;
+                build_stream_tasks(*sd, S, rows[k], (uint32_t)(dev_cus * per_cu), nblk, rmin, !(cf.tune & 0x10000u));
             }
             }
         }
@@ -589,6 +602,7 @@ static void prepare_T(sbmf_ctx* c) {
                 const Side::StreamSet& S = g->ss[k];
                 upload(g->d_stasks[k], S.stasks, st);
                 upload(g->d_xrows[k], S.xrows, st);
+                upload(g->d_qoff[k], S.qoff, st);
                 nxk[k] = std::max<size_t>(nxk[k], S.nxchunk);
                 nrk[k] = std::max<size_t>(nrk[k], S.xrows.size());
             }
@@ -597,10 +611,12 @@ static void prepare_T(sbmf_ctx* c) {
     {
         const size_t nx = c->xset_nx + std::max<size_t>(nxk[1], 1), nr = c->xset_nr + std::max<size_t>(nrk[1], 1);
         c->d_xslabs.alloc(nx * nblk * (16 * 16 + 16) * sizeof(double));
-        // + each set's task-queue head; a whole number of 16-byte words, so that clearing it
-        // is one fill kernel (a ragged size is three, and on a stream beside a persistent
+        // + each set's task-queue head, then (from a 64-byte boundary) the two sets' per-XCD
+        // queue heads, one 64-byte line each; a whole number of 16-byte words, so that clearing
+        // it is one fill kernel (a ragged size is three, and on a stream beside a persistent
         // launch the tail one waited for that launch: r04s4 trace)
-        c->d_xcnt.alloc((nr * nblk + 2 + 3) / 4 * 4 * sizeof(uint32_t));
+        c->xheads_off = (nr * nblk + 2 + HEAD_STRIDE - 1) / HEAD_STRIDE * HEAD_STRIDE;
+        c->d_xcnt.alloc((c->xheads_off + 2 * XCD_QUEUES * HEAD_STRIDE) * sizeof(uint32_t));
         c->xcnt_clean = false;
         c->d_xchunk_sq.alloc(nx * sizeof(double));
         c->d_xchunk_tr.alloc(nx * sizeof(double));
@@ -758,16 +774,32 @@ static void prepare_T(sbmf_ctx* c) {
 // equal chunks of a longer row) in one list, largest rows first, claimed in
 // order by the running workgroups of a launch of `gres` workgroups (k_gres'
 // queue); a split row's chunks are consecutive.
+//
+// Per-XCD queues (xcd): the tasks go to XCD_QUEUES queues (SplitSync), each in
+// degree-descending order with a split row's chunks consecutive.  The rows are
+// dealt largest first to the XCD with the fewest ratings so far (a split row
+// whole to one XCD: its block hand-offs are claimed by one XCD's workgroups, the
+// dequeues spread over 8 heads instead of one -- MI355X_MICROARCH.md rows
+// dequeue, handoff-payload); queue 0, claimed first by every workgroup, takes the
+// rows of more than `cx` chunks.  Deadlock freedom: each queue has at most one
+// partly claimed split row, whose claimed chunks wait for its unclaimed ones; a
+// free workgroup always claims, so the launch can only stall if every workgroup
+// waits, which needs 8 (cx - 1) + (largest queue-0 row - 1) >= resident
+// workgroups.  `rmin` is a residency every launch reaches (prepare_T), and cx is
+// the largest count that keeps the sum below it (no split rows go to the XCD
+// queues when none does).
 static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vector<uint32_t>& rows, uint32_t gres,
-                               uint32_t nblk) {
+                               uint32_t nblk, uint32_t rmin, bool xcd) {
     const uint32_t cmax = S.cmax;
     S.stasks.clear();
     S.xrows.clear();
+    S.qoff.clear();
     S.nxchunk = 0;
     S.sgrid = 0;
-    for (uint32_t r : rows) {  // rows: degree-descending
+    auto nchunks = [&](uint32_t r) { return (s.ptr[r + 1] - s.ptr[r] + cmax - 1) / cmax; };
+    auto push_row = [&](uint32_t r) {
         const uint32_t n = s.ptr[r + 1] - s.ptr[r];
-        const uint32_t nch = (n + cmax - 1) / cmax;
+        const uint32_t nch = nchunks(r);
         if (nch > gres)
             fail(SBMF_E_ARG, "row %u has %u ratings: more than %u co-resident chunks of %u", r, n, gres, cmax);
         if (nch == 1) {
@@ -783,8 +815,61 @@ static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vec
             S.xrows.push_back(SplitRow{r, slab0, nch, 0});
             S.nxchunk += nch;
         }
+    };
+    if (!xcd || rows.empty()) {
+        for (uint32_t r : rows) push_row(r);  // rows: degree-descending
+        S.sgrid = std::min<uint32_t>(gres, (uint32_t)S.stasks.size());
+        return;
+    }
+    // the largest XCD-queue chunk count cx with 8 (cx - 1) + (max queue-0 chunks - 1) < rmin
+    std::vector<uint32_t> nchs;
+    for (uint32_t r : rows) nchs.push_back(nchunks(r));  // non-increasing (rows degree-descending)
+    const uint32_t top = nchs.empty() ? 1u : nchs[0];
+    uint32_t cx = 1;
+    for (uint32_t c = top; c >= 2; --c) {
+        uint32_t g0 = 0;  // largest chunk count left to queue 0
+        for (uint32_t x : nchs)
+            if (x > c) g0 = std::max(g0, x);
+        if (8ull * (c - 1) + (g0 ? g0 - 1 : 0) < rmin) {
+            cx = c;
+            break;
+        }
+    }
+    std::vector<std::vector<uint32_t>> q(XCD_QUEUES);
+    std::vector<uint64_t> load(XCD_QUEUES - 1, 0);
+    for (size_t i = 0; i < rows.size(); ++i) {
+        if (nchs[i] > cx) {
+            q[0].push_back(rows[i]);
+            continue;
+        }
+        const size_t x = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
+        load[x] += s.ptr[rows[i] + 1] - s.ptr[rows[i]];
+        q[1 + x].push_back(rows[i]);
+    }
+    S.qoff.push_back(0);
+    for (const auto& qq : q) {
+        for (uint32_t r : qq) push_row(r);
+        S.qoff.push_back((uint32_t)S.stasks.size());
     }
     S.sgrid = std::min<uint32_t>(gres, (uint32_t)S.stasks.size());
+    // the bound above assumed rmin resident workgroups; a smaller grid tightens it
+    if (S.sgrid < rmin) {
+        uint32_t wait = 0;  // the most claimed-and-waiting chunks the queues can hold at once
+        for (uint32_t k = 0; k < XCD_QUEUES; ++k) {
+            uint32_t m = 0;
+            for (uint32_t t = S.qoff[k]; t < S.qoff[k + 1]; ++t) m = std::max(m, S.stasks[t].nch);
+            wait += m ? m - 1 : 0;
+        }
+        if (wait >= S.sgrid) {  // one queue then: its one partly claimed row waits for < sgrid peers
+            std::vector<uint32_t> all(rows);
+            S.stasks.clear();
+            S.xrows.clear();
+            S.qoff.clear();
+            S.nxchunk = 0;
+            for (uint32_t r : all) push_row(r);
+            S.sgrid = std::min<uint32_t>(gres, (uint32_t)S.stasks.size());
+        }
+    }
 }
 
 // ------------------------------------------------------------------ one sweep
@@ -1087,6 +1172,9 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 sy.lim_slab = (uint64_t)(c->d_xslabs.bytes / sizeof(double)) - ox * sy.nblk * (16 * 16 + 16);
                 sy.lim_chunk = (uint32_t)(c->d_xchunk_sq.bytes / sizeof(double) - ox);
                 sy.prof = c->kprof && set == c->kprof_set ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
+                sy.nq = S.qoff.empty() ? 0u : XCD_QUEUES;
+                sy.qoff = g.d_qoff[set].as<uint32_t>();
+                sy.heads = c->d_xcnt.as<uint32_t>() + c->xheads_off + (size_t)set * XCD_QUEUES * HEAD_STRIDE;
                 HalfArgs<T> as = a;
                 as.tune = S.tune;
                 HIPCHK(launch_gstream<T>(g.d_stasks[set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
@@ -1167,11 +1255,11 @@ static void exchange_stage(sbmf_ctx* c, bool users, uint32_t p, hipStream_t st, 
         for (size_t& x : b) x *= sizeof(T);
         return b;
     };
-    c->comm.group_begin();
+    c->comm->group_begin();
     with(p);
-    c->comm.group_end();
+    c->comm->group_end();
     const size_t s0 = g.soff.empty() ? 0 : g.soff[0];
-    c->comm.alltoallv(E.as<T>() + c->tu.size() + s0, rel(g.soff, s0), bytes(g.scnt), c->d_xrecv.as<T>() + g.rbeg,
+    c->comm->alltoallv(E.as<T>() + c->tu.size() + s0, rel(g.soff, s0), bytes(g.scnt), c->d_xrecv.as<T>() + g.rbeg,
                       rel(g.roff, g.rbeg), bytes(g.rcnt), st);
     HIPCHK(launch_unpack<T>(c->d_xrecv.as<T>() + g.rbeg, (users ? c->d_uunpack : c->d_vunpack).as<uint32_t>() + g.rbeg,
                             g.rend - g.rbeg, E.as<T>(), st));
@@ -1188,7 +1276,7 @@ static void bcast_stage(sbmf_ctx* c, const Side& s, uint32_t p, void* base, size
         lo[k] = s.sbounds[k][p];
         hi[k] = s.sbounds[k][p + 1];
     }
-    c->comm.bcast_blocks(base, unit_bytes, lo, hi, c->stc);
+    c->comm->bcast_blocks(base, unit_bytes, lo, hi, c->stc);
 }
 // A half's stages, each followed -- on the comm stream, while the next stage
 // computes -- by its exchange; the compute stream then waits for the last one.
@@ -1244,7 +1332,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                                    c->Kp, c->d_Eu.as<T>(), c->d_rtsq.as<double>(), c->d_rowsq_v.as<double>(),
                                    c->bias ? c->d_bv.as<double>() : nullptr, c->d_bu.as<double>(), c->b0, st));
             c->timing.n_launch++;
-            if (c->nranks > 1) c->comm.bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
+            if (c->nranks > 1) c->comm->bcast_ranges(c->d_rowsq_v.p, sizeof(double), c->items.bounds, st);
             exchange_residuals<T>(c, false, st);
         }
         HIPCHK(launch_sum(c->d_rowsq_v.as<double>(), c->J, d_res + RES_ESQ, scratch, st));
@@ -1253,7 +1341,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         if (c->bias) {
             double* rs2 = c->d_epart.as<double>();
             HIPCHK(launch_rowsum2<T>(c->d_uptr.as<uint32_t>(), c->users.r0, c->users.r1, c->d_Eu.as<T>(), rs2, st));
-            if (c->nranks > 1) c->comm.bcast_ranges(rs2, 2 * sizeof(double), c->users.bounds, st);
+            if (c->nranks > 1) c->comm->bcast_ranges(rs2, 2 * sizeof(double), c->users.bounds, st);
             HIPCHK(launch_sum_cols(rs2, c->I, 2, d_res + RES_ES, st));
         }
         // ---- column statistics with the current mu (:378-381, :397-401)
@@ -1430,7 +1518,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                                       c->t1, c->d_U.as<T>(), c->d_V.as<T>(), K, c->Kp, (T)c->lo, (T)c->hi,
                                       collect ? 1 : 0, div, c->d_tsum.as<double>(), c->d_tpart.as<double>(),
                                       c->bias ? c->d_bu.as<double>() : nullptr, c->d_bv.as<double>(), c->b0, se));
-                if (c->nranks > 1) c->comm.bcast_ranges(c->d_tpart.p, 2 * sizeof(double), c->tbblocks, se);
+                if (c->nranks > 1) c->comm->bcast_ranges(c->d_tpart.p, 2 * sizeof(double), c->tbblocks, se);
                 const uint32_t nb = (uint32_t)((T_ + 255) / 256);
                 HIPCHK(launch_sum_cols(c->d_tpart.as<double>(), nb, 2, d_res + RES_TEST_AVG, se));
             }
@@ -1790,6 +1878,18 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     if ((cfg->method == SBMF_METHOD_LIBFM_MCMC || cfg->method == SBMF_METHOD_ALS) && cfg->precision != SBMF_F64)
         sbmf::fail(SBMF_E_ARG, "the libFM MCMC / ALS learner computes in f64 (the reference's double) only");
     if (cfg->libfm_dim > 3) sbmf::fail(SBMF_E_ARG, "bad libfm_dim (bit 0 = w0, bit 1 = w)");
+    {
+        // the tune bits with a meaning in this build (include/sbmf.h); a bit of a removed variant
+        // is refused, so a value saved for an older build does not silently pick something else
+        // (INTEGRATION.md lists what changed between rounds)
+        constexpr uint32_t known = (1u << 1) | (1u << 2) | (1u << 3) | (1u << 7) | (1u << 8) | (1u << 9) | (1u << 10) |
+                                   (1u << 11) | (1u << 12) | (1u << 13) | (1u << 14) | (1u << 16) | (1u << 17) |
+                                   (1u << 23) | (1u << 24) | (1u << 25) | (1u << 26) | (1u << 27) | (1u << 28) |
+                                   (1u << 29) | (1u << 30);
+        if (cfg->tune & ~known)
+            sbmf::fail(SBMF_E_ARG, "tune bits 0x%x have no meaning in this build (variants removed earlier; see "
+                                   "include/sbmf.h and INTEGRATION.md)", cfg->tune & ~known);
+    }
     if (cfg->gram_threshold || cfg->row_kernel)
         sbmf::fail(SBMF_E_ARG, "gram_threshold / row_kernel are reserved (must be 0): the per-coordinate and "
                                "full-Gram row kernels were removed (measured slower than the Gram-block kernels)");
@@ -1849,7 +1949,7 @@ static void prepare_vb(sbmf_ctx* c) {
     c->J = std::max(c->J_req, imax + 1);
     c->K = c->cfg.num_factor;
     c->vb = vbo_create(c->cfg, c->tu.size(), c->tu.data(), c->ti.data(), c->tr.data(), c->su.size(), c->su.data(),
-                       c->si.data(), c->sr.data(), c->I, c->J, c->st, c->nranks > 1 ? &c->comm : nullptr);
+                       c->si.data(), c->sr.data(), c->I, c->J, c->st, c->nranks > 1 ? c->comm : nullptr);
     c->prepared = true;
 }
 
@@ -1874,7 +1974,7 @@ static void prepare_fmm(sbmf_ctx* c) {
     c->J = std::max(c->J_req, imax + 1);
     c->K = c->cfg.num_factor;
     c->fm = fmm_create(c->cfg, c->tu.size(), c->tu.data(), c->ti.data(), c->tr.data(), c->su.size(), c->su.data(),
-                       c->si.data(), c->sr.data(), c->I, c->J, c->st, c->nranks > 1 ? &c->comm : nullptr);
+                       c->si.data(), c->sr.data(), c->I, c->J, c->st, c->nranks > 1 ? c->comm : nullptr);
     c->prepared = true;
 }
 
@@ -1986,7 +2086,7 @@ int sbmf_predict(sbmf_ctx* ctx, double* out) {
         return SBMF_OK;
     }
     const uint64_t T_ = ctx->su.size();
-    if (ctx->nranks > 1) ctx->comm.bcast_ranges(ctx->d_tsum.p, sizeof(double), ctx->tbounds, ctx->st);
+    if (ctx->nranks > 1) ctx->comm->bcast_ranges(ctx->d_tsum.p, sizeof(double), ctx->tbounds, ctx->st);
     HIPCHK(hipStreamSynchronize(ctx->st));
     std::vector<double> h(T_);
     HIPCHK(hipMemcpy(h.data(), ctx->d_tsum.p, T_ * sizeof(double), hipMemcpyDeviceToHost));
@@ -2119,9 +2219,44 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
     HIPCHK(hipSetDevice(ctx->cfg.device));
     ctx->nranks = nranks;
     ctx->rank = rank;
-    if (nranks > 1) ctx->comm.init(nranks, rank, id);
+    if (ctx->comm != &ctx->own_comm) sbmf::fail(SBMF_E_STATE, "context already attached to a communicator");
+    if (nranks > 1) ctx->comm->init(nranks, rank, id);
     API_END(ctx)
 }
+
+// one communicator per process, shared by every context of the process (bench.py's
+// legs): RCCL's set-up runs once, not once per learner
+struct sbmf_comm {
+    sbmf::Comm c;
+    int nranks = 1, rank = 0;
+};
+
+int sbmf_comm_create(int nranks, int rank, const uint8_t id[128], sbmf_comm** out) {
+    sbmf_ctx* ctx = nullptr;
+    API_BEGIN
+    if (!id || !out) sbmf::fail(SBMF_E_ARG, "null argument");
+    *out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks) sbmf::fail(SBMF_E_ARG, "bad rank %d / %d", rank, nranks);
+    std::unique_ptr<sbmf_comm> cm(new sbmf_comm());
+    cm->nranks = nranks;
+    cm->rank = rank;
+    if (nranks > 1) cm->c.init(nranks, rank, id);
+    *out = cm.release();
+    API_END(ctx)
+}
+
+int sbmf_comm_attach(sbmf_ctx* ctx, sbmf_comm* comm) {
+    API_BEGIN
+    if (!ctx || !comm) sbmf::fail(SBMF_E_ARG, "null argument");
+    if (ctx->prepared) sbmf::fail(SBMF_E_STATE, "sbmf_comm_attach must precede sbmf_prepare");
+    if (ctx->own_comm.active() || ctx->virt) sbmf::fail(SBMF_E_STATE, "context already joined a communicator");
+    ctx->nranks = comm->nranks;
+    ctx->rank = comm->rank;
+    ctx->comm = &comm->c;
+    API_END(ctx)
+}
+
+void sbmf_comm_destroy(sbmf_comm* comm) { delete comm; }
 
 int sbmf_test_virtual_rank(sbmf_ctx* ctx, int nranks, int rank) {
     API_BEGIN
@@ -2129,7 +2264,8 @@ int sbmf_test_virtual_rank(sbmf_ctx* ctx, int nranks, int rank) {
     if (ctx->prepared) sbmf::fail(SBMF_E_STATE, "sbmf_test_virtual_rank must precede sbmf_prepare");
     if (nranks < 2 || rank < 0 || rank >= nranks) sbmf::fail(SBMF_E_ARG, "bad rank %d / %d", rank, nranks);
     if (ctx->cfg.method != SBMF_METHOD_MCMC) sbmf::fail(SBMF_E_ARG, "virtual ranks: the SBPMF sampler only");
-    if (ctx->comm.active()) sbmf::fail(SBMF_E_STATE, "context already joined a communicator");
+    if (ctx->comm->active() || ctx->comm != &ctx->own_comm)
+        sbmf::fail(SBMF_E_STATE, "context already joined a communicator");
     ctx->nranks = nranks;
     ctx->rank = rank;
     ctx->virt = true;

@@ -23,7 +23,7 @@ from . import _lib
 from ._lib import (F32, F64, METHOD_ALS, METHOD_LIBFM_MCMC, METHOD_MCMC, METHOD_VB, QUIRKS_BIAS2, QUIRKS_BIAS22, QUIRKS_FINAL, QUIRKS_NONE, QUIRKS_SBPMF2, RNG_PHILOX, RNG_REFERENCE, SBMF_E_ARG,
                    SBMF_E_COMM, SBMF_E_DEVICE, SBMF_E_IO, SBMF_E_NOMEM, SBMF_E_STATE, SBMF_OK)
 
-__all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "load_libfm_binary", "save_libfm_binary", "libfm_binary_kind", "device_usage", "save_triples", "config_default",
+__all__ = ["FMLearnSBPMF", "FMLearnVBOnline", "Data", "SBMFError", "load_triples", "load_libfm", "load_libfm_binary", "save_libfm_binary", "libfm_binary_kind", "device_usage", "Communicator", "save_triples", "config_default",
            "RNG_REFERENCE", "RNG_PHILOX", "QUIRKS_FINAL", "QUIRKS_SBPMF2", "QUIRKS_NONE",
            "QUIRKS_BIAS2", "QUIRKS_BIAS22", "F64", "F32"]
 
@@ -255,7 +255,10 @@ class FMLearnSBPMF:
         if rc != SBMF_OK:
             raise SBMFError(rc, lib.sbmf_last_global_error().decode())
         self.ctx = ctx
-        if comm is not None:  # (nranks, rank, 128-byte id)
+        if isinstance(comm, Communicator):  # a process-wide communicator, shared by learners in turn
+            self._comm = comm  # keeps it alive as long as this learner
+            self._check(lib.sbmf_comm_attach(self.ctx, comm.handle))
+        elif comm is not None:  # (nranks, rank, 128-byte id): a communicator of this learner's own
             nranks, rank, uid = comm
             buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
             self._check(lib.sbmf_comm_init(self.ctx, nranks, rank, buf))
@@ -376,6 +379,30 @@ def device_usage(device=0):
     if rc != SBMF_OK:
         raise SBMFError(rc, lib.sbmf_last_global_error().decode())
     return {f: getattr(u, f) for f, _ in u._fields_}
+
+
+class Communicator:
+    """sbmf_comm_create: one RCCL communicator for the process (ncclCommInitRank once),
+    attached in turn by every learner created with ``init(comm=<this>)``."""
+
+    def __init__(self, nranks, rank, uid):
+        h = C.c_void_p()
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        rc = lib.sbmf_comm_create(nranks, rank, buf, C.byref(h))
+        if rc != SBMF_OK:
+            raise SBMFError(rc, lib.sbmf_last_global_error().decode())
+        self.handle, self.nranks, self.rank = h, nranks, rank
+
+    def close(self):
+        if self.handle is not None:
+            lib.sbmf_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def comm_unique_id():

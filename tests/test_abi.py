@@ -111,3 +111,35 @@ def test_removed_row_kernels_are_refused():
         with pytest.raises(sbmf.SBMFError) as e:
             L.init()
         assert e.value.code == sbmf.SBMF_E_ARG and "reserved" in str(e.value)
+
+
+def test_unassigned_tune_bits_are_refused():
+    """A tune bit that selects nothing in this build (a variant removed in an earlier
+    round) fails with SBMF_E_ARG before any device is touched, instead of being ignored
+    or picking whatever the bit means now."""
+    import ctypes as C
+    ctx = C.c_void_p()
+    for bit in (0, 4, 5, 6, 15, 18, 19, 20, 21, 22, 31):
+        cfg = sbmf.config_default()
+        cfg.tune = 1 << bit
+        assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG, bit
+        assert "tune bits" in _lib.lib.sbmf_last_global_error().decode()
+    if not gpu_available():  # an assigned bit passes the check and reaches the device check
+        cfg = sbmf.config_default()
+        cfg.tune = (1 << 16) | (1 << 29)
+        assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_DEVICE
+
+
+def test_shared_communicator_entry_points_check_arguments():
+    """sbmf_comm_create / sbmf_comm_attach (one RCCL communicator per process, attached by
+    every context in turn): bad ranks and null handles fail before any RCCL call."""
+    import ctypes as C
+    h = C.c_void_p()
+    uid = (C.c_uint8 * 128)()
+    assert _lib.lib.sbmf_comm_create(2, 2, uid, C.byref(h)) == sbmf.SBMF_E_ARG
+    assert _lib.lib.sbmf_comm_create(0, 0, uid, C.byref(h)) == sbmf.SBMF_E_ARG
+    assert _lib.lib.sbmf_comm_create(1, 0, None, C.byref(h)) == sbmf.SBMF_E_ARG
+    # a one-rank communicator is a no-op object (no RCCL): created and destroyed without a device
+    assert _lib.lib.sbmf_comm_create(1, 0, uid, C.byref(h)) == sbmf.SBMF_OK and h.value
+    assert _lib.lib.sbmf_comm_attach(None, h) == sbmf.SBMF_E_ARG
+    _lib.lib.sbmf_comm_destroy(h)
