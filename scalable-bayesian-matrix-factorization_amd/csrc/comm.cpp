@@ -19,6 +19,7 @@
 #include <stdexcept>
 #include <string>
 #include <type_traits>
+#include <vector>
 
 namespace sbmf {
 
@@ -27,7 +28,43 @@ namespace sbmf {
 // RCCL is loaded on first use (dlopen), not linked: a single-GPU process never
 // maps librccl.so or runs its initialisers, and a library user without RCCL can
 // still run one GPU.  The entry points are RCCL's own (rccl/rccl.h prototypes).
+//
+// It is opened BY PATH, from the directory of the HIP runtime this library is bound
+// to: a process that imported torch has torch's bundled librccl.so (soname
+// librccl.so.1) mapped already, bound to torch's own copy of libamdhip64 / the HSA
+// runtime, and dlopen("librccl.so.1") returns that copy -- whose first HIP call fails
+// ("ncclCommInitRank failed: unhandled cuda error", the round-5 in-suite failure:
+// pytest had imported torch.distributed while collecting test_multirank_cpu.py, and
+// bench.py imports it for its gloo bootstrap).  Opened by path, the system RCCL is a
+// separate object whose HIP symbols bind to this library's runtime (LD_DEBUG=bindings).
+// SBMF_RCCL overrides the path.
 namespace {
+std::string hip_runtime_dir() {
+    Dl_info info{};
+    if (dladdr(reinterpret_cast<void*>(&hipGetDevice), &info) && info.dli_fname) {
+        std::string f(info.dli_fname);
+        const size_t sl = f.rfind('/');
+        if (sl != std::string::npos) return f.substr(0, sl);
+    }
+    return std::string();
+}
+void* open_rccl(std::string& where) {
+    std::vector<std::string> tries;
+    if (const char* e = std::getenv("SBMF_RCCL")) tries.push_back(e);
+    const std::string dir = hip_runtime_dir();
+    if (!dir.empty()) tries.push_back(dir + "/librccl.so.1");
+    tries.push_back("librccl.so.1");  // the loader's search (no HIP runtime path found)
+    std::string errs;
+    for (const std::string& t : tries) {
+        if (void* h = dlopen(t.c_str(), RTLD_NOW | RTLD_LOCAL)) {
+            where = t;
+            return h;
+        }
+        errs += std::string(" [") + t + ": " + dlerror() + "]";
+    }
+    where = errs;
+    return nullptr;
+}
 struct Rccl {
     decltype(&::ncclGetUniqueId) GetUniqueId;
     decltype(&::ncclCommInitRank) CommInitRank;
@@ -43,9 +80,9 @@ struct Rccl {
 };
 const Rccl& rccl() {
     static const Rccl r = [] {
-        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
-        if (!h) throw std::runtime_error(std::string("multi-GPU needs RCCL: dlopen(librccl.so.1) failed: ") + dlerror());
+        std::string where;
+        void* h = open_rccl(where);
+        if (!h) throw std::runtime_error("multi-GPU needs RCCL: dlopen failed:" + where);
         Rccl t{};
         auto sym = [&](auto& f, const char* name) {
             f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));

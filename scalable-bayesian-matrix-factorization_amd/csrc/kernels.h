@@ -38,7 +38,12 @@ struct HalfArgs {
     uint64_t lim_other;    // elements of E_other (N + multi-GPU send area)
     uint64_t lim_this;     // N (part, perm, E_this, r_this)
     uint32_t lim_rows;     // R (own rows; zbuf rows)
+    // graph replay (sweep_graph in sbmf.cpp): this sweep's scalars read from device memory,
+    // DYN_* slots, staged with the hyperparameters; null: the by-value fields above
+    const double* dyn;
 };
+// slots of the device scalar block (sbmf_ctx::d_dyn), written before each replayed sweep
+enum DynSlot { DYN_TAU = 0, DYN_DIV = 1, DYN_COLLECT = 2, DYN_SWEEP_NEXT = 3, DYN_N = 8 };
 
 // Gram-block (MFMA) row kernels.  Max ratings per row for each kind: f64
 // holds 8 vectors (32 ratings) per wave, f32 16 (64 ratings).
@@ -148,10 +153,12 @@ hipError_t launch_colstats(const T* tabA, uint32_t rA, const T* muA, double* out
 // Test predictions: pred = clamp(dot(U[u],V[i])) (+ b0 + bu[u] + bv[i] when bu
 // is non-null: the biased sampler); sum[t] += pred if collect;
 // part[b][0] += (r - sum/div)^2, part[b][1] += (r-pred)^2 per 256-rating block.
+// dyn (non-null in a replayed sweep graph): collect and div read from dyn[DYN_COLLECT], dyn[DYN_DIV]
 template <typename T>
 hipError_t launch_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t t0, uint64_t t1,
                        const T* U, const T* V, uint32_t K, uint32_t Kp, T lo, T hi, int collect, double div,
-                       double* sum, double* part, const double* bu, const double* bv, double b0, hipStream_t st);
+                       double* sum, double* part, const double* bu, const double* bv, double b0, hipStream_t st,
+                       const double* dyn = nullptr);
 
 // Biased sampler (top-level gibbs_sbpmf2.cpp, src/libfm/gibbs_sbpmf22.cpp):
 // per-row bias hyperparameters + bias draw + residual shift, one wave per row
@@ -191,9 +198,10 @@ hipError_t launch_sum_cols2(const double* in, uint32_t nchunk, double* out, cons
 // Philox init: tab[r][k] = sd * z(seed, sweep=0xffffffff, tag, r, k), rows [r0,r1).
 // z[row][k] = N(0,1) Philox normal (seed, sweep, tag, row, pair k/2) for rows [r0, r1):
 // the per-half variates of throughput mode, the same stream the kernels drew inline.
+// dyn (non-null in a replayed sweep graph): the sweep read from dyn[DYN_SWEEP_NEXT]
 template <typename T>
 hipError_t launch_philox_fill(T* z, uint32_t K, uint32_t r0, uint32_t r1, uint64_t seed, uint32_t sweep, uint32_t tag,
-                              hipStream_t st);
+                              hipStream_t st, const double* dyn = nullptr);
 template <typename T>
 hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, double sd, uint64_t seed,
                               uint32_t tag, hipStream_t st);

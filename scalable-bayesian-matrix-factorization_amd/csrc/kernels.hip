@@ -412,7 +412,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         }
     }
     asm volatile("" ::: "memory");  // read back by the other lanes of the wave (LDS keeps its order)
-    const T tau = a.tau;
+    const T tau = a.dyn ? (T)a.dyn[DYN_TAU] : a.tau;
     const T* __restrict__ orow = a.own + (size_t)CHK(row, a.lim_rows) * Kp + ci;
     stamp(0);  // row setup (ids, residuals, normals)
     // software pipeline: block b+1's slices and own/sigma/mu values are in
@@ -689,7 +689,7 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
     const int rr = lane >> 4;
     const uint32_t K = a.K, Kp = a.Kp;
     const uint32_t nblk = (K + GB - 1) / GB;
-    const T tau = a.tau;
+    const T tau = a.dyn ? (T)a.dyn[DYN_TAU] : a.tau;
     __shared__ uint32_t pjL[CAP];      // partner row offset (row * Kp) per rating slot (zero row past the end)
     __shared__ uint32_t pmL[CAP];      // residual scatter target per rating
     __shared__ T eL[CAP];              // residuals (bit-identical in the 16 lanes of a rating)
@@ -1294,7 +1294,11 @@ __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, c
                                                uint32_t Kp, T lo, T hi, int collect, double div,
                                                double* __restrict__ sum, double* __restrict__ part,
                                                const double* __restrict__ bu, const double* __restrict__ bv,
-                                               double b0) {
+                                               double b0, const double* __restrict__ dyn) {
+    if (dyn) {  // a replayed sweep graph: this sweep's values from device memory
+        collect = dyn[DYN_COLLECT] != 0.0;
+        div = dyn[DYN_DIV];
+    }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ci = lane & 15, rr = lane >> 4;
     // group rr of wave w: ratings gbase + 0..15
@@ -1440,7 +1444,9 @@ __global__ __launch_bounds__(256) void k_sum_cols(const double* __restrict__ in,
 // stream (seed, row, sweep, tag) -- one thread per pair.
 template <typename T>
 __global__ __launch_bounds__(256) void k_philox_fill(T* __restrict__ z, uint32_t K, uint32_t r0, uint32_t r1,
-                                                     uint64_t seed, uint32_t sweep, uint32_t tag) {
+                                                     uint64_t seed, uint32_t sweep, uint32_t tag,
+                                                     const double* __restrict__ dyn) {
+    if (dyn) sweep = (uint32_t)dyn[DYN_SWEEP_NEXT];  // a replayed sweep graph
     const uint32_t npair = (K + 1) / 2;
     const uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t row = r0 + (uint32_t)(x / npair), p = (uint32_t)(x % npair);
@@ -1803,17 +1809,18 @@ hipError_t launch_colstats(const T* tabA, uint32_t rA, const T* muA, double* out
 template <typename T>
 hipError_t launch_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t t0, uint64_t t1, const T* U,
                        const T* V, uint32_t K, uint32_t Kp, T lo, T hi, int collect, double div, double* sum,
-                       double* part, const double* bu, const double* bv, double b0, hipStream_t st) {
+                       double* part, const double* bu, const double* bv, double b0, hipStream_t st,
+                       const double* dyn) {
     if (t1 <= t0) return hipSuccess;
     const uint64_t nb = (t1 - t0 + 255) / 256;
     // (4 ratings x 4 k-blocks per load round instead of 2 x 8: neutral, r05s7; the user-row
     // reuse: evaluation 0.30 -> 0.26 ms, sweep 7.36 -> 7.32 ms at ML-20M K=100, r05s9)
     if (Kp <= 128)
         k_test<T, 2, 8, true><<<(uint32_t)nb, 256, 0, st>>>(tu, ti, tr, t0, t1, U, V, K, Kp, lo, hi, collect, div, sum,
-                                                            part, bu, bv, b0);
+                                                            part, bu, bv, b0, dyn);
     else
         k_test<T, 2, 8, false><<<(uint32_t)nb, 256, 0, st>>>(tu, ti, tr, t0, t1, U, V, K, Kp, lo, hi, collect, div, sum,
-                                                             part, bu, bv, b0);
+                                                             part, bu, bv, b0, dyn);
     return hipGetLastError();
 }
 
@@ -1848,10 +1855,10 @@ hipError_t launch_sum_cols2(const double* in, uint32_t nchunk, double* out, cons
 
 template <typename T>
 hipError_t launch_philox_fill(T* z, uint32_t K, uint32_t r0, uint32_t r1, uint64_t seed, uint32_t sweep, uint32_t tag,
-                              hipStream_t st) {
+                              hipStream_t st, const double* dyn) {
     if (r1 <= r0 || K == 0) return hipSuccess;
     const uint64_t n = (uint64_t)(r1 - r0) * ((K + 1) / 2);
-    k_philox_fill<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(z, K, r0, r1, seed, sweep, tag);
+    k_philox_fill<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(z, K, r0, r1, seed, sweep, tag, dyn);
     return hipGetLastError();
 }
 
@@ -1908,12 +1915,12 @@ hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, h
                                         uint32_t, T*, double*, double*, const double*, const double*, double,         \
                                         hipStream_t);                                                                \
     template hipError_t launch_philox_fill<T>(T*, uint32_t, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t,        \
-                                              hipStream_t);                                                          \
+                                              hipStream_t, const double*);                                           \
     template hipError_t launch_colstats<T>(const T*, uint32_t, const T*, double*, const T*, uint32_t, const T*,    \
                                            double*, uint32_t, uint32_t, hipStream_t);                                \
     template hipError_t launch_test<T>(const uint32_t*, const uint32_t*, const double*, uint64_t, uint64_t,         \
                                        const T*, const T*, uint32_t, uint32_t, T, T, int, double, double*, double*, \
-                                       const double*, const double*, double, hipStream_t);                          \
+                                       const double*, const double*, double, hipStream_t, const double*);           \
     template hipError_t launch_init_philox<T>(T*, uint32_t, uint32_t, uint32_t, uint32_t, double, uint64_t,          \
                                               uint32_t, hipStream_t);                                                \
     template hipError_t launch_bias_rows<T>(const uint32_t*, uint32_t, uint32_t, T*, double*, double*, double*,      \

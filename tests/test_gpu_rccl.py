@@ -38,9 +38,10 @@ def _learner(shape="ml-1m", K=50, **kw):
 
 
 def test_rccl_calls_beside_persistent_kgres_grids():
-    """Run in a fresh process (tests/workers/rccl_selftest.py): in the long GPU-suite process,
-    after ~100 tests' contexts, ncclCommInitRank once failed with "unhandled cuda error"
-    (r05s1); RCCL's set-up is kept out of that shared state."""
+    """In a fresh process (tests/workers/rccl_selftest.py), without torch: the same self-test
+    as test_gpu_resources.py's in-process one, from a clean start.  (Round 5 moved it here
+    after ncclCommInitRank failed inside the suite process; the cause was torch's bundled
+    librccl.so answering dlopen("librccl.so.1"), fixed in comm.cpp in round 6.)"""
     env = dict(os.environ, NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"))
     p = subprocess.run([sys.executable, WORKER, str(16 << 20), "8"], capture_output=True, text=True, timeout=180,
                        env=env)

@@ -1,8 +1,13 @@
 """Every learner gives back what it takes, and RCCL then initialises in the
 same long-lived process.
 
-Round 5's whole-suite process once failed ncclCommInitRank ("unhandled cuda
-error") after about a hundred tests' contexts (profiles/r05/r05s1_suite_summary.txt).
+Round 5's whole-suite process failed ncclCommInitRank ("unhandled cuda error")
+(profiles/r05/r05s1_suite_summary.txt).  The cause (round 6, r06s2): pytest had
+imported torch.distributed while collecting test_multirank_cpu.py, which maps
+torch's bundled librccl.so (soname librccl.so.1) bound to torch's own copy of the
+HIP / HSA runtime; comm.cpp's dlopen("librccl.so.1") returned that copy.  RCCL is
+now opened by path from the directory of the HIP runtime libsbmf is bound to.  This
+test imports torch.distributed itself, so it reproduces the round-5 process.
 sbmf_test_device_usage counts what the library holds -- device and pinned
 buffers, streams, events, contexts, RCCL communicators -- where each is created
 and released, next to hipMemGetInfo.  Here 150 learners of every kind (the SBPMF
@@ -40,7 +45,12 @@ def _held(u):
     return {k: u[k] for k in COUNTS}
 
 
+def _mapped(sub):
+    return sorted({l.split()[-1] for l in open("/proc/self/maps") if sub in l})
+
+
 def test_learners_give_everything_back_then_rccl_initialises_in_process():
+    import torch.distributed  # noqa: F401  (maps torch's own librccl.so, as the round-5 suite process had)
     tr, te, _ = synth.generate("ml-100k")
     gc.collect()
     base = device_usage()
@@ -76,6 +86,10 @@ def test_learners_give_everything_back_then_rccl_initialises_in_process():
     assert rc == 0, lib.sbmf_last_error(L.ctx).decode()
     assert out.n_calls == 48 and out.bad_bcast == 0 and out.bad_p2p == 0 and out.bad_allgather == 0
     assert device_usage()["comms"] == base["comms"]  # the loopback communicator is gone again
+    # the RCCL the library opened sits beside the HIP runtime libsbmf is bound to, not torch's
+    hip_dirs = {p.rsplit("/", 1)[0] for p in _mapped("libamdhip64") if "torch" not in p}
+    rccl = [p for p in _mapped("librccl") if "torch" not in p]
+    assert rccl and all(p.rsplit("/", 1)[0] in hip_dirs for p in rccl), (rccl, hip_dirs)
     # the self-test ran extra item halves on this chain: the context refuses further sweeps
     with pytest.raises(SBMFError, match="self-test"):
         L.learn(sweeps=1)
