@@ -356,6 +356,18 @@ struct sbmf_ctx {
     // use them (pre dropped by sbmf_set_factors) restores the current ones before its
     // prologue, whose column statistics read the current mu from d_hyper
     bool hyper_ahead = false;
+    // One rank, throughput mode: the steady-state sweep captured once as a hipGraph and
+    // replayed (run_sweeps_T, sweep_graph): one launch per sweep instead of ~40 host calls.
+    // Its per-sweep scalars (tau, the evaluation's collect / divisor, the next sweep's Philox
+    // index) live in d_hyper past the hyperparameters (dyn_off), staged with them.
+    bool capturing = false;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    int graph_key = -1;  // the captured prologue's recompute decision (-1: nothing captured)
+    uint32_t graph_nlaunch = 0;
+    hipEvent_t gdep[2] = {};  // capture-internal fork / join of the evaluation on sto
+    size_t dyn_off = 0;       // bytes into d_hyper
+    double* d_dyn() { return reinterpret_cast<double*>(static_cast<char*>(d_hyper.p) + dyn_off); }
     double* h_pinned = nullptr;  // pinned staging for z streams
     size_t h_pinned_bytes = 0, h_pre_bytes = 0, h_io_bytes = 0;
     size_t xheads_off = 0;  // d_xcnt: first per-XCD queue head (uint32 index)
@@ -651,8 +663,10 @@ static void prepare_T(sbmf_ctx* c) {
     c->d_rowtr_v.alloc((size_t)c->J * sizeof(double));
     HIPCHK(hipMemsetAsync(c->d_rowsq_v.p, 0, c->d_rowsq_v.bytes, st));
     HIPCHK(hipMemsetAsync(c->d_rowtr_v.p, 0, c->d_rowtr_v.bytes, st));
-    // [sig_u | mu_u | sig_v | mu_v], each Kp long and zero padded, + 16 slack for prefetch
-    c->d_hyper.alloc((4 * (size_t)c->Kp + 16) * sizeof(T));
+    // [sig_u | mu_u | sig_v | mu_v], each Kp long and zero padded, + 16 slack for prefetch,
+    // then the DYN_N per-sweep scalars of a replayed sweep graph (doubles, 8-byte aligned)
+    c->dyn_off = (4 * (size_t)c->Kp + 16) * sizeof(T);
+    c->d_hyper.alloc(c->dyn_off + DYN_N * sizeof(double));
     HIPCHK(hipMemsetAsync(c->d_hyper.p, 0, c->d_hyper.bytes, st));
     const uint32_t nchunk = (c->I + 255) / 256 + (c->J + 255) / 256;  // both tables' 256-row chunks
     c->d_colpart.alloc((size_t)nchunk * 2 * c->K * sizeof(double));
@@ -662,7 +676,7 @@ static void prepare_T(sbmf_ctx* c) {
     c->h_pre_bytes = c->h_res.size() * sizeof(double);
     pinned_alloc((void**)&c->h_pre, c->h_pre_bytes);
     pinned_free(c->h_io, c->h_io_bytes);
-    c->h_io_bytes = 128 + 4 * (size_t)c->Kp * sizeof(T);
+    c->h_io_bytes = 128 + c->dyn_off + DYN_N * sizeof(double);
     pinned_alloc(&c->h_io, c->h_io_bytes);
     c->pre.valid = false;
     c->hyper_ahead = false;
@@ -1051,6 +1065,7 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     a.tune = c->cfg.tune;
     a.prof = c->kprof ? c->d_kprof.as<unsigned long long>() + 16 + 8 * (users ? 0 : 1) : nullptr;
     a.tau = (T)c->tau;
+    a.dyn = c->capturing ? c->d_dyn() : nullptr;  // a captured sweep reads tau from device memory
     a.K = c->K;
     a.Kp = c->Kp;
     a.sd_is_var = c->sd_is_var;
@@ -1066,6 +1081,12 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     // otherwise every rank reads the residuals the exchange delivered
     a.e_from_dot = (c->cfg.tune & 2u) ? 1 : 0;
     return a;
+}
+
+// An event the host reads (timing, hipEventSynchronize): inside a captured sweep an
+// external event-record node, so that every replay records it.
+static void mark(sbmf_ctx* c, hipEvent_t e, hipStream_t s) {
+    HIPCHK(c->capturing ? hipEventRecordWithFlags(e, s, hipEventRecordExternal) : hipEventRecord(e, s));
 }
 
 template <typename T>
@@ -1123,7 +1144,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         int& lk = last[st == c->st ? 0 : st == c->sto ? 1 : 2];
         if (timed) {
             c->kpv(stage, sd, k) = (int8_t)lk;
-            if (lk < 0) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
+            if (lk < 0) mark(c, c->kev(stage, sd, k, 0), st);
             lk = k;
         } else {
             lk = -1;  // no end event behind this launch
@@ -1190,7 +1211,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
             c->xcnt_clean = true;
         }
         // (after the memset: a kind launched next on this stream starts its time at this event)
-        if (timed) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
+        if (timed) mark(c, c->kev(stage, sd, k, 1), st);
         c->timing.n_launch++;
     }
     if (side) {
@@ -1290,7 +1311,7 @@ static void run_half_pipelined(sbmf_ctx* c, bool users, F&& bcasts) {
         if (c->nranks > 1) HIPCHK(hipEventRecord(c->sev[(size_t)sd * c->nstages + p], c->st));
         if (c->virt) HIPCHK(hipEventRecord(c->tsev[tb + p + 1], c->st));
     }
-    HIPCHK(hipEventRecord(c->ev[users ? 2 : 4], c->st));
+    mark(c, c->ev[users ? 2 : 4], c->st);
     if (c->nranks <= 1) return;  // no exchange: ev[3] / ev[5] are not recorded (the sweep uses ev[2] / ev[4])
     for (uint32_t p = 0; p < c->nstages; ++p) {
         HIPCHK(hipStreamWaitEvent(c->stc, c->sev[(size_t)sd * c->nstages + p], 0));
@@ -1298,6 +1319,18 @@ static void run_half_pipelined(sbmf_ctx* c, bool users, F&& bcasts) {
     }
     HIPCHK(hipEventRecord(c->cev[sd], c->stc));
     HIPCHK(hipStreamWaitEvent(c->st, c->cev[sd], 0));
+}
+
+static bool graph_enabled() {
+    const char* e = std::getenv("SBMF_GRAPH");
+    return !(e && std::strcmp(e, "0") == 0);
+}
+static void destroy_graph(sbmf_ctx* c) {
+    if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
+    c->gexec = nullptr;
+    c->graph = nullptr;
+    c->graph_key = -1;
 }
 
 template <typename T>
@@ -1413,19 +1446,30 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
     hipEvent_t& ev5 = c->nranks > 1 ? c->ev[5] : c->ev[4];
     // the sweep's hyperparameters [sig_u | mu_u | sig_v | mu_v] into the pinned staging area
     // and on to d_hyper (stream order: after every launch already queued that reads it)
+    // + the per-sweep scalars of sweep `sw` (tau_sw) that a replayed sweep graph reads (DYN_*):
+    // the evaluation's collect flag and divisor as run_sweeps_T computes them when sweep sw's
+    // evaluation is queued (c->collected counts the sweeps collected before sw at this point)
     auto stage_hyper = [&](const std::vector<double>& su, const std::vector<double>& mu, const std::vector<double>& sv,
-                           const std::vector<double>& mv) {
+                           const std::vector<double>& mv, uint32_t sw, double tau_sw) {
         const size_t Kp = c->Kp;
         T* h = static_cast<T*>(c->h_hyper());
         HIPCHK(hipEventSynchronize(c->hev));
-        std::fill(h, h + 4 * Kp, T(0));
+        std::fill(h, h + 4 * Kp + 16, T(0));
         for (uint32_t k = 0; k < K; ++k) {
             h[k] = (T)su[k];
             h[Kp + k] = (T)mu[k];
             h[2 * Kp + k] = (T)sv[k];
             h[3 * Kp + k] = (T)mv[k];
         }
-        HIPCHK(hipMemcpyAsync(c->d_hyper.p, h, 4 * Kp * sizeof(T), hipMemcpyHostToDevice, st));
+        double* dyn = reinterpret_cast<double*>(static_cast<char*>(c->h_hyper()) + c->dyn_off);
+        const bool col = q2 ? true : (sw >= cf.burnin);
+        const uint32_t ncol = c->collected + (col ? 1u : 0u);
+        std::fill(dyn, dyn + DYN_N, 0.0);
+        dyn[DYN_TAU] = tau_sw;
+        dyn[DYN_COLLECT] = col ? 1.0 : 0.0;
+        dyn[DYN_DIV] = avg_collected(cf) ? (double)std::max(1u, ncol) : (double)(sw + 1);
+        dyn[DYN_SWEEP_NEXT] = (double)(sw + 1);
+        HIPCHK(hipMemcpyAsync(c->d_hyper.p, h, c->dyn_off + DYN_N * sizeof(double), hipMemcpyHostToDevice, st));
         HIPCHK(hipEventRecord(c->hev, st));
     };
     for (uint32_t it = 0; it < nsweeps; ++it) {
@@ -1436,7 +1480,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // throughput mode: this sweep's hyperparameters already on the device and its normals
         // filled (both queued at the end of the previous sweep)
         const bool staged = c->pre.valid && c->pre.sweep == c->sweep && c->pre.staged;
-        if (!staged && c->hyper_ahead) stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v);
+        if (!staged && c->hyper_ahead) stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v, c->sweep, c->tau);
         c->hyper_ahead = false;
         if (c->pre.valid && c->pre.sweep == c->sweep) {  // drawn at the end of the previous sweep
             c->tau = c->pre.tau;
@@ -1463,7 +1507,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         c->pre.valid = false;
         c->pre.staged = false;
         if (!staged) {
-            stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v);
+            stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v, c->sweep, c->tau);
             if (ref && c->bias) {
                 fill_bias_variates<T>(c);
             } else if (ref) {  // user variates then item variates (:485 then :529)
@@ -1474,6 +1518,16 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(hipEventRecord(c->ev[1], st));
         }
         hipEvent_t& ev1 = staged ? c->ev[0] : c->ev[1];
+        const bool collect = q2 ? true : (c->sweep >= cf.burnin);
+        if (collect) c->collected++;
+        const double div = avg_collected(cf) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
+        const uint64_t T_ = c->su.size();
+        const bool par_eval = overlap && c->nranks == 1 && !(cf.tune & 0x10000000u);
+        // The sweep's device work, from the user half to the results' copy.  With the overlap the
+        // next sweep's prologue kernels and normals are part of it; in a captured sweep (graph
+        // mode) every per-sweep scalar comes from d_dyn, staged with the hyperparameters.
+        auto body = [&]() {
+        const double* dyn = c->capturing ? c->d_dyn() : nullptr;
         // ---- 3. user half-sweep (throughput mode: this half's normals first)
         if (!ref && !staged)
             HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep, TAG_USERS, st));
@@ -1507,43 +1561,79 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // evaluation runs on the second stream beside the prologue kernels -- both only read
         // U and V and they write different result slots, so nothing changes -- where it used
         // to follow them (tune bit 28 restores that order; measured 7.64-7.73 -> 7.61 ms, r04s22)
-        const bool collect = q2 ? true : (c->sweep >= cf.burnin);
-        if (collect) c->collected++;
-        const double div = avg_collected(cf) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
-        const uint64_t T_ = c->su.size();
-        const bool par_eval = overlap && c->nranks == 1 && !(cf.tune & 0x10000000u);
         auto evaluate = [&](hipStream_t se) {
             if (cf.eval_test && T_) {
                 HIPCHK(launch_test<T>(c->d_tu.as<uint32_t>(), c->d_ti.as<uint32_t>(), c->d_tr.as<double>(), c->t0,
                                       c->t1, c->d_U.as<T>(), c->d_V.as<T>(), K, c->Kp, (T)c->lo, (T)c->hi,
                                       collect ? 1 : 0, div, c->d_tsum.as<double>(), c->d_tpart.as<double>(),
-                                      c->bias ? c->d_bu.as<double>() : nullptr, c->d_bv.as<double>(), c->b0, se));
+                                      c->bias ? c->d_bu.as<double>() : nullptr, c->d_bv.as<double>(), c->b0, se, dyn));
                 if (c->nranks > 1) c->comm->bcast_ranges(c->d_tpart.p, 2 * sizeof(double), c->tbblocks, se);
                 const uint32_t nb = (uint32_t)((T_ + 255) / 256);
                 HIPCHK(launch_sum_cols(c->d_tpart.as<double>(), nb, 2, d_res + RES_TEST_AVG, se));
             }
             if (cf.eval_train)
                 HIPCHK(launch_sum(c->d_rowtr_v.as<double>(), c->J, d_res + RES_TRSQ, scratch + c->scratch_half, se));
-            HIPCHK(hipEventRecord(c->ev[6], se));
+            mark(c, c->ev[6], se);
+            if (c->capturing && se != st) HIPCHK(hipEventRecord(c->gdep[1], se));  // the capture's join
         };
         if (par_eval) {
-            HIPCHK(hipStreamWaitEvent(c->sto, ev5, 0));
+            if (c->capturing) {  // ev5 is an external node in a capture: fork on an internal event
+                HIPCHK(hipEventRecord(c->gdep[0], st));
+                HIPCHK(hipStreamWaitEvent(c->sto, c->gdep[0], 0));
+            } else {
+                HIPCHK(hipStreamWaitEvent(c->sto, ev5, 0));
+            }
             evaluate(c->sto);
         }
         if (overlap) {  // the next sweep's prologue kernels, ahead of the evaluation
             prologue_gpu(c->sweep + 1);
-            HIPCHK(hipEventRecord(c->ev[7], st));
+            mark(c, c->ev[7], st);
             // and the next sweep's normals (Philox: a function of (seed, sweep) only; this
             // sweep's halves, which read them, are queued before)
-            HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep + 1, TAG_USERS, st));
-            HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep + 1, TAG_ITEMS, st));
-            HIPCHK(hipEventRecord(c->ev[8], st));  // the next sweep's start work ends here
+            HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep + 1, TAG_USERS,
+                                         st, dyn));
+            HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep + 1, TAG_ITEMS,
+                                         st, dyn));
+            mark(c, c->ev[8], st);  // the next sweep's start work ends here
         }
         if (par_eval)
-            HIPCHK(hipStreamWaitEvent(st, c->ev[6], 0));
+            HIPCHK(hipStreamWaitEvent(st, c->capturing ? c->gdep[1] : c->ev[6], 0));
         else
             evaluate(st);
         HIPCHK(hipMemcpyAsync(c->h_out(), d_res, 8 * sizeof(double), hipMemcpyDeviceToHost, st));
+        };
+        // Graph mode: the steady-state sweep of one rank in throughput mode (its start work staged
+        // by the previous sweep, launch kinds untimed) is captured once and replayed; a sweep of
+        // another shape (a run's first, one whose prologue recomputes differently) runs eagerly.
+        // SBMF_GRAPH=0 keeps every sweep eager (the chain is the same either way).
+        const int key = (cf.recompute_every && (c->sweep + 1) % cf.recompute_every == 0) ? 1 : 0;
+        const bool use_graph = graph_enabled() && overlap && par_eval && staged && !c->time_kinds && c->nranks == 1 &&
+                               !c->virt && !c->bias && !c->kprof && !(cf.tune & 0x1000000u);
+        if (use_graph) {
+            if (!c->gexec || c->graph_key != key) {
+                destroy_graph(c);
+                HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+                c->capturing = true;
+                try {
+                    body();
+                } catch (...) {
+                    c->capturing = false;
+                    hipGraph_t g = nullptr;
+                    (void)hipStreamEndCapture(st, &g);
+                    if (g) (void)hipGraphDestroy(g);
+                    throw;
+                }
+                c->capturing = false;
+                HIPCHK(hipStreamEndCapture(st, &c->graph));
+                HIPCHK(hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0));
+                c->graph_key = key;
+                c->graph_nlaunch = c->timing.n_launch;
+            }
+            HIPCHK(hipGraphLaunch(c->gexec, st));
+            c->timing.n_launch = c->graph_nlaunch;
+        } else {
+            body();
+        }
         if (overlap) {  // the next sweep's draws while the evaluation runs; this sweep's values kept
             HIPCHK(hipEventSynchronize(c->ev[7]));
             HostStream hs;
@@ -1572,7 +1662,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             c->pre.valid = true;
             // the next sweep's hyperparameters to the device now (every launch of this sweep that
             // reads d_hyper -- the halves and the prologue's column statistics -- is queued before)
-            stage_hyper(c->pre.sig_u, c->pre.mu_u, c->pre.sig_v, c->pre.mu_v);
+            stage_hyper(c->pre.sig_u, c->pre.mu_u, c->pre.sig_v, c->pre.mu_v, c->sweep + 1, c->pre.tau);
             c->pre.staged = true;
             c->hyper_ahead = true;
         }
@@ -1667,6 +1757,8 @@ sbmf_ctx::~sbmf_ctx() {
     vbo_destroy(vb);
     fmm_destroy(fm);
     using namespace sbmf;
+    destroy_graph(this);
+    for (hipEvent_t& e : gdep) event_destroy(e);
     pinned_free(h_pinned, h_pinned_bytes);
     pinned_free(h_pre, h_pre_bytes);
     pinned_free(h_io, h_io_bytes);
@@ -1923,6 +2015,7 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     sbmf::stream_create(&c->sto2);
     for (auto& e : c->oev) sbmf::event_create(&e, hipEventDisableTiming);
     sbmf::event_create(&c->hev, hipEventDisableTiming);
+    for (auto& e : c->gdep) sbmf::event_create(&e, hipEventDisableTiming);
     *out = c.release();
     API_END(ctx)
 }

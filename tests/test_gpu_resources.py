@@ -91,7 +91,7 @@ def test_learners_give_everything_back_then_rccl_initialises_in_process():
     rccl = [p for p in _mapped("librccl") if "torch" not in p]
     assert rccl and all(p.rsplit("/", 1)[0] in hip_dirs for p in rccl), (rccl, hip_dirs)
     # the self-test ran extra item halves on this chain: the context refuses further sweeps
-    with pytest.raises(SBMFError, match="self-test"):
+    with pytest.raises(SBMFError, match="rccl_selftest ran extra item halves"):
         L.learn(sweeps=1)
     L.close()
     gc.collect()
