@@ -227,5 +227,6 @@ def test_sweep_graph_changes_nothing(ml100k, kw, monkeypatch):
         assert np.array_equal(x, y)
     t = L.timing()
     assert L.history[-1]["ms_sweep"] > 0 and t.ms_user_half > 0 and t.ms_item_half > 0 and t.ms_eval > 0
-    assert t.kern_ms[1][5] > 0  # the streaming kind's events are replayed too
+    # the streaming kind's events are replayed too (f32: no ML-100k row passes its 512-rating threshold)
+    assert t.kern_ms[1][5] > 0 or t.kern_rows[1][5] == 0
     assert np.array_equal(L.predict(), a.predict())
