@@ -363,7 +363,7 @@ def cpu_baseline(train, test, dims, K, seconds, quirks="final"):
     return out
 
 
-def mk_comm(world, rank):
+def mk_comm(world, rank, local):
     """The process's one communicator (sbmf_comm_create: ncclCommInitRank once), from a
     fresh RCCL unique id made by rank 0 and shared over the gloo bootstrap group; every
     learner of this process attaches to it in turn (sbmf_comm_attach)."""
@@ -373,7 +373,7 @@ def mk_comm(world, rank):
     from sbmf import Communicator, comm_unique_id
     obj = [comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
-    return Communicator(world, rank, obj[0])
+    return Communicator(world, rank, obj[0], device=local)
 
 
 def vb_main(args):
@@ -386,7 +386,7 @@ def vb_main(args):
     train, test, dims = synth.generate(args.shape)
     say("[bench vb] %d train ratings in %.0f s" % (len(train[0]), time.time() - t0))
     n_train = len(train[0])
-    comm = mk_comm(world, rank)
+    comm = mk_comm(world, rank, local)
     L = FMLearnVBOnline(num_factor=args.K, seed=2015, rng="philox", device=local)
     L.init(comm=comm)
     t0 = time.time()
@@ -497,7 +497,7 @@ def libfm_main(args):
     train, test, dims = synth.generate(args.shape)
     n_train, n_test, K = len(train[0]), len(test[0]), args.K
     als = args.method == "als"
-    comm = mk_comm(world, rank)
+    comm = mk_comm(world, rank, local)
     L = FMLearnSBPMF(num_factor=K, seed=2015, rng="philox", method="als" if als else "mcmc", order="libfm",
                      regular=(0.0, 0.0, 10.0) if als else (0.0, 0.0, 0.0), init_stdev=0.1, device=local)
     L.init(comm=comm)
@@ -575,7 +575,7 @@ def main():
     from sbmf._lib import KIND_NAMES, NKIND
     KIND_STREAM_IDX = list(KIND_NAMES).index("gres_stage")
     train, test, dims = synth.generate(args.shape)
-    comm = mk_comm(world, rank)  # one communicator for every leg below
+    comm = mk_comm(world, rank, local)  # one communicator for every leg below
     main_res = measure(args, world, rank, local, args.precision, train, test, comm)
     if args.quirks != "final":  # the extra legs (f32, time-to-RMSE, loads) belong to the headline sampler
         args.no_f32 = args.no_ttr = args.no_load = True

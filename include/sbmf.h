@@ -286,9 +286,10 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]);
  * set-up (ncclCommInitRank) runs once.  sbmf_comm_attach joins a context to it
  * in place of sbmf_comm_init (before sbmf_prepare); the communicator must
  * outlive every context attached to it.  Contexts attached to one communicator
- * must not run at the same time. */
+ * must not run at the same time.  `device` is this rank's HIP device (the contexts'
+ * sbmf_config.device); RCCL binds the communicator to it. */
 typedef struct sbmf_comm sbmf_comm;
-int sbmf_comm_create(int nranks, int rank, const uint8_t id[128], sbmf_comm** out);
+int sbmf_comm_create(int device, int nranks, int rank, const uint8_t id[128], sbmf_comm** out);
 int sbmf_comm_attach(sbmf_ctx* ctx, sbmf_comm* comm);
 void sbmf_comm_destroy(sbmf_comm* comm);
 

@@ -598,11 +598,14 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
 
 
 // ------------------------------------------------- register-resident streaming rows
-// The default kernel for rows above the Gram-block bins: one 8-wave workgroup
-// per task of at most CAP = 4*NW*VW ratings (a whole row, or one equal chunk
-// of a longer row), in one persistent cooperative launch per half-sweep, with
-// k_gstream's rounds (a split row's chunks share a round, so they are
-// co-resident).  Wave w owns vectors w, w+NW, ... (4 ratings x 16 k each).
+// The default kernel for rows above the Gram-block bins: one NW-wave workgroup
+// (4, 8 or 16 waves) per task of at most CAP = 4*NW*VW ratings (a whole row, or
+// one equal chunk of a longer row), in one ordinary persistent launch per stream
+// set, tasks claimed from queue heads (per XCD by default) by whichever workgroup
+// is free; a split row's chunks are consecutive in one queue, so a chunk waits
+// only for peers the next free workgroups claim (no co-residency requirement
+// beyond the host's chunk caps).  Wave w owns vectors w, w+NW, ... (4 ratings x
+// 16 k each).
 // The partner slice of the current k-block stays in VGPRs from the accumulate
 // (G_B = S^T S by MFMA, c_B = S^T e) until the apply (e -= S_B D_B) after the
 // block's draws, so each slice is gathered once per half-sweep (k_gstream

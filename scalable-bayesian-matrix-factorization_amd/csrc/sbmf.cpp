@@ -2321,19 +2321,25 @@ int sbmf_comm_init(sbmf_ctx* ctx, int nranks, int rank, const uint8_t id[128]) {
 // legs): RCCL's set-up runs once, not once per learner
 struct sbmf_comm {
     sbmf::Comm c;
-    int nranks = 1, rank = 0;
+    int device = 0, nranks = 1, rank = 0;
 };
 
-int sbmf_comm_create(int nranks, int rank, const uint8_t id[128], sbmf_comm** out) {
+int sbmf_comm_create(int device, int nranks, int rank, const uint8_t id[128], sbmf_comm** out) {
     sbmf_ctx* ctx = nullptr;
     API_BEGIN
     if (!id || !out) sbmf::fail(SBMF_E_ARG, "null argument");
     *out = nullptr;
     if (nranks < 1 || rank < 0 || rank >= nranks) sbmf::fail(SBMF_E_ARG, "bad rank %d / %d", rank, nranks);
+    if (device < 0) sbmf::fail(SBMF_E_ARG, "bad device %d", device);
     std::unique_ptr<sbmf_comm> cm(new sbmf_comm());
+    cm->device = device;
     cm->nranks = nranks;
     cm->rank = rank;
-    if (nranks > 1) cm->c.init(nranks, rank, id);
+    if (nranks > 1) {
+        // RCCL binds the communicator to the current device: this rank's, set first
+        HIPCHK(hipSetDevice(device));
+        cm->c.init(nranks, rank, id);
+    }
     *out = cm.release();
     API_END(ctx)
 }
@@ -2343,6 +2349,8 @@ int sbmf_comm_attach(sbmf_ctx* ctx, sbmf_comm* comm) {
     if (!ctx || !comm) sbmf::fail(SBMF_E_ARG, "null argument");
     if (ctx->prepared) sbmf::fail(SBMF_E_STATE, "sbmf_comm_attach must precede sbmf_prepare");
     if (ctx->own_comm.active() || ctx->virt) sbmf::fail(SBMF_E_STATE, "context already joined a communicator");
+    if (comm->nranks > 1 && comm->device != ctx->cfg.device)
+        sbmf::fail(SBMF_E_ARG, "communicator on device %d, context on device %d", comm->device, ctx->cfg.device);
     ctx->nranks = comm->nranks;
     ctx->rank = comm->rank;
     ctx->comm = &comm->c;

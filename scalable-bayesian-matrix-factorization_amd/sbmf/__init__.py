@@ -385,10 +385,10 @@ class Communicator:
     """sbmf_comm_create: one RCCL communicator for the process (ncclCommInitRank once),
     attached in turn by every learner created with ``init(comm=<this>)``."""
 
-    def __init__(self, nranks, rank, uid):
+    def __init__(self, nranks, rank, uid, device=0):
         h = C.c_void_p()
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
-        rc = lib.sbmf_comm_create(nranks, rank, buf, C.byref(h))
+        rc = lib.sbmf_comm_create(device, nranks, rank, buf, C.byref(h))
         if rc != SBMF_OK:
             raise SBMFError(rc, lib.sbmf_last_global_error().decode())
         self.handle, self.nranks, self.rank = h, nranks, rank

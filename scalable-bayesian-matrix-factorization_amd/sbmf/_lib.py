@@ -104,7 +104,7 @@ SIGNATURES = {
     "sbmf_get_timing": (C.c_int, [C.c_void_p, C.POINTER(Timing)]),
     "sbmf_comm_unique_id": (C.c_int, [_P_U8]),
     "sbmf_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _P_U8]),
-    "sbmf_comm_create": (C.c_int, [C.c_int, C.c_int, _P_U8, C.POINTER(C.c_void_p)]),
+    "sbmf_comm_create": (C.c_int, [C.c_int, C.c_int, C.c_int, _P_U8, C.POINTER(C.c_void_p)]),
     "sbmf_comm_attach": (C.c_int, [C.c_void_p, C.c_void_p]),
     "sbmf_comm_destroy": (None, [C.c_void_p]),
     "sbmf_load_triples": (C.c_int, [C.c_char_p, C.POINTER(Ratings)]),

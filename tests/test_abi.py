@@ -136,10 +136,11 @@ def test_shared_communicator_entry_points_check_arguments():
     import ctypes as C
     h = C.c_void_p()
     uid = (C.c_uint8 * 128)()
-    assert _lib.lib.sbmf_comm_create(2, 2, uid, C.byref(h)) == sbmf.SBMF_E_ARG
-    assert _lib.lib.sbmf_comm_create(0, 0, uid, C.byref(h)) == sbmf.SBMF_E_ARG
-    assert _lib.lib.sbmf_comm_create(1, 0, None, C.byref(h)) == sbmf.SBMF_E_ARG
+    assert _lib.lib.sbmf_comm_create(0, 2, 2, uid, C.byref(h)) == sbmf.SBMF_E_ARG
+    assert _lib.lib.sbmf_comm_create(0, 0, 0, uid, C.byref(h)) == sbmf.SBMF_E_ARG
+    assert _lib.lib.sbmf_comm_create(0, 1, 0, None, C.byref(h)) == sbmf.SBMF_E_ARG
+    assert _lib.lib.sbmf_comm_create(-1, 1, 0, uid, C.byref(h)) == sbmf.SBMF_E_ARG
     # a one-rank communicator is a no-op object (no RCCL): created and destroyed without a device
-    assert _lib.lib.sbmf_comm_create(1, 0, uid, C.byref(h)) == sbmf.SBMF_OK and h.value
+    assert _lib.lib.sbmf_comm_create(0, 1, 0, uid, C.byref(h)) == sbmf.SBMF_OK and h.value
     assert _lib.lib.sbmf_comm_attach(None, h) == sbmf.SBMF_E_ARG
     _lib.lib.sbmf_comm_destroy(h)

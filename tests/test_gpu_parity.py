@@ -97,8 +97,8 @@ def test_streaming_kernel_matches_oracle(ml100k, thr, K):
 @pytest.mark.parametrize("chunk", [16, 64, 150])
 @pytest.mark.parametrize("K", [20, 100])
 def test_split_rows_match_oracle(ml100k, chunk, K):
-    """Long rows split over several co-resident workgroups that exchange their
-    per-block (G, c) partials through global memory (cooperative launch)."""
+    """Long rows split over several workgroups (k_gres tasks claimed from the per-XCD
+    queues) that exchange their per-block (G, c) partials through global memory."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=K, iters=3, seed=9)
     L = _run(tr, te, 3, num_factor=K, seed=9, stream_threshold=40, split_chunk=chunk)

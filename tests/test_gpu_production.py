@@ -3,9 +3,11 @@
 bench.py runs the sampler with residuals carried across sweeps
 (recompute_every=0: every half reads the residuals the previous half
 scattered; tau's sum of squares comes from the item half's per-row sums), the
-Philox stream (rng="philox"), the default kernel selection (Gram-block bins,
-the persistent streaming kernel with split rows over co-resident workgroups,
-LDS-capacity task size) and f64.  These tests run exactly that configuration:
+Philox stream (rng="philox"), the default kernel selection (whole-row k_grow
+and Gram-block bins, the queue-claimed streaming kernel k_gres with split rows
+over several workgroups, per-XCD task queues, register-capacity task size), the
+sweep graph (one rank: the steady-state sweep captured once and replayed) and
+f64.  These tests run exactly that configuration:
 
   * ML-100k, reference stream, 100 sweeps: the running-mean test RMSE tracks
     the compiled reference's golden within 1e-6 (as the recompute_every=1
