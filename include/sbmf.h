@@ -137,8 +137,6 @@ typedef struct sbmf_config {
                                  bit 13 = f64 user streaming rows all on one 4-wave k_gres set
                                           (default: rows above 512 ratings on a second, 8-wave set),
                                  bit 14 = (experiment) that second user set on 16-wave workgroups,
-                                 bit 16 = k_gres claims from one task queue (default since round 6:
-                                          per-XCD queues, each split row on one XCD),
                                  bit 17 = k_gres on 16-wave workgroups (both sides),
                                  bit 23 = f64 user streaming rows all on 8-wave k_gres workgroups
                                           (default: up to 512 ratings on 4-wave ones, 512-rating
@@ -161,13 +159,12 @@ typedef struct sbmf_config {
                                  bit 28 = (one rank) the test evaluation after the next sweep's
                                           prologue kernels on the compute stream (default: on the
                                           second stream beside them; the results are the same).
-                                 Every other bit is refused (SBMF_E_ARG): bits 0, 4-6, 15, 18-22
-                                 and 31 selected variants removed in rounds 1-5 (measured slower
-                                 or neutral, kept in git history).  Bits whose meaning changed
-                                 between rounds: 16 (round-4 ablation, now the
-                                 single queue), 24 (round 4: ordinary launch; since round 5 the
-                                 cooperative one), 25 (round-4 LDS-DMA prefetch; since round 5 one
-                                 side stream).  */
+                                 Every other bit is refused (SBMF_E_ARG): bits 0, 4-6, 15, 16,
+                                 18-22 and 31 selected variants removed in rounds 1-6 (measured
+                                 slower or neutral, kept in git history).  Bits whose meaning
+                                 changed between rounds: 24 (round 4: ordinary
+                                 launch; since round 5 the cooperative one), 25 (round-4 LDS-DMA
+                                 prefetch; since round 5 one side stream).  */
     uint32_t method;          /* enum sbmf_method: -method mcmc (default) | vb                   */
     uint32_t vb_batches;      /* online VB: mini-batches per epoch (0 = the reference's 30,
                                  fm_learn_vb_online_simultaneous.h:62)                           */

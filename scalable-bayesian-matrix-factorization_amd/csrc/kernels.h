@@ -38,12 +38,7 @@ struct HalfArgs {
     uint64_t lim_other;    // elements of E_other (N + multi-GPU send area)
     uint64_t lim_this;     // N (part, perm, E_this, r_this)
     uint32_t lim_rows;     // R (own rows; zbuf rows)
-    // graph replay (sweep_graph in sbmf.cpp): this sweep's scalars read from device memory,
-    // DYN_* slots, staged with the hyperparameters; null: the by-value fields above
-    const double* dyn;
 };
-// slots of the device scalar block (sbmf_ctx::d_dyn), written before each replayed sweep
-enum DynSlot { DYN_TAU = 0, DYN_DIV = 1, DYN_COLLECT = 2, DYN_SWEEP_NEXT = 3, DYN_N = 8 };
 
 // Gram-block (MFMA) row kernels.  Max ratings per row for each kind: f64
 // holds 8 vectors (32 ratings) per wave, f32 16 (64 ratings).
@@ -97,17 +92,7 @@ struct SplitSync {
     unsigned long long* prof;  // [8] phase cycles of wave 0 (SBMF_KPROF diagnostics) or null
     uint64_t lim_slab;   // doubles of `slabs` (CHECK=1 builds)
     uint32_t lim_chunk;  // entries of chunk_sq / chunk_tr (and rows of newown)
-    // Per-XCD task queues (nq = 9; nq = 0: the single queue at counters[ncounters]):
-    // queue q holds tasks [qoff[q], qoff[q+1]); queue 0 takes the rows too long to keep
-    // on one XCD, queue 1 + x the rest of XCD x's share.  A workgroup reads its XCD
-    // from HW_REG_XCC_ID and claims from queue 0, then its own XCD's, then the others'
-    // (x+1, x+2, ...), each through its head heads[16 q] (one 64-byte line per head).
-    uint32_t* heads;
-    const uint32_t* qoff;
-    uint32_t nq;
 };
-constexpr uint32_t XCD_QUEUES = 9;  // queue 0 + one per XCD
-constexpr uint32_t HEAD_STRIDE = 16;
 // Task capacity (ratings) of the streaming kernel k_gres for the variant `tune`:
 // 4 * waves * vectors-per-wave, the partner slices held in VGPRs.
 template <typename T>
@@ -118,10 +103,9 @@ int gstream_wg_target(uint32_t tune);
 template <typename T>
 int gstream_blocks_per_cu(uint32_t cmax, uint32_t tune);
 // All streaming tasks of a half-sweep in one persistent launch of `grid`
-// (<= residency) workgroups.  Tasks are claimed in order from queue heads by
-// whichever workgroup is free (one queue, or per-XCD queues: SplitSync); a
-// split row's chunks are consecutive in its queue, so a chunk only waits for
-// peers that the next free workgroups claim.  Split rows
+// (<= residency) workgroups.  Tasks are one list, claimed in order from a queue
+// head by whichever workgroup is free; a split row's chunks are consecutive, so
+// a chunk only waits for peers that the next free workgroups claim.  Split rows
 // are then published by k_split_finish.  sy.counters[0..ncounters] must be zero
 // when the launch starts: sbmf.cpp clears every set's counters with one memset
 // per half, ahead of the half's launches.
@@ -153,12 +137,10 @@ hipError_t launch_colstats(const T* tabA, uint32_t rA, const T* muA, double* out
 // Test predictions: pred = clamp(dot(U[u],V[i])) (+ b0 + bu[u] + bv[i] when bu
 // is non-null: the biased sampler); sum[t] += pred if collect;
 // part[b][0] += (r - sum/div)^2, part[b][1] += (r-pred)^2 per 256-rating block.
-// dyn (non-null in a replayed sweep graph): collect and div read from dyn[DYN_COLLECT], dyn[DYN_DIV]
 template <typename T>
 hipError_t launch_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t t0, uint64_t t1,
                        const T* U, const T* V, uint32_t K, uint32_t Kp, T lo, T hi, int collect, double div,
-                       double* sum, double* part, const double* bu, const double* bv, double b0, hipStream_t st,
-                       const double* dyn = nullptr);
+                       double* sum, double* part, const double* bu, const double* bv, double b0, hipStream_t st);
 
 // Biased sampler (top-level gibbs_sbpmf2.cpp, src/libfm/gibbs_sbpmf22.cpp):
 // per-row bias hyperparameters + bias draw + residual shift, one wave per row
@@ -198,10 +180,9 @@ hipError_t launch_sum_cols2(const double* in, uint32_t nchunk, double* out, cons
 // Philox init: tab[r][k] = sd * z(seed, sweep=0xffffffff, tag, r, k), rows [r0,r1).
 // z[row][k] = N(0,1) Philox normal (seed, sweep, tag, row, pair k/2) for rows [r0, r1):
 // the per-half variates of throughput mode, the same stream the kernels drew inline.
-// dyn (non-null in a replayed sweep graph): the sweep read from dyn[DYN_SWEEP_NEXT]
 template <typename T>
 hipError_t launch_philox_fill(T* z, uint32_t K, uint32_t r0, uint32_t r1, uint64_t seed, uint32_t sweep, uint32_t tag,
-                              hipStream_t st, const double* dyn = nullptr);
+                              hipStream_t st);
 template <typename T>
 hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, double sd, uint64_t seed,
                               uint32_t tag, hipStream_t st);

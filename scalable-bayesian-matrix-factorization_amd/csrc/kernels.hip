@@ -412,7 +412,7 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
         }
     }
     asm volatile("" ::: "memory");  // read back by the other lanes of the wave (LDS keeps its order)
-    const T tau = a.dyn ? (T)a.dyn[DYN_TAU] : a.tau;
+    const T tau = a.tau;
     const T* __restrict__ orow = a.own + (size_t)CHK(row, a.lim_rows) * Kp + ci;
     stamp(0);  // row setup (ids, residuals, normals)
     // software pipeline: block b+1's slices and own/sigma/mu values are in
@@ -601,11 +601,10 @@ __global__ __launch_bounds__(64 * (NW > 1 ? NW : RPW), GBLOCK_OCC(T, V)) void k_
 // The default kernel for rows above the Gram-block bins: one NW-wave workgroup
 // (4, 8 or 16 waves) per task of at most CAP = 4*NW*VW ratings (a whole row, or
 // one equal chunk of a longer row), in one ordinary persistent launch per stream
-// set, tasks claimed from queue heads (per XCD by default) by whichever workgroup
-// is free; a split row's chunks are consecutive in one queue, so a chunk waits
-// only for peers the next free workgroups claim (no co-residency requirement
-// beyond the host's chunk caps).  Wave w owns vectors w, w+NW, ... (4 ratings x
-// 16 k each).
+// set, tasks claimed in list order from a queue head by whichever workgroup is
+// free; a split row's chunks are consecutive, so a chunk waits only for peers
+// the next free workgroups claim (no co-residency requirement).  Wave w owns
+// vectors w, w+NW, ... (4 ratings x 16 k each).
 // The partner slice of the current k-block stays in VGPRs from the accumulate
 // (G_B = S^T S by MFMA, c_B = S^T e) until the apply (e -= S_B D_B) after the
 // block's draws, so each slice is gathered once per half-sweep (k_gstream
@@ -692,7 +691,7 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
     const int rr = lane >> 4;
     const uint32_t K = a.K, Kp = a.Kp;
     const uint32_t nblk = (K + GB - 1) / GB;
-    const T tau = a.dyn ? (T)a.dyn[DYN_TAU] : a.tau;
+    const T tau = a.tau;
     __shared__ uint32_t pjL[CAP];      // partner row offset (row * Kp) per rating slot (zero row past the end)
     __shared__ uint32_t pmL[CAP];      // residual scatter target per rating
     __shared__ T eL[CAP];              // residuals (bit-identical in the 16 lanes of a rating)
@@ -745,17 +744,8 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
     auto eS = [&](uint32_t j) -> T& { return eL[j * JS + lb]; };
 
     // task order: a queue claimed in list order, one returning atomic per task,
-    // so a split row's chunks start as soon as enough workgroups are free.  Per-XCD
-    // queues (sy.nq = 9, the default): the workgroup's XCD from HW_REG_XCC_ID (hwreg
-    // 20, bits 3:0; tests/hip/xcc_probe.hip), queue 0 first, then its own XCD's, then
-    // the other XCDs' in turn once its own is drained.  Only the head a workgroup
-    // claims from decides where a task runs: results never depend on it.  A split
-    // row's chunks sit consecutively in one queue, so each queue has at most one
-    // partly claimed row; the host caps the chunk counts so that all those rows'
-    // waiting chunks together stay below the resident workgroups (build_stream_tasks).
+    // so a split row's chunks start as soon as enough workgroups are free
     __shared__ uint32_t qti;
-    const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 7u;
-    uint32_t qdone = 0;  // thread 0: queues found drained
     // (the task loop in this form, also for the one-task LIST case: written as a task lambda
     // called once or in the loop, k_grow compiles to 50-70 spilled VGPRs instead of 1-2)
     for (uint32_t it = 0;; ++it) {
@@ -764,29 +754,8 @@ __device__ __forceinline__ void gres_run(const SplitTask* __restrict__ tasks, co
             ti = blockIdx.x;
             if (it > 0 || ti >= ntask) break;
         } else {
-            if (threadIdx.x == 0) {
-                if (sy.nq == 0) {
-                    qti = __hip_atomic_fetch_add(sy.counters + sy.ncounters, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    uint32_t got = ntask;
-                    for (uint32_t i = 0; i < sy.nq; ++i) {
-                        const uint32_t q = i == 0 ? 0u : 1u + ((xcc + i - 1u) & 7u);
-                        if (qdone & (1u << q)) continue;
-                        const uint32_t b = sy.qoff[q], e = sy.qoff[q + 1];
-                        if (b < e) {
-                            const uint32_t k = __hip_atomic_fetch_add(sy.heads + HEAD_STRIDE * q, 1u, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT);
-                            if (k < e - b) {
-                                got = b + k;
-                                break;
-                            }
-                        }
-                        qdone |= 1u << q;
-                    }
-                    qti = got;
-                }
-            }
+            if (threadIdx.x == 0)
+                qti = __hip_atomic_fetch_add(sy.counters + sy.ncounters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
             ti = qti;
             __syncthreads();  // every thread has its ticket before thread 0 claims the next
@@ -1297,11 +1266,7 @@ __global__ __launch_bounds__(256) void k_test(const uint32_t* __restrict__ tu, c
                                                uint32_t Kp, T lo, T hi, int collect, double div,
                                                double* __restrict__ sum, double* __restrict__ part,
                                                const double* __restrict__ bu, const double* __restrict__ bv,
-                                               double b0, const double* __restrict__ dyn) {
-    if (dyn) {  // a replayed sweep graph: this sweep's values from device memory
-        collect = dyn[DYN_COLLECT] != 0.0;
-        div = dyn[DYN_DIV];
-    }
+                                               double b0) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ci = lane & 15, rr = lane >> 4;
     // group rr of wave w: ratings gbase + 0..15
@@ -1447,9 +1412,7 @@ __global__ __launch_bounds__(256) void k_sum_cols(const double* __restrict__ in,
 // stream (seed, row, sweep, tag) -- one thread per pair.
 template <typename T>
 __global__ __launch_bounds__(256) void k_philox_fill(T* __restrict__ z, uint32_t K, uint32_t r0, uint32_t r1,
-                                                     uint64_t seed, uint32_t sweep, uint32_t tag,
-                                                     const double* __restrict__ dyn) {
-    if (dyn) sweep = (uint32_t)dyn[DYN_SWEEP_NEXT];  // a replayed sweep graph
+                                                     uint64_t seed, uint32_t sweep, uint32_t tag) {
     const uint32_t npair = (K + 1) / 2;
     const uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t row = r0 + (uint32_t)(x / npair), p = (uint32_t)(x % npair);
@@ -1812,18 +1775,17 @@ hipError_t launch_colstats(const T* tabA, uint32_t rA, const T* muA, double* out
 template <typename T>
 hipError_t launch_test(const uint32_t* tu, const uint32_t* ti, const double* tr, uint64_t t0, uint64_t t1, const T* U,
                        const T* V, uint32_t K, uint32_t Kp, T lo, T hi, int collect, double div, double* sum,
-                       double* part, const double* bu, const double* bv, double b0, hipStream_t st,
-                       const double* dyn) {
+                       double* part, const double* bu, const double* bv, double b0, hipStream_t st) {
     if (t1 <= t0) return hipSuccess;
     const uint64_t nb = (t1 - t0 + 255) / 256;
     // (4 ratings x 4 k-blocks per load round instead of 2 x 8: neutral, r05s7; the user-row
     // reuse: evaluation 0.30 -> 0.26 ms, sweep 7.36 -> 7.32 ms at ML-20M K=100, r05s9)
     if (Kp <= 128)
         k_test<T, 2, 8, true><<<(uint32_t)nb, 256, 0, st>>>(tu, ti, tr, t0, t1, U, V, K, Kp, lo, hi, collect, div, sum,
-                                                            part, bu, bv, b0, dyn);
+                                                            part, bu, bv, b0);
     else
         k_test<T, 2, 8, false><<<(uint32_t)nb, 256, 0, st>>>(tu, ti, tr, t0, t1, U, V, K, Kp, lo, hi, collect, div, sum,
-                                                             part, bu, bv, b0, dyn);
+                                                             part, bu, bv, b0);
     return hipGetLastError();
 }
 
@@ -1858,10 +1820,10 @@ hipError_t launch_sum_cols2(const double* in, uint32_t nchunk, double* out, cons
 
 template <typename T>
 hipError_t launch_philox_fill(T* z, uint32_t K, uint32_t r0, uint32_t r1, uint64_t seed, uint32_t sweep, uint32_t tag,
-                              hipStream_t st, const double* dyn) {
+                              hipStream_t st) {
     if (r1 <= r0 || K == 0) return hipSuccess;
     const uint64_t n = (uint64_t)(r1 - r0) * ((K + 1) / 2);
-    k_philox_fill<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(z, K, r0, r1, seed, sweep, tag, dyn);
+    k_philox_fill<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(z, K, r0, r1, seed, sweep, tag);
     return hipGetLastError();
 }
 
@@ -1918,12 +1880,12 @@ hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, h
                                         uint32_t, T*, double*, double*, const double*, const double*, double,         \
                                         hipStream_t);                                                                \
     template hipError_t launch_philox_fill<T>(T*, uint32_t, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t,        \
-                                              hipStream_t, const double*);                                           \
+                                              hipStream_t);                                                          \
     template hipError_t launch_colstats<T>(const T*, uint32_t, const T*, double*, const T*, uint32_t, const T*,    \
                                            double*, uint32_t, uint32_t, hipStream_t);                                \
     template hipError_t launch_test<T>(const uint32_t*, const uint32_t*, const double*, uint64_t, uint64_t,         \
                                        const T*, const T*, uint32_t, uint32_t, T, T, int, double, double*, double*, \
-                                       const double*, const double*, double, hipStream_t, const double*);           \
+                                       const double*, const double*, double, hipStream_t);                          \
     template hipError_t launch_init_philox<T>(T*, uint32_t, uint32_t, uint32_t, uint32_t, double, uint64_t,          \
                                               uint32_t, hipStream_t);                                                \
     template hipError_t launch_bias_rows<T>(const uint32_t*, uint32_t, uint32_t, T*, double*, double*, double*,      \

@@ -69,7 +69,6 @@ struct Side {
         uint32_t sgrid = 0;             // persistent grid of the launch
         uint32_t cmax = 0;              // task capacity (ratings)
         uint32_t tune = 0;              // kernel variant bits of the launch
-        std::vector<uint32_t> qoff;     // per-XCD queues: [XCD_QUEUES + 1] task bounds (empty: one queue)
     };
     // A stage: the rows [r0, r1) of this rank's block, binned for their own launches.
     // One stage per half unless the multi-GPU exchange is pipelined: then the block is
@@ -81,7 +80,7 @@ struct Side {
         std::vector<uint32_t> bin_rows[NBIN];  // kinds: GK_* (0..4), KIND_STREAM (5)
         StreamSet ss[2];
         std::vector<std::array<uint32_t, 3>> gsub[GK_NUM];  // multi-wave bins: (waves, offset, count) sub-ranges
-        DBuf d_bins[NBIN], d_stasks[2], d_xrows[2], d_qoff[2];
+        DBuf d_bins[NBIN], d_stasks[2], d_xrows[2];
         // multi-GPU residual exchange of this stage: [peer] segments of the send / receive areas
         std::vector<size_t> soff, scnt, roff, rcnt;
         size_t rbeg = 0, rend = 0;  // this stage's receive elements [rbeg, rend)
@@ -356,21 +355,8 @@ struct sbmf_ctx {
     // use them (pre dropped by sbmf_set_factors) restores the current ones before its
     // prologue, whose column statistics read the current mu from d_hyper
     bool hyper_ahead = false;
-    // One rank, throughput mode: the steady-state sweep captured once as a hipGraph and
-    // replayed (run_sweeps_T, sweep_graph): one launch per sweep instead of ~40 host calls.
-    // Its per-sweep scalars (tau, the evaluation's collect / divisor, the next sweep's Philox
-    // index) live in d_hyper past the hyperparameters (dyn_off), staged with them.
-    bool capturing = false;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t gexec = nullptr;
-    int graph_key = -1;  // the captured prologue's recompute decision (-1: nothing captured)
-    uint32_t graph_nlaunch = 0;
-    hipEvent_t gdep[2] = {};  // capture-internal fork / join of the evaluation on sto
-    size_t dyn_off = 0;       // bytes into d_hyper
-    double* d_dyn() { return reinterpret_cast<double*>(static_cast<char*>(d_hyper.p) + dyn_off); }
     double* h_pinned = nullptr;  // pinned staging for z streams
     size_t h_pinned_bytes = 0, h_pre_bytes = 0, h_io_bytes = 0;
-    size_t xheads_off = 0;  // d_xcnt: first per-XCD queue head (uint32 index)
     sbmf_timing timing{};
     VBLearner* vb = nullptr;  // -method vb (vbo.cpp)
     FMLearner* fm = nullptr;  // -method mcmc --order libfm / als (fmm.cpp)
@@ -420,7 +406,7 @@ static void ensure_pinned(sbmf_ctx* c, size_t bytes) {
 
 static void fill_kernel_bytes(sbmf_ctx* c);
 static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vector<uint32_t>& rows, uint32_t gres,
-                               uint32_t nblk, uint32_t rmin, bool xcd);
+                               uint32_t nblk);
 
 // ------------------------------------------------------------------ prepare
 template <typename T>
@@ -542,28 +528,20 @@ static void prepare_T(sbmf_ctx* c) {
                 const uint32_t d = sd->ptr[r + 1] - sd->ptr[r];
                 rows[(item16 && d > 1024u) || (user2 && d > 512u) ? 1 : 0].push_back(r);
             }
-            bool splits[2] = {false, false};  // the set has rows longer than one task
             for (int k = 0; k < 2; ++k) {
                 Side::StreamSet& S = gp->ss[k];
                 S.tune = stunes[k];
                 // task capacity: the kernel's on-chip maximum, or smaller if split_chunk asks
                 S.cmax = gstream_cmax<T>(S.tune);
                 if (cf.split_chunk) S.cmax = std::min(S.cmax, std::max(cf.split_chunk, 1u));
-                for (uint32_t r : rows[k]) splits[k] = splits[k] || sd->ptr[r + 1] - sd->ptr[r] > S.cmax;
-            }
-            for (int k = 0; k < 2; ++k) {
-                Side::StreamSet& S = gp->ss[k];
                 // (fewer persistent workgroups per CU, leaving CU slots to the Gram-block launches
                 // beside the streaming one from its start: user 3 / 2 per CU +0.03 / +0.13 ms, item
                 // 8-wave set 1 per CU +0.2 ms per sweep, r05s8)
                 const int per_cu =
                     std::max(1, std::min(gstream_wg_target(S.tune), gstream_blocks_per_cu<T>(S.cmax, S.tune)));
-                // per-XCD task queues (default; tune bit 16 keeps the single queue).  The residency
-                // every launch reaches: its workgroups on every CU (the two sets of a half run side
-                // by side: on half the CUs when the other set has split rows too, whose waiting
-                // chunks may hold the rest)
-                const uint32_t rmin = (uint32_t)(splits[1 - k] ? dev_cus / 2 : dev_cus) * (uint32_t)per_cu;
-                build_stream_tasks(*sd, S, rows[k], (uint32_t)(dev_cus * per_cu), nblk, rmin, !(cf.tune & 0x10000u));
+                // (per-XCD task queues, each split row on one XCD: item stage 3.59 -> 3.77 ms standalone,
+                // r06s3; removed, profiles/r06/ab/r06s3_xcd_queues.patch)
+                build_stream_tasks(*sd, S, rows[k], (uint32_t)(dev_cus * per_cu), nblk);
             }
             }
         }
@@ -614,7 +592,6 @@ static void prepare_T(sbmf_ctx* c) {
                 const Side::StreamSet& S = g->ss[k];
                 upload(g->d_stasks[k], S.stasks, st);
                 upload(g->d_xrows[k], S.xrows, st);
-                upload(g->d_qoff[k], S.qoff, st);
                 nxk[k] = std::max<size_t>(nxk[k], S.nxchunk);
                 nrk[k] = std::max<size_t>(nrk[k], S.xrows.size());
             }
@@ -623,12 +600,10 @@ static void prepare_T(sbmf_ctx* c) {
     {
         const size_t nx = c->xset_nx + std::max<size_t>(nxk[1], 1), nr = c->xset_nr + std::max<size_t>(nrk[1], 1);
         c->d_xslabs.alloc(nx * nblk * (16 * 16 + 16) * sizeof(double));
-        // + each set's task-queue head, then (from a 64-byte boundary) the two sets' per-XCD
-        // queue heads, one 64-byte line each; a whole number of 16-byte words, so that clearing
-        // it is one fill kernel (a ragged size is three, and on a stream beside a persistent
+        // + each set's task-queue head; a whole number of 16-byte words, so that clearing it
+        // is one fill kernel (a ragged size is three, and on a stream beside a persistent
         // launch the tail one waited for that launch: r04s4 trace)
-        c->xheads_off = (nr * nblk + 2 + HEAD_STRIDE - 1) / HEAD_STRIDE * HEAD_STRIDE;
-        c->d_xcnt.alloc((c->xheads_off + 2 * XCD_QUEUES * HEAD_STRIDE) * sizeof(uint32_t));
+        c->d_xcnt.alloc((nr * nblk + 2 + 3) / 4 * 4 * sizeof(uint32_t));
         c->xcnt_clean = false;
         c->d_xchunk_sq.alloc(nx * sizeof(double));
         c->d_xchunk_tr.alloc(nx * sizeof(double));
@@ -663,10 +638,8 @@ static void prepare_T(sbmf_ctx* c) {
     c->d_rowtr_v.alloc((size_t)c->J * sizeof(double));
     HIPCHK(hipMemsetAsync(c->d_rowsq_v.p, 0, c->d_rowsq_v.bytes, st));
     HIPCHK(hipMemsetAsync(c->d_rowtr_v.p, 0, c->d_rowtr_v.bytes, st));
-    // [sig_u | mu_u | sig_v | mu_v], each Kp long and zero padded, + 16 slack for prefetch,
-    // then the DYN_N per-sweep scalars of a replayed sweep graph (doubles, 8-byte aligned)
-    c->dyn_off = (4 * (size_t)c->Kp + 16) * sizeof(T);
-    c->d_hyper.alloc(c->dyn_off + DYN_N * sizeof(double));
+    // [sig_u | mu_u | sig_v | mu_v], each Kp long and zero padded, + 16 slack for prefetch
+    c->d_hyper.alloc((4 * (size_t)c->Kp + 16) * sizeof(T));
     HIPCHK(hipMemsetAsync(c->d_hyper.p, 0, c->d_hyper.bytes, st));
     const uint32_t nchunk = (c->I + 255) / 256 + (c->J + 255) / 256;  // both tables' 256-row chunks
     c->d_colpart.alloc((size_t)nchunk * 2 * c->K * sizeof(double));
@@ -676,7 +649,7 @@ static void prepare_T(sbmf_ctx* c) {
     c->h_pre_bytes = c->h_res.size() * sizeof(double);
     pinned_alloc((void**)&c->h_pre, c->h_pre_bytes);
     pinned_free(c->h_io, c->h_io_bytes);
-    c->h_io_bytes = 128 + c->dyn_off + DYN_N * sizeof(double);
+    c->h_io_bytes = 128 + 4 * (size_t)c->Kp * sizeof(T);
     pinned_alloc(&c->h_io, c->h_io_bytes);
     c->pre.valid = false;
     c->hyper_ahead = false;
@@ -788,32 +761,16 @@ static void prepare_T(sbmf_ctx* c) {
 // equal chunks of a longer row) in one list, largest rows first, claimed in
 // order by the running workgroups of a launch of `gres` workgroups (k_gres'
 // queue); a split row's chunks are consecutive.
-//
-// Per-XCD queues (xcd): the tasks go to XCD_QUEUES queues (SplitSync), each in
-// degree-descending order with a split row's chunks consecutive.  The rows are
-// dealt largest first to the XCD with the fewest ratings so far (a split row
-// whole to one XCD: its block hand-offs are claimed by one XCD's workgroups, the
-// dequeues spread over 8 heads instead of one -- MI355X_MICROARCH.md rows
-// dequeue, handoff-payload); queue 0, claimed first by every workgroup, takes the
-// rows of more than `cx` chunks.  Deadlock freedom: each queue has at most one
-// partly claimed split row, whose claimed chunks wait for its unclaimed ones; a
-// free workgroup always claims, so the launch can only stall if every workgroup
-// waits, which needs 8 (cx - 1) + (largest queue-0 row - 1) >= resident
-// workgroups.  `rmin` is a residency every launch reaches (prepare_T), and cx is
-// the largest count that keeps the sum below it (no split rows go to the XCD
-// queues when none does).
 static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vector<uint32_t>& rows, uint32_t gres,
-                               uint32_t nblk, uint32_t rmin, bool xcd) {
+                               uint32_t nblk) {
     const uint32_t cmax = S.cmax;
     S.stasks.clear();
     S.xrows.clear();
-    S.qoff.clear();
     S.nxchunk = 0;
     S.sgrid = 0;
-    auto nchunks = [&](uint32_t r) { return (s.ptr[r + 1] - s.ptr[r] + cmax - 1) / cmax; };
-    auto push_row = [&](uint32_t r) {
+    for (uint32_t r : rows) {  // rows: degree-descending
         const uint32_t n = s.ptr[r + 1] - s.ptr[r];
-        const uint32_t nch = nchunks(r);
+        const uint32_t nch = (n + cmax - 1) / cmax;
         if (nch > gres)
             fail(SBMF_E_ARG, "row %u has %u ratings: more than %u co-resident chunks of %u", r, n, gres, cmax);
         if (nch == 1) {
@@ -829,61 +786,8 @@ static void build_stream_tasks(const Side& s, Side::StreamSet& S, const std::vec
             S.xrows.push_back(SplitRow{r, slab0, nch, 0});
             S.nxchunk += nch;
         }
-    };
-    if (!xcd || rows.empty()) {
-        for (uint32_t r : rows) push_row(r);  // rows: degree-descending
-        S.sgrid = std::min<uint32_t>(gres, (uint32_t)S.stasks.size());
-        return;
-    }
-    // the largest XCD-queue chunk count cx with 8 (cx - 1) + (max queue-0 chunks - 1) < rmin
-    std::vector<uint32_t> nchs;
-    for (uint32_t r : rows) nchs.push_back(nchunks(r));  // non-increasing (rows degree-descending)
-    const uint32_t top = nchs.empty() ? 1u : nchs[0];
-    uint32_t cx = 1;
-    for (uint32_t c = top; c >= 2; --c) {
-        uint32_t g0 = 0;  // largest chunk count left to queue 0
-        for (uint32_t x : nchs)
-            if (x > c) g0 = std::max(g0, x);
-        if (8ull * (c - 1) + (g0 ? g0 - 1 : 0) < rmin) {
-            cx = c;
-            break;
-        }
-    }
-    std::vector<std::vector<uint32_t>> q(XCD_QUEUES);
-    std::vector<uint64_t> load(XCD_QUEUES - 1, 0);
-    for (size_t i = 0; i < rows.size(); ++i) {
-        if (nchs[i] > cx) {
-            q[0].push_back(rows[i]);
-            continue;
-        }
-        const size_t x = (size_t)(std::min_element(load.begin(), load.end()) - load.begin());
-        load[x] += s.ptr[rows[i] + 1] - s.ptr[rows[i]];
-        q[1 + x].push_back(rows[i]);
-    }
-    S.qoff.push_back(0);
-    for (const auto& qq : q) {
-        for (uint32_t r : qq) push_row(r);
-        S.qoff.push_back((uint32_t)S.stasks.size());
     }
     S.sgrid = std::min<uint32_t>(gres, (uint32_t)S.stasks.size());
-    // the bound above assumed rmin resident workgroups; a smaller grid tightens it
-    if (S.sgrid < rmin) {
-        uint32_t wait = 0;  // the most claimed-and-waiting chunks the queues can hold at once
-        for (uint32_t k = 0; k < XCD_QUEUES; ++k) {
-            uint32_t m = 0;
-            for (uint32_t t = S.qoff[k]; t < S.qoff[k + 1]; ++t) m = std::max(m, S.stasks[t].nch);
-            wait += m ? m - 1 : 0;
-        }
-        if (wait >= S.sgrid) {  // one queue then: its one partly claimed row waits for < sgrid peers
-            std::vector<uint32_t> all(rows);
-            S.stasks.clear();
-            S.xrows.clear();
-            S.qoff.clear();
-            S.nxchunk = 0;
-            for (uint32_t r : all) push_row(r);
-            S.sgrid = std::min<uint32_t>(gres, (uint32_t)S.stasks.size());
-        }
-    }
 }
 
 // ------------------------------------------------------------------ one sweep
@@ -1065,7 +969,6 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     a.tune = c->cfg.tune;
     a.prof = c->kprof ? c->d_kprof.as<unsigned long long>() + 16 + 8 * (users ? 0 : 1) : nullptr;
     a.tau = (T)c->tau;
-    a.dyn = c->capturing ? c->d_dyn() : nullptr;  // a captured sweep reads tau from device memory
     a.K = c->K;
     a.Kp = c->Kp;
     a.sd_is_var = c->sd_is_var;
@@ -1081,12 +984,6 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     // otherwise every rank reads the residuals the exchange delivered
     a.e_from_dot = (c->cfg.tune & 2u) ? 1 : 0;
     return a;
-}
-
-// An event the host reads (timing, hipEventSynchronize): inside a captured sweep an
-// external event-record node, so that every replay records it.
-static void mark(sbmf_ctx* c, hipEvent_t e, hipStream_t s) {
-    HIPCHK(c->capturing ? hipEventRecordWithFlags(e, s, hipEventRecordExternal) : hipEventRecord(e, s));
 }
 
 template <typename T>
@@ -1144,7 +1041,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         int& lk = last[st == c->st ? 0 : st == c->sto ? 1 : 2];
         if (timed) {
             c->kpv(stage, sd, k) = (int8_t)lk;
-            if (lk < 0) mark(c, c->kev(stage, sd, k, 0), st);
+            if (lk < 0) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
             lk = k;
         } else {
             lk = -1;  // no end event behind this launch
@@ -1193,9 +1090,6 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 sy.lim_slab = (uint64_t)(c->d_xslabs.bytes / sizeof(double)) - ox * sy.nblk * (16 * 16 + 16);
                 sy.lim_chunk = (uint32_t)(c->d_xchunk_sq.bytes / sizeof(double) - ox);
                 sy.prof = c->kprof && set == c->kprof_set ? c->d_kprof.as<unsigned long long>() + 8 * (users ? 0 : 1) : nullptr;
-                sy.nq = S.qoff.empty() ? 0u : XCD_QUEUES;
-                sy.qoff = g.d_qoff[set].as<uint32_t>();
-                sy.heads = c->d_xcnt.as<uint32_t>() + c->xheads_off + (size_t)set * XCD_QUEUES * HEAD_STRIDE;
                 HalfArgs<T> as = a;
                 as.tune = S.tune;
                 HIPCHK(launch_gstream<T>(g.d_stasks[set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
@@ -1211,7 +1105,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
             c->xcnt_clean = true;
         }
         // (after the memset: a kind launched next on this stream starts its time at this event)
-        if (timed) mark(c, c->kev(stage, sd, k, 1), st);
+        if (timed) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
         c->timing.n_launch++;
     }
     if (side) {
@@ -1311,7 +1205,7 @@ static void run_half_pipelined(sbmf_ctx* c, bool users, F&& bcasts) {
         if (c->nranks > 1) HIPCHK(hipEventRecord(c->sev[(size_t)sd * c->nstages + p], c->st));
         if (c->virt) HIPCHK(hipEventRecord(c->tsev[tb + p + 1], c->st));
     }
-    mark(c, c->ev[users ? 2 : 4], c->st);
+    HIPCHK(hipEventRecord(c->ev[users ? 2 : 4], c->st));
     if (c->nranks <= 1) return;  // no exchange: ev[3] / ev[5] are not recorded (the sweep uses ev[2] / ev[4])
     for (uint32_t p = 0; p < c->nstages; ++p) {
         HIPCHK(hipStreamWaitEvent(c->stc, c->sev[(size_t)sd * c->nstages + p], 0));
@@ -1319,18 +1213,6 @@ static void run_half_pipelined(sbmf_ctx* c, bool users, F&& bcasts) {
     }
     HIPCHK(hipEventRecord(c->cev[sd], c->stc));
     HIPCHK(hipStreamWaitEvent(c->st, c->cev[sd], 0));
-}
-
-static bool graph_enabled() {
-    const char* e = std::getenv("SBMF_GRAPH");
-    return !(e && std::strcmp(e, "0") == 0);
-}
-static void destroy_graph(sbmf_ctx* c) {
-    if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
-    if (c->graph) (void)hipGraphDestroy(c->graph);
-    c->gexec = nullptr;
-    c->graph = nullptr;
-    c->graph_key = -1;
 }
 
 template <typename T>
@@ -1446,30 +1328,19 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
     hipEvent_t& ev5 = c->nranks > 1 ? c->ev[5] : c->ev[4];
     // the sweep's hyperparameters [sig_u | mu_u | sig_v | mu_v] into the pinned staging area
     // and on to d_hyper (stream order: after every launch already queued that reads it)
-    // + the per-sweep scalars of sweep `sw` (tau_sw) that a replayed sweep graph reads (DYN_*):
-    // the evaluation's collect flag and divisor as run_sweeps_T computes them when sweep sw's
-    // evaluation is queued (c->collected counts the sweeps collected before sw at this point)
     auto stage_hyper = [&](const std::vector<double>& su, const std::vector<double>& mu, const std::vector<double>& sv,
-                           const std::vector<double>& mv, uint32_t sw, double tau_sw) {
+                           const std::vector<double>& mv) {
         const size_t Kp = c->Kp;
         T* h = static_cast<T*>(c->h_hyper());
         HIPCHK(hipEventSynchronize(c->hev));
-        std::fill(h, h + 4 * Kp + 16, T(0));
+        std::fill(h, h + 4 * Kp, T(0));
         for (uint32_t k = 0; k < K; ++k) {
             h[k] = (T)su[k];
             h[Kp + k] = (T)mu[k];
             h[2 * Kp + k] = (T)sv[k];
             h[3 * Kp + k] = (T)mv[k];
         }
-        double* dyn = reinterpret_cast<double*>(static_cast<char*>(c->h_hyper()) + c->dyn_off);
-        const bool col = q2 ? true : (sw >= cf.burnin);
-        const uint32_t ncol = c->collected + (col ? 1u : 0u);
-        std::fill(dyn, dyn + DYN_N, 0.0);
-        dyn[DYN_TAU] = tau_sw;
-        dyn[DYN_COLLECT] = col ? 1.0 : 0.0;
-        dyn[DYN_DIV] = avg_collected(cf) ? (double)std::max(1u, ncol) : (double)(sw + 1);
-        dyn[DYN_SWEEP_NEXT] = (double)(sw + 1);
-        HIPCHK(hipMemcpyAsync(c->d_hyper.p, h, c->dyn_off + DYN_N * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(c->d_hyper.p, h, 4 * Kp * sizeof(T), hipMemcpyHostToDevice, st));
         HIPCHK(hipEventRecord(c->hev, st));
     };
     for (uint32_t it = 0; it < nsweeps; ++it) {
@@ -1480,7 +1351,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         // throughput mode: this sweep's hyperparameters already on the device and its normals
         // filled (both queued at the end of the previous sweep)
         const bool staged = c->pre.valid && c->pre.sweep == c->sweep && c->pre.staged;
-        if (!staged && c->hyper_ahead) stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v, c->sweep, c->tau);
+        if (!staged && c->hyper_ahead) stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v);
         c->hyper_ahead = false;
         if (c->pre.valid && c->pre.sweep == c->sweep) {  // drawn at the end of the previous sweep
             c->tau = c->pre.tau;
@@ -1507,7 +1378,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         c->pre.valid = false;
         c->pre.staged = false;
         if (!staged) {
-            stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v, c->sweep, c->tau);
+            stage_hyper(c->sig_u, c->mu_u, c->sig_v, c->mu_v);
             if (ref && c->bias) {
                 fill_bias_variates<T>(c);
             } else if (ref) {  // user variates then item variates (:485 then :529)
@@ -1523,11 +1394,12 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         const double div = avg_collected(cf) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
         const uint64_t T_ = c->su.size();
         const bool par_eval = overlap && c->nranks == 1 && !(cf.tune & 0x10000000u);
-        // The sweep's device work, from the user half to the results' copy.  With the overlap the
-        // next sweep's prologue kernels and normals are part of it; in a captured sweep (graph
-        // mode) every per-sweep scalar comes from d_dyn, staged with the hyperparameters.
-        auto body = [&]() {
-        const double* dyn = c->capturing ? c->d_dyn() : nullptr;
+        // The sweep's device work, from the user half to the results' copy (with the overlap the
+        // next sweep's prologue kernels and normals are part of it).  (Captured once as a hipGraph
+        // and replayed, one rank: ML-1M K=50 0.45 -> 0.77-0.90 ms, ML-20M 7.11 -> 7.57-7.82 ms
+        // per sweep, r06s3 -- the halves unchanged, the replay slower than the eager launches;
+        // removed, profiles/r06/ab/r06s3_sweep_graph.patch)
+        {
         // ---- 3. user half-sweep (throughput mode: this half's normals first)
         if (!ref && !staged)
             HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep, TAG_USERS, st));
@@ -1566,73 +1438,35 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 HIPCHK(launch_test<T>(c->d_tu.as<uint32_t>(), c->d_ti.as<uint32_t>(), c->d_tr.as<double>(), c->t0,
                                       c->t1, c->d_U.as<T>(), c->d_V.as<T>(), K, c->Kp, (T)c->lo, (T)c->hi,
                                       collect ? 1 : 0, div, c->d_tsum.as<double>(), c->d_tpart.as<double>(),
-                                      c->bias ? c->d_bu.as<double>() : nullptr, c->d_bv.as<double>(), c->b0, se, dyn));
+                                      c->bias ? c->d_bu.as<double>() : nullptr, c->d_bv.as<double>(), c->b0, se));
                 if (c->nranks > 1) c->comm->bcast_ranges(c->d_tpart.p, 2 * sizeof(double), c->tbblocks, se);
                 const uint32_t nb = (uint32_t)((T_ + 255) / 256);
                 HIPCHK(launch_sum_cols(c->d_tpart.as<double>(), nb, 2, d_res + RES_TEST_AVG, se));
             }
             if (cf.eval_train)
                 HIPCHK(launch_sum(c->d_rowtr_v.as<double>(), c->J, d_res + RES_TRSQ, scratch + c->scratch_half, se));
-            mark(c, c->ev[6], se);
-            if (c->capturing && se != st) HIPCHK(hipEventRecord(c->gdep[1], se));  // the capture's join
+            HIPCHK(hipEventRecord(c->ev[6], se));
         };
         if (par_eval) {
-            if (c->capturing) {  // ev5 is an external node in a capture: fork on an internal event
-                HIPCHK(hipEventRecord(c->gdep[0], st));
-                HIPCHK(hipStreamWaitEvent(c->sto, c->gdep[0], 0));
-            } else {
-                HIPCHK(hipStreamWaitEvent(c->sto, ev5, 0));
-            }
+            HIPCHK(hipStreamWaitEvent(c->sto, ev5, 0));
             evaluate(c->sto);
         }
         if (overlap) {  // the next sweep's prologue kernels, ahead of the evaluation
             prologue_gpu(c->sweep + 1);
-            mark(c, c->ev[7], st);
+            HIPCHK(hipEventRecord(c->ev[7], st));
             // and the next sweep's normals (Philox: a function of (seed, sweep) only; this
             // sweep's halves, which read them, are queued before)
             HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep + 1, TAG_USERS,
-                                         st, dyn));
+                                         st));
             HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep + 1, TAG_ITEMS,
-                                         st, dyn));
-            mark(c, c->ev[8], st);  // the next sweep's start work ends here
+                                         st));
+            HIPCHK(hipEventRecord(c->ev[8], st));  // the next sweep's start work ends here
         }
         if (par_eval)
-            HIPCHK(hipStreamWaitEvent(st, c->capturing ? c->gdep[1] : c->ev[6], 0));
+            HIPCHK(hipStreamWaitEvent(st, c->ev[6], 0));
         else
             evaluate(st);
         HIPCHK(hipMemcpyAsync(c->h_out(), d_res, 8 * sizeof(double), hipMemcpyDeviceToHost, st));
-        };
-        // Graph mode: the steady-state sweep of one rank in throughput mode (its start work staged
-        // by the previous sweep, launch kinds untimed) is captured once and replayed; a sweep of
-        // another shape (a run's first, one whose prologue recomputes differently) runs eagerly.
-        // SBMF_GRAPH=0 keeps every sweep eager (the chain is the same either way).
-        const int key = (cf.recompute_every && (c->sweep + 1) % cf.recompute_every == 0) ? 1 : 0;
-        const bool use_graph = graph_enabled() && overlap && par_eval && staged && !c->time_kinds && c->nranks == 1 &&
-                               !c->virt && !c->bias && !c->kprof && !(cf.tune & 0x1000000u);
-        if (use_graph) {
-            if (!c->gexec || c->graph_key != key) {
-                destroy_graph(c);
-                HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-                c->capturing = true;
-                try {
-                    body();
-                } catch (...) {
-                    c->capturing = false;
-                    hipGraph_t g = nullptr;
-                    (void)hipStreamEndCapture(st, &g);
-                    if (g) (void)hipGraphDestroy(g);
-                    throw;
-                }
-                c->capturing = false;
-                HIPCHK(hipStreamEndCapture(st, &c->graph));
-                HIPCHK(hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0));
-                c->graph_key = key;
-                c->graph_nlaunch = c->timing.n_launch;
-            }
-            HIPCHK(hipGraphLaunch(c->gexec, st));
-            c->timing.n_launch = c->graph_nlaunch;
-        } else {
-            body();
         }
         if (overlap) {  // the next sweep's draws while the evaluation runs; this sweep's values kept
             HIPCHK(hipEventSynchronize(c->ev[7]));
@@ -1662,7 +1496,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             c->pre.valid = true;
             // the next sweep's hyperparameters to the device now (every launch of this sweep that
             // reads d_hyper -- the halves and the prologue's column statistics -- is queued before)
-            stage_hyper(c->pre.sig_u, c->pre.mu_u, c->pre.sig_v, c->pre.mu_v, c->sweep + 1, c->pre.tau);
+            stage_hyper(c->pre.sig_u, c->pre.mu_u, c->pre.sig_v, c->pre.mu_v);
             c->pre.staged = true;
             c->hyper_ahead = true;
         }
@@ -1757,8 +1591,6 @@ sbmf_ctx::~sbmf_ctx() {
     vbo_destroy(vb);
     fmm_destroy(fm);
     using namespace sbmf;
-    destroy_graph(this);
-    for (hipEvent_t& e : gdep) event_destroy(e);
     pinned_free(h_pinned, h_pinned_bytes);
     pinned_free(h_pre, h_pre_bytes);
     pinned_free(h_io, h_io_bytes);
@@ -1975,7 +1807,7 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
         // is refused, so a value saved for an older build does not silently pick something else
         // (INTEGRATION.md lists what changed between rounds)
         constexpr uint32_t known = (1u << 1) | (1u << 2) | (1u << 3) | (1u << 7) | (1u << 8) | (1u << 9) | (1u << 10) |
-                                   (1u << 11) | (1u << 12) | (1u << 13) | (1u << 14) | (1u << 16) | (1u << 17) |
+                                   (1u << 11) | (1u << 12) | (1u << 13) | (1u << 14) | (1u << 17) |
                                    (1u << 23) | (1u << 24) | (1u << 25) | (1u << 26) | (1u << 27) | (1u << 28) |
                                    (1u << 29) | (1u << 30);
         if (cfg->tune & ~known)
@@ -2015,7 +1847,6 @@ int sbmf_create(const sbmf_config* cfg, sbmf_ctx** out) {
     sbmf::stream_create(&c->sto2);
     for (auto& e : c->oev) sbmf::event_create(&e, hipEventDisableTiming);
     sbmf::event_create(&c->hev, hipEventDisableTiming);
-    for (auto& e : c->gdep) sbmf::event_create(&e, hipEventDisableTiming);
     *out = c.release();
     API_END(ctx)
 }

@@ -119,14 +119,14 @@ def test_unassigned_tune_bits_are_refused():
     or picking whatever the bit means now."""
     import ctypes as C
     ctx = C.c_void_p()
-    for bit in (0, 4, 5, 6, 15, 18, 19, 20, 21, 22, 31):
+    for bit in (0, 4, 5, 6, 15, 16, 18, 19, 20, 21, 22, 31):
         cfg = sbmf.config_default()
         cfg.tune = 1 << bit
         assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_ARG, bit
         assert "tune bits" in _lib.lib.sbmf_last_global_error().decode()
     if not gpu_available():  # an assigned bit passes the check and reaches the device check
         cfg = sbmf.config_default()
-        cfg.tune = (1 << 16) | (1 << 29)
+        cfg.tune = (1 << 17) | (1 << 29)
         assert _lib.lib.sbmf_create(C.byref(cfg), C.byref(ctx)) == sbmf.SBMF_E_DEVICE
 
 

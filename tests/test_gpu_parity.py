@@ -97,8 +97,8 @@ def test_streaming_kernel_matches_oracle(ml100k, thr, K):
 @pytest.mark.parametrize("chunk", [16, 64, 150])
 @pytest.mark.parametrize("K", [20, 100])
 def test_split_rows_match_oracle(ml100k, chunk, K):
-    """Long rows split over several workgroups (k_gres tasks claimed from the per-XCD
-    queues) that exchange their per-block (G, c) partials through global memory."""
+    """Long rows split over several workgroups (k_gres tasks claimed from the task
+    queue) that exchange their per-block (G, c) partials through global memory."""
     tr, te = ml100k
     o = oracle.run(tr, te, K=K, iters=3, seed=9)
     L = _run(tr, te, 3, num_factor=K, seed=9, stream_threshold=40, split_chunk=chunk)
@@ -199,34 +199,3 @@ def test_philox_deterministic_and_init_matches_host(ml100k):
     Ub, Vb = b.factors()
     assert np.array_equal(Ua, Ub) and np.array_equal(Va, Vb)
     assert np.array_equal(a.rmse_trajectory, b.rmse_trajectory)
-
-
-@pytest.mark.parametrize("kw", [dict(recompute_every=0), dict(recompute_every=1),
-                                dict(recompute_every=3, burnin=2, average="collected"),
-                                dict(recompute_every=0, precision="f32")])
-def test_sweep_graph_changes_nothing(ml100k, kw, monkeypatch):
-    """Graph mode (one rank, throughput mode): the steady-state sweep -- both halves, the
-    evaluation beside the next sweep's prologue and normals, the results' copy -- is
-    captured once as a hipGraph and replayed, its per-sweep scalars (tau, the evaluation's
-    collect flag and divisor, the next sweep's Philox index) read from device memory.
-    The chain, the per-sweep reports and the factors equal the eager launches' bit for
-    bit (SBMF_GRAPH=0), across runs (learn called twice), a burn-in that flips the collect
-    flag, and prologues that recompute on some sweeps only (two captured shapes)."""
-    tr, te = ml100k
-    base = dict(num_factor=30, seed=8, rng="philox", eval_train=True, **kw)
-    monkeypatch.setenv("SBMF_GRAPH", "0")
-    a = _run(tr, te, 8, **base)
-    monkeypatch.setenv("SBMF_GRAPH", "1")
-    L = FMLearnSBPMF(**base)
-    L.set_data(Data(*tr), Data(*te))
-    L.learn(sweeps=5)
-    L.learn(sweeps=3)
-    for f in ("rmse_avg", "rmse_this", "rmse_train", "tau", "sweep"):
-        assert np.array_equal([h[f] for h in a.history], [h[f] for h in L.history]), f
-    for x, y in zip(a.factors(), L.factors()):
-        assert np.array_equal(x, y)
-    t = L.timing()
-    assert L.history[-1]["ms_sweep"] > 0 and t.ms_user_half > 0 and t.ms_item_half > 0 and t.ms_eval > 0
-    # the streaming kind's events are replayed too (f32: no ML-100k row passes its 512-rating threshold)
-    assert t.kern_ms[1][5] > 0 or t.kern_rows[1][5] == 0
-    assert np.array_equal(L.predict(), a.predict())

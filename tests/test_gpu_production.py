@@ -5,9 +5,8 @@ bench.py runs the sampler with residuals carried across sweeps
 scattered; tau's sum of squares comes from the item half's per-row sums), the
 Philox stream (rng="philox"), the default kernel selection (whole-row k_grow
 and Gram-block bins, the queue-claimed streaming kernel k_gres with split rows
-over several workgroups, per-XCD task queues, register-capacity task size), the
-sweep graph (one rank: the steady-state sweep captured once and replayed) and
-f64.  These tests run exactly that configuration:
+over several workgroups, register-capacity task size) and f64.  These tests run
+exactly that configuration:
 
   * ML-100k, reference stream, 100 sweeps: the running-mean test RMSE tracks
     the compiled reference's golden within 1e-6 (as the recompute_every=1
