@@ -121,6 +121,11 @@ def device_sync():
         raise RuntimeError("hipDeviceSynchronize failed: %d" % rc)
 
 
+def _lib_kind_names():
+    from sbmf._lib import KIND_NAMES
+    return KIND_NAMES
+
+
 def make_learner(args, world, rank, local, precision, comm):
     from sbmf import Data, FMLearnSBPMF
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=precision, device=local,
@@ -143,9 +148,15 @@ def measure(args, world, rank, local, precision, train, test, comm):
     from sbmf._lib import NKIND
     kern_ms = np.zeros((2, NKIND))
 
-    def per_sweep(_rec):  # each sweep's launch-kind times (HIP events), read from the callback
+    # each sweep's streaming-kind times (HIP events), read from the callback; the other kinds are
+    # timed on a run's first sweep only (their values then stay), so they are read once below
+    KS = list(_lib_kind_names()).index("gres_stage")
+    stream_ms = np.zeros(2)
+
+    def per_sweep(_rec):
         t = L.timing()
-        kern_ms[:] += np.array([[t.kern_ms[s][k] for k in range(NKIND)] for s in range(2)])
+        stream_ms[0] += t.kern_ms[0][KS]
+        stream_ms[1] += t.kern_ms[1][KS]
         return False
 
     # one run of K sweeps (sweep s+1's start is queued at the end of sweep s; the Gram-block
@@ -156,6 +167,8 @@ def measure(args, world, rank, local, precision, train, test, comm):
     dt = time.perf_counter() - t0
     dt = max_over_ranks(world, dt)
     t = L.timing()
+    kern_ms[:] = np.array([[t.kern_ms[s][k] for k in range(NKIND)] for s in range(2)]) * args.steps
+    kern_ms[:, KS] = stream_ms
     kbytes = np.array([[t.kern_bytes[s][k] for k in range(NKIND)] for s in range(2)], dtype=np.float64)
     krows = np.array([[t.kern_rows[s][k] for k in range(NKIND)] for s in range(2)])
     res = {

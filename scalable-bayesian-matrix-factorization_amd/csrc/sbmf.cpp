@@ -1013,7 +1013,16 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     // With two stream sets (items: rows > 1024 on 16-wave workgroups, set 1, and the
     // rest on 8-wave ones, set 0), set 1 runs on `st` and set 0 on `sto` beside it
     // (tune bit 30: one after the other), each with split-row areas of its own.
-    const bool sov = ovl && !(c->cfg.tune & 0x40000000u) && !g.ss[0].stasks.empty() && !g.ss[1].stasks.empty();
+    // Side by side pays nothing at ML-20M (r05s32, neutral) and costs on small stages (ML-1M K=50:
+    // 0.424-0.453 ms side by side, 0.416-0.423 in turn, r05s43): below kSetsSideMin ratings in the
+    // stage (ML-1M, a rank's stage of an 8-way ML-20M split) the sets run one after the other
+    // (SBMF_SETS_SIDE_MIN overrides the threshold: measurements only)
+    static const uint64_t kSetsSideMin = [] {
+        const char* e = std::getenv("SBMF_SETS_SIDE_MIN");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)4000000;
+    }();
+    const bool big = (uint64_t)(s.ptr[g.r1] - s.ptr[g.r0]) >= kSetsSideMin;
+    const bool sov = ovl && big && !(c->cfg.tune & 0x40000000u) && !g.ss[0].stasks.empty() && !g.ss[1].stasks.empty();
     // Beside two streaming sets every Gram-block kind goes to sto2: on sto it would queue behind
     // set 0 (r05s14 trace: two item kinds, 0.18 ms, ran after the stage; measured neutral, 6.91
     // ms both ways, r05s15: the persistent sets hold every CU, so the kinds' work only moves)
