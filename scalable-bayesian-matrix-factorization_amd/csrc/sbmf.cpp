@@ -304,6 +304,11 @@ struct sbmf_ctx {
     // back to back on a stream cost ~12 us of idle device between the launches (r04f trace).
     std::vector<int8_t> kprev;
     int8_t& kpv(uint32_t stage, int side, int kind) { return kprev[((size_t)stage * 2 + side) * SBMF_NKIND + kind]; }
+    // [stage][side][kind]: the begin event a kind's time is read from when kprev is -1 -- its own
+    // kev(.., 0), or an event its half's caller had just recorded on the compute stream (the
+    // sweep start, the user half's end), which then also forks the side streams
+    std::vector<hipEvent_t> kbegin;
+    hipEvent_t& kbg(uint32_t stage, int side, int kind) { return kbegin[((size_t)stage * 2 + side) * SBMF_NKIND + kind]; }
     uint32_t nstages = 1;          // stages per half (see Side::Stage); > 1 only with several ranks
     hipStream_t stc = nullptr;     // multi-GPU: the exchange of stage p runs here while stage p+1 computes
     std::vector<hipEvent_t> sev;   // [side][stage]: stage computed (compute stream)
@@ -745,6 +750,7 @@ static void prepare_T(sbmf_ctx* c) {
     for (hipEvent_t& e : c->sev) event_destroy(e);
     c->kevs.assign((size_t)c->nstages * 2 * SBMF_NKIND * 2, nullptr);
     c->kprev.assign((size_t)c->nstages * 2 * SBMF_NKIND, (int8_t)-1);
+    c->kbegin.assign((size_t)c->nstages * 2 * SBMF_NKIND, nullptr);
     c->sev.assign((size_t)2 * c->nstages, nullptr);
     for (hipEvent_t& e : c->kevs) event_create(&e);
     for (hipEvent_t& e : c->sev) event_create(&e, hipEventDisableTiming);
@@ -986,8 +992,13 @@ static HalfArgs<T> half_args(sbmf_ctx* c, bool users) {
     return a;
 }
 
+// `start` (optional): a timing event the caller has just recorded on the compute stream with
+// nothing queued there since.  The half then forks its side streams from it and, when nothing
+// precedes its first kind on the compute stream, times that kind from it: two event records
+// back to back on a stream leave the device idle ~6 us each (r04f trace; ML-1M K=50 r05s42:
+// 37 us between the user half's end and the item half's streaming launch).
 template <typename T>
-static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
+static void run_half(sbmf_ctx* c, bool users, uint32_t stage, hipEvent_t start = nullptr) {
     Side& s = users ? c->users : c->items;
     Side::Stage& g = *s.stg[stage];
     HalfArgs<T> a = half_args<T>(c, users);
@@ -1038,12 +1049,17 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
     const bool lfirst = sov && side && (kLongFirst & (users ? 1 : 2));
     // the split-row counters and queue heads of both stream sets, zeroed before the fork
     // (cleared at the end of the previous streaming stage on this stream, off the path, unless not)
-    if (!g.bin_rows[KIND_STREAM].empty() && !c->xcnt_clean) HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
+    bool st_busy = false;  // something queued on the compute stream since `start`
+    if (!g.bin_rows[KIND_STREAM].empty() && !c->xcnt_clean) {
+        HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
+        st_busy = true;
+    }
     if (!g.bin_rows[KIND_STREAM].empty()) c->xcnt_clean = false;
     auto fork = [&] {
-        HIPCHK(hipEventRecord(c->oev[0], c->st));
-        HIPCHK(hipStreamWaitEvent(c->sto, c->oev[0], 0));
-        if (two) HIPCHK(hipStreamWaitEvent(c->sto2, c->oev[0], 0));
+        hipEvent_t f = start && !st_busy ? start : c->oev[0];
+        if (f == c->oev[0]) HIPCHK(hipEventRecord(c->oev[0], c->st));
+        HIPCHK(hipStreamWaitEvent(c->sto, f, 0));
+        if (two) HIPCHK(hipStreamWaitEvent(c->sto2, f, 0));
     };
     if (side && !lfirst) fork();
     // (the Gram-block launches on `sto` ahead of set 0 instead of behind it: neutral, r04s22)
@@ -1059,7 +1075,14 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
         int& lk = last[st == c->st ? 0 : st == c->sto ? 1 : 2];
         if (timed) {
             c->kpv(stage, sd, k) = (int8_t)lk;
-            if (lk < 0) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
+            if (lk < 0) {
+                if (st == c->st && start && !st_busy) {
+                    c->kbg(stage, sd, k) = start;  // the caller's event is this kind's start
+                } else {
+                    HIPCHK(hipEventRecord(c->kev(stage, sd, k, 0), st));
+                    c->kbg(stage, sd, k) = c->kev(stage, sd, k, 0);
+                }
+            }
             lk = k;
         } else {
             lk = -1;  // no end event behind this launch
@@ -1112,6 +1135,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
                 as.tune = S.tune;
                 HIPCHK(launch_gstream<T>(g.d_stasks[set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
                                          g.d_xrows[set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, ss));
+                if (ss == c->st) st_busy = true;
                 if (lfirst && set == 1) fork();  // everything else after the long-row set
             }
             if (sov) {  // the streaming stage ends with both sets
@@ -1123,6 +1147,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage) {
             HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
             c->xcnt_clean = true;
         }
+        if (st == c->st) st_busy = true;
         // (after the memset: a kind launched next on this stream starts its time at this event)
         if (timed) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
         c->timing.n_launch++;
@@ -1215,12 +1240,12 @@ static void bcast_stage(sbmf_ctx* c, const Side& s, uint32_t p, void* base, size
 // A half's stages, each followed -- on the comm stream, while the next stage
 // computes -- by its exchange; the compute stream then waits for the last one.
 template <typename T, class F>
-static void run_half_pipelined(sbmf_ctx* c, bool users, F&& bcasts) {
+static void run_half_pipelined(sbmf_ctx* c, bool users, F&& bcasts, hipEvent_t start = nullptr) {
     const int sd = users ? 0 : 1;
     const size_t tb = (size_t)sd * (c->nstages + 1);
     if (c->virt) HIPCHK(hipEventRecord(c->tsev[tb], c->st));
     for (uint32_t p = 0; p < c->nstages; ++p) {
-        run_half<T>(c, users, p);
+        run_half<T>(c, users, p, p == 0 && !c->virt ? start : nullptr);
         if (c->nranks > 1) HIPCHK(hipEventRecord(c->sev[(size_t)sd * c->nstages + p], c->st));
         if (c->virt) HIPCHK(hipEventRecord(c->tsev[tb + p + 1], c->st));
     }
@@ -1427,11 +1452,12 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                                        c->d_bu.as<double>(), c->d_mbu.as<double>(), c->d_sbu.as<double>(),
                                        ref ? c->d_var3u.as<double>() : nullptr, bias_args(c, true, d0), st));
         // several ranks: each stage's fresh U (and b_i) blocks (one RCCL group), then its
-        // residuals, while the next stage computes
+        // residuals, while the next stage computes.  One rank: the half starts from the sweep's
+        // start event when nothing was queued after it (staged start work, no bias pass)
         run_half_pipelined<T>(c, true, [&](uint32_t p) {
             bcast_stage(c, c->users, p, c->d_U.p, c->Kp * sizeof(T));
             if (c->bias) bcast_stage(c, c->users, p, c->d_bu.p, sizeof(double));
-        });
+        }, c->nranks == 1 && staged && !c->bias ? ev1 : nullptr);
         if (c->nranks > 1) HIPCHK(hipEventRecord(c->ev[3], st));
         // ---- 4. item half-sweep
         if (!ref && !staged)
@@ -1440,13 +1466,14 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(launch_bias_rows<T>(c->d_vptr.as<uint32_t>(), c->items.r0, c->items.r1, c->d_Ev.as<T>(),
                                        c->d_bv.as<double>(), c->d_mbv.as<double>(), c->d_sbv.as<double>(),
                                        ref ? c->d_var3v.as<double>() : nullptr, bias_args(c, false, 0.0), st));
-        // fresh V (and b_j) blocks and the per-row sums (one RCCL group), then the residuals
+        // fresh V (and b_j) blocks and the per-row sums (one RCCL group), then the residuals.  One
+        // rank: the half starts from the user half's end event (ev[2], just recorded)
         run_half_pipelined<T>(c, false, [&](uint32_t p) {
             bcast_stage(c, c->items, p, c->d_V.p, c->Kp * sizeof(T));
             if (c->bias) bcast_stage(c, c->items, p, c->d_bv.p, sizeof(double));
             bcast_stage(c, c->items, p, c->d_rowsq_v.p, sizeof(double));
             if (cf.eval_train) bcast_stage(c, c->items, p, c->d_rowtr_v.p, sizeof(double));
-        });
+        }, c->nranks == 1 && staged && !c->bias ? c->ev[2] : nullptr);
         if (c->nranks > 1) HIPCHK(hipEventRecord(c->ev[5], st));
         // ---- 5. evaluation, and (overlap) the next sweep's prologue kernels.  One rank: the
         // evaluation runs on the second stream beside the prologue kernels -- both only read
@@ -1591,7 +1618,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                     const Side::Stage& g = *sdd.stg[p];
                     const bool ran = k < NBIN && !g.bin_rows[k].empty();
                     const int kp = ran ? c->kpv(p, sd, k) : -1;
-                    if (ran) ms += ev_ms(kp >= 0 ? c->kev(p, sd, kp, 1) : c->kev(p, sd, k, 0), c->kev(p, sd, k, 1));
+                    if (ran) ms += ev_ms(kp >= 0 ? c->kev(p, sd, kp, 1) : c->kbg(p, sd, k), c->kev(p, sd, k, 1));
                 }
                 c->timing.kern_ms[sd][k] = ms;
             }
