@@ -1039,14 +1039,9 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage, hipEvent_t start =
     // ms both ways, r05s15: the persistent sets hold every CU, so the kinds' work only moves)
     const bool two = !serial && (others >= 2 || sov) && !(c->cfg.tune & 0x2000000u);
     const bool side = ovl || two;
-    // (measurement knob SBMF_LONG_FIRST: 1 users, 2 items, 3 both -- the long-row set alone first,
-    // every other launch of the half after it: its split rows' chunks then share no CU with
-    // the other launches' workgroups)
-    static const int kLongFirst = [] {
-        const char* e = std::getenv("SBMF_LONG_FIRST");
-        return e ? std::atoi(e) : 0;
-    }();
-    const bool lfirst = sov && side && (kLongFirst & (users ? 1 : 2));
+    // (the long-row set alone first, every other launch of the half after it, so its split rows'
+    // chunks share no CU with other launches' workgroups: user half 2.77-2.81 -> 2.86-3.04 ms,
+    // item half neutral, r06s6; not kept)
     // the split-row counters and queue heads of both stream sets, zeroed before the fork
     // (cleared at the end of the previous streaming stage on this stream, off the path, unless not)
     bool st_busy = false;  // something queued on the compute stream since `start`
@@ -1061,7 +1056,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage, hipEvent_t start =
         HIPCHK(hipStreamWaitEvent(c->sto, f, 0));
         if (two) HIPCHK(hipStreamWaitEvent(c->sto2, f, 0));
     };
-    if (side && !lfirst) fork();
+    if (side) fork();
     // (the Gram-block launches on `sto` ahead of set 0 instead of behind it: neutral, r04s22)
     int last[3] = {-1, -1, -1};  // the last kind launched on st / sto / sto2 (its end event recorded there)
     int nside = 0;  // Gram-block kinds launched so far (two: even ones on sto, odd ones on sto2)
@@ -1136,7 +1131,6 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage, hipEvent_t start =
                 HIPCHK(launch_gstream<T>(g.d_stasks[set].as<SplitTask>(), (uint32_t)S.stasks.size(), S.sgrid,
                                          g.d_xrows[set].as<SplitRow>(), (uint32_t)S.xrows.size(), as, sy, ss));
                 if (ss == c->st) st_busy = true;
-                if (lfirst && set == 1) fork();  // everything else after the long-row set
             }
             if (sov) {  // the streaming stage ends with both sets
                 HIPCHK(hipEventRecord(c->oev[2], c->sto));

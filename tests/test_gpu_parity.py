@@ -81,6 +81,21 @@ def test_f32_ref_stream_within_north_star_tolerance(ml100k, tune):
     assert err.max() < 1e-3
 
 
+@pytest.mark.parametrize("K", [130, 200])
+def test_f32_wide_factor_counts_within_north_star(ml100k, K):
+    """f32 at K above 128: k_grow's KL = 256 register form (sigma and mu read from
+    memory) for the 17..512-rating rows, 9..13 k-blocks in the f32 Gram-block and
+    streaming kinds.  RMSE within 1e-3 of the f64 oracle over 3 sweeps, same RNG stream."""
+    tr, te = ml100k
+    o = oracle.run(tr, te, K=K, iters=3, seed=3)
+    L = _run(tr, te, 3, num_factor=K, seed=3, precision="f32")
+    err = np.abs(L.rmse_trajectory - o["rmse"])
+    print("f32 K=%d max |dRMSE| = %.3e" % (K, err.max()))
+    assert err.max() < 1e-3
+    U, V = L.factors()
+    assert np.abs(U - o["U"]).max() < 5e-2 and np.abs(V - o["V"]).max() < 5e-2
+
+
 @pytest.mark.parametrize("thr", [1, 40, 200])
 @pytest.mark.parametrize("K", [20, 100, 200])
 def test_streaming_kernel_matches_oracle(ml100k, thr, K):
