@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-ttr", action="store_true", help="skip the time-to-RMSE runs")
     ap.add_argument("--no-load", action="store_true", help="skip the text / binary load timing")
     ap.add_argument("--tune", type=int, default=0, help="kernel-variant bits (sbmf_config.tune)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="sbmf_config.pipeline = 0: each sweep is reported before the next one is queued")
     ap.add_argument("--split-chunk", type=int, default=0, help="streaming task size (0 = the register capacity of the workgroup shape: 512 / 1024 / 2048 f64 ratings for 4 / 8 / 16 waves)")
     ap.add_argument("--stream-threshold", type=int, default=0, help="rows above this use the streaming kernel")
     ap.add_argument("--device", type=int, default=-1,
@@ -130,7 +132,8 @@ def make_learner(args, world, rank, local, precision, comm):
     from sbmf import Data, FMLearnSBPMF
     L = FMLearnSBPMF(num_factor=args.K, seed=2015, rng="philox", precision=precision, device=local,
                      quirks=args.quirks, recompute_every=0, eval_train=False, tune=args.tune,
-                     split_chunk=args.split_chunk, stream_threshold=args.stream_threshold)
+                     split_chunk=args.split_chunk, stream_threshold=args.stream_threshold,
+                     pipeline=0 if args.no_pipeline else 1)
     L.init(comm=comm)
     return L, Data
 

@@ -176,6 +176,14 @@ typedef struct sbmf_config {
                                  global bias w0, bit 1 = attribute biases w (default 3)          */
     double reg0, regw, regv;  /* LIBFM_MCMC / ALS: -regular 'r0,r1,r2' (libfm.cpp:484-513): ALS's
                                  fixed precisions, MCMC's starting w / v precisions (default 0) */
+    uint32_t pipeline;        /* SBPMF sampler, throughput mode (Philox, prologue overlap on): 1 =
+                                 sweep s+1's start (its hyperparameter upload and user half) is
+                                 queued before sweep s is reported to the run callback, so the
+                                 device does not idle through the host's per-sweep work.  The
+                                 chain and the reports are the same; the callback must not read
+                                 device state (factors, predictions), and a stop it asks for takes
+                                 effect after sweep s+1.  0 (default): each sweep is reported with
+                                 the device idle after it                                         */
 } sbmf_config;
 
 /* Per-sweep report passed to the run callback. */

@@ -81,7 +81,7 @@ struct SplitRow {
 };
 struct SplitSync {
     double* slabs;       // [nchunk_total][nblk][16*16+16]
-    uint32_t* counters;  // [nsplit_rows * nblk], then the task-queue head: zero at launch (the caller clears them)
+    uint32_t* counters;  // [nsplit_rows * nblk], then the task-queue head: zero at launch (k_split_finish clears them)
     uint32_t ncounters;
     uint32_t nblk;       // ceil(K/16)
     double* chunk_sq;    // [nchunk_total]
@@ -183,6 +183,11 @@ hipError_t launch_sum_cols2(const double* in, uint32_t nchunk, double* out, cons
 template <typename T>
 hipError_t launch_philox_fill(T* z, uint32_t K, uint32_t r0, uint32_t r1, uint64_t seed, uint32_t sweep, uint32_t tag,
                               hipStream_t st);
+// Both tables' normals of one sweep in one launch: launch_philox_fill over users [u0, u1) with
+// tagu and over items [v0, v1) with tagv.
+template <typename T>
+hipError_t launch_philox_fill2(T* zu, uint32_t u0, uint32_t u1, uint32_t tagu, T* zv, uint32_t v0, uint32_t v1,
+                               uint32_t tagv, uint32_t K, uint64_t seed, uint32_t sweep, hipStream_t st);
 template <typename T>
 hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, double sd, uint64_t seed,
                               uint32_t tag, hipStream_t st);

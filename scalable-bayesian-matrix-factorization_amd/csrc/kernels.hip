@@ -1116,10 +1116,18 @@ __global__ __launch_bounds__(64 * NW, 4) void k_grow(
     gres_run<T, NW, SIDE, true, KL>(nullptr, rows, nrows, a, sy);
 }
 
-// Split rows: publish the new own rows and fold the chunk partial sums.
+// Split rows: publish the new own rows and fold the chunk partial sums; and (every launch, with
+// at least one block) put the set's split-row counters and queue head back to zero for the next
+// streaming launch on this area, in stream order after k_gres.  (That clear was a fill launch per
+// streaming stage on the compute stream: a kernel and a packet gap, r06s10 trace.  Done by
+// k_gres's last workgroup instead, the exit count kept sy alive across the task loop: spilled
+// SGPRs 80 -> 93 and VGPRs 14 -> 20 in the 16-wave item kernel, item half 3.57 -> 3.83-3.92 ms,
+// r06s11 / r06s12.)
 template <typename T>
 __global__ __launch_bounds__(64) void k_split_finish(const SplitRow* __restrict__ srows, uint32_t nrows, HalfArgs<T> a,
                                                      SplitSync sy) {
+    for (uint32_t i = blockIdx.x * 64 + threadIdx.x; i <= sy.ncounters; i += gridDim.x * 64) sy.counters[i] = 0u;
+    if (blockIdx.x >= nrows) return;
     const SplitRow sr = srows[blockIdx.x];
     const uint32_t K = a.K, Kp = a.Kp;
     for (uint32_t k = threadIdx.x; k < K; k += 64) a.own[(size_t)sr.row * Kp + k] = static_cast<const T*>(sy.newown)[(size_t)sr.slab0 * Kp + k];
@@ -1419,6 +1427,25 @@ __global__ __launch_bounds__(256) void k_philox_fill(T* __restrict__ z, uint32_t
     if (row >= r1) return;
     double z0, z1;
     philox_normal_pair(seed, row, sweep, tag, p, z0, z1);
+    z[(size_t)row * K + 2 * p] = (T)z0;
+    if (2 * p + 1 < K) z[(size_t)row * K + 2 * p + 1] = (T)z1;
+}
+
+// Both tables' normals of one sweep in one launch: blocks [0, nbu) fill the user rows, the rest
+// the item rows (each thread the pair k_philox_fill's thread would draw)
+template <typename T>
+__global__ __launch_bounds__(256) void k_philox_fill2(T* __restrict__ zu, uint32_t u0, uint32_t u1, T* __restrict__ zv,
+                                                      uint32_t v0, uint32_t v1, uint32_t K, uint32_t nbu,
+                                                      uint64_t seed, uint32_t sweep, uint32_t tagu, uint32_t tagv) {
+    const uint32_t npair = (K + 1) / 2;
+    const bool users = blockIdx.x < nbu;
+    const uint64_t x = (uint64_t)(users ? blockIdx.x : blockIdx.x - nbu) * 256 + threadIdx.x;
+    T* const z = users ? zu : zv;
+    const uint32_t r0 = users ? u0 : v0, r1 = users ? u1 : v1;
+    const uint32_t row = r0 + (uint32_t)(x / npair), p = (uint32_t)(x % npair);
+    if (row >= r1) return;
+    double z0, z1;
+    philox_normal_pair(seed, row, sweep, users ? tagu : tagv, p, z0, z1);
     z[(size_t)row * K + 2 * p] = (T)z0;
     if (2 * p + 1 < K) z[(size_t)row * K + 2 * p + 1] = (T)z1;
 }
@@ -1737,8 +1764,8 @@ hipError_t launch_gstream(const SplitTask* tasks, uint32_t ntask, uint32_t grid,
     else
         err = hipLaunchKernel(fn, g, b, args, 0, st);
     if (err != hipSuccess) return err;
-    if (nsrow) {
-        k_split_finish<T><<<nsrow, 64, 0, st>>>(srows, nsrow, a, sy);
+    {  // (no split rows: one block, the counter clear only)
+        k_split_finish<T><<<std::max(nsrow, 1u), 64, 0, st>>>(srows, nsrow, a, sy);
         return hipGetLastError();
     }
     return hipSuccess;
@@ -1828,6 +1855,18 @@ hipError_t launch_philox_fill(T* z, uint32_t K, uint32_t r0, uint32_t r1, uint64
 }
 
 template <typename T>
+hipError_t launch_philox_fill2(T* zu, uint32_t u0, uint32_t u1, uint32_t tagu, T* zv, uint32_t v0, uint32_t v1,
+                               uint32_t tagv, uint32_t K, uint64_t seed, uint32_t sweep, hipStream_t st) {
+    const uint64_t npair = (K + 1) / 2;
+    const uint64_t nbu = ((uint64_t)(u1 > u0 ? u1 - u0 : 0) * npair + 255) / 256;
+    const uint64_t nbv = ((uint64_t)(v1 > v0 ? v1 - v0 : 0) * npair + 255) / 256;
+    if (nbu + nbv == 0) return hipSuccess;
+    k_philox_fill2<T><<<(unsigned)(nbu + nbv), 256, 0, st>>>(zu, u0, u1, zv, v0, v1, K, (uint32_t)nbu, seed, sweep, tagu,
+                                                             tagv);
+    return hipGetLastError();
+}
+
+template <typename T>
 hipError_t launch_init_philox(T* tab, uint32_t K, uint32_t Kp, uint32_t r0, uint32_t r1, double sd, uint64_t seed,
                               uint32_t tag, hipStream_t st) {
     if (r1 <= r0) return hipSuccess;
@@ -1881,6 +1920,8 @@ hipError_t launch_unpack(const T* recv, const uint32_t* idx, uint64_t n, T* E, h
                                         hipStream_t);                                                                \
     template hipError_t launch_philox_fill<T>(T*, uint32_t, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t,        \
                                               hipStream_t);                                                          \
+    template hipError_t launch_philox_fill2<T>(T*, uint32_t, uint32_t, uint32_t, T*, uint32_t, uint32_t, uint32_t,   \
+                                               uint32_t, uint64_t, uint32_t, hipStream_t);                           \
     template hipError_t launch_colstats<T>(const T*, uint32_t, const T*, double*, const T*, uint32_t, const T*,    \
                                            double*, uint32_t, uint32_t, hipStream_t);                                \
     template hipError_t launch_test<T>(const uint32_t*, const uint32_t*, const double*, uint64_t, uint64_t,         \

@@ -294,7 +294,7 @@ struct sbmf_ctx {
     Comm* comm = &own_comm;   // ... or a process-wide one it borrows (sbmf_comm_attach)
     // device
     hipStream_t st = nullptr;
-    hipEvent_t ev[9] = {};
+    hipEvent_t ev[10] = {};
     std::vector<hipEvent_t> kevs;  // [stage][side][kind][begin, end] launch timing
     hipEvent_t& kev(uint32_t stage, int side, int kind, int e) {
         return kevs[(((size_t)stage * 2 + side) * SBMF_NKIND + kind) * 2 + e];
@@ -330,8 +330,7 @@ struct sbmf_ctx {
     int kprof_set = 0;  // SBMF_KPROF_SET: which streaming launch of a half is stamped (0: the 8-wave one)
     DBuf d_kprof;
     DBuf d_rtasks, d_rtptr, d_rtsq;  // residual recompute (item side)
-    DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown, d_xtimeout;
-    bool xcnt_clean = false;  // d_xcnt zeroed (queued) since its last use: the next streaming stage skips its clear
+    DBuf d_xslabs, d_xcnt, d_xchunk_sq, d_xchunk_tr, d_xnewown;
     bool time_kinds = true;   // this sweep records every launch kind's events (else the streaming kind's only)
     size_t xset_nx = 1, xset_nr = 1;  // set 0's split chunks / rows: set 1's areas follow them
     DBuf d_tu, d_ti, d_tr, d_tsum, d_tpart;
@@ -344,7 +343,6 @@ struct sbmf_ctx {
     // hyperparameter upload [sig_u | mu_u | sig_v | mu_v] (4 Kp of T)
     void* h_io = nullptr;
     double* h_out() { return static_cast<double*>(h_io); }
-    uint32_t* h_timeout() { return reinterpret_cast<uint32_t*>(static_cast<char*>(h_io) + 64); }
     void* h_hyper() { return static_cast<char*>(h_io) + 128; }
     hipEvent_t hev = nullptr;  // the last upload from h_hyper done (the area is rewritten after it)
     // throughput mode: the next sweep's hyperparameters, drawn at the end of the
@@ -371,7 +369,9 @@ struct sbmf_ctx {
 namespace sbmf {
 
 // result slots in d_res
-enum { RES_ESQ = 0, RES_TRSQ = 1, RES_TEST_AVG = 2, RES_TEST_THIS = 3, RES_ES = 4, RES_ESQ2 = 5, RES_COL = 8 };
+// d_res slots; RES_TIMEOUT holds k_gres's split-row timeout flag (a uint32, sticky), so the
+// sweep's one result copy carries it
+enum { RES_ESQ = 0, RES_TRSQ = 1, RES_TEST_AVG = 2, RES_TEST_THIS = 3, RES_ES = 4, RES_ESQ2 = 5, RES_TIMEOUT = 7, RES_COL = 8 };
 
 static size_t tsize(const sbmf_ctx* c) { return c->cfg.precision == SBMF_F32 ? 4 : 8; }
 
@@ -605,17 +605,14 @@ static void prepare_T(sbmf_ctx* c) {
     {
         const size_t nx = c->xset_nx + std::max<size_t>(nxk[1], 1), nr = c->xset_nr + std::max<size_t>(nrk[1], 1);
         c->d_xslabs.alloc(nx * nblk * (16 * 16 + 16) * sizeof(double));
-        // + each set's task-queue head; a whole number of 16-byte words, so that clearing it
-        // is one fill kernel (a ragged size is three, and on a stream beside a persistent
-        // launch the tail one waited for that launch: r04s4 trace)
+        // + each set's task-queue head.  Zeroed once here: every streaming launch leaves its set's
+        // area zero again (k_split_finish clears it after k_gres)
         c->d_xcnt.alloc((nr * nblk + 2 + 3) / 4 * 4 * sizeof(uint32_t));
-        c->xcnt_clean = false;
+        HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
         c->d_xchunk_sq.alloc(nx * sizeof(double));
         c->d_xchunk_tr.alloc(nx * sizeof(double));
         HIPCHK(hipMemsetAsync(c->d_xchunk_tr.p, 0, c->d_xchunk_tr.bytes, st));
         c->d_xnewown.alloc(nx * c->Kp * sizeof(T));
-        c->d_xtimeout.alloc(sizeof(uint32_t));
-        HIPCHK(hipMemsetAsync(c->d_xtimeout.p, 0, sizeof(uint32_t), st));
     }
     // factor tables [rows + 2][Kp]: row `rows` stays zero (the sentinel partner of
     // padded rating slots), row `rows + 1` is slack for the next-block prefetch
@@ -650,6 +647,7 @@ static void prepare_T(sbmf_ctx* c) {
     c->d_colpart.alloc((size_t)nchunk * 2 * c->K * sizeof(double));
     c->h_res.assign(RES_COL + 4 * (size_t)c->K, 0.0);
     c->d_res.alloc(c->h_res.size() * sizeof(double));
+    HIPCHK(hipMemsetAsync(c->d_res.p, 0, c->d_res.bytes, st));
     pinned_free(c->h_pre, c->h_pre_bytes);
     c->h_pre_bytes = c->h_res.size() * sizeof(double);
     pinned_alloc((void**)&c->h_pre, c->h_pre_bytes);
@@ -1042,14 +1040,9 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage, hipEvent_t start =
     // (the long-row set alone first, every other launch of the half after it, so its split rows'
     // chunks share no CU with other launches' workgroups: user half 2.77-2.81 -> 2.86-3.04 ms,
     // item half neutral, r06s6; not kept)
-    // the split-row counters and queue heads of both stream sets, zeroed before the fork
-    // (cleared at the end of the previous streaming stage on this stream, off the path, unless not)
+    // (the split-row counters and queue heads of both stream sets are zero: each streaming
+    // launch's k_split_finish clears its own)
     bool st_busy = false;  // something queued on the compute stream since `start`
-    if (!g.bin_rows[KIND_STREAM].empty() && !c->xcnt_clean) {
-        HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
-        st_busy = true;
-    }
-    if (!g.bin_rows[KIND_STREAM].empty()) c->xcnt_clean = false;
     auto fork = [&] {
         hipEvent_t f = start && !st_busy ? start : c->oev[0];
         if (f == c->oev[0]) HIPCHK(hipEventRecord(c->oev[0], c->st));
@@ -1121,7 +1114,7 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage, hipEvent_t start =
                 sy.chunk_sq = c->d_xchunk_sq.as<double>() + ox;
                 sy.chunk_tr = c->d_xchunk_tr.as<double>() + ox;
                 sy.newown = c->d_xnewown.as<T>() + ox * c->Kp;
-                sy.timeout = c->d_xtimeout.as<uint32_t>();
+                sy.timeout = reinterpret_cast<uint32_t*>(c->d_res.as<double>() + RES_TIMEOUT);
                 sy.cmax = S.cmax;
                 sy.lim_slab = (uint64_t)(c->d_xslabs.bytes / sizeof(double)) - ox * sy.nblk * (16 * 16 + 16);
                 sy.lim_chunk = (uint32_t)(c->d_xchunk_sq.bytes / sizeof(double) - ox);
@@ -1137,12 +1130,8 @@ static void run_half(sbmf_ctx* c, bool users, uint32_t stage, hipEvent_t start =
                 HIPCHK(hipStreamWaitEvent(st, c->oev[2], 0));
             }
         }
-        if (k == KIND_STREAM && c->d_xcnt.p) {  // the next streaming stage's counters, cleared now
-            HIPCHK(hipMemsetAsync(c->d_xcnt.p, 0, c->d_xcnt.bytes, st));
-            c->xcnt_clean = true;
-        }
         if (st == c->st) st_busy = true;
-        // (after the memset: a kind launched next on this stream starts its time at this event)
+        // (a kind launched next on this stream starts its time at this event)
         if (timed) HIPCHK(hipEventRecord(c->kev(stage, sd, k, 1), st));
         c->timing.n_launch++;
     }
@@ -1272,8 +1261,9 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
     // sweep.  The inputs are the same (U, V and the residuals do not change in
     // between), so the chain is bitwise the same.  Tune bit 26 turns it off.
     const bool overlap = !ref && !(cf.tune & 0x4000000u);
-    // ---- 1. the prologue's kernels for sweep sw; its sums land in c->h_pre
-    auto prologue_gpu = [&](uint32_t sw) {
+    // ---- 1. the prologue's kernels for sweep sw; its sums land in c->h_pre (copy: here; the
+    // overlapped prologue's sums travel with the sweep's results in one copy)
+    auto prologue_gpu = [&](uint32_t sw, bool copy = true) {
         // ---- 1. residual sum of squares (E recompute at sweep start, :317-334)
         const bool recompute = sw == 0 || (cf.recompute_every && sw % cf.recompute_every == 0);
         if (recompute) {
@@ -1306,7 +1296,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         HIPCHK(launch_sum_cols2(colpart, (c->I + 255) / 256, d_res + RES_COL, colpart_v, (c->J + 255) / 256,
                                 d_res + RES_COL + 2 * K, 2 * K, st));
         c->timing.n_launch += 3;
-        HIPCHK(hipMemcpyAsync(c->h_pre, d_res, c->h_res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (copy) HIPCHK(hipMemcpyAsync(c->h_pre, d_res, c->h_res.size() * sizeof(double), hipMemcpyDeviceToHost, st));
     };
     // ---- 2. host draws (:339-342, :375-414) from the prologue's sums: updates
     // c->tau, sigma / mu (and the biased sampler's globals); returns d0
@@ -1381,8 +1371,10 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
         HIPCHK(hipMemcpyAsync(c->d_hyper.p, h, 4 * Kp * sizeof(T), hipMemcpyHostToDevice, st));
         HIPCHK(hipEventRecord(c->hev, st));
     };
-    for (uint32_t it = 0; it < nsweeps; ++it) {
-        c->time_kinds = it == 0;  // every launch kind timed on the first sweep of the run
+    // A sweep's start: its hyperparameters (drawn here, or staged at the end of the previous sweep in
+    // throughput mode) and its user half.  Returns whether the start work was staged ahead.
+    auto start_sweep = [&](bool first) -> bool {
+        c->time_kinds = first;  // every launch kind timed on the first sweep of the run
         c->timing.n_launch = 0;
         HIPCHK(hipEventRecord(c->ev[0], st));
         double d0;
@@ -1409,7 +1401,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 PhiloxStream ps(cf.seed, c->sweep, 0);
                 draw_hyper_variates(ps, c, hs);
             }
-            prologue_gpu(c->sweep);
+            prologue_gpu(c->sweep, true);
             HIPCHK(hipStreamSynchronize(st));
             d0 = host_draw(hs);
         }
@@ -1427,17 +1419,6 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             HIPCHK(hipEventRecord(c->ev[1], st));
         }
         hipEvent_t& ev1 = staged ? c->ev[0] : c->ev[1];
-        const bool collect = q2 ? true : (c->sweep >= cf.burnin);
-        if (collect) c->collected++;
-        const double div = avg_collected(cf) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
-        const uint64_t T_ = c->su.size();
-        const bool par_eval = overlap && c->nranks == 1 && !(cf.tune & 0x10000000u);
-        // The sweep's device work, from the user half to the results' copy (with the overlap the
-        // next sweep's prologue kernels and normals are part of it).  (Captured once as a hipGraph
-        // and replayed, one rank: ML-1M K=50 0.45 -> 0.77-0.90 ms, ML-20M 7.11 -> 7.57-7.82 ms
-        // per sweep, r06s3 -- the halves unchanged, the replay slower than the eager launches;
-        // removed, profiles/r06/ab/r06s3_sweep_graph.patch)
-        {
         // ---- 3. user half-sweep (throughput mode: this half's normals first)
         if (!ref && !staged)
             HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep, TAG_USERS, st));
@@ -1453,6 +1434,27 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             if (c->bias) bcast_stage(c, c->users, p, c->d_bu.p, sizeof(double));
         }, c->nranks == 1 && staged && !c->bias ? ev1 : nullptr);
         if (c->nranks > 1) HIPCHK(hipEventRecord(c->ev[3], st));
+        return staged;
+    };
+    // cfg.pipeline (throughput mode): sweep s+1's start is queued before sweep s is reported, so
+    // the device does not idle through the host's per-sweep work (the report, the callback, the
+    // next sweep's enqueue).  A stop the callback asks for then takes effect after sweep s+1.
+    bool queued = false, q_staged = false, stop_after = false;
+    for (uint32_t it = 0; it < nsweeps; ++it) {
+        const bool staged = queued ? q_staged : start_sweep(it == 0);
+        queued = false;
+        hipEvent_t& ev1 = staged ? c->ev[0] : c->ev[1];
+        const bool collect = q2 ? true : (c->sweep >= cf.burnin);
+        if (collect) c->collected++;
+        const double div = avg_collected(cf) ? (double)std::max(1u, c->collected) : (double)(c->sweep + 1);
+        const uint64_t T_ = c->su.size();
+        const bool par_eval = overlap && c->nranks == 1 && !(cf.tune & 0x10000000u);
+        // The sweep's device work, from the item half to the results' copy (with the overlap the
+        // next sweep's prologue kernels and normals are part of it).  (Captured once as a hipGraph
+        // and replayed, one rank: ML-1M K=50 0.45 -> 0.77-0.90 ms, ML-20M 7.11 -> 7.57-7.82 ms
+        // per sweep, r06s3 -- the halves unchanged, the replay slower than the eager launches;
+        // removed, profiles/r06/ab/r06s3_sweep_graph.patch)
+        {
         // ---- 4. item half-sweep
         if (!ref && !staged)
             HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep, TAG_ITEMS, st));
@@ -1492,23 +1494,26 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             evaluate(c->sto);
         }
         if (overlap) {  // the next sweep's prologue kernels, ahead of the evaluation
-            prologue_gpu(c->sweep + 1);
-            HIPCHK(hipEventRecord(c->ev[7], st));
-            // and the next sweep's normals (Philox: a function of (seed, sweep) only; this
-            // sweep's halves, which read them, are queued before)
-            HIPCHK(launch_philox_fill<T>(c->d_zU.as<T>(), K, c->users.r0, c->users.r1, cf.seed, c->sweep + 1, TAG_USERS,
-                                         st));
-            HIPCHK(launch_philox_fill<T>(c->d_zV.as<T>(), K, c->items.r0, c->items.r1, cf.seed, c->sweep + 1, TAG_ITEMS,
-                                         st));
+            prologue_gpu(c->sweep + 1, true);
+            HIPCHK(hipEventRecord(c->ev[7], st));  // the host draws from here on
+            // and the next sweep's normals, both tables in one launch (Philox: a function of (seed,
+            // sweep) only; this sweep's halves, which read them, are queued before)
+            HIPCHK(launch_philox_fill2<T>(c->d_zU.as<T>(), c->users.r0, c->users.r1, TAG_USERS, c->d_zV.as<T>(),
+                                          c->items.r0, c->items.r1, TAG_ITEMS, K, cf.seed, c->sweep + 1, st));
             HIPCHK(hipEventRecord(c->ev[8], st));  // the next sweep's start work ends here
         }
         if (par_eval)
             HIPCHK(hipStreamWaitEvent(st, c->ev[6], 0));
         else
             evaluate(st);
+        // the results, with the split-row timeout flag in the same copy (one copy less per sweep;
+        // the prologue's sums go to the host ahead of them, so the host draws while the
+        // evaluation and the normals run: one copy of everything after them put the host round
+        // trip on the path, ML-1M 0.40 -> 0.43 ms, r06s11)
         HIPCHK(hipMemcpyAsync(c->h_out(), d_res, 8 * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(c->ev[9], st));  // this sweep's device work ends here
         }
-        if (overlap) {  // the next sweep's draws while the evaluation runs; this sweep's values kept
+        if (overlap) {  // the next sweep's draws from the copied sums; this sweep's values kept
             HIPCHK(hipEventSynchronize(c->ev[7]));
             HostStream hs;
             PhiloxStream ps(cf.seed, c->sweep + 1, 0);
@@ -1540,12 +1545,47 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             c->pre.staged = true;
             c->hyper_ahead = true;
         }
-        *c->h_timeout() = 0;
-        if (c->d_xtimeout.p)
-            HIPCHK(hipMemcpyAsync(c->h_timeout(), c->d_xtimeout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        std::copy(c->h_out(), c->h_out() + 8, c->h_res.begin());
-        const uint32_t split_timeout = *c->h_timeout();
+        // ---- 6. the report.  With the overlap the host is past ev[7]: every event up to the item
+        // half's end is done, so the half and launch-kind times are read first; cfg.pipeline then
+        // queues the next sweep's start (which records those events again) before the host waits
+        // for this sweep's results (ev[9]) and runs the callback
+        const uint32_t s_cur = c->sweep;
+        if (!overlap) HIPCHK(hipEventSynchronize(c->ev[9]));
+        sbmf_sweep_info info{};
+        info.sweep = s_cur;
+        info.collected = collect ? 1u : 0u;
+        info.tau = c->tau;
+        const double ms_start = staged ? 0.0 : ev_ms(c->ev[0], ev1);
+        c->timing.ms_user_half = ev_ms(ev1, c->ev[2]);
+        c->timing.ms_item_half = ev_ms(ev3, c->ev[4]);
+        c->timing.ms_comm = c->nranks > 1 ? ev_ms(c->ev[2], c->ev[3]) + ev_ms(c->ev[4], c->ev[5]) : 0.0;
+        for (int sd = 0; sd < 2; ++sd) {
+            const Side& sdd = sd == 0 ? c->users : c->items;
+            for (int k = 0; k < SBMF_NKIND; ++k) {
+                if (!c->time_kinds && k != KIND_STREAM) continue;  // kept from the run's first sweep
+                double ms = 0.0;
+                for (uint32_t p = 0; p < c->nstages; ++p) {
+                    const Side::Stage& g = *sdd.stg[p];
+                    const bool ran = k < NBIN && !g.bin_rows[k].empty();
+                    const int kp = ran ? c->kpv(p, sd, k) : -1;
+                    if (ran) ms += ev_ms(kp >= 0 ? c->kev(p, sd, kp, 1) : c->kbg(p, sd, k), c->kev(p, sd, k, 1));
+                }
+                c->timing.kern_ms[sd][k] = ms;
+            }
+        }
+        info.ms_sweep = ev_ms(c->ev[0], ev5);
+        c->sweep++;
+        if (overlap && cf.pipeline && it + 1 < nsweeps && !c->kprof && !stop_after) {
+            const uint32_t nl = c->timing.n_launch;
+            q_staged = start_sweep(false);
+            queued = true;
+            c->timing.n_launch = nl;  // (this sweep's count in its report; the next start's is redone)
+        }
+        if (overlap) HIPCHK(hipEventSynchronize(c->ev[9]));  // this sweep's results (not the upload after them)
+        const double* res8 = c->h_out();
+        std::copy(res8, res8 + 8, c->h_res.begin());
+        uint32_t split_timeout;
+        std::memcpy(&split_timeout, res8 + RES_TIMEOUT, sizeof(split_timeout));
         if (c->kprof) {
             unsigned long long h[96];
             HIPCHK(hipMemcpy(h, c->d_kprof.p, sizeof(h), hipMemcpyDeviceToHost));
@@ -1556,7 +1596,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 double tot = 0;
                 for (int k = 0; k < 7; ++k) tot += (double)h[16 + 8 * sd + k];
                 if (tot == 0) continue;
-                std::fprintf(stderr, "[kprof] sweep %u %s gblock multi-wave rows (wave-0 Gcycles total):", c->sweep,
+                std::fprintf(stderr, "[kprof] sweep %u %s gblock multi-wave rows (wave-0 Gcycles total):", s_cur,
                              sd ? "items" : "users");
                 for (int k = 0; k < 7; ++k)
                     std::fprintf(stderr, " %s %.3f (%.0f%%)", gn[k], (double)h[16 + 8 * sd + k] / 1e9,
@@ -1569,7 +1609,7 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
                 double tot = 0;
                 for (int k = 0; k < 7; ++k) tot += (double)h[8 * sd + k];
                 if (tot == 0) continue;
-                std::fprintf(stderr, "[kprof] sweep %u gres %s (grid %u, %zu tasks, wave-0 Mcycles per WG):", c->sweep,
+                std::fprintf(stderr, "[kprof] sweep %u gres %s (grid %u, %zu tasks, wave-0 Mcycles per WG):", s_cur,
                              sd ? "items" : "users", S.stg[0]->ss[c->kprof_set].sgrid,
                              S.stg[0]->ss[c->kprof_set].stasks.size());
                 for (int k = 0; k < 7; ++k)
@@ -1587,40 +1627,21 @@ static void run_sweeps_T(sbmf_ctx* c, uint32_t nsweeps, sbmf_sweep_cb cb, void* 
             }
         }
         if (split_timeout)  // a bounded spin in k_gres gave up: the sweep's results are not valid
-            fail(SBMF_E_STATE, "sweep %u: split-row hand-off timed out (workgroups not co-resident)", c->sweep);
-
-        sbmf_sweep_info info{};
-        info.sweep = c->sweep;
-        info.collected = collect ? 1u : 0u;
-        info.tau = c->tau;
+            fail(SBMF_E_STATE, "sweep %u: split-row hand-off timed out (workgroups not co-resident)", s_cur);
         info.rmse_avg = (cf.eval_test && T_) ? std::sqrt(c->h_res[RES_TEST_AVG] / T_) : NAN;
         info.rmse_this = (cf.eval_test && T_) ? std::sqrt(c->h_res[RES_TEST_THIS] / T_) : NAN;
         info.rmse_train = cf.eval_train && N ? std::sqrt(c->h_res[RES_TRSQ] / N) : NAN;
         // with the overlap the next sweep's start work -- the prologue's kernels and both
-        // normal fills -- runs between ev[5] and ev[8], counted here
-        c->timing.ms_hyper = (staged ? 0.0 : ev_ms(c->ev[0], ev1)) + (overlap ? ev_ms(ev5, c->ev[8]) : 0.0);
-        c->timing.ms_user_half = ev_ms(ev1, c->ev[2]);
-        c->timing.ms_item_half = ev_ms(ev3, c->ev[4]);
-        c->timing.ms_comm = c->nranks > 1 ? ev_ms(c->ev[2], c->ev[3]) + ev_ms(c->ev[4], c->ev[5]) : 0.0;
+        // tables' normals -- runs between ev[5] and ev[8], counted here
+        c->timing.ms_hyper = ms_start + (overlap ? ev_ms(ev5, c->ev[8]) : 0.0);
         c->timing.ms_eval = overlap && !par_eval ? ev_ms(c->ev[8], c->ev[6]) : ev_ms(ev5, c->ev[6]);
-        for (int sd = 0; sd < 2; ++sd) {
-            const Side& sdd = sd == 0 ? c->users : c->items;
-            for (int k = 0; k < SBMF_NKIND; ++k) {
-                if (!c->time_kinds && k != KIND_STREAM) continue;  // kept from the run's first sweep
-                double ms = 0.0;
-                for (uint32_t p = 0; p < c->nstages; ++p) {
-                    const Side::Stage& g = *sdd.stg[p];
-                    const bool ran = k < NBIN && !g.bin_rows[k].empty();
-                    const int kp = ran ? c->kpv(p, sd, k) : -1;
-                    if (ran) ms += ev_ms(kp >= 0 ? c->kev(p, sd, kp, 1) : c->kbg(p, sd, k), c->kev(p, sd, k, 1));
-                }
-                c->timing.kern_ms[sd][k] = ms;
-            }
-        }
-        info.ms_sweep = ev_ms(c->ev[0], ev5);
         info.ms_eval = c->timing.ms_eval;
-        c->sweep++;
-        if (cb && cb(&info, user)) break;
+        if (cb && cb(&info, user)) {
+            if (!queued) break;
+            stop_after = true;  // the next sweep's start is queued: it completes, then the run stops
+        } else if (stop_after) {
+            break;
+        }
     }
 }
 

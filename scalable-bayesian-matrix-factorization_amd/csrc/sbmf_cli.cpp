@@ -439,6 +439,9 @@ int main(int argc, char** argv) {
         cfg.seed = (uint64_t)cl.getl("seed", 1);
         const std::string rng = cl.get("rng", "ref");
         cfg.rng_mode = rng == "philox" ? SBMF_RNG_PHILOX : SBMF_RNG_REFERENCE;
+        // on_sweep prints and appends to files, never stops the run and reads no device state: in
+        // Philox mode the next sweep's start is queued before it runs (sbmf_config.pipeline)
+        cfg.pipeline = 1;
         if (q == "sbpmf2")
             cfg.quirks = SBMF_QUIRKS_SBPMF2;
         else if (q == "none")

@@ -32,7 +32,7 @@ class Config(C.Structure):
         ("gram_threshold", C.c_uint32), ("row_kernel", C.c_uint32), ("stream_threshold", C.c_uint32),
         ("split_chunk", C.c_uint32), ("tune", C.c_uint32), ("method", C.c_uint32), ("vb_batches", C.c_uint32),
         ("average", C.c_uint32), ("libfm_dim", C.c_uint32), ("reg0", C.c_double), ("regw", C.c_double),
-        ("regv", C.c_double),
+        ("regv", C.c_double), ("pipeline", C.c_uint32),
     ]
 
 

@@ -168,6 +168,31 @@ def test_evaluation_order_changes_nothing(ml100k):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("quirks", ["final", "bias2"])
+def test_pipelined_sweeps_change_nothing(ml100k, quirks):
+    """sbmf_config.pipeline: sweep s+1's start (hyperparameter upload, user half) is queued
+    before sweep s is reported.  The chain, every per-sweep report and the factors are the
+    same bit for bit; a stop asked for at sweep s takes effect after sweep s+1."""
+    tr, te = ml100k
+    kw = dict(num_factor=30, seed=8, rng="philox", eval_train=True, quirks=quirks)
+    a = _run(tr, te, 6, **kw)
+    b = _run(tr, te, 6, pipeline=1, **kw)
+    for f in ("sweep", "rmse_avg", "rmse_this", "rmse_train", "tau", "collected"):
+        assert np.array_equal([h[f] for h in a.history], [h[f] for h in b.history]), f
+    for x, y in zip(a.factors(), b.factors()):
+        assert np.array_equal(x, y)
+    # two runs in a row on one learner (the second starts from the staged sweep 6)
+    b.learn(sweeps=3)
+    a.learn(sweeps=3)
+    assert np.array_equal(a.rmse_trajectory, b.rmse_trajectory)
+    # a stop at sweep 2: sweep 3 is already queued, so the run ends after it
+    L = FMLearnSBPMF(pipeline=1, **kw)
+    L.set_data(Data(*tr), Data(*te))
+    L.learn(sweeps=6, callback=lambda h: h["sweep"] == 2)
+    assert [h["sweep"] for h in L.history] == [0, 1, 2, 3]
+    assert np.array_equal(L.rmse_trajectory, a.rmse_trajectory[:4])
+
+
 @pytest.mark.parametrize("kw", [{}, {"stream_threshold": 40, "split_chunk": 64}, {"stream_threshold": 16}])
 def test_multigpu_residual_mode_matches_oracle(ml100k, kw):
     """The residual form every rank uses with several GPUs (e0 = r - own.partner
