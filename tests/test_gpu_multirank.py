@@ -78,6 +78,27 @@ def test_ranks_on_one_gpu_match_single_rank(ml100k, tmp_path, nranks, rng, tune,
             assert np.array_equal(z["bu"], bu1) and np.array_equal(z["bv"], bv1) and z["b0"][0] == b01
 
 
+@pytest.mark.parametrize("nranks,quirks", [(3, "final"), (2, "bias2")])
+def test_pipelined_ranks_match_single_rank(ml100k, tmp_path, nranks, quirks):
+    """sbmf_config.pipeline on every rank (bench.py's setting at N > 1): each rank queues sweep
+    s+1's start -- its user half and that half's block broadcasts and residual exchange --
+    before reporting sweep s.  The ranks still end with the single-rank chain bit for bit."""
+    K, sweeps, seed = 30, 4, 6
+    tr, te = ml100k
+    L = FMLearnSBPMF(num_factor=K, seed=seed, rng="philox", quirks=quirks)
+    L.set_data(Data(*tr), Data(*te))
+    L.learn(sweeps=sweeps)
+    U1, V1 = L.factors()
+    rmse1 = L.rmse_trajectory
+    L.close()
+    outs = _run_ranks(tmp_path, nranks, [str(K), str(sweeps), str(seed), "philox", "0", quirks],
+                      env={"SBMF_WORKER_PIPELINE": "1"})
+    for r in range(nranks):
+        z = np.load(outs[r])
+        assert np.array_equal(z["U"], U1) and np.array_equal(z["V"], V1), r
+        assert np.array_equal(z["rmse"], rmse1)
+
+
 @pytest.mark.parametrize("nranks,data,K,seed,epochs,rng", [(2, "ml100k", 8, 1, 10, "ref"), (3, "ml100k", 20, 7, 5, "ref"),
                                                            (3, "ragged", 8, 2, 20, "ref"), (2, "ml100k", 8, 5, 4, "philox")])
 def test_vb_ranks_on_one_gpu(ml100k, ragged, tmp_path, nranks, data, K, seed, epochs, rng):

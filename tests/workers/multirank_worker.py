@@ -55,7 +55,8 @@ def main():
                          method="als" if method == "als" else "mcmc", k0=k0, k1=k1,
                          regular=tuple(float(x) for x in reg.split(",")), init_stdev=0.1)
     else:
-        L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, tune=tune, quirks=quirks)
+        L = FMLearnSBPMF(num_factor=int(K), seed=int(seed), rng=rng, device=0, tune=tune, quirks=quirks,
+                         pipeline=int(os.environ.get("SBMF_WORKER_PIPELINE", "0")))
     L.init(comm=(int(nranks), int(rank), bytes.fromhex(idhex)))
     L.set_data(Data(*tr), Data(*te), num_users=dims[0], num_items=dims[1])
     L.learn(sweeps=int(sweeps))
