@@ -427,6 +427,14 @@ def vb_main(args):
     # (2K of them) the {e,t} record read + written (32), the partner mean and
     # variance (16) and its ids (8)
     bytes_epoch = n_train * (32.0 * K + 2 * K * 56.0)
+    bytes_factor = n_train * 2 * K * 56.0  # the factor passes alone: the epoch's dominant kernels
+    factor_ms = float(L.timing().ms_vb_factor)
+    vb_traffic = vb_traffic_src = None
+    pv = os.path.join(REPO, "profiles", "pmc_vb_traffic.json")
+    if os.path.exists(pv) and not one_device and world == 1:
+        pm = json.load(open(pv))
+        vb_traffic = pm.get("vb_factor_passes")
+        vb_traffic_src = "profiles/pmc_vb_traffic.json (%s)" % pm.get("_run", "run not recorded")
     out = {
         "metric": "ratings/sec per online-VB epoch, %s K=%d" % ({"netflix": "synthetic 100M (Netflix-shaped)"}.get(
             args.shape, args.shape), K),
@@ -444,9 +452,19 @@ def vb_main(args):
                    "num_users": dims[0], "num_items": dims[1], "n_train": n_train, "n_test": len(test[0]), "K": K,
                    "rng": "philox", "prep_s": prep_s, "gpu_ms_per_epoch": gpu_ms,
                    "test_rmse_after": hist[-1]["rmse_avg"], "epochs_run": len(L.history)},
-        "roofline": {"kernel": "epoch (all VB kernels)", "bound": "hbm", "achieved": bytes_epoch / (gpu_ms * 1e-3) / 1e9,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": bytes_epoch / (gpu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": None, "bytes_per_epoch": bytes_epoch},
+        "roofline": {"kernel": "factor passes (every mini-batch's 2K k_user_v / k_item_vp launches)", "bound": "hbm",
+                     "achieved": bytes_factor / (factor_ms * 1e-3) / 1e9 if factor_ms > 0 else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": bytes_factor / (factor_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if factor_ms > 0 else None,
+                     "traffic": vb_traffic, "traffic_source": vb_traffic_src or (
+                         "none: rocprofv3 --pmc FETCH_SIZE over this line segfaulted in a profiler thread right "
+                         "after HSA init (profiles/r06/r06s19_vb_pmc_fetch_crash.log); round 3's VB passes "
+                         "(profiles/r03_vb_*) predate the current kernels"), "bytes_per_epoch": bytes_factor,
+                     "ms_per_epoch": factor_ms,
+                     "timing": "HIP events around each mini-batch's factor loop on the compute stream "
+                               "(sbmf_timing.ms_vb_factor), mean over the timed epochs",
+                     "epoch_aggregate": {"kernels": "every VB kernel of the epoch", "bytes": bytes_epoch,
+                                         "ms": gpu_ms, "frac": bytes_epoch / (gpu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
     }
     L.close()
     if not args.no_cpu and rank == 0 and world == 1:

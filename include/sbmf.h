@@ -277,6 +277,10 @@ typedef struct sbmf_timing {
     uint32_t kern_rows[2][SBMF_NKIND];
     uint64_t bytes_algorithmic;  /* whole sweep, both halves                                    */
     uint32_t n_launch;           /* kernel launches in the last sweep                           */
+    double ms_vb_factor;         /* online VB: device time of an epoch's factor passes (the 2K
+                                    vbo_user_v / vbo_item_v launches of every mini-batch, HIP
+                                    events around each batch's factor loop), mean over the last
+                                    run's epochs (round 6); 0 for the other learners              */
 } sbmf_timing;
 int sbmf_get_timing(sbmf_ctx* ctx, sbmf_timing* t);
 

@@ -2035,6 +2035,7 @@ int sbmf_run(sbmf_ctx* ctx, uint32_t sweeps, sbmf_sweep_cb cb, void* user) {
         vbo_run(ctx->vb, sweeps, cb, user);
         ctx->timing = sbmf_timing{};
         ctx->timing.n_launch = vbo_launches(ctx->vb);
+        ctx->timing.ms_vb_factor = vbo_factor_ms(ctx->vb);
         return SBMF_OK;
     }
     if (ctx->fm) {

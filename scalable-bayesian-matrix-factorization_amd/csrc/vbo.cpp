@@ -109,10 +109,16 @@ struct VBLearner {
     double last_rmse = NAN, last_alpha = NAN;
     double ms_layout = 0.0;
     uint32_t n_launch = 0;
+    // [batch][begin, end]: each mini-batch's 2K factor passes (vbo_user_v / vbo_item_v), timed
+    // with HIP events on the compute stream -- the epoch's dominant kernels (bench.py's roofline)
+    std::vector<hipEvent_t> fev;
+    double ms_factor_sum = 0.0;  // the last run's epochs: factor-pass time summed ...
+    uint32_t n_factor_epochs = 0;  // ... over this many epochs
 
     ~VBLearner() {
         if (worker.joinable()) worker.join();
         for (auto& e : ev) event_destroy(e);
+        for (auto& e : fev) event_destroy(e);
         for (hipEvent_t* e : {&uev[0], &uev[1], &done[0], &done[1]}) event_destroy(*e);
         stream_destroy(ust);
     }
@@ -277,6 +283,8 @@ void VBLearner::init(const sbmf_config& c, uint64_t n, const uint32_t* u, const 
     shuffle.resize(N);
     for (uint32_t x = 0; x < N; ++x) shuffle[x] = x + 1;
     for (auto& e : ev) event_create(&e);
+    fev.assign(2 * (size_t)NB, nullptr);
+    for (auto& e : fev) event_create(&e);
     HIPCHK(hipGetDevice(&dev));
     stream_create(&ust);
     for (int k = 0; k < 2; ++k) {
@@ -711,6 +719,7 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
                 if (XS > 1) HIPCHK(vbo_item_update(gi_, nG, sums, (int)XS, 0, 0, tb, D, st));
             }
             int pend = VB_PEND_W;
+            HIPCHK(hipEventRecord(fev[2 * (size_t)b], st));
             for (uint32_t f = 0; f < K; ++f) {
                 HIPCHK(vbo_user_v(ut, nut, ur_, upart_, f, pend, f - 1, tb, D, ETu, VS, st));
                 if (R > 1) {
@@ -721,6 +730,7 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
                 }
                 pend = VB_PEND_V;
             }
+            HIPCHK(hipEventRecord(fev[2 * (size_t)b + 1], st));
             HIPCHK(vbo_user_flush(ut, nut, ur_, upart_, pend, K - 1, tb, D, ETu, st));
             if (R > 1) {  // the blends from every rank's alpha sum and user-range sig sums
                 HIPCHK(vbo_hyper_local(ETu.at(L.bbase[b]), B, tb, u0, u1, part, part_cap, d_send.as<double>(), st));
@@ -772,6 +782,12 @@ void VBLearner::run(uint32_t epochs, sbmf_sweep_cb cb, void* user) {
         float ms_epoch = 0.f, ms_eval = 0.f;
         (void)hipEventElapsedTime(&ms_epoch, ev[0], ev[1]);
         (void)hipEventElapsedTime(&ms_eval, ev[1], ev[2]);
+        for (uint32_t b = 0; b < NB; ++b) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, fev[2 * (size_t)b], fev[2 * (size_t)b + 1]);
+            ms_factor_sum += ms;
+        }
+        ++n_factor_epochs;
         sbmf_sweep_info info{};
         info.sweep = epoch;
         info.collected = 1;
@@ -795,7 +811,11 @@ VBLearner* vbo_create(const sbmf_config& c, uint64_t n, const uint32_t* u, const
     return L.release();
 }
 void vbo_destroy(VBLearner* L) { delete L; }
-void vbo_run(VBLearner* L, uint32_t epochs, sbmf_sweep_cb cb, void* user) { L->run(epochs, cb, user); }
+void vbo_run(VBLearner* L, uint32_t epochs, sbmf_sweep_cb cb, void* user) {
+    L->ms_factor_sum = 0.0;
+    L->n_factor_epochs = 0;
+    L->run(epochs, cb, user);
+}
 void vbo_predict_out(VBLearner* L, double* out) {
     HIPCHK(hipStreamSynchronize(L->st));
     if (!L->su.empty()) HIPCHK(hipMemcpy(out, L->d_pred.p, L->su.size() * sizeof(double), hipMemcpyDeviceToHost));
@@ -839,5 +859,6 @@ void vbo_hyper_out(VBLearner* L, double* h4k, double* alpha) {
 }
 double vbo_layout_ms(const VBLearner* L) { return L->ms_layout; }
 uint32_t vbo_launches(const VBLearner* L) { return L->n_launch; }
+double vbo_factor_ms(const VBLearner* L) { return L->n_factor_epochs ? L->ms_factor_sum / L->n_factor_epochs : 0.0; }
 
 }  // namespace sbmf

@@ -144,6 +144,9 @@ void vbo_biases(VBLearner* L, double* bu, double* bv, double* b0);
 void vbo_hyper_out(VBLearner* L, double* h4k, double* alpha);  // [sigma_v | 0 | 0 | 0], alpha
 double vbo_layout_ms(const VBLearner* L);  // host time of the last epoch's shuffle + batch layout
 uint32_t vbo_launches(const VBLearner* L);
+// device time of an epoch's factor passes (every mini-batch's 2K vbo_user_v / vbo_item_v launches,
+// HIP events around each batch's factor loop), averaged over the last vbo_run's epochs
+double vbo_factor_ms(const VBLearner* L);
 
 // scratch doubles vbo_update_w0 / vbo_hyper (one rank) and vbo_hyper_local /
 // vbo_hyper_final (several ranks) need for B cases:

@@ -49,7 +49,7 @@ class Timing(C.Structure):
         ("ms_eval", C.c_double), ("ms_comm", C.c_double),
         ("kern_ms", (C.c_double * NKIND) * 2), ("kern_bytes", (C.c_uint64 * NKIND) * 2),
         ("kern_rows", (C.c_uint32 * NKIND) * 2),
-        ("bytes_algorithmic", C.c_uint64), ("n_launch", C.c_uint32),
+        ("bytes_algorithmic", C.c_uint64), ("n_launch", C.c_uint32), ("ms_vb_factor", C.c_double),
     ]
 
 
